@@ -1,0 +1,146 @@
+/*
+ * lislam — MI355X (gfx950) implementation of the per-scan hot path of
+ * himhan34/Intensity_based_LiDAR_SLAM_for_me-: Ouster cloud -> range/intensity images ->
+ * LOAM curvature features -> scan-to-scan kNN association -> point-to-line / point-to-plane
+ * residual + Jacobian -> Ceres-semantics pose solve.
+ *
+ * C ABI (plain pointers and sizes; no C++ or torch types).  Every function returns an int
+ * status (LISLAM_OK == 0); lislam_last_error() describes the last failure of a context.
+ * A context owns one HIP device + stream and is not internally thread safe; use one context
+ * per callback thread / GPU (the reference runs one ROS node per process, scanRegistration.cpp:738).
+ *
+ * Reference interfaces replaced (file:line in the reference tree):
+ *   lislam_scan_registration  <- ImageHandler::cloud_handler        src/image_handler.h_ouster:103
+ *                                + laserCloudHandler                   src/scanRegistration.cpp:189-658
+ *   lislam_odom_step          <- laserOdometry main-loop body          src/laserOdometry.cpp:313-808
+ *   lislam_batch_*            <- the same two stages for a batch of scans resident in HBM
+ *                                (independent scans / chains of scans)
+ *   lislam_eval_factors       <- ceres::CostFunction::Evaluate of LidarEdgeFactor /
+ *                                LidarPlaneFactor / LidarPlaneNormFactor
+ *                                                                      src/lidarFeaturePointsFunction.hpp:143-293
+ */
+#ifndef LISLAM_H_
+#define LISLAM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LISLAM_OK 0
+#define LISLAM_ERR_ARG (-1)      /* invalid argument / unsupported configuration */
+#define LISLAM_ERR_DEVICE (-2)   /* HIP runtime error */
+#define LISLAM_ERR_CAPACITY (-3) /* caller buffer too small */
+#define LISLAM_ERR_STATE (-4)    /* call out of order */
+
+typedef struct lislam_ctx lislam_ctx;
+typedef struct lislam_batch lislam_batch;
+typedef struct lislam_odom lislam_odom;
+
+/* Parameters the reference reads from the ROS parameter server / compile-time constants. */
+typedef struct {
+  int32_t n_scans;        /* N_SCANS = image_height (scanRegistration.cpp:692; spot.yaml:8): 16/32/64/128 */
+  int32_t width;          /* image_width (spot.yaml:7) */
+  float min_range;        /* MINIMUM_RANGE = remove_radius (scanRegistration.cpp:695; spot.yaml:49) */
+  int32_t max_iterations; /* ceres max_num_iterations of the odometry solve (laserOdometry.cpp:707) */
+  int32_t want_images;    /* materialize image_range / image_intensity / cloud_track (a1) */
+} lislam_config;
+
+/* Field layout of a sensor_msgs/PointCloud2 point (fromROSMsg, image_handler.h_ouster:106). */
+typedef struct {
+  uint32_t point_step; /* bytes per point (Ouster: 48; PCL PointXYZI: 32; packed xyzI: 16) */
+  uint32_t off_x, off_y, off_z, off_intensity; /* byte offsets of the float32 fields */
+} lislam_point_layout;
+
+/* Features of one scan as published by scanRegistration (scanRegistration.cpp:592-642).
+ * Points are float32 (x, y, z, intensity) quadruples; intensity = scanID + 0.1 * relTime.
+ * Capacities are in points; on return n_* hold the counts.  Null pointers are skipped. */
+typedef struct {
+  float* laser_cloud; int32_t cap_laser_cloud; int32_t n_laser_cloud;   /* /velodyne_cloud_2 */
+  float* sharp; int32_t cap_sharp; int32_t n_sharp;                     /* /laser_cloud_sharp */
+  float* less_sharp; int32_t cap_less_sharp; int32_t n_less_sharp;      /* /laser_cloud_less_sharp */
+  float* flat; int32_t cap_flat; int32_t n_flat;                        /* /laser_cloud_flat */
+  float* less_flat; int32_t cap_less_flat; int32_t n_less_flat;         /* /laser_cloud_less_flat */
+  uint8_t* image_range; uint8_t* image_intensity;                       /* H*W each (cloud_handler) */
+  float* cloud_track;                                                   /* H*W*4 (cloud_handler) */
+} lislam_scan_out;
+
+/* One frame of features as consumed by laserOdometry (laserOdometry.cpp:336-377). */
+typedef struct {
+  const float* sharp; int32_t n_sharp;
+  const float* less_sharp; int32_t n_less_sharp;
+  const float* flat; int32_t n_flat;
+  const float* less_flat; int32_t n_less_flat;
+} lislam_frame;
+
+/* ---------------------------------------------------------------- context */
+int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out);
+int lislam_ctx_destroy(lislam_ctx* ctx);
+const char* lislam_last_error(const lislam_ctx* ctx);
+int lislam_synchronize(lislam_ctx* ctx);
+/* Use an external hipStream_t (e.g. a torch stream) instead of the context's own. */
+int lislam_set_stream(lislam_ctx* ctx, void* hip_stream);
+int lislam_get_stream(lislam_ctx* ctx, void** hip_stream);
+
+/* ---------------------------------------------------------------- single scan (drop-in) */
+/* laserCloudHandler: one organized cloud of n_scans*width points (host memory) -> features. */
+int lislam_scan_registration(lislam_ctx* ctx, const void* points, const lislam_point_layout* layout,
+                             lislam_scan_out* out);
+
+/* laserOdometry node: state = last corner/surf clouds, para_q/para_t, q_w_curr/t_w_curr. */
+int lislam_odom_create(lislam_ctx* ctx, lislam_odom** out);
+int lislam_odom_destroy(lislam_odom* od);
+/* Process one frame.  para_out[7] = (q_last_curr x,y,z,w, t_last_curr), pose_out[7] = (q_w_curr,
+ * t_w_curr), stats_out[8] = corner/plane correspondences of the two outer passes, LM iterations
+ * of each pass, termination of each pass (0 max-iterations, 1 convergence, 2 failure). */
+int lislam_odom_step(lislam_odom* od, const lislam_frame* frame, double* para_out, double* pose_out,
+                     int32_t* stats_out);
+
+/* ---------------------------------------------------------------- batch (device resident) */
+int lislam_batch_create(lislam_ctx* ctx, int32_t max_scans, lislam_batch** out);
+int lislam_batch_destroy(lislam_batch* b);
+/* Copy n_scans clouds from host memory (contiguous, n_scans*n_scans_cfg*width points). */
+int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout);
+/* Device pointer of the packed float4 (x,y,z,intensity) input buffer [max_scans][H*W]. */
+int lislam_batch_input_device_ptr(lislam_batch* b, void** dptr);
+/* a1..a7 for scans [0, n_scans) of the batch. */
+int lislam_batch_extract(lislam_batch* b, int32_t n_scans);
+/* a12..a18 for scans [0, n_scans): ceil((n_scans-1)/chain_len) independent chains, chain c is a
+ * fresh laserOdometry node over scans [c*chain_len, min((c+1)*chain_len, n_scans-1)]. */
+int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len);
+/* Enable per-kernel HIP-event timing of the next calls; times are read with kernel_times. */
+int lislam_batch_set_timing(lislam_batch* b, int32_t enable);
+/* ms of the last extract / odometry calls: [front, lines, compact, odometry]. */
+int lislam_batch_kernel_times(lislam_batch* b, float* ms4);
+
+#define LISLAM_OUT_IMAGE_RANGE 0     /* uint8  [H*W] */
+#define LISLAM_OUT_IMAGE_INTENSITY 1 /* uint8  [H*W] */
+#define LISLAM_OUT_CLOUD_TRACK 2     /* float4 [H*W] */
+#define LISLAM_OUT_LASER_CLOUD 3     /* float4 [n]   */
+#define LISLAM_OUT_CURVATURE 4       /* float  [n]   */
+#define LISLAM_OUT_LABEL 5           /* int8   [n]   */
+#define LISLAM_OUT_LINE_OFFSETS 6    /* int32  [H+1] */
+#define LISLAM_OUT_SHARP 7           /* float4 [n]   */
+#define LISLAM_OUT_LESS_SHARP 8      /* float4 [n]   */
+#define LISLAM_OUT_FLAT 9            /* float4 [n]   */
+#define LISLAM_OUT_LESS_FLAT 10      /* float4 [n]   */
+#define LISLAM_OUT_PARA 11           /* double [7]   */
+#define LISLAM_OUT_POSE 12           /* double [7]   */
+#define LISLAM_OUT_STATS 13          /* int32  [8]   */
+/* Copy one output of one scan to host memory; cap/n count elements of the listed type. */
+int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n);
+
+/* ---------------------------------------------------------------- cost functors */
+/* Evaluate n residual blocks at (q[4] = x,y,z,w, t[3]) on the GPU.  kind[i]: 0 LidarEdgeFactor
+ * (pts: curr, a, b), 1 LidarPlaneFactor (curr, j, l, m), 2 LidarPlaneNormFactor (curr, n, d);
+ * pts holds 12 doubles per block.  Outputs residuals[3n] (unused entries 0) and local-
+ * parameterization Jacobians jac[3n x 6] (d/d delta-theta, d/d t), both optional. */
+int lislam_eval_factors(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,
+                        const double* t, double* residuals, double* jac);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LISLAM_H_ */

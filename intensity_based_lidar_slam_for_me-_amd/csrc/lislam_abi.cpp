@@ -1,0 +1,489 @@
+// C ABI of liblislam (include/lislam.h): contexts, device-resident batches, the single-scan
+// scanRegistration / laserOdometry drop-ins and the batched functor evaluation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lislam.h"
+#include "lislam_internal.hpp"
+
+using namespace lislam;
+
+struct lislam_ctx {
+  lislam_config cfg;
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  lislam_batch* single = nullptr;  // 2-scan batch behind lislam_scan_registration / odom_step
+};
+
+struct lislam_batch {
+  lislam_ctx* ctx = nullptr;
+  int max_scans = 0, H = 0, W = 0, N = 0;
+  int cap_sharp = 0, cap_less_sharp = 0, cap_flat = 0;
+  std::vector<void*> allocs;
+  FeatureArgs fa{};
+  OdomArgs oa{};
+  double* d_init = nullptr;
+  bool timing = false;
+  hipEvent_t ev[6] = {};
+  float ms[4] = {0, 0, 0, 0};
+  int extracted = 0;
+};
+
+struct lislam_odom {
+  lislam_ctx* ctx = nullptr;
+  bool have_last = false;
+  double state[14] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0};
+  int frames = 0;
+};
+
+namespace {
+
+int fail(lislam_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(ctx, x)                                                                  \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fail(ctx, LISLAM_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename T>
+int dalloc(lislam_batch* b, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+  if (e != hipSuccess) return fail(b->ctx, LISLAM_ERR_DEVICE, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+  b->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return LISLAM_OK;
+}
+
+bool valid_lines(int n) { return n == 16 || n == 32 || n == 64 || n == 128; }
+
+// Pack host PointCloud2-style points into float4 (x, y, z, intensity).
+void pack_points(const void* src, size_t n, const lislam_point_layout* L, std::vector<float>& out) {
+  out.resize(n * 4);
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* p = s + i * L->point_step;
+    std::memcpy(&out[i * 4 + 0], p + L->off_x, 4);
+    std::memcpy(&out[i * 4 + 1], p + L->off_y, 4);
+    std::memcpy(&out[i * 4 + 2], p + L->off_z, 4);
+    std::memcpy(&out[i * 4 + 3], p + L->off_intensity, 4);
+  }
+}
+
+bool is_packed(const lislam_point_layout* L) {
+  return !L || (L->point_step == 16 && L->off_x == 0 && L->off_y == 4 && L->off_z == 8 && L->off_intensity == 12);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out) {
+  if (!cfg || !out) return LISLAM_ERR_ARG;
+  *out = nullptr;
+  if (!valid_lines(cfg->n_scans) || cfg->width <= 0 || cfg->max_iterations < 0) return LISLAM_ERR_ARG;
+  lislam_ctx* c = new lislam_ctx();
+  c->cfg = *cfg;
+  c->device = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || device < 0 || device >= ndev) {
+    delete c;
+    return LISLAM_ERR_DEVICE;
+  }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return LISLAM_ERR_DEVICE;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return LISLAM_OK;
+}
+
+int lislam_ctx_destroy(lislam_ctx* c) {
+  if (!c) return LISLAM_OK;
+  hipSetDevice(c->device);
+  if (c->single) lislam_batch_destroy(c->single);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return LISLAM_OK;
+}
+
+const char* lislam_last_error(const lislam_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int lislam_synchronize(lislam_ctx* c) {
+  if (!c) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return LISLAM_OK;
+}
+
+int lislam_set_stream(lislam_ctx* c, void* s) {
+  if (!c) return LISLAM_ERR_ARG;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return LISLAM_OK;
+}
+
+int lislam_get_stream(lislam_ctx* c, void** s) {
+  if (!c || !s) return LISLAM_ERR_ARG;
+  *s = c->stream;
+  return LISLAM_OK;
+}
+
+// ------------------------------------------------------------------------------ batch
+int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
+  if (!c || !out || max_scans < 1) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  lislam_batch* b = new lislam_batch();
+  b->ctx = c;
+  const int S = max_scans, H = c->cfg.n_scans, W = c->cfg.width, N = H * W;
+  b->max_scans = S; b->H = H; b->W = W; b->N = N;
+  b->cap_sharp = kCapSharpPerLine * H;
+  b->cap_less_sharp = kCapLessSharpPerLine * H;
+  b->cap_flat = kCapFlatPerLine * H;
+  FeatureArgs& f = b->fa;
+  f.S = S; f.H = H; f.W = W; f.N = N; f.min_range = c->cfg.min_range;
+  const size_t SN = (size_t)S * N;
+  int rc = LISLAM_OK;
+  P4* pts = nullptr;
+  rc |= dalloc(b, &pts, SN);
+  f.pts = pts;
+  if (c->cfg.want_images) {
+    rc |= dalloc(b, &f.img_range, SN);
+    rc |= dalloc(b, &f.img_int, SN);
+    rc |= dalloc(b, &f.track, SN);
+  }
+  rc |= dalloc(b, &f.cloud, SN);
+  rc |= dalloc(b, &f.n_cloud, S);
+  rc |= dalloc(b, &f.line_off, (size_t)S * (H + 1));
+  rc |= dalloc(b, &f.curv, SN);
+  rc |= dalloc(b, &f.label, SN);
+  rc |= dalloc(b, &f.stg_sharp, (size_t)S * H * kCapSharpPerLine);
+  rc |= dalloc(b, &f.stg_less_sharp, (size_t)S * H * kCapLessSharpPerLine);
+  rc |= dalloc(b, &f.stg_flat, (size_t)S * H * kCapFlatPerLine);
+  rc |= dalloc(b, &f.stg_less_flat, SN);
+  rc |= dalloc(b, &f.line_counts, (size_t)S * H * 4);
+  rc |= dalloc(b, &f.scr_picked, SN);
+  rc |= dalloc(b, &f.scr_keys, 2 * SN);
+  rc |= dalloc(b, &f.scr_list, SN);
+  rc |= dalloc(b, &f.sharp, (size_t)S * b->cap_sharp);
+  rc |= dalloc(b, &f.less_sharp, (size_t)S * b->cap_less_sharp);
+  rc |= dalloc(b, &f.flat, (size_t)S * b->cap_flat);
+  rc |= dalloc(b, &f.less_flat, SN);
+  rc |= dalloc(b, &f.n_feat, (size_t)S * 4);
+  f.cap_sharp = b->cap_sharp; f.cap_less_sharp = b->cap_less_sharp; f.cap_flat = b->cap_flat;
+  OdomArgs& o = b->oa;
+  o.S = S; o.N = N;
+  o.sharp = f.sharp; o.less_sharp = f.less_sharp; o.flat = f.flat; o.less_flat = f.less_flat;
+  o.n_feat = f.n_feat;
+  o.cap_sharp = b->cap_sharp; o.cap_less_sharp = b->cap_less_sharp; o.cap_flat = b->cap_flat;
+  o.max_iterations = c->cfg.max_iterations;
+  rc |= dalloc(b, &o.blk, (size_t)S * (b->cap_sharp + b->cap_flat) * 9);
+  rc |= dalloc(b, &o.blk_kind, (size_t)S * (b->cap_sharp + b->cap_flat));
+  rc |= dalloc(b, &o.para, (size_t)S * 7);
+  rc |= dalloc(b, &o.pose, (size_t)S * 7);
+  rc |= dalloc(b, &o.stats, (size_t)S * 8);
+  rc |= dalloc(b, &b->d_init, (size_t)S * 14);
+  for (int i = 0; i < 6 && rc == LISLAM_OK; i++)
+    if (hipEventCreate(&b->ev[i]) != hipSuccess) rc = fail(c, LISLAM_ERR_DEVICE, "hipEventCreate");
+  if (rc != LISLAM_OK) {
+    lislam_batch_destroy(b);
+    return LISLAM_ERR_DEVICE;
+  }
+  *out = b;
+  return LISLAM_OK;
+}
+
+int lislam_batch_destroy(lislam_batch* b) {
+  if (!b) return LISLAM_OK;
+  hipSetDevice(b->ctx->device);
+  hipStreamSynchronize(b->ctx->stream);
+  for (void* p : b->allocs) hipFree(p);
+  for (auto& e : b->ev)
+    if (e) hipEventDestroy(e);
+  delete b;
+  return LISLAM_OK;
+}
+
+int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
+  if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  const size_t n = (size_t)n_scans * b->N;
+  if (is_packed(layout)) {
+    HIPCHK(c, hipMemcpyAsync((void*)b->fa.pts, points, n * 16, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  } else {
+    if (layout->point_step < 4 || std::max({layout->off_x, layout->off_y, layout->off_z, layout->off_intensity}) + 4 > layout->point_step)
+      return fail(c, LISLAM_ERR_ARG, "bad point layout");
+    std::vector<float> tmp;
+    pack_points(points, n, layout, tmp);
+    HIPCHK(c, hipMemcpyAsync((void*)b->fa.pts, tmp.data(), n * 16, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return LISLAM_OK;
+}
+
+int lislam_batch_input_device_ptr(lislam_batch* b, void** dptr) {
+  if (!b || !dptr) return LISLAM_ERR_ARG;
+  *dptr = (void*)b->fa.pts;
+  return LISLAM_OK;
+}
+
+int lislam_batch_set_timing(lislam_batch* b, int32_t enable) {
+  if (!b) return LISLAM_ERR_ARG;
+  b->timing = enable != 0;
+  return LISLAM_OK;
+}
+
+int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
+  if (!b || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  FeatureArgs f = b->fa;
+  f.S = n_scans;
+  launch_features(f, c->stream, b->timing ? b->ev : nullptr);
+  HIPCHK(c, hipGetLastError());
+  if (b->timing) {
+    HIPCHK(c, hipEventSynchronize(b->ev[3]));
+    hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]);
+    hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]);
+    hipEventElapsedTime(&b->ms[2], b->ev[2], b->ev[3]);
+  }
+  b->extracted = n_scans;
+  return LISLAM_OK;
+}
+
+static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const double* init_host) {
+  lislam_ctx* c = b->ctx;
+  OdomArgs o = b->oa;
+  o.S = n_scans;
+  o.chain_len = chain_len;
+  o.n_chains = n_scans > 1 ? (n_scans - 1 + chain_len - 1) / chain_len : 0;
+  o.init_state = nullptr;
+  if (init_host) {
+    HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
+    o.init_state = b->d_init;
+  }
+  launch_odometry(o, c->stream, b->timing ? b->ev + 4 : nullptr);
+  HIPCHK(c, hipGetLastError());
+  if (b->timing) {
+    HIPCHK(c, hipEventSynchronize(b->ev[5]));
+    hipEventElapsedTime(&b->ms[3], b->ev[4], b->ev[5]);
+  }
+  return LISLAM_OK;
+}
+
+int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len) {
+  if (!b || n_scans < 1 || n_scans > b->max_scans || chain_len < 1) return LISLAM_ERR_ARG;
+  if (b->extracted < n_scans) return fail(b->ctx, LISLAM_ERR_STATE, "extract %d scans before odometry", n_scans);
+  hipSetDevice(b->ctx->device);
+  return run_odometry(b, n_scans, chain_len, nullptr);
+}
+
+int lislam_batch_kernel_times(lislam_batch* b, float* ms4) {
+  if (!b || !ms4) return LISLAM_ERR_ARG;
+  std::memcpy(ms4, b->ms, sizeof(b->ms));
+  return LISLAM_OK;
+}
+
+int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n) {
+  if (!b || !dst || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t N = b->N;
+  const FeatureArgs& f = b->fa;
+  const OdomArgs& o = b->oa;
+  int cnt = 0;
+  const void* src = nullptr;
+  size_t esz = 0;
+  auto devint = [&](const int* p, int* v) -> int {
+    HIPCHK(c, hipMemcpy(v, p, sizeof(int), hipMemcpyDeviceToHost));
+    return LISLAM_OK;
+  };
+  int ncloud = 0;
+  switch (what) {
+    case LISLAM_OUT_IMAGE_RANGE: src = f.img_range ? f.img_range + scan * N : nullptr; cnt = (int)N; esz = 1; break;
+    case LISLAM_OUT_IMAGE_INTENSITY: src = f.img_int ? f.img_int + scan * N : nullptr; cnt = (int)N; esz = 1; break;
+    case LISLAM_OUT_CLOUD_TRACK: src = f.track ? f.track + scan * N : nullptr; cnt = (int)N; esz = 16; break;
+    case LISLAM_OUT_LASER_CLOUD:
+    case LISLAM_OUT_CURVATURE:
+    case LISLAM_OUT_LABEL:
+      if (devint(f.n_cloud + scan, &ncloud) != LISLAM_OK) return LISLAM_ERR_DEVICE;
+      cnt = ncloud;
+      if (what == LISLAM_OUT_LASER_CLOUD) { src = f.cloud + scan * N; esz = 16; }
+      else if (what == LISLAM_OUT_CURVATURE) { src = f.curv + scan * N; esz = 4; }
+      else { src = f.label + scan * N; esz = 1; }
+      break;
+    case LISLAM_OUT_LINE_OFFSETS: src = f.line_off + (size_t)scan * (b->H + 1); cnt = b->H + 1; esz = 4; break;
+    case LISLAM_OUT_SHARP:
+    case LISLAM_OUT_LESS_SHARP:
+    case LISLAM_OUT_FLAT:
+    case LISLAM_OUT_LESS_FLAT: {
+      const int k = what - LISLAM_OUT_SHARP;
+      if (devint(f.n_feat + scan * 4 + k, &cnt) != LISLAM_OK) return LISLAM_ERR_DEVICE;
+      esz = 16;
+      src = k == 0 ? (const void*)(f.sharp + (size_t)scan * b->cap_sharp)
+          : k == 1 ? (const void*)(f.less_sharp + (size_t)scan * b->cap_less_sharp)
+          : k == 2 ? (const void*)(f.flat + (size_t)scan * b->cap_flat)
+                   : (const void*)(f.less_flat + scan * N);
+      break;
+    }
+    case LISLAM_OUT_PARA: src = o.para + (size_t)scan * 7; cnt = 7; esz = 8; break;
+    case LISLAM_OUT_POSE: src = o.pose + (size_t)scan * 7; cnt = 7; esz = 8; break;
+    case LISLAM_OUT_STATS: src = o.stats + (size_t)scan * 8; cnt = 8; esz = 4; break;
+    default: return fail(c, LISLAM_ERR_ARG, "unknown output %d", what);
+  }
+  if (!src) return fail(c, LISLAM_ERR_STATE, "output %d not materialized (want_images=0?)", what);
+  if (n) *n = cnt;
+  if (cnt > cap) return fail(c, LISLAM_ERR_CAPACITY, "output %d needs %d elements, cap %d", what, cnt, cap);
+  if (cnt > 0) HIPCHK(c, hipMemcpy(dst, src, (size_t)cnt * esz, hipMemcpyDeviceToHost));
+  return LISLAM_OK;
+}
+
+// ------------------------------------------------------------------------------ single scan
+static int ensure_single(lislam_ctx* c) {
+  if (c->single) return LISLAM_OK;
+  return lislam_batch_create(c, 2, &c->single);
+}
+
+int lislam_scan_registration(lislam_ctx* c, const void* points, const lislam_point_layout* layout, lislam_scan_out* out) {
+  if (!c || !points || !out) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  int rc = ensure_single(c);
+  if (rc) return rc;
+  lislam_batch* b = c->single;
+  if ((rc = lislam_batch_upload(b, points, 1, layout))) return rc;
+  if ((rc = lislam_batch_extract(b, 1))) return rc;
+  int n = 0;
+  struct Item { int what; float* dst; int cap; int* n; };
+  Item items[] = {{LISLAM_OUT_LASER_CLOUD, out->laser_cloud, out->cap_laser_cloud, &out->n_laser_cloud},
+                  {LISLAM_OUT_SHARP, out->sharp, out->cap_sharp, &out->n_sharp},
+                  {LISLAM_OUT_LESS_SHARP, out->less_sharp, out->cap_less_sharp, &out->n_less_sharp},
+                  {LISLAM_OUT_FLAT, out->flat, out->cap_flat, &out->n_flat},
+                  {LISLAM_OUT_LESS_FLAT, out->less_flat, out->cap_less_flat, &out->n_less_flat}};
+  for (const Item& it : items) {
+    if (!it.dst) continue;
+    if ((rc = lislam_batch_download(b, it.what, 0, it.dst, it.cap, it.n))) return rc;
+  }
+  const int N = b->N;
+  if (out->image_range && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_RANGE, 0, out->image_range, N, &n))) return rc;
+  if (out->image_intensity && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_INTENSITY, 0, out->image_intensity, N, &n))) return rc;
+  if (out->cloud_track && (rc = lislam_batch_download(b, LISLAM_OUT_CLOUD_TRACK, 0, out->cloud_track, N, &n))) return rc;
+  return LISLAM_OK;
+}
+
+// ------------------------------------------------------------------------------ odometry node
+int lislam_odom_create(lislam_ctx* c, lislam_odom** out) {
+  if (!c || !out) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  int rc = ensure_single(c);
+  if (rc) return rc;
+  *out = new lislam_odom();
+  (*out)->ctx = c;
+  return LISLAM_OK;
+}
+
+int lislam_odom_destroy(lislam_odom* od) {
+  delete od;
+  return LISLAM_OK;
+}
+
+static int put_frame(lislam_batch* b, int slot, const lislam_frame* fr) {
+  lislam_ctx* c = b->ctx;
+  if (fr->n_sharp > b->cap_sharp || fr->n_less_sharp > b->cap_less_sharp || fr->n_flat > b->cap_flat ||
+      fr->n_less_flat > b->N || fr->n_sharp < 0 || fr->n_less_sharp < 0 || fr->n_flat < 0 || fr->n_less_flat < 0)
+    return fail(c, LISLAM_ERR_CAPACITY, "frame exceeds feature capacities");
+  const FeatureArgs& f = b->fa;
+  auto cp = [&](P4* dst, const float* src, int n) -> int {
+    if (n > 0) HIPCHK(c, hipMemcpyAsync(dst, src, (size_t)n * 16, hipMemcpyHostToDevice, c->stream));
+    return LISLAM_OK;
+  };
+  int rc = 0;
+  rc |= cp(f.sharp + (size_t)slot * b->cap_sharp, fr->sharp, fr->n_sharp);
+  rc |= cp(f.less_sharp + (size_t)slot * b->cap_less_sharp, fr->less_sharp, fr->n_less_sharp);
+  rc |= cp(f.flat + (size_t)slot * b->cap_flat, fr->flat, fr->n_flat);
+  rc |= cp(f.less_flat + (size_t)slot * b->N, fr->less_flat, fr->n_less_flat);
+  const int cnt[4] = {fr->n_sharp, fr->n_less_sharp, fr->n_flat, fr->n_less_flat};
+  HIPCHK(c, hipMemcpyAsync(f.n_feat + slot * 4, cnt, sizeof(cnt), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return rc ? LISLAM_ERR_DEVICE : LISLAM_OK;
+}
+
+int lislam_odom_step(lislam_odom* od, const lislam_frame* fr, double* para_out, double* pose_out, int32_t* stats_out) {
+  if (!od || !fr) return LISLAM_ERR_ARG;
+  lislam_ctx* c = od->ctx;
+  hipSetDevice(c->device);
+  lislam_batch* b = c->single;
+  int rc;
+  int32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!od->have_last) {  // first frame: initialization only (laserOdometry.cpp:382-389)
+    if ((rc = put_frame(b, 0, fr))) return rc;
+    od->have_last = true;
+  } else {
+    if ((rc = put_frame(b, 1, fr))) return rc;
+    b->extracted = 2;
+    if ((rc = run_odometry(b, 2, 1, od->state))) return rc;
+    int n;
+    if ((rc = lislam_batch_download(b, LISLAM_OUT_PARA, 1, od->state, 7, &n))) return rc;
+    if ((rc = lislam_batch_download(b, LISLAM_OUT_POSE, 1, od->state + 7, 7, &n))) return rc;
+    if ((rc = lislam_batch_download(b, LISLAM_OUT_STATS, 1, st, 8, &n))) return rc;
+    // the current frame becomes the last frame (laserOdometry.cpp:793-808)
+    if ((rc = put_frame(b, 0, fr))) return rc;
+  }
+  od->frames++;
+  if (para_out) std::memcpy(para_out, od->state, 7 * sizeof(double));
+  if (pose_out) std::memcpy(pose_out, od->state + 7, 7 * sizeof(double));
+  if (stats_out) std::memcpy(stats_out, st, sizeof(st));
+  return LISLAM_OK;
+}
+
+// ------------------------------------------------------------------------------ functors
+int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const double* pts, const double* q,
+                        const double* t, double* residuals, double* jac) {
+  if (!c || n < 0 || (n > 0 && (!kind || !pts)) || !q || !t) return LISLAM_ERR_ARG;
+  if (n == 0) return LISLAM_OK;
+  hipSetDevice(c->device);
+  int* dk = nullptr;
+  double *dp = nullptr, *dx = nullptr, *dr = nullptr, *dj = nullptr;
+  double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
+  auto cleanup = [&]() { hipFree(dk); hipFree(dp); hipFree(dx); hipFree(dr); hipFree(dj); };
+  if (hipMalloc(&dk, n * sizeof(int)) != hipSuccess || hipMalloc(&dp, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&dx, 7 * sizeof(double)) != hipSuccess || hipMalloc(&dr, (size_t)n * 3 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&dj, (size_t)n * 18 * sizeof(double)) != hipSuccess) {
+    cleanup();
+    return fail(c, LISLAM_ERR_DEVICE, "hipMalloc failed in lislam_eval_factors");
+  }
+  hipMemcpy(dk, kind, n * sizeof(int), hipMemcpyHostToDevice);
+  hipMemcpy(dp, pts, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice);
+  hipMemcpy(dx, x, sizeof(x), hipMemcpyHostToDevice);
+  FactorArgs a{n, dk, dp, dx, dr, dj};
+  launch_factors(a, c->stream);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && residuals) e = hipMemcpy(residuals, dr, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && jac) e = hipMemcpy(jac, dj, (size_t)n * 18 * sizeof(double), hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors: %s", hipGetErrorString(e));
+  return LISLAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// Device-side helpers shared by the lislam HIP kernels (gfx950 / CDNA4, wave64).
+//
+// FP semantics: every translation unit is built with -ffp-contract=off so that each a*b+c in
+// the reference's float/double expressions rounds twice, exactly as the reference build
+// (x86-64 SSE2, no -march, CMakeLists.txt:6) does.  Float atan/atan2 are the correctly rounded
+// float of the double function (DESIGN.md "FP semantics"); float division and sqrt are IEEE.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lislam {
+
+constexpr double kPi = 3.14159265358979323846;  // M_PI
+
+struct __attribute__((aligned(16))) P4 {
+  float x, y, z, i;
+};
+
+__device__ __forceinline__ float atan2_f(float y, float x) {
+  return (float)atan2((double)y, (double)x);
+}
+__device__ __forceinline__ float atan_f(float v) { return (float)atan((double)v); }
+
+__device__ __forceinline__ P4 ld4(const P4* p) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  return P4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void st4(P4* p, const P4& v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v.x, v.y, v.z, v.i);
+}
+
+// scanRegistration.cpp:290-331: scan line of a point from its elevation; -1 = dropped.
+__device__ __forceinline__ int scan_id_of(float angle, int n_scans) {
+  int id;
+  if (n_scans == 16) {
+    id = int((angle + 15) / 2 + 0.5);
+  } else if (n_scans == 32) {
+    id = int((angle + 92.0 / 3.0) * 3.0 / 4.0);
+  } else if (n_scans == 64) {
+    id = int((angle + 22.5) * 1.41 + 0.5) - 1;
+  } else {
+    id = int((angle + 22.5) * 2.83 + 0.5) - 1;
+  }
+  return (id > n_scans - 1 || id < 0) ? -1 : id;
+}
+
+__device__ __forceinline__ float elevation_deg(const P4& p) {
+  // atan(z / sqrt(x*x + y*y)) * 180 / M_PI with float atan/sqrt (scanRegistration.cpp:285)
+  return (float)((double)(atan_f(p.z / sqrtf(p.x * p.x + p.y * p.y)) * 180) / kPi);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// ---------------------------------------------------------------- double 3-vectors / quats
+struct D3 {
+  double x, y, z;
+};
+__device__ __forceinline__ D3 operator+(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ D3 operator-(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ D3 operator*(double s, D3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ D3 cross(D3 a, D3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+struct DQ {
+  double x, y, z, w;
+};
+
+// Eigen's Quaternion * Vector3 (_transformVector): uv = 2 (q.vec x v); v + w uv + q.vec x uv.
+__device__ __forceinline__ D3 qrot(const DQ& q, D3 v) {
+  D3 qv{q.x, q.y, q.z};
+  D3 uv = cross(qv, v);
+  uv = uv + uv;
+  D3 wuv{q.w * uv.x, q.w * uv.y, q.w * uv.z};
+  return (v + wuv) + cross(qv, uv);
+}
+
+// Quaternion product in the term grouping of Eigen 3.3's SSE2 quat_product<double>.
+__device__ __forceinline__ DQ qmul(const DQ& a, const DQ& b) {
+  DQ r;
+  r.x = (a.w * b.x + a.y * b.z) + (-(a.z * b.y - a.x * b.w));
+  r.y = (a.w * b.y + a.y * b.w) + (a.z * b.x - a.x * b.z);
+  r.z = (a.w * b.z - a.y * b.x) + (a.z * b.w + a.x * b.y);
+  r.w = (a.w * b.w - a.y * b.y) + (-(a.z * b.z + a.x * b.x));
+  return r;
+}
+
+}  // namespace lislam

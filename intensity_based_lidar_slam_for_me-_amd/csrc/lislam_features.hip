@@ -1,0 +1,534 @@
+// lislam feature front end on gfx950: ImageHandler::cloud_handler + scanRegistration's
+// laserCloudHandler (a1..a7 of SURVEY.md §8(a)) for a batch of S organized scans resident in HBM.
+//
+//   k_scan_front   one 1024-thread workgroup per scan.  Streams the ring-ordered xyzI buffer
+//                  twice with 16-B coalesced loads:
+//                    pass 1: range/intensity images + cloud_track (image_handler.h_ouster:112-139),
+//                            close-point filter (scanRegistration.cpp:152-186), scan line
+//                            histogram (:285-331) and the index where halfPassed flips
+//                            (:336-353) as an LDS atomicMin — the only sequential state of the
+//                            loop is a monotone flag, so it reduces to "first index where".
+//                    pass 2: ori/relTime/intensity (:334-371) and a stable counting sort by
+//                            scanID (= the per-line push_back + concatenation, :373-394) using
+//                            64-lane ballot peer masks for in-wave ranks.
+//   k_scan_lines   one wave per (scan, line): curvature (:397-412), per-segment bitonic sort of
+//                  (curvature, index) keys in LDS (:445), the sharp / flat greedy walks with
+//                  ±5 neighbour suppression as ballot scans (:450-568), the less-flat collection
+//                  (:570-577) and a PCL-semantics VoxelGrid(0.2) of the line (:579-589).
+//   k_scan_compact one workgroup per scan: concatenates the per-line outputs in line order.
+#include <hip/hip_runtime.h>
+
+#include "lislam_device.hpp"
+#include "lislam_internal.hpp"
+
+namespace lislam {
+
+// ------------------------------------------------------------------------------- pass kernel
+constexpr int kFrontThreads = 1024;
+constexpr int kFrontWaves = kFrontThreads / 64;
+
+struct FrontShared {
+  int cnt[kMaxLines];
+  int base[kMaxLines];
+  int wcnt[kFrontWaves][kMaxLines];
+  int wpre[kFrontWaves][kMaxLines];
+  int first, last, flip;
+  float startOri, endOri;
+  int tmp;
+};
+
+__device__ __forceinline__ bool keep_point(const P4& p, float thr2) {
+  return !(p.x * p.x + p.y * p.y + p.z * p.z < thr2);
+}
+
+// ori before halfPassed (scanRegistration.cpp:339-347)
+__device__ __forceinline__ float ori_not_passed(float ori, float startOri) {
+  if ((double)ori < (double)startOri - kPi / 2)
+    ori = (float)((double)ori + 2 * kPi);
+  else if ((double)ori > (double)startOri + kPi * 3 / 2)
+    ori = (float)((double)ori - 2 * kPi);
+  return ori;
+}
+// ori after halfPassed (scanRegistration.cpp:357-365)
+__device__ __forceinline__ float ori_passed(float ori, float endOri) {
+  ori = (float)((double)ori + 2 * kPi);
+  if ((double)ori < (double)endOri - kPi * 3 / 2)
+    ori = (float)((double)ori + 2 * kPi);
+  else if ((double)ori > (double)endOri + kPi / 2)
+    ori = (float)((double)ori - 2 * kPi);
+  return ori;
+}
+
+__global__ __launch_bounds__(kFrontThreads) void k_scan_front(FeatureArgs a) {
+  __shared__ FrontShared sh;
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int N = a.N, H = a.H;
+  const P4* pts = a.pts + (size_t)s * N;
+  const float thr = a.min_range;
+  const float thr2 = thr * thr;
+
+  if (tid == 0) { sh.first = N; sh.last = -1; sh.flip = N; }
+  for (int l = tid; l < H; l += kFrontThreads) sh.cnt[l] = 0;
+  __syncthreads();
+  // ---- first / last kept point -> startOri / endOri (scanRegistration.cpp:247-262)
+  for (int b = 0; b < N; b += kFrontThreads) {
+    const int i = b + tid;
+    if (i < N && keep_point(ld4(pts + i), thr2)) atomicMin(&sh.first, i);
+    __syncthreads();
+    const int f = sh.first;
+    __syncthreads();
+    if (f < N) break;
+  }
+  for (int b = N - 1; b >= 0; b -= kFrontThreads) {
+    const int i = b - tid;
+    if (i >= 0 && keep_point(ld4(pts + i), thr2)) atomicMax(&sh.last, i);
+    __syncthreads();
+    const int l = sh.last;
+    __syncthreads();
+    if (l >= 0) break;
+  }
+  if (tid == 0 && sh.first < N) {
+    const P4 p0 = ld4(pts + sh.first), p1 = ld4(pts + sh.last);
+    const float so = -atan2_f(p0.y, p0.x);
+    float eo = (float)((double)(-atan2_f(p1.y, p1.x)) + 2 * kPi);
+    if ((double)(eo - so) > 3 * kPi)
+      eo = (float)((double)eo - 2 * kPi);
+    else if ((double)(eo - so) < kPi)
+      eo = (float)((double)eo + 2 * kPi);
+    sh.startOri = so;
+    sh.endOri = eo;
+  }
+  __syncthreads();
+  const bool any = sh.first < N;
+  const float startOri = sh.startOri, endOri = sh.endOri;
+
+  // ---- pass 1: images, filter, line histogram, halfPassed flip index
+  uint8_t* img_r = a.img_range ? a.img_range + (size_t)s * N : nullptr;
+  uint8_t* img_i = a.img_int ? a.img_int + (size_t)s * N : nullptr;
+  P4* track = a.track ? a.track + (size_t)s * N : nullptr;
+  for (int b = 0; b < N; b += kFrontThreads) {
+    const int i = b + tid;
+    if (i >= N) break;
+    const P4 p = ld4(pts + i);
+    const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
+    const float range = sqrtf(d2);
+    const float inten = fminf(p.i, 255.0f);
+    if (img_r) img_r[i] = (uint8_t)fminf(range * 20, 255.0f);
+    if (img_i) img_i[i] = (uint8_t)inten;
+    if (track) st4(track + i, (double)range >= 0.1 ? P4{p.x, p.y, p.z, inten} : P4{0.f, 0.f, 0.f, 0.f});
+    if (!(d2 < thr2) && any) {
+      const int sid = scan_id_of(elevation_deg(p), H);
+      if (sid >= 0) {
+        atomicAdd(&sh.cnt[sid], 1);
+        const float ori = ori_not_passed(-atan2_f(p.y, p.x), startOri);
+        if ((double)(ori - startOri) > kPi) atomicMin(&sh.flip, i);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- line offsets (scanStartInd = off + 5, scanEndInd = off + len - 6)
+  if (tid == 0) {
+    int acc = 0;
+    for (int l = 0; l < H; l++) {
+      sh.base[l] = acc;
+      a.line_off[(size_t)s * (H + 1) + l] = acc;
+      acc += sh.cnt[l];
+    }
+    a.line_off[(size_t)s * (H + 1) + H] = acc;
+    a.n_cloud[s] = acc;
+  }
+  __syncthreads();
+  if (!any) return;
+  const int flip = sh.flip;
+  P4* cloud = a.cloud + (size_t)s * N;
+  // ---- pass 2: relTime / intensity + stable scatter by scanID
+  const uint64_t lt = lanemask_lt();
+  for (int b = 0; b < N; b += kFrontThreads) {
+    const int i = b + tid;
+    P4 p{0.f, 0.f, 0.f, 0.f};
+    int sid = -1;
+    if (i < N) {
+      p = ld4(pts + i);
+      if (keep_point(p, thr2)) sid = scan_id_of(elevation_deg(p), H);
+    }
+    if (sid >= 0) {
+      float ori = -atan2_f(p.y, p.x);
+      ori = (i <= flip) ? ori_not_passed(ori, startOri) : ori_passed(ori, endOri);
+      const float relTime = (ori - startOri) / (endOri - startOri);
+      p.i = (float)((double)sid + 0.1 * (double)relTime);
+    }
+    // peer mask of lanes with the same scan line
+    const uint64_t valid = __ballot(sid >= 0);
+    uint64_t peers = valid;
+    for (int bit = 0; bit < 7; bit++) {
+      const uint64_t m = __ballot((sid >> bit) & 1);
+      peers &= ((sid >> bit) & 1) ? m : ~m;
+    }
+    for (int l = tid; l < kFrontWaves * H; l += kFrontThreads) sh.wcnt[l / H][l % H] = 0;
+    __syncthreads();
+    int rank = 0;
+    if (sid >= 0) {
+      rank = __popcll(peers & lt);
+      if (rank == 0) sh.wcnt[wave][sid] = __popcll(peers);
+    }
+    __syncthreads();
+    for (int e = tid; e < kFrontWaves * H; e += kFrontThreads) {
+      const int w = e / H, l = e % H;
+      int acc = 0;
+      for (int k = 0; k < w; k++) acc += sh.wcnt[k][l];
+      sh.wpre[w][l] = acc;
+    }
+    __syncthreads();
+    if (sid >= 0) st4(cloud + sh.base[sid] + sh.wpre[wave][sid] + rank, p);
+    __syncthreads();
+    for (int l = tid; l < H; l += kFrontThreads)
+      sh.base[l] += sh.wpre[kFrontWaves - 1][l] + sh.wcnt[kFrontWaves - 1][l];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------- line kernel
+// LDS capacities of the fast path; longer lines run the same code on global scratch.
+constexpr int kLineCap = 2048;
+
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // workgroup == one wave
+
+// Bitonic sort (ascending) of P (power of two) 64-bit keys by one wave.
+template <typename KeyPtr>
+__device__ void bitonic_sort(KeyPtr keys, int P) {
+  const int lane = lane_id();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < P; i += 64) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = keys[i], b = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) { keys[i] = b; keys[ixj] = a; }
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t first_lane(uint64_t m) { return (uint64_t)__builtin_ctzll(m); }
+
+struct LineCounts {
+  int sharp, less_sharp, flat, less_flat;
+};
+
+// ±5 neighbour suppression of a picked point (scanRegistration.cpp:481-504), wave-parallel:
+// lanes 1..5 test the forward chain, lanes 6..10 the backward one; a link breaks the chain at
+// the first squared step > 0.05.
+template <typename BytePtr>
+__device__ __forceinline__ void suppress(const P4* cloud, int off, int ind, BytePtr picked) {
+  const int lane = lane_id();
+  bool brk = false;
+  int tgt = -1;
+  if (lane >= 1 && lane <= 5) {
+    const int l = lane;
+    const P4 a = ld4(cloud + off + ind + l), b = ld4(cloud + off + ind + l - 1);
+    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+    brk = (double)(dx * dx + dy * dy + dz * dz) > 0.05;
+    tgt = ind + l;
+  } else if (lane >= 6 && lane <= 10) {
+    const int l = -(lane - 5);
+    const P4 a = ld4(cloud + off + ind + l), b = ld4(cloud + off + ind + l + 1);
+    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+    brk = (double)(dx * dx + dy * dy + dz * dz) > 0.05;
+    tgt = ind + l;
+  }
+  const uint64_t bm = __ballot(brk);
+  const uint64_t fwd = bm & 0x3Eull, bwd = bm & 0x7C0ull;
+  const int ffirst = fwd ? (int)first_lane(fwd) : 6;    // first breaking forward lane
+  const int bfirst = bwd ? (int)first_lane(bwd) : 11;   // first breaking backward lane
+  const bool mark = (lane >= 1 && lane < ffirst) || (lane >= 6 && lane < bfirst);
+  if (mark) picked[tgt] = 1;
+  wave_sync();
+}
+
+template <bool kLds>
+__device__ void line_body(const FeatureArgs& a, int s, int line, uint8_t* lds_picked, int8_t* lds_label,
+                          uint64_t* lds_keys, int* lds_list) {
+  const int lane = lane_id();
+  const int N = a.N, H = a.H;
+  const int* lo = a.line_off + (size_t)s * (H + 1);
+  const int off = lo[line];
+  const int len = lo[line + 1] - off;
+  const int total = lo[H];
+  const P4* cloud = a.cloud + (size_t)s * N;
+  float* curv = a.curv + (size_t)s * N;
+  int8_t* glabel = a.label + (size_t)s * N;
+  uint8_t* picked = kLds ? lds_picked : a.scr_picked + (size_t)s * N + off;
+  int8_t* label = kLds ? lds_label : glabel + off;
+  uint64_t* keys = kLds ? lds_keys : a.scr_keys + 2 * ((size_t)s * N + off);  // pow2 padding <= 2 len
+  int* list = kLds ? lds_list : a.scr_list + (size_t)s * N + off;
+
+  // curvature (scanRegistration.cpp:397-412), left-to-right float sums
+  for (int k = lane; k < len; k += 64) {
+    const int i = off + k;
+    float c = 0.f;
+    if (i >= 5 && i < total - 5) {
+      P4 q[11];
+      for (int d = 0; d < 11; d++) q[d] = ld4(cloud + i - 5 + d);
+      const float dX = q[0].x + q[1].x + q[2].x + q[3].x + q[4].x - 10 * q[5].x + q[6].x + q[7].x + q[8].x + q[9].x + q[10].x;
+      const float dY = q[0].y + q[1].y + q[2].y + q[3].y + q[4].y - 10 * q[5].y + q[6].y + q[7].y + q[8].y + q[9].y + q[10].y;
+      const float dZ = q[0].z + q[1].z + q[2].z + q[3].z + q[4].z - 10 * q[5].z + q[6].z + q[7].z + q[8].z + q[9].z + q[10].z;
+      c = dX * dX + dY * dY + dZ * dZ;
+    }
+    curv[i] = c;
+    picked[k] = 0;
+    label[k] = 0;
+  }
+  wave_sync();
+
+  LineCounts cnt{0, 0, 0, 0};
+  P4* o_sharp = a.stg_sharp + ((size_t)s * H + line) * kCapSharpPerLine;
+  P4* o_lsharp = a.stg_less_sharp + ((size_t)s * H + line) * kCapLessSharpPerLine;
+  P4* o_flat = a.stg_flat + ((size_t)s * H + line) * kCapFlatPerLine;
+  P4* o_lflat = a.stg_less_flat + (size_t)s * N + off;
+  const int sI = 5, eI = len - 6;  // scanStartInd / scanEndInd relative to off
+  int nlist = 0;
+  if (eI - sI >= 6) {
+    for (int j = 0; j < 6; j++) {
+      const int sp = sI + (eI - sI) * j / 6;
+      const int ep = sI + (eI - sI) * (j + 1) / 6 - 1;
+      const int seg = ep - sp + 1;
+      int P = 64;
+      while (P < seg) P <<= 1;
+      for (int k = lane; k < P; k += 64) {
+        uint64_t key = ~0ull;
+        if (k < seg) {
+          const float c = curv[off + sp + k];
+          key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)(sp + k);
+        }
+        keys[k] = key;
+      }
+      wave_sync();
+      bitonic_sort(keys, P);
+      // ---- sharp walk: from the largest curvature down (:450-506)
+      int largest = 0;
+      int pos = seg - 1;
+      bool done = false;
+      while (pos >= 0 && !done) {
+        const int p = pos - lane;
+        bool q = false, stop_c = false;
+        if (p >= 0) {
+          const uint64_t key = keys[p];
+          const int ind = (int)(uint32_t)key;
+          const float c = __uint_as_float((uint32_t)(key >> 32));
+          q = picked[ind] == 0 && (double)c > 0.1;
+          stop_c = !((double)c > 0.1);
+        }
+        const uint64_t qm = __ballot(q);
+        if (qm == 0) {
+          // sorted ascending: once a curvature fails "> 0.1" no later entry can pass
+          if (__ballot(stop_c)) break;
+          pos -= 64;
+          continue;
+        }
+        const int fl = (int)first_lane(qm);
+        const int ind = (int)(uint32_t)keys[pos - fl];
+        largest++;
+        if (largest <= 20) {
+          const P4 pt = ld4(cloud + off + ind);
+          if (lane == 0) {
+            if (largest <= 2) {
+              label[ind] = 2;
+              st4(o_sharp + cnt.sharp, pt);
+            } else {
+              label[ind] = 1;
+            }
+            st4(o_lsharp + cnt.less_sharp, pt);
+            picked[ind] = 1;
+          }
+          if (largest <= 2) cnt.sharp++;
+          cnt.less_sharp++;
+          wave_sync();
+          suppress(cloud, off, ind, picked);
+          pos = pos - fl - 1;
+        } else {
+          done = true;
+        }
+      }
+      // ---- flat walk: from the smallest curvature up (:511-568)
+      int smallest = 0;
+      pos = 0;
+      while (pos < seg) {
+        const int p = pos + lane;
+        bool q = false, stop_c = false;
+        if (p < seg) {
+          const uint64_t key = keys[p];
+          const int ind = (int)(uint32_t)key;
+          const float c = __uint_as_float((uint32_t)(key >> 32));
+          q = picked[ind] == 0 && (double)c < 0.1;
+          stop_c = !((double)c < 0.1);
+        }
+        const uint64_t qm = __ballot(q);
+        if (qm == 0) {
+          if (__ballot(stop_c)) break;
+          pos += 64;
+          continue;
+        }
+        const int fl = (int)first_lane(qm);
+        const int ind = (int)(uint32_t)keys[pos + fl];
+        const P4 pt = ld4(cloud + off + ind);
+        if (lane == 0) {
+          label[ind] = -1;
+          st4(o_flat + cnt.flat, pt);
+        }
+        cnt.flat++;
+        smallest++;
+        if (smallest >= 4) { wave_sync(); break; }
+        if (lane == 0) picked[ind] = 1;
+        wave_sync();
+        suppress(cloud, off, ind, picked);
+        pos = pos + fl + 1;
+      }
+      wave_sync();
+      // ---- less-flat collection in index order (:570-577)
+      for (int b = sp; b <= ep; b += 64) {
+        const int k = b + lane;
+        const bool f = k <= ep && label[k] <= 0;
+        const uint64_t m = __ballot(f);
+        if (f) list[nlist + __popcll(m & lanemask_lt())] = k;
+        nlist += __popcll(m);
+      }
+      wave_sync();
+    }
+  }
+  // write labels of the line for the parity tests
+  for (int k = lane; k < len; k += 64) glabel[off + k] = label[k];
+
+  // ---- VoxelGrid(0.2) of the line's less-flat points (PCL VoxelGrid::applyFilter semantics)
+  if (nlist > 0) {
+    const float inv = 1.0f / 0.2f;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int k = lane; k < nlist; k += 64) {
+      const P4 p = ld4(cloud + off + list[k]);
+      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+    }
+    for (int d = 0; d < 3; d++) {
+      for (int o = 32; o > 0; o >>= 1) {
+        mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+        mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+      }
+    }
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)2147483647) {  // PCL: leaf too small -> copy the input
+      for (int k = lane; k < nlist; k += 64) st4(o_lflat + k, ld4(cloud + off + list[k]));
+      cnt.less_flat = nlist;
+    } else {
+      int minb[3], divb[3];
+      for (int d = 0; d < 3; d++) {
+        minb[d] = (int)floorf(mn[d] * inv);
+        divb[d] = (int)floorf(mx[d] * inv) - minb[d] + 1;
+      }
+      const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+      int P = 64;
+      while (P < nlist) P <<= 1;
+      // the key buffer of the fast path holds kLineCap keys; the list never exceeds the line
+      for (int k = lane; k < P; k += 64) {
+        uint64_t key = ~0ull;
+        if (k < nlist) {
+          const P4 p = ld4(cloud + off + list[k]);
+          const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+          const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+          const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+          const uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+          key = ((uint64_t)idx << 32) | (uint32_t)k;
+        }
+        keys[k] = key;
+      }
+      wave_sync();
+      bitonic_sort(keys, P);
+      int nout = 0;
+      for (int b = 0; b < nlist; b += 64) {
+        const int k = b + lane;
+        bool start = false;
+        if (k < nlist) start = (k == 0) || ((keys[k] >> 32) != (keys[k - 1] >> 32));
+        const uint64_t m = __ballot(start);
+        if (start) {
+          const uint32_t v = (uint32_t)(keys[k] >> 32);
+          P4 c = ld4(cloud + off + list[(uint32_t)keys[k]]);
+          int e = k + 1;
+          while (e < nlist && (uint32_t)(keys[e] >> 32) == v) {
+            const P4 p = ld4(cloud + off + list[(uint32_t)keys[e]]);
+            c.x += p.x; c.y += p.y; c.z += p.z; c.i += p.i;
+            e++;
+          }
+          const float n = (float)(e - k);
+          c.x /= n; c.y /= n; c.z /= n; c.i /= n;
+          st4(o_lflat + nout + __popcll(m & lanemask_lt()), c);
+        }
+        nout += __popcll(m);
+      }
+      cnt.less_flat = nout;
+    }
+  }
+  if (lane == 0) {
+    int* c = a.line_counts + ((size_t)s * H + line) * 4;
+    c[0] = cnt.sharp; c[1] = cnt.less_sharp; c[2] = cnt.flat; c[3] = cnt.less_flat;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
+  __shared__ uint8_t picked[kLineCap];
+  __shared__ int8_t label[kLineCap];
+  __shared__ uint64_t keys[kLineCap];
+  __shared__ int list[kLineCap];
+  const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
+  const int* lo = a.line_off + (size_t)s * (a.H + 1);
+  const int len = lo[line + 1] - lo[line];
+  if (len <= kLineCap)
+    line_body<true>(a, s, line, picked, label, keys, list);
+  else  // a line longer than the LDS fast path (non ring-ordered input): global scratch
+    line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr);
+}
+
+// ------------------------------------------------------------------------------- compaction
+__global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
+  const int s = blockIdx.x;
+  const int H = a.H, N = a.N;
+  __shared__ int pre[4][kMaxLines + 1];
+  const int* lc = a.line_counts + (size_t)s * H * 4;
+  if (threadIdx.x < 4) {
+    const int f = threadIdx.x;
+    int acc = 0;
+    for (int l = 0; l < H; l++) { pre[f][l] = acc; acc += lc[l * 4 + f]; }
+    pre[f][H] = acc;
+    a.n_feat[s * 4 + f] = acc;
+  }
+  __syncthreads();
+  const int* lo = a.line_off + (size_t)s * (H + 1);
+  for (int l = 0; l < H; l++) {
+    const size_t stg = (size_t)s * H + l;
+    for (int k = threadIdx.x; k < lc[l * 4 + 0]; k += 256)
+      st4(a.sharp + (size_t)s * a.cap_sharp + pre[0][l] + k, ld4(a.stg_sharp + stg * kCapSharpPerLine + k));
+    for (int k = threadIdx.x; k < lc[l * 4 + 1]; k += 256)
+      st4(a.less_sharp + (size_t)s * a.cap_less_sharp + pre[1][l] + k,
+          ld4(a.stg_less_sharp + stg * kCapLessSharpPerLine + k));
+    for (int k = threadIdx.x; k < lc[l * 4 + 2]; k += 256)
+      st4(a.flat + (size_t)s * a.cap_flat + pre[2][l] + k, ld4(a.stg_flat + stg * kCapFlatPerLine + k));
+    for (int k = threadIdx.x; k < lc[l * 4 + 3]; k += 256)
+      st4(a.less_flat + (size_t)s * N + pre[3][l] + k, ld4(a.stg_less_flat + (size_t)s * N + lo[l] + k));
+  }
+}
+
+void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev) {
+  if (ev) (void)hipEventRecord(ev[0], st);
+  hipLaunchKernelGGL(k_scan_front, dim3(a.S), dim3(kFrontThreads), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[1], st);
+  hipLaunchKernelGGL(k_scan_lines, dim3(a.S * a.H), dim3(64), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[2], st);
+  hipLaunchKernelGGL(k_scan_compact, dim3(a.S), dim3(256), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[3], st);
+}
+
+}  // namespace lislam

@@ -1,0 +1,82 @@
+// Internal (not exported) kernel argument blocks and launch entry points of liblislam.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lislam_device.hpp"
+
+namespace lislam {
+
+constexpr int kMaxLines = 128;               // N_SCANS in {16, 32, 64, 128}
+constexpr int kCapSharpPerLine = 12;         // 2 per segment x 6 (scanRegistration.cpp:459)
+constexpr int kCapLessSharpPerLine = 120;    // 20 per segment x 6 (:466)
+constexpr int kCapFlatPerLine = 24;          // 4 per segment x 6 (:530)
+
+// Device-resident batch of S organized scans and every per-scan output of a1..a7.
+struct FeatureArgs {
+  const P4* pts;  // [S][N] xyzI, ring-major (u * W + v)
+  int S, H, W, N;
+  float min_range;
+  // a1 outputs (nullable)
+  uint8_t* img_range;  // [S][N]
+  uint8_t* img_int;    // [S][N]
+  P4* track;           // [S][N]
+  // a2..a5
+  P4* cloud;      // [S][N] laserCloud, scan-grouped
+  int* n_cloud;   // [S]
+  int* line_off;  // [S][H+1]
+  float* curv;    // [S][N]
+  int8_t* label;  // [S][N]
+  // per-line staging
+  P4* stg_sharp;       // [S][H][12]
+  P4* stg_less_sharp;  // [S][H][120]
+  P4* stg_flat;        // [S][H][24]
+  P4* stg_less_flat;   // [S][N] (line regions at line_off)
+  int* line_counts;    // [S][H][4]
+  // scratch for lines longer than the LDS fast path
+  uint8_t* scr_picked;  // [S][N]
+  uint64_t* scr_keys;   // [S][2N]
+  int* scr_list;        // [S][N]
+  // a6/a7 outputs, concatenated in line order
+  P4* sharp;       // [S][cap_sharp]
+  P4* less_sharp;  // [S][cap_less_sharp]
+  P4* flat;        // [S][cap_flat]
+  P4* less_flat;   // [S][N]
+  int* n_feat;     // [S][4] = sharp, less_sharp, flat, less_flat
+  int cap_sharp, cap_less_sharp, cap_flat;
+};
+
+// Scan-to-scan odometry over chains of consecutive scans (a12..a18).
+struct OdomArgs {
+  int S, N;
+  const P4* sharp; const P4* less_sharp; const P4* flat; const P4* less_flat;
+  const int* n_feat;
+  int cap_sharp, cap_less_sharp, cap_flat;
+  int chain_len;   // pairs per chain; chain c starts (fresh node) at scan c * chain_len
+  int n_chains;
+  int max_iterations;  // ceres max_num_iterations (4, laserOdometry.cpp:707)
+  const double* init_state;  // [n_chains][14] = para(7) + pose(7) at the chain start, or null
+  // block scratch per chain: [n_chains][cap_sharp + cap_flat] records
+  double* blk;     // 9 doubles per record
+  int* blk_kind;   // -1 invalid, 0 edge, 1 plane
+  // outputs per scan
+  double* para;    // [S][7] q_last_curr (x,y,z,w), t_last_curr after this scan
+  double* pose;    // [S][7] q_w_curr, t_w_curr in the chain's frame
+  int* stats;      // [S][8] corners/planes for outer 0/1, LM iterations 0/1, terminations 0/1
+};
+
+// Batched evaluation of the cost functors (lislam_eval_factors).
+struct FactorArgs {
+  int n;
+  const int* kind;     // 0 edge, 1 plane, 2 plane-norm
+  const double* pts;   // [n][12]
+  const double* x;     // q(4), t(3)
+  double* res;         // [n][3] or null
+  double* jac;         // [n][3][6] or null
+};
+
+void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/);
+void launch_odometry(const OdomArgs& a, hipStream_t st, hipEvent_t* ev /*2 or null*/);
+void launch_factors(const FactorArgs& a, hipStream_t st);
+
+}  // namespace lislam

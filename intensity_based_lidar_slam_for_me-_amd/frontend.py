@@ -1,0 +1,197 @@
+"""Host-side mirror of the reference's per-scan interfaces over the lislam C ABI.
+
+``ScanRegistration.laser_cloud_handler`` plays ``laserCloudHandler``
+(``src/scanRegistration.cpp:189``) and returns the clouds that node publishes
+(``:592-642``); ``LaserOdometry.step`` plays one pass of the laserOdometry main loop
+(``src/laserOdometry.cpp:313-808``) in forced-geometric mode; ``Batch`` runs both stages for a
+batch of scans resident in HBM.  All compute runs in ``liblislam.so`` on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import native as nat
+
+CAP_SHARP_PER_LINE, CAP_LESS_SHARP_PER_LINE, CAP_FLAT_PER_LINE = 12, 120, 24
+
+PACKED_XYZI = nat.PointLayout(16, 0, 4, 8, 12)
+OUSTER_LAYOUT = nat.PointLayout(48, 0, 4, 8, 16)  # os_cloud_node/points: x y z pad intensity ...
+
+
+class Context:
+    """One HIP device + stream (lislam_ctx)."""
+
+    def __init__(self, n_scans: int = 64, width: int = 1024, min_range: float = 0.3, max_iterations: int = 4,
+                 want_images: bool = True, device: int = 0):
+        self.lib = nat.load()
+        self.n_scans, self.width = n_scans, width
+        cfg = nat.Config(n_scans, width, min_range, max_iterations, int(want_images))
+        h = ctypes.c_void_p()
+        rc = self.lib.lislam_ctx_create(ctypes.byref(cfg), device, ctypes.byref(h))
+        if rc != nat.OK:
+            raise nat.LislamError(f"lislam_ctx_create failed ({rc}) for n_scans={n_scans} width={width} device={device}")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.lislam_ctx_destroy(self.h)
+            self.h = None
+
+    def synchronize(self):
+        nat.check(self.lib.lislam_synchronize(self.h), self.h, "lislam_synchronize")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class Features:
+    laser_cloud: np.ndarray
+    sharp: np.ndarray
+    less_sharp: np.ndarray
+    flat: np.ndarray
+    less_flat: np.ndarray
+    image_range: np.ndarray | None = None
+    image_intensity: np.ndarray | None = None
+    cloud_track: np.ndarray | None = None
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class ScanRegistration:
+    """scanRegistration node: PointCloud2 -> images + the five feature clouds."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def laser_cloud_handler(self, points: np.ndarray, layout: nat.PointLayout | None = None) -> Features:
+        c = self.ctx
+        H, W = c.n_scans, c.width
+        N = H * W
+        pts = np.ascontiguousarray(points)
+        lay = layout or PACKED_XYZI
+        cloud = np.zeros((N, 4), np.float32)
+        sh = np.zeros((CAP_SHARP_PER_LINE * H, 4), np.float32)
+        ls = np.zeros((CAP_LESS_SHARP_PER_LINE * H, 4), np.float32)
+        fl = np.zeros((CAP_FLAT_PER_LINE * H, 4), np.float32)
+        lf = np.zeros((N, 4), np.float32)
+        ir = np.zeros(N, np.uint8)
+        ii = np.zeros(N, np.uint8)
+        tr = np.zeros((N, 4), np.float32)
+        out = nat.ScanOut(_fp(cloud), N, 0, _fp(sh), sh.shape[0], 0, _fp(ls), ls.shape[0], 0, _fp(fl), fl.shape[0], 0,
+                          _fp(lf), N, 0, ir.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                          ii.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _fp(tr))
+        rc = c.lib.lislam_scan_registration(c.h, nat.ptr(pts), ctypes.byref(lay), ctypes.byref(out))
+        nat.check(rc, c.h, "lislam_scan_registration")
+        return Features(cloud[: out.n_laser_cloud], sh[: out.n_sharp], ls[: out.n_less_sharp], fl[: out.n_flat],
+                        lf[: out.n_less_flat], ir.reshape(H, W), ii.reshape(H, W), tr.reshape(H, W, 4))
+
+
+class LaserOdometry:
+    """laserOdometry node in forced-geometric mode (every frame is optimized)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        nat.check(ctx.lib.lislam_odom_create(ctx.h, ctypes.byref(h)), ctx.h, "lislam_odom_create")
+        self.h = h
+
+    def step(self, f: Features):
+        arrs = [np.ascontiguousarray(a, np.float32) for a in (f.sharp, f.less_sharp, f.flat, f.less_flat)]
+        fr = nat.Frame(_fp(arrs[0]), arrs[0].shape[0], _fp(arrs[1]), arrs[1].shape[0], _fp(arrs[2]), arrs[2].shape[0],
+                       _fp(arrs[3]), arrs[3].shape[0])
+        para = np.zeros(7)
+        pose = np.zeros(7)
+        st = np.zeros(8, np.int32)
+        rc = self.ctx.lib.lislam_odom_step(self.h, ctypes.byref(fr), nat.ptr(para), nat.ptr(pose), nat.ptr(st))
+        nat.check(rc, self.ctx.h, "lislam_odom_step")
+        return para, pose, st
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lislam_odom_destroy(self.h)
+            self.h = None
+
+
+class Batch:
+    """A device-resident batch of scans (a1..a7 + a12..a18 on HBM-resident data)."""
+
+    def __init__(self, ctx: Context, max_scans: int):
+        self.ctx = ctx
+        self.max_scans = max_scans
+        h = ctypes.c_void_p()
+        nat.check(ctx.lib.lislam_batch_create(ctx.h, max_scans, ctypes.byref(h)), ctx.h, "lislam_batch_create")
+        self.h = h
+
+    def upload(self, scans: np.ndarray, layout: nat.PointLayout | None = None):
+        a = np.ascontiguousarray(scans)
+        n = a.shape[0]
+        rc = self.ctx.lib.lislam_batch_upload(self.h, nat.ptr(a), n, ctypes.byref(layout or PACKED_XYZI))
+        nat.check(rc, self.ctx.h, "lislam_batch_upload")
+
+    def extract(self, n: int):
+        nat.check(self.ctx.lib.lislam_batch_extract(self.h, n), self.ctx.h, "lislam_batch_extract")
+
+    def odometry(self, n: int, chain_len: int):
+        nat.check(self.ctx.lib.lislam_batch_odometry(self.h, n, chain_len), self.ctx.h, "lislam_batch_odometry")
+
+    def set_timing(self, on: bool):
+        nat.check(self.ctx.lib.lislam_batch_set_timing(self.h, int(on)), self.ctx.h, "lislam_batch_set_timing")
+
+    def kernel_times(self):
+        ms = np.zeros(4, np.float32)
+        nat.check(self.ctx.lib.lislam_batch_kernel_times(self.h, _fp(ms)), self.ctx.h, "lislam_batch_kernel_times")
+        return ms
+
+    _DT = {nat.OUT_IMAGE_RANGE: (np.uint8, 1), nat.OUT_IMAGE_INTENSITY: (np.uint8, 1), nat.OUT_CLOUD_TRACK: (np.float32, 4),
+           nat.OUT_LASER_CLOUD: (np.float32, 4), nat.OUT_CURVATURE: (np.float32, 1), nat.OUT_LABEL: (np.int8, 1),
+           nat.OUT_LINE_OFFSETS: (np.int32, 1), nat.OUT_SHARP: (np.float32, 4), nat.OUT_LESS_SHARP: (np.float32, 4),
+           nat.OUT_FLAT: (np.float32, 4), nat.OUT_LESS_FLAT: (np.float32, 4), nat.OUT_PARA: (np.float64, 1),
+           nat.OUT_POSE: (np.float64, 1), nat.OUT_STATS: (np.int32, 1)}
+
+    def download(self, what: int, scan: int) -> np.ndarray:
+        dt, w = self._DT[what]
+        N = self.ctx.n_scans * self.ctx.width
+        cap = max(N, 16)
+        buf = np.zeros((cap, w) if w > 1 else cap, dt)
+        n = ctypes.c_int32()
+        rc = self.ctx.lib.lislam_batch_download(self.h, what, scan, nat.ptr(buf), cap, ctypes.byref(n))
+        nat.check(rc, self.ctx.h, "lislam_batch_download")
+        return buf[: n.value].copy()
+
+    def features(self, scan: int) -> Features:
+        return Features(self.download(nat.OUT_LASER_CLOUD, scan), self.download(nat.OUT_SHARP, scan),
+                        self.download(nat.OUT_LESS_SHARP, scan), self.download(nat.OUT_FLAT, scan),
+                        self.download(nat.OUT_LESS_FLAT, scan))
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lislam_batch_destroy(self.h)
+            self.h = None
+
+
+def eval_factors(ctx: Context, kind: np.ndarray, pts: np.ndarray, q: np.ndarray, t: np.ndarray):
+    """GPU evaluation of LidarEdgeFactor / LidarPlaneFactor / LidarPlaneNormFactor blocks."""
+    kind = np.ascontiguousarray(kind, np.int32)
+    pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 12)
+    n = kind.shape[0]
+    r = np.zeros((n, 3))
+    J = np.zeros((n, 3, 6))
+    rc = ctx.lib.lislam_eval_factors(ctx.h, n, nat.ptr(kind), nat.ptr(pts), nat.ptr(np.ascontiguousarray(q, np.float64)),
+                                     nat.ptr(np.ascontiguousarray(t, np.float64)), nat.ptr(r), nat.ptr(J))
+    nat.check(rc, ctx.h, "lislam_eval_factors")
+    return r, J

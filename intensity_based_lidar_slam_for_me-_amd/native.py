@@ -1,0 +1,130 @@
+"""ctypes binding of ``liblislam.so`` (the C ABI declared in ``include/lislam.h``).
+
+The HIP library is the only compute path: if it is missing this module raises, it never falls
+back to a CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblislam.so")
+
+OK = 0
+ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_STATE = -1, -2, -3, -4
+
+OUT_IMAGE_RANGE, OUT_IMAGE_INTENSITY, OUT_CLOUD_TRACK, OUT_LASER_CLOUD = 0, 1, 2, 3
+OUT_CURVATURE, OUT_LABEL, OUT_LINE_OFFSETS = 4, 5, 6
+OUT_SHARP, OUT_LESS_SHARP, OUT_FLAT, OUT_LESS_FLAT = 7, 8, 9, 10
+OUT_PARA, OUT_POSE, OUT_STATS = 11, 12, 13
+
+EXPORTED_SYMBOLS = (
+    "lislam_ctx_create", "lislam_ctx_destroy", "lislam_last_error", "lislam_synchronize",
+    "lislam_set_stream", "lislam_get_stream", "lislam_scan_registration", "lislam_odom_create",
+    "lislam_odom_destroy", "lislam_odom_step", "lislam_batch_create", "lislam_batch_destroy",
+    "lislam_batch_upload", "lislam_batch_input_device_ptr", "lislam_batch_extract",
+    "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
+    "lislam_batch_download", "lislam_eval_factors",
+)
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("n_scans", ctypes.c_int32), ("width", ctypes.c_int32), ("min_range", ctypes.c_float),
+                ("max_iterations", ctypes.c_int32), ("want_images", ctypes.c_int32)]
+
+
+class PointLayout(ctypes.Structure):
+    _fields_ = [("point_step", ctypes.c_uint32), ("off_x", ctypes.c_uint32), ("off_y", ctypes.c_uint32),
+                ("off_z", ctypes.c_uint32), ("off_intensity", ctypes.c_uint32)]
+
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_i32 = ctypes.c_int32
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+class ScanOut(ctypes.Structure):
+    _fields_ = [("laser_cloud", _fp), ("cap_laser_cloud", _i32), ("n_laser_cloud", _i32),
+                ("sharp", _fp), ("cap_sharp", _i32), ("n_sharp", _i32),
+                ("less_sharp", _fp), ("cap_less_sharp", _i32), ("n_less_sharp", _i32),
+                ("flat", _fp), ("cap_flat", _i32), ("n_flat", _i32),
+                ("less_flat", _fp), ("cap_less_flat", _i32), ("n_less_flat", _i32),
+                ("image_range", ctypes.POINTER(ctypes.c_uint8)), ("image_intensity", ctypes.POINTER(ctypes.c_uint8)),
+                ("cloud_track", _fp)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("sharp", _fp), ("n_sharp", _i32), ("less_sharp", _fp), ("n_less_sharp", _i32),
+                ("flat", _fp), ("n_flat", _i32), ("less_flat", _fp), ("n_less_flat", _i32)]
+
+
+_LIB = None
+
+
+def _preload_torch_runtime():
+    """Load torch's HIP runtime first (when torch is importable) so that liblislam binds to the
+    same libamdhip64 instance as torch in processes that use both."""
+    if os.environ.get("LISLAM_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional plumbing
+        pass
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP library; raises if it is missing (no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"liblislam.so not built ({path}); run __graft_entry__.build()")
+    _preload_torch_runtime()
+    L = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    L.lislam_ctx_create.argtypes = [ctypes.POINTER(Config), _i32, ctypes.POINTER(vp)]
+    L.lislam_ctx_destroy.argtypes = [vp]
+    L.lislam_last_error.argtypes = [vp]
+    L.lislam_last_error.restype = ctypes.c_char_p
+    L.lislam_synchronize.argtypes = [vp]
+    L.lislam_set_stream.argtypes = [vp, vp]
+    L.lislam_get_stream.argtypes = [vp, ctypes.POINTER(vp)]
+    L.lislam_scan_registration.argtypes = [vp, vp, ctypes.POINTER(PointLayout), ctypes.POINTER(ScanOut)]
+    L.lislam_odom_create.argtypes = [vp, ctypes.POINTER(vp)]
+    L.lislam_odom_destroy.argtypes = [vp]
+    L.lislam_odom_step.argtypes = [vp, ctypes.POINTER(Frame), vp, vp, vp]
+    L.lislam_batch_create.argtypes = [vp, _i32, ctypes.POINTER(vp)]
+    L.lislam_batch_destroy.argtypes = [vp]
+    L.lislam_batch_upload.argtypes = [vp, vp, _i32, ctypes.POINTER(PointLayout)]
+    L.lislam_batch_input_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
+    L.lislam_batch_extract.argtypes = [vp, _i32]
+    L.lislam_batch_odometry.argtypes = [vp, _i32, _i32]
+    L.lislam_batch_set_timing.argtypes = [vp, _i32]
+    L.lislam_batch_kernel_times.argtypes = [vp, _fp]
+    L.lislam_batch_download.argtypes = [vp, _i32, _i32, vp, _i32, _i32p]
+    L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
+    for name in EXPORTED_SYMBOLS:
+        getattr(L, name).restype = getattr(L, name).restype or ctypes.c_int
+    L.lislam_last_error.restype = ctypes.c_char_p
+    _LIB = L
+    return L
+
+
+class LislamError(RuntimeError):
+    pass
+
+
+def check(rc: int, ctx=None, what: str = ""):
+    if rc != OK:
+        msg = ""
+        if ctx:
+            raw = load().lislam_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise LislamError(f"{what} failed with status {rc}: {msg}")
+
+
+def ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)

@@ -1,0 +1,175 @@
+"""Seeded synthetic Ouster-style organized scans of a corridor.
+
+The reference ships no data (its example bag is an external download,
+``README.md:152-171``), so every benchmark and parity test runs on scans made
+here.  The layout is the organized ring-by-ring cloud that
+``ImageHandler::cloud_handler`` indexes as ``u * W + v``
+(``src/image_handler.h_ouster:113-117``): ``H x W x 4`` float32 =
+``(x, y, z, intensity)`` in the sensor frame.
+
+Design choices that keep the reference's order-dependent logic well defined:
+
+* Beam ``k`` sits at the centre of its ``scanID`` bin of
+  ``scanRegistration.cpp:290-325`` so the bin assignment cannot flip on a
+  1-ulp difference of ``atan``.
+* Azimuth columns carry a fractional offset so no point lands exactly on an
+  ``ori`` wrap boundary of ``scanRegistration.cpp:336-366``.
+* Range noise N(0, 1 cm) makes exact curvature ties rare.
+* 2 % dropouts are ``(0, 0, 0, 0)`` points, which exercise the ``range < 0.1``
+  branch of ``cloud_handler`` and ``removeClosedPointCloud``.
+* Pillar faces are retro-reflective (intensity up to 300) so the 255 clamp of
+  ``image_handler.h_ouster:121`` is exercised.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+BASE_SEED = 20250204
+
+# corridor geometry (metres, world frame)
+WALL_Y = 1.5
+FLOOR_Z = -0.6
+CEIL_Z = 2.0
+X_MIN = -20.0
+X_MAX = 200.0
+PILLAR_PITCH = 6.0
+PILLAR_SIZE = 0.4
+BEAM_PITCH = 4.0
+BEAM_DEPTH = 0.3
+BEAM_DROP = 0.35
+
+
+def beam_elevations_deg(n_scans: int) -> np.ndarray:
+    """Elevation of beam k at the centre of its scanID bin (scanRegistration.cpp:290-325)."""
+    k = np.arange(n_scans, dtype=np.float64)
+    if n_scans == 16:
+        # scanID = int((angle + 15) / 2 + 0.5)
+        return 2.0 * k - 15.0
+    if n_scans == 32:
+        # scanID = int((angle + 92/3) * 3/4)
+        return (k + 0.5) / 0.75 - 92.0 / 3.0
+    if n_scans == 64:
+        # scanID = int((angle + 22.5) * 1.41 + 0.5) - 1
+        return (k + 1.0) / 1.41 - 22.5
+    if n_scans == 128:
+        # scanID = int((angle + 22.5) * 2.83 + 0.5) - 1
+        return (k + 1.0) / 2.83 - 22.5
+    raise ValueError("only 16/32/64/128 scan lines are supported (scanRegistration.cpp:701)")
+
+
+@dataclass
+class Pose:
+    x: float
+    y: float
+    yaw: float
+
+    def as_qt(self):
+        """(q[x,y,z,w], t[3]) of sensor->world."""
+        h = 0.5 * self.yaw
+        return (np.array([0.0, 0.0, math.sin(h), math.cos(h)]), np.array([self.x, self.y, 0.0]))
+
+
+def ground_truth_pose(scan_idx: int, rate_hz: float = 10.0) -> Pose:
+    t = scan_idx / rate_hz
+    return Pose(x=1.0 * t, y=0.1 * math.sin(0.3 * t), yaw=0.05 * math.sin(0.2 * t))
+
+
+def _pillars():
+    """Wall pillars (alternating sides) and transverse ceiling beams: the x-facing faces and the
+    vertical / horizontal edges that keep motion along the corridor observable."""
+    xs = np.arange(PILLAR_PITCH, X_MAX - 1.0, PILLAR_PITCH)
+    lo, hi = [], []
+    for i, xc in enumerate(xs):
+        side = 1.0 if i % 2 == 0 else -1.0
+        lo.append((xc - PILLAR_SIZE / 2, WALL_Y - PILLAR_SIZE if side > 0 else -WALL_Y, FLOOR_Z))
+        hi.append((xc + PILLAR_SIZE / 2, WALL_Y if side > 0 else -WALL_Y + PILLAR_SIZE, CEIL_Z))
+    for xc in np.arange(BEAM_PITCH / 2, X_MAX - 1.0, BEAM_PITCH):
+        lo.append((xc - BEAM_DEPTH / 2, -WALL_Y, CEIL_Z - BEAM_DROP))
+        hi.append((xc + BEAM_DEPTH / 2, WALL_Y, CEIL_Z))
+    return np.array(lo), np.array(hi)
+
+
+_PILLAR_LO, _PILLAR_HI = _pillars()
+
+
+def _cast(origin: np.ndarray, dirs: np.ndarray):
+    """Nearest hit distance and surface class of rays from inside the corridor box."""
+    n = dirs.shape[0]
+    box_lo = np.array([X_MIN, -WALL_Y, FLOOR_Z])
+    box_hi = np.array([X_MAX, WALL_Y, CEIL_Z])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / dirs
+        t_axes = np.where(dirs > 0, (box_hi - origin) * inv, (box_lo - origin) * inv)
+        t_axes = np.where(np.abs(dirs) < 1e-12, np.inf, t_axes)
+    axis = np.argmin(t_axes, axis=1)
+    t_hit = t_axes[np.arange(n), axis]
+    surf = axis.copy()  # 0: end walls, 1: side walls, 2: floor/ceiling, 3: pillar
+    # pillars (slab test)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t0 = (_PILLAR_LO[None, :, :] - origin[None, None, :]) * inv[:, None, :]
+        t1 = (_PILLAR_HI[None, :, :] - origin[None, None, :]) * inv[:, None, :]
+    tmin = np.nanmax(np.minimum(t0, t1), axis=2)
+    tmax = np.nanmin(np.maximum(t0, t1), axis=2)
+    hit = (tmax >= tmin) & (tmin > 1e-6)
+    tp = np.where(hit, tmin, np.inf)
+    jp = np.argmin(tp, axis=1)
+    tpm = tp[np.arange(n), jp]
+    closer = tpm < t_hit
+    t_hit = np.where(closer, tpm, t_hit)
+    surf = np.where(closer, 3, surf)
+    return t_hit, surf
+
+
+def make_scan(scan_idx: int, n_scans: int = 64, width: int = 1024, seed_base: int = BASE_SEED,
+              pose: Pose | None = None) -> np.ndarray:
+    """One organized scan, ``(n_scans, width, 4)`` float32, row 0 = top beam (Ouster order)."""
+    rng = np.random.default_rng(seed_base + scan_idx)
+    pose = pose or ground_truth_pose(scan_idx)
+    el = np.deg2rad(beam_elevations_deg(n_scans))[::-1]          # row u -> beam H-1-u
+    col = np.arange(width, dtype=np.float64)
+    az = -2.0 * math.pi * (col + 0.37) / width                   # clockwise sweep like an Ouster
+    cel, sel = np.cos(el)[:, None], np.sin(el)[:, None]
+    d_sensor = np.stack([np.broadcast_to(cel * np.cos(az)[None, :], (n_scans, width)),
+                         np.broadcast_to(cel * np.sin(az)[None, :], (n_scans, width)),
+                         np.broadcast_to(sel, (n_scans, width))], axis=-1).reshape(-1, 3)
+    cy, sy = math.cos(pose.yaw), math.sin(pose.yaw)
+    rot = np.array([[cy, -sy, 0.0], [sy, cy, 0.0], [0.0, 0.0, 1.0]])
+    d_world = d_sensor @ rot.T
+    origin = np.array([pose.x, pose.y, 0.0])
+    t_hit, surf = _cast(origin, d_world)
+    rng_noise = rng.normal(0.0, 0.01, size=t_hit.shape)
+    r = t_hit + rng_noise
+    p_world = origin + d_world * t_hit[:, None]
+    # checker texture in surface coordinates (0.5 m period)
+    u = np.where(surf == 0, p_world[:, 1], p_world[:, 0])
+    v = np.where(surf == 2, p_world[:, 1], p_world[:, 2])
+    checker = (np.floor(u / 0.5) + np.floor(v / 0.5)).astype(np.int64) & 1
+    inten = np.where(surf == 3, 260.0 + 30.0 * checker, 40.0 + 180.0 * checker)
+    inten = np.clip(inten + rng.normal(0.0, 5.0, size=inten.shape), 0.0, 300.0)
+    pts = np.empty((n_scans * width, 4), dtype=np.float64)
+    pts[:, :3] = d_sensor * r[:, None]
+    pts[:, 3] = inten
+    drop = rng.random(t_hit.shape) < 0.02
+    pts[drop] = 0.0
+    return pts.astype(np.float32).reshape(n_scans, width, 4)
+
+
+def make_sequence(n: int, n_scans: int = 64, width: int = 1024, start: int = 0) -> np.ndarray:
+    """``n`` consecutive scans of the 10 Hz corridor drive, ``(n, H, W, 4)`` float32."""
+    out = np.empty((n, n_scans, width, 4), dtype=np.float32)
+    for i in range(n):
+        out[i] = make_scan(start + i, n_scans, width)
+    return out
+
+
+def relative_ground_truth(k: int):
+    """Ground-truth T_{k-1 <- k} as (q[x,y,z,w], t)."""
+    a, b = ground_truth_pose(k - 1), ground_truth_pose(k)
+    dyaw = b.yaw - a.yaw
+    ca, sa = math.cos(a.yaw), math.sin(a.yaw)
+    dx, dy = b.x - a.x, b.y - a.y
+    t = np.array([ca * dx + sa * dy, -sa * dx + ca * dy, 0.0])
+    return np.array([0.0, 0.0, math.sin(dyaw / 2), math.cos(dyaw / 2)]), t

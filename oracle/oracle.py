@@ -1,0 +1,137 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper of ``liboracle.so`` (the C++ restatement in this directory).  Imported only by
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py``; the product
+package never imports it.  See ``oracle_common.hpp`` for the parity status.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_i8p = np.ctypeslib.ndpointer(dtype=np.int8, flags="C_CONTIGUOUS")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        L.oracle_scan_registration.argtypes = [
+            _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+            _u8p, _u8p, _f32p, _f32p, _i32p, _i32p, _i32p, _f32p, _i8p,
+            _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p]
+        L.oracle_scan_registration.restype = ctypes.c_int
+        L.oracle_voxel_grid.argtypes = [_f32p, ctypes.c_int, ctypes.c_float, ctypes.c_int, _f32p, _i32p]
+        L.oracle_odometry_chain.argtypes = [
+            ctypes.c_int, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f64p, _f64p, _i32p]
+        L.oracle_nn1.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, _i32p, _f32p]
+        L.oracle_eval_factor.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, _f64p, _f64p]
+        _LIB = L
+    return _LIB
+
+
+@dataclass
+class ScanFeatures:
+    """Outputs of scanRegistration for one scan (all float32 (n, 4) = x, y, z, intensity)."""
+    img_range: np.ndarray
+    img_intensity: np.ndarray
+    cloud_track: np.ndarray
+    laser_cloud: np.ndarray
+    scan_start: np.ndarray
+    scan_end: np.ndarray
+    curvature: np.ndarray
+    label: np.ndarray
+    sharp: np.ndarray
+    less_sharp: np.ndarray
+    flat: np.ndarray
+    less_flat: np.ndarray
+
+
+def scan_registration(scan: np.ndarray, min_range: float = 0.3, canonical: bool = True) -> ScanFeatures:
+    scan = np.ascontiguousarray(scan, dtype=np.float32)
+    H, W = scan.shape[:2]
+    N = H * W
+    L = lib()
+    img_r = np.zeros(N, np.uint8)
+    img_i = np.zeros(N, np.uint8)
+    track = np.zeros((N, 4), np.float32)
+    cloud = np.zeros((N, 4), np.float32)
+    ncl = np.zeros(1, np.int32)
+    ss = np.zeros(H, np.int32)
+    se = np.zeros(H, np.int32)
+    curv = np.zeros(N, np.float32)
+    lab = np.zeros(N, np.int8)
+    sh = np.zeros((12 * H, 4), np.float32)
+    ls = np.zeros((120 * H, 4), np.float32)
+    fl = np.zeros((24 * H, 4), np.float32)
+    lf = np.zeros((N, 4), np.float32)
+    n = [np.zeros(1, np.int32) for _ in range(4)]
+    L.oracle_scan_registration(scan.reshape(-1), H, W, H, min_range, int(canonical), img_r, img_i,
+                               track.reshape(-1), cloud.reshape(-1), ncl, ss, se, curv, lab,
+                               sh.reshape(-1), n[0], ls.reshape(-1), n[1], fl.reshape(-1), n[2],
+                               lf.reshape(-1), n[3])
+    c = int(ncl[0])
+    return ScanFeatures(img_r.reshape(H, W), img_i.reshape(H, W), track.reshape(H, W, 4), cloud[:c], ss, se,
+                        curv[:c], lab[:c], sh[:n[0][0]], ls[:n[1][0]], fl[:n[2][0]], lf[:n[3][0]])
+
+
+def voxel_grid(points: np.ndarray, leaf: float, canonical: bool = True) -> np.ndarray:
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    out = np.zeros_like(pts)
+    n = np.zeros(1, np.int32)
+    lib().oracle_voxel_grid(pts.reshape(-1), pts.shape[0], leaf, int(canonical), out.reshape(-1), n)
+    return out[: n[0]]
+
+
+def _pack(arrs):
+    off = np.zeros(len(arrs) + 1, np.int32)
+    off[1:] = np.cumsum([a.shape[0] for a in arrs])
+    cat = np.concatenate([a.reshape(-1, 4) for a in arrs]) if off[-1] else np.zeros((1, 4), np.float32)
+    return np.ascontiguousarray(cat, np.float32).reshape(-1), off
+
+
+def odometry_chain(feats: list[ScanFeatures]):
+    """Fresh laserOdometry node over ``feats``; returns (world poses (n,7), para (n,7), stats (n,6))."""
+    n = len(feats)
+    s, so = _pack([f.sharp for f in feats])
+    ls, lso = _pack([f.less_sharp for f in feats])
+    fl, flo = _pack([f.flat for f in feats])
+    lf, lfo = _pack([f.less_flat for f in feats])
+    pose = np.zeros((n, 7), np.float64)
+    rel = np.zeros((n, 7), np.float64)
+    st = np.zeros((n, 6), np.int32)
+    lib().oracle_odometry_chain(n, s, so, ls, lso, fl, flo, lf, lfo, pose.reshape(-1), rel.reshape(-1),
+                                st.reshape(-1))
+    return pose, rel, st
+
+
+def nn1(target: np.ndarray, queries: np.ndarray):
+    t = np.ascontiguousarray(target, np.float32)
+    q = np.ascontiguousarray(queries, np.float32)
+    idx = np.zeros(q.shape[0], np.int32)
+    d2 = np.zeros(q.shape[0], np.float32)
+    lib().oracle_nn1(t.reshape(-1), t.shape[0], q.reshape(-1), q.shape[0], idx, d2)
+    return idx, d2
+
+
+def eval_factor(kind: int, pts: np.ndarray, q: np.ndarray, t: np.ndarray):
+    R = 3 if kind == 0 else 1
+    r = np.zeros(R)
+    J = np.zeros((R, 7))
+    lib().oracle_eval_factor(kind, np.ascontiguousarray(pts, np.float64).reshape(-1),
+                             np.ascontiguousarray(q, np.float64), np.ascontiguousarray(t, np.float64), r,
+                             J.reshape(-1))
+    return r, J
