@@ -110,10 +110,13 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans);
 /* a12..a18 for scans [0, n_scans): ceil((n_scans-1)/chain_len) independent chains, chain c is a
  * fresh laserOdometry node over scans [c*chain_len, min((c+1)*chain_len, n_scans-1)]. */
 int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len);
-/* Enable per-kernel HIP-event timing of the next calls; times are read with kernel_times. */
+/* Enable per-kernel HIP-event timing: every following extract / odometry call records events on
+ * the stream (no host synchronization). */
 int lislam_batch_set_timing(lislam_batch* b, int32_t enable);
-/* ms of the last extract / odometry calls: [front, lines, compact, odometry]. */
-int lislam_batch_kernel_times(lislam_batch* b, float* ms4);
+/* Synchronize, then return the average ms per call of [k_scan_front, k_scan_lines,
+ * k_scan_compact, k_odom_chain] over the calls recorded since the previous read; calls2 (may
+ * be null) receives the number of extract and odometry calls averaged.  Clears the record. */
+int lislam_batch_kernel_times(lislam_batch* b, float* ms4, int32_t* calls2);
 
 #define LISLAM_OUT_IMAGE_RANGE 0     /* uint8  [H*W] */
 #define LISLAM_OUT_IMAGE_INTENSITY 1 /* uint8  [H*W] */

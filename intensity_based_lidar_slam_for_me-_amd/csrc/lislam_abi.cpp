@@ -32,9 +32,17 @@ struct lislam_batch {
   OdomArgs oa{};
   double* d_init = nullptr;
   bool timing = false;
-  hipEvent_t ev[6] = {};
-  float ms[4] = {0, 0, 0, 0};
+  // per-call event sets recorded on the stream while timing is on; read back (and released)
+  // by lislam_batch_kernel_times, so the timed region never blocks on the host.
+  std::vector<std::vector<hipEvent_t>> ext_ev, odo_ev;
+  std::vector<hipEvent_t> pool;
   int extracted = 0;
+  hipEvent_t get_event() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+  }
 };
 
 struct lislam_odom {
@@ -202,8 +210,6 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.pose, (size_t)S * 7);
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
-  for (int i = 0; i < 6 && rc == LISLAM_OK; i++)
-    if (hipEventCreate(&b->ev[i]) != hipSuccess) rc = fail(c, LISLAM_ERR_DEVICE, "hipEventCreate");
   if (rc != LISLAM_OK) {
     lislam_batch_destroy(b);
     return LISLAM_ERR_DEVICE;
@@ -217,8 +223,9 @@ int lislam_batch_destroy(lislam_batch* b) {
   hipSetDevice(b->ctx->device);
   hipStreamSynchronize(b->ctx->stream);
   for (void* p : b->allocs) hipFree(p);
-  for (auto& e : b->ev)
-    if (e) hipEventDestroy(e);
+  for (auto& v : b->ext_ev) for (hipEvent_t e : v) hipEventDestroy(e);
+  for (auto& v : b->odo_ev) for (hipEvent_t e : v) hipEventDestroy(e);
+  for (hipEvent_t e : b->pool) hipEventDestroy(e);
   delete b;
   return LISLAM_OK;
 }
@@ -260,14 +267,14 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   hipSetDevice(c->device);
   FeatureArgs f = b->fa;
   f.S = n_scans;
-  launch_features(f, c->stream, b->timing ? b->ev : nullptr);
-  HIPCHK(c, hipGetLastError());
+  hipEvent_t* ev = nullptr;
   if (b->timing) {
-    HIPCHK(c, hipEventSynchronize(b->ev[3]));
-    hipEventElapsedTime(&b->ms[0], b->ev[0], b->ev[1]);
-    hipEventElapsedTime(&b->ms[1], b->ev[1], b->ev[2]);
-    hipEventElapsedTime(&b->ms[2], b->ev[2], b->ev[3]);
+    b->ext_ev.emplace_back();
+    for (int i = 0; i < 4; i++) b->ext_ev.back().push_back(b->get_event());
+    ev = b->ext_ev.back().data();
   }
+  launch_features(f, c->stream, ev);
+  HIPCHK(c, hipGetLastError());
   b->extracted = n_scans;
   return LISLAM_OK;
 }
@@ -283,12 +290,14 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
     o.init_state = b->d_init;
   }
-  launch_odometry(o, c->stream, b->timing ? b->ev + 4 : nullptr);
-  HIPCHK(c, hipGetLastError());
+  hipEvent_t* ev = nullptr;
   if (b->timing) {
-    HIPCHK(c, hipEventSynchronize(b->ev[5]));
-    hipEventElapsedTime(&b->ms[3], b->ev[4], b->ev[5]);
+    b->odo_ev.emplace_back();
+    for (int i = 0; i < 2; i++) b->odo_ev.back().push_back(b->get_event());
+    ev = b->odo_ev.back().data();
   }
+  launch_odometry(o, c->stream, ev);
+  HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
 
@@ -299,9 +308,32 @@ int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len) {
   return run_odometry(b, n_scans, chain_len, nullptr);
 }
 
-int lislam_batch_kernel_times(lislam_batch* b, float* ms4) {
+int lislam_batch_kernel_times(lislam_batch* b, float* ms4, int32_t* calls2) {
   if (!b || !ms4) return LISLAM_ERR_ARG;
-  std::memcpy(ms4, b->ms, sizeof(b->ms));
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  double acc[4] = {0, 0, 0, 0};
+  for (auto& v : b->ext_ev) {
+    for (int i = 0; i < 3; i++) {
+      float ms = 0;
+      HIPCHK(c, hipEventElapsedTime(&ms, v[i], v[i + 1]));
+      acc[i] += ms;
+    }
+    for (hipEvent_t e : v) b->pool.push_back(e);
+  }
+  for (auto& v : b->odo_ev) {
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, v[0], v[1]));
+    acc[3] += ms;
+    for (hipEvent_t e : v) b->pool.push_back(e);
+  }
+  const int ne = (int)b->ext_ev.size(), no = (int)b->odo_ev.size();
+  for (int i = 0; i < 3; i++) ms4[i] = ne ? (float)(acc[i] / ne) : 0.f;
+  ms4[3] = no ? (float)(acc[3] / no) : 0.f;
+  if (calls2) { calls2[0] = ne; calls2[1] = no; }
+  b->ext_ev.clear();
+  b->odo_ev.clear();
   return LISLAM_OK;
 }
 

@@ -103,7 +103,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_extract.argtypes = [vp, _i32]
     L.lislam_batch_odometry.argtypes = [vp, _i32, _i32]
     L.lislam_batch_set_timing.argtypes = [vp, _i32]
-    L.lislam_batch_kernel_times.argtypes = [vp, _fp]
+    L.lislam_batch_kernel_times.argtypes = [vp, _fp, _i32p]
     L.lislam_batch_download.argtypes = [vp, _i32, _i32, vp, _i32, _i32p]
     L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:

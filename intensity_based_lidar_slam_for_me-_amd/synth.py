@@ -78,49 +78,64 @@ def ground_truth_pose(scan_idx: int, rate_hz: float = 10.0) -> Pose:
 
 
 def _pillars():
-    """Wall pillars (alternating sides) and transverse ceiling beams: the x-facing faces and the
-    vertical / horizontal edges that keep motion along the corridor observable."""
-    xs = np.arange(PILLAR_PITCH, X_MAX - 1.0, PILLAR_PITCH)
-    lo, hi = [], []
-    for i, xc in enumerate(xs):
-        side = 1.0 if i % 2 == 0 else -1.0
-        lo.append((xc - PILLAR_SIZE / 2, WALL_Y - PILLAR_SIZE if side > 0 else -WALL_Y, FLOOR_Z))
-        hi.append((xc + PILLAR_SIZE / 2, WALL_Y if side > 0 else -WALL_Y + PILLAR_SIZE, CEIL_Z))
-    for xc in np.arange(BEAM_PITCH / 2, X_MAX - 1.0, BEAM_PITCH):
-        lo.append((xc - BEAM_DEPTH / 2, -WALL_Y, CEIL_Z - BEAM_DROP))
-        hi.append((xc + BEAM_DEPTH / 2, WALL_Y, CEIL_Z))
-    return np.array(lo), np.array(hi)
+    """Wall pillars: full-height boxes (x-lo, x-hi, y-lo, y-hi) on alternating sides."""
+    out = []
+    for i, xc in enumerate(np.arange(PILLAR_PITCH, X_MAX - 1.0, PILLAR_PITCH)):
+        ylo, yhi = (WALL_Y - PILLAR_SIZE, WALL_Y) if i % 2 == 0 else (-WALL_Y, -WALL_Y + PILLAR_SIZE)
+        out.append((xc - PILLAR_SIZE / 2, xc + PILLAR_SIZE / 2, ylo, yhi))
+    return np.array(out)
 
 
-_PILLAR_LO, _PILLAR_HI = _pillars()
+def _beams():
+    """Transverse ceiling beams: full-width boxes (x-lo, x-hi, z-lo, z-hi)."""
+    xs = np.arange(BEAM_PITCH / 2, X_MAX - 1.0, BEAM_PITCH)
+    return np.stack([xs - BEAM_DEPTH / 2, xs + BEAM_DEPTH / 2, np.full_like(xs, CEIL_Z - BEAM_DROP),
+                     np.full_like(xs, CEIL_Z)], axis=1)
 
 
-def _cast(origin: np.ndarray, dirs: np.ndarray):
-    """Nearest hit distance and surface class of rays from inside the corridor box."""
-    n = dirs.shape[0]
-    box_lo = np.array([X_MIN, -WALL_Y, FLOOR_Z])
-    box_hi = np.array([X_MAX, WALL_Y, CEIL_Z])
+_PILLARS = _pillars()
+_BEAMS = _beams()
+
+
+def _slab2(o0, o1, d0, d1, lo0, hi0, lo1, hi1):
+    """Entry distance of 2-D rays (o + t d) into axis-aligned rectangles; inf if missed."""
     with np.errstate(divide="ignore", invalid="ignore"):
-        inv = 1.0 / dirs
-        t_axes = np.where(dirs > 0, (box_hi - origin) * inv, (box_lo - origin) * inv)
-        t_axes = np.where(np.abs(dirs) < 1e-12, np.inf, t_axes)
-    axis = np.argmin(t_axes, axis=1)
-    t_hit = t_axes[np.arange(n), axis]
-    surf = axis.copy()  # 0: end walls, 1: side walls, 2: floor/ceiling, 3: pillar
-    # pillars (slab test)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        t0 = (_PILLAR_LO[None, :, :] - origin[None, None, :]) * inv[:, None, :]
-        t1 = (_PILLAR_HI[None, :, :] - origin[None, None, :]) * inv[:, None, :]
-    tmin = np.nanmax(np.minimum(t0, t1), axis=2)
-    tmax = np.nanmin(np.maximum(t0, t1), axis=2)
+        i0, i1 = 1.0 / d0, 1.0 / d1
+        a0, b0 = (lo0 - o0) * i0, (hi0 - o0) * i0
+        a1, b1 = (lo1 - o1) * i1, (hi1 - o1) * i1
+    tmin = np.maximum(np.minimum(a0, b0), np.minimum(a1, b1))
+    tmax = np.minimum(np.maximum(a0, b0), np.maximum(a1, b1))
     hit = (tmax >= tmin) & (tmin > 1e-6)
-    tp = np.where(hit, tmin, np.inf)
-    jp = np.argmin(tp, axis=1)
-    tpm = tp[np.arange(n), jp]
-    closer = tpm < t_hit
-    t_hit = np.where(closer, tpm, t_hit)
-    surf = np.where(closer, 3, surf)
-    return t_hit, surf
+    return np.where(hit, tmin, np.inf)
+
+
+def _cast(origin, az_w, el):
+    """Nearest hit distance and surface class of every (elevation row, azimuth column) ray from
+    inside the corridor.  Surfaces: 0 end walls, 1 side walls, 2 floor/ceiling, 3 pillar/beam."""
+    ce, se = np.cos(el)[:, None], np.sin(el)[:, None]              # (H, 1)
+    ca, sa = np.cos(az_w)[None, :], np.sin(az_w)[None, :]          # (1, W)
+    dx, dy, dz = ce * ca, ce * sa, np.broadcast_to(se, (el.size, az_w.size))
+    box_lo = (X_MIN, -WALL_Y, FLOOR_Z)
+    box_hi = (X_MAX, WALL_Y, CEIL_Z)
+    ts = []
+    for ax, d in enumerate((dx, dy, dz)):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = np.where(d > 0, (box_hi[ax] - origin[ax]) / d, (box_lo[ax] - origin[ax]) / d)
+        ts.append(np.where(np.abs(d) < 1e-12, np.inf, t))
+    ts = np.stack(ts)                                               # (3, H, W)
+    surf = np.argmin(ts, axis=0)
+    t_hit = np.min(ts, axis=0)
+    # pillars span floor to ceiling: a horizontal 2-D test per azimuth column, scaled by 1/cos(el)
+    sp = _slab2(origin[0], origin[1], ca.ravel()[:, None], sa.ravel()[:, None], _PILLARS[None, :, 0],
+                _PILLARS[None, :, 1], _PILLARS[None, :, 2], _PILLARS[None, :, 3]).min(axis=1)
+    tp = sp[None, :] / ce
+    # beams span wall to wall: a 2-D (x, z) test per ray
+    tb = _slab2(origin[0], origin[2], dx[..., None], dz[..., None], _BEAMS[:, 0], _BEAMS[:, 1], _BEAMS[:, 2],
+                _BEAMS[:, 3]).min(axis=2)
+    tob = np.minimum(tp, tb)
+    closer = tob < t_hit
+    return np.where(closer, tob, t_hit).ravel(), np.where(closer, 3, surf).ravel(), \
+        np.stack([dx, dy, dz], axis=-1).reshape(-1, 3)
 
 
 def make_scan(scan_idx: int, n_scans: int = 64, width: int = 1024, seed_base: int = BASE_SEED,
@@ -135,11 +150,8 @@ def make_scan(scan_idx: int, n_scans: int = 64, width: int = 1024, seed_base: in
     d_sensor = np.stack([np.broadcast_to(cel * np.cos(az)[None, :], (n_scans, width)),
                          np.broadcast_to(cel * np.sin(az)[None, :], (n_scans, width)),
                          np.broadcast_to(sel, (n_scans, width))], axis=-1).reshape(-1, 3)
-    cy, sy = math.cos(pose.yaw), math.sin(pose.yaw)
-    rot = np.array([[cy, -sy, 0.0], [sy, cy, 0.0], [0.0, 0.0, 1.0]])
-    d_world = d_sensor @ rot.T
     origin = np.array([pose.x, pose.y, 0.0])
-    t_hit, surf = _cast(origin, d_world)
+    t_hit, surf, d_world = _cast(origin, az + pose.yaw, el)
     rng_noise = rng.normal(0.0, 0.01, size=t_hit.shape)
     r = t_hit + rng_noise
     p_world = origin + d_world * t_hit[:, None]

@@ -1,0 +1,192 @@
+"""CPU tests of the oracle restatement: pinned against the committed golden fixtures, an
+independent numpy / pure-Python restatement, scipy's exact kNN and finite differences.
+
+The reference ships no tests or golden vectors: these pins are the build's own.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import restate_np as R
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def small():
+    return dict(np.load(os.path.join(GOLD, "scan16x256_chain3.npz")))
+
+
+def test_golden_small_scan_features(oracle, small):
+    for k in range(3):
+        f = oracle.scan_registration(small["scans"][k])
+        for name in ("img_range", "img_intensity", "cloud_track", "laser_cloud", "scan_start", "scan_end",
+                     "curvature", "label", "sharp", "less_sharp", "flat", "less_flat"):
+            assert np.array_equal(getattr(f, name), small[f"s{k}_{name}"]), name
+
+
+def test_golden_small_chain(oracle, small):
+    feats = [oracle.scan_registration(s) for s in small["scans"]]
+    pose, rel, st = oracle.odometry_chain(feats)
+    np.testing.assert_allclose(rel, small["odom_para"], atol=1e-12)
+    np.testing.assert_allclose(pose, small["odom_pose"], atol=1e-12)
+    assert np.array_equal(st, small["odom_stats"])
+
+
+def test_generator_matches_golden_inputs(synth, small):
+    assert np.array_equal(synth.make_sequence(3, 16, 256), small["scans"])
+
+
+@pytest.mark.parametrize("seed", [0, 7])
+def test_front_end_vs_numpy_restatement(oracle, synth, seed):
+    """a1..a5 of the oracle equal a vectorized numpy restatement, bit for bit."""
+    scan = synth.make_scan(seed, 32, 512)
+    f = oracle.scan_registration(scan)
+    ir, ii, tr = R.cloud_handler(scan)
+    assert np.array_equal(ir, f.img_range.ravel())
+    assert np.array_equal(ii, f.img_intensity.ravel())
+    assert np.array_equal(tr, f.cloud_track.reshape(-1, 4))
+    cl, off = R.laser_cloud(scan, 32)
+    assert np.array_equal(cl, f.laser_cloud)
+    assert np.array_equal(off[:-1] + 5, f.scan_start)
+    assert np.array_equal(off[1:] - 6, f.scan_end)
+    assert np.array_equal(R.curvature(cl), f.curvature)
+
+
+def test_selection_vs_python_loops(oracle, synth):
+    scan = synth.make_scan(3, 16, 512)
+    f = oracle.scan_registration(scan)
+    cl, off = R.laser_cloud(scan, 16)
+    sh, ls, fl, lf, lab = R.select_features(cl, off, f.curvature, 16)
+    assert np.array_equal(sh, f.sharp) and np.array_equal(ls, f.less_sharp)
+    assert np.array_equal(fl, f.flat) and np.array_equal(lf, f.less_flat)
+    assert np.array_equal(lab, f.label)
+
+
+def test_feature_limits(oracle, synth):
+    """Per line at most 12 sharp / 120 less-sharp / 24 flat (scanRegistration.cpp:459,466,530)."""
+    f = oracle.scan_registration(synth.make_scan(1))
+    ids = lambda a: np.floor(a[:, 3]).astype(int)  # noqa: E731
+    for arr, cap in ((f.sharp, 12), (f.less_sharp, 120), (f.flat, 24)):
+        assert arr.shape[0] <= cap * 64
+        assert np.bincount(np.clip(ids(arr), 0, 63), minlength=64).max() <= cap
+    assert np.all(np.diff(ids(f.laser_cloud)) >= -1)  # scan-grouped (relTime < 0 quirk: id - 1)
+    # sharp curvature > 0.1, flat curvature < 0.1 (labels 2/1 and -1)
+    assert np.all(f.curvature[f.label > 0] > 0.1)
+    assert np.all(f.curvature[f.label == -1] < 0.1)
+
+
+def test_empty_and_out_of_fov_scans(oracle):
+    f = oracle.scan_registration(np.zeros((16, 256, 4), np.float32))
+    assert f.laser_cloud.shape[0] == 0 and f.sharp.shape[0] == 0 and f.less_flat.shape[0] == 0
+    up = np.zeros((16, 256, 4), np.float32)
+    up[..., 2] = 10.0  # straight up: elevation 90 deg, outside every scanID bin -> count--
+    f = oracle.scan_registration(up)
+    assert f.laser_cloud.shape[0] == 0
+
+
+def test_voxel_grid_vs_python(oracle):
+    rng = np.random.default_rng(5)
+    pts = rng.uniform(-2, 2, size=(500, 4)).astype(np.float32)
+    got = oracle.voxel_grid(pts, 0.2, canonical=True)
+    ref = R.voxel_grid(pts, 0.2)
+    assert np.array_equal(got, ref)
+    # non-canonical (PCL std::sort) differs at most in float rounding of centroids
+    nc = oracle.voxel_grid(pts, 0.2, canonical=False)
+    assert nc.shape == ref.shape and np.allclose(nc, ref, atol=1e-6)
+
+
+def test_nn1_vs_scipy(oracle):
+    g = np.load(os.path.join(GOLD, "nn1_scipy.npz"))
+    idx, d2 = oracle.nn1(g["target"], g["queries"])
+    assert np.array_equal(idx, g["idx"])
+    np.testing.assert_allclose(np.sqrt(d2), g["dist"], rtol=1e-5, atol=1e-6)
+
+
+def test_nn1_random_vs_bruteforce(oracle):
+    rng = np.random.default_rng(11)
+    tgt = rng.normal(size=(3000, 4)).astype(np.float32)
+    q = rng.normal(size=(400, 4)).astype(np.float32)
+    idx, d2 = oracle.nn1(tgt, q)
+    d = tgt[None, :, :3] - q[:, None, :3]
+    dd = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    assert np.array_equal(idx, np.argmin(dd, axis=1))
+    assert np.array_equal(d2, dd.min(axis=1))
+
+
+def _quat_plus(q, d):
+    nd = np.linalg.norm(d)
+    if nd == 0:
+        return q.copy()
+    dq = np.concatenate([np.sin(nd) / nd * d, [np.cos(nd)]])
+    x1, y1, z1, w1 = dq
+    x2, y2, z2, w2 = q
+    return np.array([w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2, w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                     w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2, w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2])
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_functor_jacobian_vs_finite_differences(oracle, kind):
+    rng = np.random.default_rng(kind)
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    t = rng.normal(size=3)
+    pts = rng.normal(size=12)
+    if kind == 2:
+        n = rng.normal(size=3)
+        pts[3:6] = n / np.linalg.norm(n)
+    r, J = oracle.eval_factor(kind, pts, q, t)
+    P = np.array([[q[3], q[2], -q[1]], [-q[2], q[3], q[0]], [q[1], -q[0], q[3]], [-q[0], -q[1], -q[2]]])
+    Jl = np.concatenate([J[:, :4] @ P, J[:, 4:]], axis=1)
+    h = 1e-6
+    for c in range(6):
+        d = np.zeros(3)
+        qq, tt = q, t.copy()
+        if c < 3:
+            d[c] = h
+            qp, qm = _quat_plus(q, d), _quat_plus(q, -d)
+            rp, _ = oracle.eval_factor(kind, pts, qp, t)
+            rm, _ = oracle.eval_factor(kind, pts, qm, t)
+        else:
+            tp, tm = t.copy(), t.copy()
+            tp[c - 3] += h
+            tm[c - 3] -= h
+            rp, _ = oracle.eval_factor(kind, pts, qq, tp)
+            rm, _ = oracle.eval_factor(kind, pts, qq, tm)
+        np.testing.assert_allclose((rp - rm) / (2 * h), Jl[:, c], rtol=1e-5, atol=1e-6)
+
+
+def test_odometry_recovers_known_motion(oracle, synth):
+    """Scan-to-itself under a known rigid motion: the LM recovers it (LidarEdge/PlaneFactor + LM)."""
+    import copy
+
+    f0 = oracle.scan_registration(synth.make_scan(0))
+    yaw, t = 0.01, np.array([0.1, 0.02, -0.01])
+    c, s = np.cos(yaw), np.sin(yaw)
+    Rm = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+    f1 = copy.copy(f0)
+    for k in ("sharp", "less_sharp", "flat", "less_flat"):
+        a = getattr(f0, k).copy()
+        a[:, :3] = ((a[:, :3].astype(np.float64) - t) @ Rm).astype(np.float32)
+        setattr(f1, k, a)
+    _, rel, st = oracle.odometry_chain([f0, f1])
+    assert abs(rel[1][2] - np.sin(yaw / 2)) < 2e-4
+    np.testing.assert_allclose(rel[1][4:], t, atol=3e-3)
+
+
+def test_full_size_digests(oracle, synth):
+    """64x1024 / 128x2048 oracle outputs are stable (sha256 of every feature array)."""
+    import hashlib
+
+    rec = json.load(open(os.path.join(GOLD, "full_size_digests.json")))
+    e = rec["64x1024"]
+    scans = synth.make_sequence(3, 64, 1024)
+    for k, s in enumerate(scans):
+        assert hashlib.sha256(np.ascontiguousarray(s).tobytes()).hexdigest() == e["input_sha256"][k]
+        f = oracle.scan_registration(s)
+        for name, v in e["scans"][k].items():
+            a = getattr(f, name)
+            assert a.shape[0] == v["n"], name
+            assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == v["sha256"], name
