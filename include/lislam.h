@@ -113,10 +113,14 @@ int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len);
 /* Enable per-kernel HIP-event timing: every following extract / odometry call records events on
  * the stream (no host synchronization). */
 int lislam_batch_set_timing(lislam_batch* b, int32_t enable);
-/* Synchronize, then return the average ms per call of [k_scan_front, k_scan_lines,
- * k_scan_compact, k_odom_chain] over the calls recorded since the previous read; calls2 (may
- * be null) receives the number of extract and odometry calls averaged.  Clears the record. */
-int lislam_batch_kernel_times(lislam_batch* b, float* ms4, int32_t* calls2);
+/* Kernels timed by lislam_batch_kernel_times, in this order. */
+#define LISLAM_NUM_KERNELS 6 /* k_scan_front, k_scan_lines, k_scan_compact, k_target_index,
+                                k_odom_assoc, k_odom_lm (the latter includes k_odom_init) */
+/* Synchronize, then return, over the calls recorded since the previous read, the average ms
+ * per call spent in each kernel (ms_per_call[6]) and the launches per call of each kernel
+ * (launches_per_call[6], may be null); calls[2] (may be null) = extract / odometry calls
+ * averaged.  Clears the record. */
+int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls);
 
 #define LISLAM_OUT_IMAGE_RANGE 0     /* uint8  [H*W] */
 #define LISLAM_OUT_IMAGE_INTENSITY 1 /* uint8  [H*W] */

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,6 +44,7 @@ struct lislam_batch {
     hipEventCreate(&e);
     return e;
   }
+  static hipEvent_t event_cb(void* self) { return static_cast<lislam_batch*>(self)->get_event(); }
 };
 
 struct lislam_odom {
@@ -197,11 +199,31 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &f.flat, (size_t)S * b->cap_flat);
   rc |= dalloc(b, &f.less_flat, SN);
   rc |= dalloc(b, &f.n_feat, (size_t)S * 4);
+  rc |= dalloc(b, &f.feat_loff, (size_t)S * 2 * (H + 1));
   f.cap_sharp = b->cap_sharp; f.cap_less_sharp = b->cap_less_sharp; f.cap_flat = b->cap_flat;
   OdomArgs& o = b->oa;
-  o.S = S; o.N = N;
+  o.S = S; o.N = N; o.H = H;
   o.sharp = f.sharp; o.less_sharp = f.less_sharp; o.flat = f.flat; o.less_flat = f.less_flat;
   o.n_feat = f.n_feat;
+  o.feat_loff = f.feat_loff;
+  o.idx_ls.nchunk = (b->cap_less_sharp + kChunk - 1) / kChunk;
+  o.idx_ls.nsuper = (o.idx_ls.nchunk + kChunk - 1) / kChunk;
+  o.idx_lf.nchunk = (N + kChunk - 1) / kChunk;
+  o.idx_lf.nsuper = (o.idx_lf.nchunk + kChunk - 1) / kChunk;
+  o.idx_ls.cap = b->cap_less_sharp;
+  o.idx_lf.cap = N;
+  for (TargetIndex* ti : {&o.idx_ls, &o.idx_lf}) {
+    rc |= dalloc(b, &ti->chunk, (size_t)S * ti->nchunk * 2);
+    rc |= dalloc(b, &ti->super, (size_t)S * ti->nsuper * 2);
+    rc |= dalloc(b, &ti->nn_chunk, (size_t)S * ti->nchunk * 2);
+    rc |= dalloc(b, &ti->nn_super, (size_t)S * ti->nsuper * 2);
+    rc |= dalloc(b, &ti->sorted, (size_t)S * ti->cap);
+    rc |= dalloc(b, &ti->keys, (size_t)S * 2 * ti->cap);
+  }
+  rc |= dalloc(b, &o.qperm_sharp, (size_t)S * b->cap_sharp);
+  rc |= dalloc(b, &o.qperm_flat, (size_t)S * b->cap_flat);
+  rc |= dalloc(b, &o.state, (size_t)S * 16);
+  rc |= dalloc(b, &o.counters, (size_t)S * 2);
   o.cap_sharp = b->cap_sharp; o.cap_less_sharp = b->cap_less_sharp; o.cap_flat = b->cap_flat;
   o.max_iterations = c->cfg.max_iterations;
   rc |= dalloc(b, &o.blk, (size_t)S * (b->cap_sharp + b->cap_flat) * 9);
@@ -270,10 +292,12 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   hipEvent_t* ev = nullptr;
   if (b->timing) {
     b->ext_ev.emplace_back();
-    for (int i = 0; i < 4; i++) b->ext_ev.back().push_back(b->get_event());
+    for (int i = 0; i < 5; i++) b->ext_ev.back().push_back(b->get_event());
     ev = b->ext_ev.back().data();
   }
   launch_features(f, c->stream, ev);
+  launch_target_index(b->oa, n_scans, c->stream);  // spatial index of the clouds odometry searches
+  if (ev) HIPCHK(c, hipEventRecord(ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   b->extracted = n_scans;
   return LISLAM_OK;
@@ -286,17 +310,17 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   o.chain_len = chain_len;
   o.n_chains = n_scans > 1 ? (n_scans - 1 + chain_len - 1) / chain_len : 0;
   o.init_state = nullptr;
+  o.dbg = getenv("LISLAM_ASSOC_DEBUG") ? atoi(getenv("LISLAM_ASSOC_DEBUG")) : 0;
   if (init_host) {
     HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
     o.init_state = b->d_init;
   }
-  hipEvent_t* ev = nullptr;
+  std::vector<hipEvent_t>* ev = nullptr;
   if (b->timing) {
     b->odo_ev.emplace_back();
-    for (int i = 0; i < 2; i++) b->odo_ev.back().push_back(b->get_event());
-    ev = b->odo_ev.back().data();
+    ev = &b->odo_ev.back();
   }
-  launch_odometry(o, c->stream, ev);
+  launch_odometry(o, c->stream, ev, &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -308,30 +332,39 @@ int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len) {
   return run_odometry(b, n_scans, chain_len, nullptr);
 }
 
-int lislam_batch_kernel_times(lislam_batch* b, float* ms4, int32_t* calls2) {
-  if (!b || !ms4) return LISLAM_ERR_ARG;
+int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls) {
+  if (!b || !ms_per_call) return LISLAM_ERR_ARG;
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  double acc[4] = {0, 0, 0, 0};
+  double acc[LISLAM_NUM_KERNELS] = {0};
+  int launches[LISLAM_NUM_KERNELS] = {0};
+  auto el = [&](hipEvent_t a0, hipEvent_t a1) -> double {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, a0, a1) != hipSuccess) return 0.0;
+    return ms;
+  };
   for (auto& v : b->ext_ev) {
-    for (int i = 0; i < 3; i++) {
-      float ms = 0;
-      HIPCHK(c, hipEventElapsedTime(&ms, v[i], v[i + 1]));
-      acc[i] += ms;
-    }
+    for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += 1; }
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   for (auto& v : b->odo_ev) {
-    float ms = 0;
-    HIPCHK(c, hipEventElapsedTime(&ms, v[0], v[1]));
-    acc[3] += ms;
+    // [start, after init, then after every assoc / lm launch]
+    if (v.size() >= 2) { acc[5] += el(v[0], v[1]); launches[5] += 1; }
+    for (size_t i = 1; i + 1 < v.size(); i++) {
+      const int k = (i % 2 == 1) ? 4 : 5;  // odd gaps: k_odom_assoc, even gaps: k_odom_lm
+      acc[k] += el(v[i], v[i + 1]);
+      launches[k] += 1;
+    }
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   const int ne = (int)b->ext_ev.size(), no = (int)b->odo_ev.size();
-  for (int i = 0; i < 3; i++) ms4[i] = ne ? (float)(acc[i] / ne) : 0.f;
-  ms4[3] = no ? (float)(acc[3] / no) : 0.f;
-  if (calls2) { calls2[0] = ne; calls2[1] = no; }
+  for (int k = 0; k < LISLAM_NUM_KERNELS; k++) {
+    const int ncall = k < 4 ? ne : no;
+    ms_per_call[k] = ncall ? (float)(acc[k] / ncall) : 0.f;
+    if (launches_per_call) launches_per_call[k] = ncall ? launches[k] / ncall : 0;
+  }
+  if (calls) { calls[0] = ne; calls[1] = no; }
   b->ext_ev.clear();
   b->odo_ev.clear();
   return LISLAM_OK;
@@ -457,6 +490,39 @@ static int put_frame(lislam_batch* b, int slot, const lislam_frame* fr) {
   rc |= cp(f.less_flat + (size_t)slot * b->N, fr->less_flat, fr->n_less_flat);
   const int cnt[4] = {fr->n_sharp, fr->n_less_sharp, fr->n_flat, fr->n_less_flat};
   HIPCHK(c, hipMemcpyAsync(f.n_feat + slot * 4, cnt, sizeof(cnt), hipMemcpyHostToDevice, c->stream));
+  // per-line offsets of less_sharp / less_flat (first index whose int(intensity) >= line); they
+  // only seed the 1-NN bound, so any non-decreasing array within [0, n] keeps results exact
+  const int H = b->H;
+  std::vector<int> loff(2 * (H + 1));
+  const float* src[2] = {fr->less_sharp, fr->less_flat};
+  const int nsrc[2] = {fr->n_less_sharp, fr->n_less_flat};
+  for (int w = 0; w < 2; w++) {
+    int j = 0;
+    for (int l = 0; l <= H; l++) {
+      while (j < nsrc[w] && (l == H || (int)src[w][4 * j + 3] < l)) j++;
+      loff[w * (H + 1) + l] = j;
+    }
+  }
+  HIPCHK(c, hipMemcpyAsync(f.feat_loff + (size_t)slot * 2 * (H + 1), loff.data(), loff.size() * sizeof(int),
+                           hipMemcpyHostToDevice, c->stream));
+  OdomArgs o = b->oa;
+  o.less_sharp = f.less_sharp + (size_t)slot * b->cap_less_sharp;
+  o.less_flat = f.less_flat + (size_t)slot * b->N;
+  o.sharp = f.sharp + (size_t)slot * b->cap_sharp;
+  o.flat = f.flat + (size_t)slot * b->cap_flat;
+  o.qperm_sharp += (size_t)slot * b->cap_sharp;
+  o.qperm_flat += (size_t)slot * b->cap_flat;
+  o.n_feat = f.n_feat + slot * 4;
+  for (TargetIndex* ti : {&o.idx_ls, &o.idx_lf}) {
+    ti->chunk += (size_t)slot * ti->nchunk * 2;
+    ti->super += (size_t)slot * ti->nsuper * 2;
+    ti->nn_chunk += (size_t)slot * ti->nchunk * 2;
+    ti->nn_super += (size_t)slot * ti->nsuper * 2;
+    ti->sorted += (size_t)slot * ti->cap;
+    ti->keys += (size_t)slot * 2 * ti->cap;
+  }
+  launch_target_index(o, 1, c->stream);
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return rc ? LISLAM_ERR_DEVICE : LISLAM_OK;
 }

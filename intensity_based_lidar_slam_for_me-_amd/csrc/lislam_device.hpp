@@ -21,12 +21,28 @@ __device__ __forceinline__ float atan2_f(float y, float x) {
 }
 __device__ __forceinline__ float atan_f(float v) { return (float)atan((double)v); }
 
-__device__ __forceinline__ P4 ld4(const P4* p) {
-  float4 v = *reinterpret_cast<const float4*>(p);
+// Explicit address spaces: a generic pointer would make hipcc emit flat_* accesses, which count on
+// both vmcnt and lgkmcnt and serialize every wait.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f4v gf4v;
+typedef __attribute__((address_space(1))) f4v gf4v_mut;
+typedef const __attribute__((address_space(3))) f4v sf4v;
+
+__device__ __forceinline__ float4 ldg(const void* p) {  // global memory only
+  const f4v v = *(gf4v*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 lds4(const void* p) {  // LDS only
+  const f4v v = *(sf4v*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ P4 ld4(const P4* p) {  // global memory only
+  const f4v v = *(gf4v*)p;
   return P4{v.x, v.y, v.z, v.w};
 }
-__device__ __forceinline__ void st4(P4* p, const P4& v) {
-  *reinterpret_cast<float4*>(p) = make_float4(v.x, v.y, v.z, v.i);
+__device__ __forceinline__ void st4(P4* p, const P4& v) {  // global memory only
+  f4v w = {v.x, v.y, v.z, v.i};
+  *(gf4v_mut*)p = w;
 }
 
 // scanRegistration.cpp:290-331: scan line of a point from its elevation; -1 = dropped.

@@ -197,7 +197,7 @@ __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // workgroup =
 
 // Bitonic sort (ascending) of P (power of two) 64-bit keys by one wave.
 template <typename KeyPtr>
-__device__ void bitonic_sort(KeyPtr keys, int P) {
+__device__ __forceinline__ void bitonic_sort(KeyPtr keys, int P) {
   const int lane = lane_id();
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -251,7 +251,7 @@ __device__ __forceinline__ void suppress(const P4* cloud, int off, int ind, Byte
 }
 
 template <bool kLds>
-__device__ void line_body(const FeatureArgs& a, int s, int line, uint8_t* lds_picked, int8_t* lds_label,
+__device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line, uint8_t* lds_picked, int8_t* lds_label,
                           uint64_t* lds_keys, int* lds_list) {
   const int lane = lane_id();
   const int N = a.N, H = a.H;
@@ -504,6 +504,10 @@ __global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
     for (int l = 0; l < H; l++) { pre[f][l] = acc; acc += lc[l * 4 + f]; }
     pre[f][H] = acc;
     a.n_feat[s * 4 + f] = acc;
+    if (f == 1 || f == 3) {  // line offsets of the clouds the odometry searches
+      int* lo = a.feat_loff + ((size_t)s * 2 + (f == 1 ? 0 : 1)) * (H + 1);
+      for (int l = 0; l <= H; l++) lo[l] = pre[f][l];
+    }
   }
   __syncthreads();
   const int* lo = a.line_off + (size_t)s * (H + 1);
@@ -522,6 +526,7 @@ __global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
 }
 
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev) {
+  // ev (nullable): 4 events bracketing k_scan_front, k_scan_lines, k_scan_compact
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(k_scan_front, dim3(a.S), dim3(kFrontThreads), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);

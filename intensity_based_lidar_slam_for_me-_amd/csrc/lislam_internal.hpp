@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "lislam_device.hpp"
 
 namespace lislam {
@@ -43,26 +45,53 @@ struct FeatureArgs {
   P4* flat;        // [S][cap_flat]
   P4* less_flat;   // [S][N]
   int* n_feat;     // [S][4] = sharp, less_sharp, flat, less_flat
+  int* feat_loff;  // [S][2][H+1] per-line offsets of less_sharp / less_flat
   int cap_sharp, cap_less_sharp, cap_flat;
 };
 
-// Scan-to-scan odometry over chains of consecutive scans (a12..a18).
+// Spatial index of a feature cloud: chunks of kChunk consecutive points (in the cloud's own,
+// scan-line-major order) and super-chunks of kChunk chunks, each with an AABB whose w lanes hold
+// the min / max scan line label int(intensity) of its points.
+constexpr int kChunk = 16;
+constexpr int kSuper = kChunk * kChunk;
+
+struct TargetIndex {
+  // scan-line (original) order: used by the scan-line searches
+  float4* chunk;  // [S][nchunk][2] (lo, hi)
+  float4* super;  // [S][nsuper][2]
+  // Morton (z-order) order: used by the 1-NN; w of a sorted point = original index (int bits)
+  float4* sorted;    // [S][cap] points
+  float4* nn_chunk;  // [S][nchunk][2]
+  float4* nn_super;  // [S][nsuper][2]
+  uint64_t* keys;    // [S][2 * cap] sort scratch for clouds beyond the LDS sort
+  int cap, nchunk, nsuper;
+};
+
+// Scan-to-scan odometry over chains of consecutive scans (a12..a18).  Chain c is a fresh
+// laserOdometry node over scans [c*L, min(c*L + L, S-1)]; round r processes pair k = c*L + r + 1
+// of every chain in two phases per outer pass (association, then the Ceres-semantics solve).
 struct OdomArgs {
-  int S, N;
+  int S, N, H;
   const P4* sharp; const P4* less_sharp; const P4* flat; const P4* less_flat;
   const int* n_feat;
+  const int* feat_loff;  // [S][2][H+1] line offsets of less_sharp / less_flat
+  TargetIndex idx_ls, idx_lf;
+  int* qperm_sharp;  // [S][cap_sharp] sharp queries in Morton order (association thread -> query)
+  int* qperm_flat;   // [S][cap_flat]
   int cap_sharp, cap_less_sharp, cap_flat;
-  int chain_len;   // pairs per chain; chain c starts (fresh node) at scan c * chain_len
+  int chain_len;
   int n_chains;
   int max_iterations;  // ceres max_num_iterations (4, laserOdometry.cpp:707)
   const double* init_state;  // [n_chains][14] = para(7) + pose(7) at the chain start, or null
-  // block scratch per chain: [n_chains][cap_sharp + cap_flat] records
-  double* blk;     // 9 doubles per record
+  double* state;             // [n_chains][16] = para(7), q_w(4), t_w(3)
+  int* counters;             // [n_chains][2] correspondences of the current association
+  double* blk;     // [n_chains][cap_sharp + cap_flat][9] residual block records
   int* blk_kind;   // -1 invalid, 0 edge, 1 plane
   // outputs per scan
   double* para;    // [S][7] q_last_curr (x,y,z,w), t_last_curr after this scan
   double* pose;    // [S][7] q_w_curr, t_w_curr in the chain's frame
   int* stats;      // [S][8] corners/planes for outer 0/1, LM iterations 0/1, terminations 0/1
+  int dbg;         // ablation switch for profiling (0 in production): 1 skip 1-NN, 2 skip line search
 };
 
 // Batched evaluation of the cost functors (lislam_eval_factors).
@@ -76,7 +105,10 @@ struct FactorArgs {
 };
 
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/);
-void launch_odometry(const OdomArgs& a, hipStream_t st, hipEvent_t* ev /*2 or null*/);
+void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st);
+// Issues the whole round/phase schedule; ev (nullable) receives the boundaries of every launch.
+void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>* ev,
+                     hipEvent_t (*get_event)(void*), void* ev_owner);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
 }  // namespace lislam

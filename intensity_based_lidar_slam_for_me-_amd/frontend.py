@@ -153,13 +153,16 @@ class Batch:
         nat.check(self.ctx.lib.lislam_batch_set_timing(self.h, int(on)), self.ctx.h, "lislam_batch_set_timing")
 
     def kernel_times(self):
-        """Average ms per call of [front, lines, compact, odometry] since the last read, and the
-        number of (extract, odometry) calls averaged."""
-        ms = np.zeros(4, np.float32)
+        """Per kernel (native.KERNELS): average ms per call and launches per call since the last
+        read, plus the number of (extract, odometry) calls averaged."""
+        ms = np.zeros(len(nat.KERNELS), np.float32)
+        launches = np.zeros(len(nat.KERNELS), np.int32)
         calls = np.zeros(2, np.int32)
-        rc = self.ctx.lib.lislam_batch_kernel_times(self.h, _fp(ms), calls.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        rc = self.ctx.lib.lislam_batch_kernel_times(self.h, _fp(ms), launches.ctypes.data_as(i32p),
+                                                    calls.ctypes.data_as(i32p))
         nat.check(rc, self.ctx.h, "lislam_batch_kernel_times")
-        return ms, calls
+        return ms, launches, calls
 
     _DT = {nat.OUT_IMAGE_RANGE: (np.uint8, 1), nat.OUT_IMAGE_INTENSITY: (np.uint8, 1), nat.OUT_CLOUD_TRACK: (np.float32, 4),
            nat.OUT_LASER_CLOUD: (np.float32, 4), nat.OUT_CURVATURE: (np.float32, 1), nat.OUT_LABEL: (np.int8, 1),

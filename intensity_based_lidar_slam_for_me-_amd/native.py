@@ -21,6 +21,8 @@ OUT_CURVATURE, OUT_LABEL, OUT_LINE_OFFSETS = 4, 5, 6
 OUT_SHARP, OUT_LESS_SHARP, OUT_FLAT, OUT_LESS_FLAT = 7, 8, 9, 10
 OUT_PARA, OUT_POSE, OUT_STATS = 11, 12, 13
 
+KERNELS = ("k_scan_front", "k_scan_lines", "k_scan_compact", "k_target_index", "k_odom_assoc", "k_odom_lm")
+
 EXPORTED_SYMBOLS = (
     "lislam_ctx_create", "lislam_ctx_destroy", "lislam_last_error", "lislam_synchronize",
     "lislam_set_stream", "lislam_get_stream", "lislam_scan_registration", "lislam_odom_create",
@@ -103,7 +105,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_extract.argtypes = [vp, _i32]
     L.lislam_batch_odometry.argtypes = [vp, _i32, _i32]
     L.lislam_batch_set_timing.argtypes = [vp, _i32]
-    L.lislam_batch_kernel_times.argtypes = [vp, _fp, _i32p]
+    L.lislam_batch_kernel_times.argtypes = [vp, _fp, _i32p, _i32p]
     L.lislam_batch_download.argtypes = [vp, _i32, _i32, vp, _i32, _i32p]
     L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:

@@ -11,6 +11,10 @@ b = pkg.Batch(ctx, S)
 b.upload(scans)
 b.extract(S); b.odometry(S, L); ctx.synchronize()
 b.set_timing(True)
+t=time.perf_counter()
 for _ in range(3):
     b.extract(S); b.odometry(S, L)
-print('kernel ms', b.kernel_times(), flush=True)
+ctx.synchronize(); el=(time.perf_counter()-t)/3
+ms, la, calls = b.kernel_times()
+print(f'S={S} L={L} step {el*1e3:.2f} ms -> {S/el:.0f} scans/s', flush=True)
+for k, m, l in zip(pkg.native.KERNELS, ms, la): print(f'  {k:16s} {m:9.3f} ms/step {l:5d} launches', flush=True)
