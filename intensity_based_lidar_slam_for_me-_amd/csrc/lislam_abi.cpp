@@ -194,6 +194,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &f.scr_picked, SN);
   rc |= dalloc(b, &f.scr_keys, 2 * SN);
   rc |= dalloc(b, &f.scr_list, SN);
+  rc |= dalloc(b, &f.scr_link, SN);
   rc |= dalloc(b, &f.sharp, (size_t)S * b->cap_sharp);
   rc |= dalloc(b, &f.less_sharp, (size_t)S * b->cap_less_sharp);
   rc |= dalloc(b, &f.flat, (size_t)S * b->cap_flat);
@@ -345,7 +346,7 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
     return ms;
   };
   for (auto& v : b->ext_ev) {
-    for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += 1; }
+    for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += i == 3 ? 2 : 1; }  // k_target_index: 2 launches
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   for (auto& v : b->odo_ev) {

@@ -190,69 +190,141 @@ __global__ __launch_bounds__(kFrontThreads) void k_scan_front(FeatureArgs a) {
 }
 
 // ------------------------------------------------------------------------------- line kernel
+// Optional per-phase cycle accounting (built only with -DLISLAM_PHASE_PROF, scripts/phase_prof.py).
+#ifdef LISLAM_PHASE_PROF
+__device__ unsigned long long g_phase_cycles[16];
+#define PHASE_BEGIN uint64_t t_ph = __builtin_readcyclecounter()
+#define PHASE(i)                                                     \
+  do {                                                               \
+    const uint64_t now_ = __builtin_readcyclecounter();              \
+    if (lane_id() == 0) atomicAdd(&g_phase_cycles[i], now_ - t_ph);  \
+    t_ph = now_;                                                     \
+  } while (0)
+#else
+#define PHASE_BEGIN
+#define PHASE(i)
+#endif
 // LDS capacities of the fast path; longer lines run the same code on global scratch.
 constexpr int kLineCap = 2048;
 
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // workgroup == one wave
+// Line kernel workgroups are one wave.  With the line in LDS, a wave's LDS accesses complete in
+// issue order, so ordering them only needs the LDS counter drained and a compiler barrier (no
+// s_barrier, and no wait on the wave's outstanding global stores); the long-line path keeps its
+// state in global scratch and uses a full workgroup barrier.
+template <bool kLds>
+__device__ __forceinline__ void wave_sync() {
+  if (kLds) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
 
-// Bitonic sort (ascending) of P (power of two) 64-bit keys by one wave.
-template <typename KeyPtr>
+// Bitonic sort (ascending) of P (power of two, >= 64) 64-bit keys by one wave.  Each stage loads
+// all of a lane's pairs before it compares and stores any, so a stage costs one LDS round trip
+// (kMaxT = P/128 bound of the fast path); the long-line path keeps the simple loop.
+template <int kMaxT, typename KeyPtr>
 __device__ __forceinline__ void bitonic_sort(KeyPtr keys, int P) {
   const int lane = lane_id();
+  const int npairs = P >> 1;
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = lane; i < P; i += 64) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = keys[i], b = keys[ixj];
+      if (kMaxT > 0) {
+        uint64_t A[kMaxT > 0 ? kMaxT : 1], B[kMaxT > 0 ? kMaxT : 1];
+        int I[kMaxT > 0 ? kMaxT : 1];
+#pragma unroll
+        for (int t = 0; t < kMaxT; t++) {
+          const int q = lane + 64 * t;
+          I[t] = -1;
+          if (q < npairs) {
+            const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+            I[t] = i;
+            A[t] = keys[i];
+            B[t] = keys[i | j];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < kMaxT; t++) {
+          const int i = I[t];
+          if (i >= 0) {
+            const bool up = (i & k) == 0;
+            if ((A[t] > B[t]) == up) { keys[i] = B[t]; keys[i | j] = A[t]; }
+          }
+        }
+      } else {
+        for (int q = lane; q < npairs; q += 64) {
+          const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+          const uint64_t x = keys[i], y = keys[i | j];
           const bool up = (i & k) == 0;
-          if ((a > b) == up) { keys[i] = b; keys[ixj] = a; }
+          if ((x > y) == up) { keys[i] = y; keys[i | j] = x; }
         }
       }
-      wave_sync();
+      wave_sync<(kMaxT > 0)>();
     }
   }
 }
 
 __device__ __forceinline__ uint64_t first_lane(uint64_t m) { return (uint64_t)__builtin_ctzll(m); }
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
 struct LineCounts {
   int sharp, less_sharp, flat, less_flat;
 };
 
-// ±5 neighbour suppression of a picked point (scanRegistration.cpp:481-504), wave-parallel:
-// lanes 1..5 test the forward chain, lanes 6..10 the backward one; a link breaks the chain at
-// the first squared step > 0.05.
-template <typename BytePtr>
-__device__ __forceinline__ void suppress(const P4* cloud, int off, int ind, BytePtr picked) {
+// ±5 neighbour suppression of a picked point (scanRegistration.cpp:481-504) from precomputed
+// links: link[k] = |p[k+1] - p[k]|^2 <= 0.05 (float sums, compared in double); the reference's
+// backward differences p[k] - p[k+1] square to the same bits.  Forward marks ind+1.. while
+// link[ind], link[ind+1], ... hold (at most 5); backward marks ind-1.. while link[ind-1], ... hold.
+template <bool kLds, typename BytePtr>
+__device__ __forceinline__ void suppress(const BytePtr link, int ind, BytePtr picked) {
   const int lane = lane_id();
   bool brk = false;
-  int tgt = -1;
-  if (lane >= 1 && lane <= 5) {
-    const int l = lane;
-    const P4 a = ld4(cloud + off + ind + l), b = ld4(cloud + off + ind + l - 1);
-    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
-    brk = (double)(dx * dx + dy * dy + dz * dz) > 0.05;
-    tgt = ind + l;
-  } else if (lane >= 6 && lane <= 10) {
-    const int l = -(lane - 5);
-    const P4 a = ld4(cloud + off + ind + l), b = ld4(cloud + off + ind + l + 1);
-    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
-    brk = (double)(dx * dx + dy * dy + dz * dz) > 0.05;
-    tgt = ind + l;
-  }
+  if (lane < 5) brk = link[ind + lane] == 0;                  // forward link ind+lane
+  else if (lane < 10) brk = link[ind - 1 - (lane - 5)] == 0;  // backward link ind-1-(lane-5)
   const uint64_t bm = __ballot(brk);
-  const uint64_t fwd = bm & 0x3Eull, bwd = bm & 0x7C0ull;
-  const int ffirst = fwd ? (int)first_lane(fwd) : 6;    // first breaking forward lane
-  const int bfirst = bwd ? (int)first_lane(bwd) : 11;   // first breaking backward lane
-  const bool mark = (lane >= 1 && lane < ffirst) || (lane >= 6 && lane < bfirst);
-  if (mark) picked[tgt] = 1;
-  wave_sync();
+  const uint64_t fwd = bm & 0x1Full, bwd = bm & 0x3E0ull;
+  const int nf = fwd ? (int)first_lane(fwd) : 5;      // marked forward neighbours
+  const int nb = bwd ? (int)first_lane(bwd) - 5 : 5;  // marked backward neighbours
+  if (lane < nf) picked[ind + 1 + lane] = 1;
+  else if (lane >= 5 && lane - 5 < nb) picked[ind - 1 - (lane - 5)] = 1;
+  wave_sync<kLds>();
 }
 
+struct LineLists {
+  int sharp[kCapSharpPerLine];
+  int less_sharp[kCapLessSharpPerLine];
+  int flat[kCapFlatPerLine];
+};
+
+// One scan line: curvature, the six-segment sharp/flat selection and the line's VoxelGrid.
+//
+// The reference sorts each segment by curvature (std::sort, scanRegistration.cpp:440-448; the
+// canonical tie order is the point index) and walks it from the largest (sharp, :450-506) and
+// smallest (flat, :511-568) end, skipping points already picked.  Suppression only ever adds
+// picked points and the walk never revisits a position, so the k-th pick of a walk is the
+// extreme (curvature, index) key among the still-unpicked points that pass the curvature test:
+// each pick is one wave-wide max/min reduction instead of a sorted segment.
 template <bool kLds>
 __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line, uint8_t* lds_picked, int8_t* lds_label,
-                          uint64_t* lds_keys, int* lds_list) {
+                                          uint64_t* lds_keys, int* lds_list, uint8_t* lds_link, LineLists& ll,
+                                          P4* stage) {
   const int lane = lane_id();
   const int N = a.N, H = a.H;
   const int* lo = a.line_off + (size_t)s * (H + 1);
@@ -265,7 +337,10 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
   uint8_t* picked = kLds ? lds_picked : a.scr_picked + (size_t)s * N + off;
   int8_t* label = kLds ? lds_label : glabel + off;
   uint64_t* keys = kLds ? lds_keys : a.scr_keys + 2 * ((size_t)s * N + off);  // pow2 padding <= 2 len
+  float* curvL = kLds ? (float*)lds_keys : curv + off;  // the walks run before the voxel keys exist
   int* list = kLds ? lds_list : a.scr_list + (size_t)s * N + off;
+  uint8_t* link = kLds ? lds_link : a.scr_link + (size_t)s * N + off;
+  PHASE_BEGIN;
 
   // curvature (scanRegistration.cpp:397-412), left-to-right float sums
   for (int k = lane; k < len; k += 64) {
@@ -280,10 +355,19 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
       c = dX * dX + dY * dY + dZ * dZ;
     }
     curv[i] = c;
+    if (kLds) curvL[k] = c;
     picked[k] = 0;
     label[k] = 0;
+    uint8_t lk = 0;
+    if (k + 1 < len) {
+      const P4 p0 = ld4(cloud + i), p1 = ld4(cloud + i + 1);
+      const float dx = p1.x - p0.x, dy = p1.y - p0.y, dz = p1.z - p0.z;
+      lk = !((double)(dx * dx + dy * dy + dz * dz) > 0.05);
+    }
+    link[k] = lk;
   }
-  wave_sync();
+  wave_sync<kLds>();
+  PHASE(0);
 
   LineCounts cnt{0, 0, 0, 0};
   P4* o_sharp = a.stg_sharp + ((size_t)s * H + line) * kCapSharpPerLine;
@@ -296,99 +380,60 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
     for (int j = 0; j < 6; j++) {
       const int sp = sI + (eI - sI) * j / 6;
       const int ep = sI + (eI - sI) * (j + 1) / 6 - 1;
-      const int seg = ep - sp + 1;
-      int P = 64;
-      while (P < seg) P <<= 1;
-      for (int k = lane; k < P; k += 64) {
-        uint64_t key = ~0ull;
-        if (k < seg) {
-          const float c = curv[off + sp + k];
-          key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)(sp + k);
-        }
-        keys[k] = key;
-      }
-      wave_sync();
-      bitonic_sort(keys, P);
-      // ---- sharp walk: from the largest curvature down (:450-506)
-      int largest = 0;
-      int pos = seg - 1;
-      bool done = false;
-      while (pos >= 0 && !done) {
-        const int p = pos - lane;
-        bool q = false, stop_c = false;
-        if (p >= 0) {
-          const uint64_t key = keys[p];
-          const int ind = (int)(uint32_t)key;
-          const float c = __uint_as_float((uint32_t)(key >> 32));
-          q = picked[ind] == 0 && (double)c > 0.1;
-          stop_c = !((double)c > 0.1);
-        }
-        const uint64_t qm = __ballot(q);
-        if (qm == 0) {
-          // sorted ascending: once a curvature fails "> 0.1" no later entry can pass
-          if (__ballot(stop_c)) break;
-          pos -= 64;
-          continue;
-        }
-        const int fl = (int)first_lane(qm);
-        const int ind = (int)(uint32_t)keys[pos - fl];
-        largest++;
-        if (largest <= 20) {
-          const P4 pt = ld4(cloud + off + ind);
-          if (lane == 0) {
-            if (largest <= 2) {
-              label[ind] = 2;
-              st4(o_sharp + cnt.sharp, pt);
-            } else {
-              label[ind] = 1;
-            }
-            st4(o_lsharp + cnt.less_sharp, pt);
-            picked[ind] = 1;
+      // ---- sharp picks: largest curvature first (:450-506); at most 20 per segment
+      for (int largest = 1; largest <= 20; largest++) {
+        uint64_t best = 0;
+        for (int k = sp + lane; k <= ep; k += 64) {
+          const float c = curvL[k];
+          if (picked[k] == 0 && (double)c > 0.1) {
+            const uint64_t key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)k;
+            best = key > best ? key : best;
           }
-          if (largest <= 2) cnt.sharp++;
-          cnt.less_sharp++;
-          wave_sync();
-          suppress(cloud, off, ind, picked);
-          pos = pos - fl - 1;
-        } else {
-          done = true;
         }
+        best = wave_max_u64(best);
+        if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
+        const int ind = (int)(uint32_t)best;
+        if (lane == 0) {
+          if (largest <= 2) {
+            label[ind] = 2;
+            ll.sharp[cnt.sharp] = ind;
+          } else {
+            label[ind] = 1;
+          }
+          ll.less_sharp[cnt.less_sharp] = ind;
+          picked[ind] = 1;
+        }
+        if (largest <= 2) cnt.sharp++;
+        cnt.less_sharp++;
+        wave_sync<kLds>();
+        suppress<kLds>(link, ind, picked);
       }
-      // ---- flat walk: from the smallest curvature up (:511-568)
-      int smallest = 0;
-      pos = 0;
-      while (pos < seg) {
-        const int p = pos + lane;
-        bool q = false, stop_c = false;
-        if (p < seg) {
-          const uint64_t key = keys[p];
-          const int ind = (int)(uint32_t)key;
-          const float c = __uint_as_float((uint32_t)(key >> 32));
-          q = picked[ind] == 0 && (double)c < 0.1;
-          stop_c = !((double)c < 0.1);
+      PHASE(2);
+      // ---- flat picks: smallest curvature first (:511-568); the 4th pick ends the walk unmarked
+      for (int smallest = 1; smallest <= 4; smallest++) {
+        uint64_t best = ~0ull;
+        for (int k = sp + lane; k <= ep; k += 64) {
+          const float c = curvL[k];
+          if (picked[k] == 0 && (double)c < 0.1) {
+            const uint64_t key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)k;
+            best = key < best ? key : best;
+          }
         }
-        const uint64_t qm = __ballot(q);
-        if (qm == 0) {
-          if (__ballot(stop_c)) break;
-          pos += 64;
-          continue;
-        }
-        const int fl = (int)first_lane(qm);
-        const int ind = (int)(uint32_t)keys[pos + fl];
-        const P4 pt = ld4(cloud + off + ind);
+        best = wave_min_u64(best);
+        if (best == ~0ull) break;
+        const int ind = (int)(uint32_t)best;
         if (lane == 0) {
           label[ind] = -1;
-          st4(o_flat + cnt.flat, pt);
+          ll.flat[cnt.flat] = ind;
         }
         cnt.flat++;
-        smallest++;
-        if (smallest >= 4) { wave_sync(); break; }
+        if (smallest == 4) break;
         if (lane == 0) picked[ind] = 1;
-        wave_sync();
-        suppress(cloud, off, ind, picked);
-        pos = pos + fl + 1;
+        wave_sync<kLds>();
+        suppress<kLds>(link, ind, picked);
       }
-      wave_sync();
+      wave_sync<kLds>();
+      PHASE(3);
       // ---- less-flat collection in index order (:570-577)
       for (int b = sp; b <= ep; b += 64) {
         const int k = b + lane;
@@ -397,11 +442,17 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
         if (f) list[nlist + __popcll(m & lanemask_lt())] = k;
         nlist += __popcll(m);
       }
-      wave_sync();
+      wave_sync<kLds>();
+      PHASE(4);
     }
   }
-  // write labels of the line for the parity tests
+  // write labels of the line (parity tests) and the picked points, in pick order
   for (int k = lane; k < len; k += 64) glabel[off + k] = label[k];
+  for (int k = lane; k < cnt.sharp; k += 64) st4(o_sharp + k, ld4(cloud + off + ll.sharp[k]));
+  for (int k = lane; k < cnt.less_sharp; k += 64) st4(o_lsharp + k, ld4(cloud + off + ll.less_sharp[k]));
+  for (int k = lane; k < cnt.flat; k += 64) st4(o_flat + k, ld4(cloud + off + ll.flat[k]));
+  wave_sync<kLds>();  // curvL aliases the key buffer
+  PHASE(5);
 
   // ---- VoxelGrid(0.2) of the line's less-flat points (PCL VoxelGrid::applyFilter semantics)
   if (nlist > 0) {
@@ -446,30 +497,85 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
         }
         keys[k] = key;
       }
-      wave_sync();
-      bitonic_sort(keys, P);
+      wave_sync<kLds>();
+      PHASE(6);
+      bitonic_sort<kLds ? kLineCap / 128 : 0>(keys, P);
+      PHASE(7);
+      // centroids in sorted order (sums in input order within a voxel): 64 sorted points at a
+      // time are staged in LDS; the voxel still open at the end of a window carries over.
       int nout = 0;
+      P4 carry{0.f, 0.f, 0.f, 0.f};
+      int carry_n = 0;
       for (int b = 0; b < nlist; b += 64) {
         const int k = b + lane;
-        bool start = false;
-        if (k < nlist) start = (k == 0) || ((keys[k] >> 32) != (keys[k - 1] >> 32));
-        const uint64_t m = __ballot(start);
-        if (start) {
-          const uint32_t v = (uint32_t)(keys[k] >> 32);
-          P4 c = ld4(cloud + off + list[(uint32_t)keys[k]]);
-          int e = k + 1;
-          while (e < nlist && (uint32_t)(keys[e] >> 32) == v) {
-            const P4 p = ld4(cloud + off + list[(uint32_t)keys[e]]);
-            c.x += p.x; c.y += p.y; c.z += p.z; c.i += p.i;
-            e++;
-          }
-          const float n = (float)(e - k);
-          c.x /= n; c.y /= n; c.z /= n; c.i /= n;
-          st4(o_lflat + nout + __popcll(m & lanemask_lt()), c);
+        const int wl = min(64, nlist - b);  // window length
+        const bool valid = k < nlist;
+        uint32_t v = 0xffffffffu, vprev = 0xffffffffu;
+        if (valid) {
+          const uint64_t key = keys[k];
+          v = (uint32_t)(key >> 32);
+          stage[lane] = ld4(cloud + off + list[(uint32_t)key]);
+          if (k > 0) vprev = (uint32_t)(keys[k - 1] >> 32);
         }
-        nout += __popcll(m);
+        const bool start = valid && (k == 0 || v != vprev);
+        const uint64_t m = __ballot(start);
+        wave_sync<kLds>();
+        const bool last = b + 64 >= nlist;
+        const bool cont = carry_n > 0 && !(m & 1ull);  // window opens inside the carried voxel
+        int extra = 0;
+        if (carry_n > 0 && (m & 1ull)) {  // the carried voxel closed exactly at the window edge
+          if (lane == 0) {
+            const float n = (float)carry_n;
+            P4 c = carry;
+            c.x /= n; c.y /= n; c.z /= n; c.i /= n;
+            st4(o_lflat + nout, c);
+          }
+          extra = 1;
+        }
+        const bool head = start || (lane == 0 && cont);
+        const uint64_t after = lane == 63 ? 0ull : (m >> (lane + 1)) << (lane + 1);
+        const int end = after ? (int)first_lane(after) : wl;
+        const bool closed = head && (end < wl || last);
+        P4 c{0.f, 0.f, 0.f, 0.f};
+        int n = 0;
+        if (head) {
+          int e = lane;
+          if (start) {
+            c = stage[lane];
+            e = lane + 1;
+            n = 1;
+          } else {
+            c = carry;
+            n = carry_n;
+          }
+          for (; e < end; e++) {
+            const P4 p = stage[e];
+            c.x += p.x; c.y += p.y; c.z += p.z; c.i += p.i;
+            n++;
+          }
+        }
+        const uint64_t cm = __ballot(closed);
+        if (closed) {
+          const float fn = (float)n;
+          P4 o = c;
+          o.x /= fn; o.y /= fn; o.z /= fn; o.i /= fn;
+          st4(o_lflat + nout + extra + __popcll(cm & lanemask_lt()), o);
+        }
+        nout += extra + __popcll(cm);
+        // the open voxel (a head that reached the window end) becomes the carry
+        const uint64_t om = __ballot(head && !closed);
+        if (om) {
+          const int src = (int)first_lane(om);
+          carry.x = __shfl(c.x, src); carry.y = __shfl(c.y, src);
+          carry.z = __shfl(c.z, src); carry.i = __shfl(c.i, src);
+          carry_n = __shfl(n, src);
+        } else {
+          carry_n = 0;
+        }
+        wave_sync<kLds>();
       }
       cnt.less_flat = nout;
+      PHASE(8);
     }
   }
   if (lane == 0) {
@@ -483,14 +589,25 @@ __global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
   __shared__ int8_t label[kLineCap];
   __shared__ uint64_t keys[kLineCap];
   __shared__ int list[kLineCap];
+  __shared__ uint8_t link[kLineCap];
+  __shared__ LineLists ll;
+  __shared__ P4 stage[64];
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
   if (len <= kLineCap)
-    line_body<true>(a, s, line, picked, label, keys, list);
+    line_body<true>(a, s, line, picked, label, keys, list, link, ll, stage);
   else  // a line longer than the LDS fast path (non ring-ordered input): global scratch
-    line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr);
+    line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, ll, stage);
 }
+
+#ifdef LISLAM_PHASE_PROF
+extern "C" int lislam_debug_phase_cycles(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(g_phase_cycles)) != hipSuccess) return -2;
+  static const unsigned long long zero[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // ------------------------------------------------------------------------------- compaction
 __global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {

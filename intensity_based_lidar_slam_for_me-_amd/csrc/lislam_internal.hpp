@@ -39,6 +39,7 @@ struct FeatureArgs {
   uint8_t* scr_picked;  // [S][N]
   uint64_t* scr_keys;   // [S][2N]
   int* scr_list;        // [S][N]
+  uint8_t* scr_link;    // [S][N]
   // a6/a7 outputs, concatenated in line order
   P4* sharp;       // [S][cap_sharp]
   P4* less_sharp;  // [S][cap_less_sharp]

@@ -49,30 +49,35 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every 
   return v;
 }
 
+__device__ __forceinline__ void stg4(float4* p, float4 v) {
+  f4v w = {v.x, v.y, v.z, v.w};
+  *(gf4v_mut*)p = w;
+}
+
 __device__ __forceinline__ void chunk_boxes(const float4* pts, int n, bool label_from_w, float4* chunk, float4* super) {
   const int nch = (n + kChunk - 1) / kChunk;
   for (int c = threadIdx.x; c < nch; c += kIdxThreads) {
     float4 lo = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 1e9f), hi = make_float4(-3.4e38f, -3.4e38f, -3.4e38f, -1e9f);
     for (int j = c * kChunk; j < min(n, c * kChunk + kChunk); j++) {
-      const float4 p = pts[j];
+      const float4 p = ldg(pts + j);
       const float l = label_from_w ? (float)int(p.w) : 0.f;
       lo.x = fminf(lo.x, p.x); lo.y = fminf(lo.y, p.y); lo.z = fminf(lo.z, p.z); lo.w = fminf(lo.w, l);
       hi.x = fmaxf(hi.x, p.x); hi.y = fmaxf(hi.y, p.y); hi.z = fmaxf(hi.z, p.z); hi.w = fmaxf(hi.w, l);
     }
-    chunk[2 * c] = lo;
-    chunk[2 * c + 1] = hi;
+    stg4(chunk + 2 * c, lo);
+    stg4(chunk + 2 * c + 1, hi);
   }
   __syncthreads();
   const int nsu = (nch + kChunk - 1) / kChunk;
   for (int c = threadIdx.x; c < nsu; c += kIdxThreads) {
     float4 lo = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 1e9f), hi = make_float4(-3.4e38f, -3.4e38f, -3.4e38f, -1e9f);
     for (int k = c * kChunk; k < min(nch, c * kChunk + kChunk); k++) {
-      const float4 l = chunk[2 * k], h = chunk[2 * k + 1];
+      const float4 l = ldg(chunk + 2 * k), h = ldg(chunk + 2 * k + 1);
       lo.x = fminf(lo.x, l.x); lo.y = fminf(lo.y, l.y); lo.z = fminf(lo.z, l.z); lo.w = fminf(lo.w, l.w);
       hi.x = fmaxf(hi.x, h.x); hi.y = fmaxf(hi.y, h.y); hi.z = fmaxf(hi.z, h.z); hi.w = fmaxf(hi.w, h.w);
     }
-    super[2 * c] = lo;
-    super[2 * c + 1] = hi;
+    stg4(super + 2 * c, lo);
+    stg4(super + 2 * c + 1, hi);
   }
   __syncthreads();
 }
@@ -93,10 +98,14 @@ __device__ __forceinline__ void block_bitonic(KeyPtr keys, int P) {
   }
 }
 
-__global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a) {
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// which_map: blockIdx.x -> (scan, cloud) for the launch (0 less-sharp, 1 less-flat, 2 sharp, 3 flat)
+__global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2, int lds_keys) {
   extern __shared__ __attribute__((aligned(16))) uint64_t skeys[];
   __shared__ float red[6][kIdxThreads / 64];
-  const int s = blockIdx.x >> 2, which = blockIdx.x & 3;  // 0 less-sharp, 1 less-flat, 2 sharp, 3 flat
+  const int s = blockIdx.x / per_scan, wi = blockIdx.x % per_scan;
+  const int which = wi == 0 ? w0 : wi == 1 ? w1 : w2;
   const bool query = which >= 2;
   const TargetIndex& ix = (which & 1) ? a.idx_lf : a.idx_ls;
   const float4* pts = reinterpret_cast<const float4*>(
@@ -108,7 +117,7 @@ __global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a) {
   // cloud AABB
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   for (int j = threadIdx.x; j < n; j += kIdxThreads) {
-    const float4 p = pts[j];
+    const float4 p = ldg(pts + j);
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
   }
@@ -129,31 +138,34 @@ __global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a) {
   const float inv = 1023.0f / ext;  // cubic cells
   int P = 64;
   while (P < n) P <<= 1;
-  uint64_t* keys = (P <= kSortCap || query) ? skeys : ix.keys + (size_t)s * 2 * ix.cap;
+  const bool in_lds = P <= lds_keys;
+  gu64* gkeys = (gu64*)(ix.keys + (size_t)s * 2 * ix.cap);
   for (int j = threadIdx.x; j < P; j += kIdxThreads) {
     uint64_t key = ~0ull;
     if (j < n) {
-      const float4 p = pts[j];
+      const float4 p = ldg(pts + j);
       const uint32_t qx = (uint32_t)fminf(fmaxf((p.x - mn[0]) * inv, 0.f), 1023.f);
       const uint32_t qy = (uint32_t)fminf(fmaxf((p.y - mn[1]) * inv, 0.f), 1023.f);
       const uint32_t qz = (uint32_t)fminf(fmaxf((p.z - mn[2]) * inv, 0.f), 1023.f);
       const uint32_t code = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
       key = ((uint64_t)code << 32) | (uint32_t)j;
     }
-    keys[j] = key;
+    if (in_lds) skeys[j] = key;
+    else gkeys[j] = key;
   }
   __syncthreads();
-  block_bitonic(keys, P);
+  if (in_lds) block_bitonic(skeys, P);
+  else block_bitonic(gkeys, P);
   if (query) {  // association threads take their queries in this order (spatially coherent waves)
     int* perm = which == 2 ? a.qperm_sharp + (size_t)s * a.cap_sharp : a.qperm_flat + (size_t)s * a.cap_flat;
-    for (int j = threadIdx.x; j < n; j += kIdxThreads) perm[j] = (int)(uint32_t)keys[j];
+    for (int j = threadIdx.x; j < n; j += kIdxThreads) perm[j] = (int)(uint32_t)(in_lds ? skeys[j] : gkeys[j]);
     return;
   }
   float4* sorted = ix.sorted + (size_t)s * ix.cap;
   for (int j = threadIdx.x; j < n; j += kIdxThreads) {
-    const uint32_t o = (uint32_t)keys[j];
-    const float4 p = pts[o];
-    sorted[j] = make_float4(p.x, p.y, p.z, __int_as_float((int)o));
+    const uint32_t o = (uint32_t)(in_lds ? skeys[j] : gkeys[j]);
+    const float4 p = ldg(pts + o);
+    stg4(sorted + j, make_float4(p.x, p.y, p.z, __int_as_float((int)o)));
   }
   __syncthreads();
   chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
@@ -811,7 +823,11 @@ void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st) {
                               kSortCap * sizeof(uint64_t));
     attr = true;
   }
-  hipLaunchKernelGGL(k_target_index, dim3(4 * n_scans), dim3(kIdxThreads), kSortCap * sizeof(uint64_t), st, a);
+  // less-flat clouds: 128 KiB of LDS keys; less-sharp + query clouds: 64 KiB (two workgroups per CU)
+  hipLaunchKernelGGL(k_target_index, dim3(n_scans), dim3(kIdxThreads), kSortCap * sizeof(uint64_t), st, a, 1, 1, 1, 1,
+                     kSortCap);
+  hipLaunchKernelGGL(k_target_index, dim3(3 * n_scans), dim3(kIdxThreads), (kSortCap / 2) * sizeof(uint64_t), st, a,
+                     3, 0, 2, 3, kSortCap / 2);
 }
 
 void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>* ev, hipEvent_t (*get_event)(void*),
