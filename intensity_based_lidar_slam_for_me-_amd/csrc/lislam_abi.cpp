@@ -224,7 +224,6 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.qperm_sharp, (size_t)S * b->cap_sharp);
   rc |= dalloc(b, &o.qperm_flat, (size_t)S * b->cap_flat);
   rc |= dalloc(b, &o.state, (size_t)S * 16);
-  rc |= dalloc(b, &o.counters, (size_t)S * 2);
   o.cap_sharp = b->cap_sharp; o.cap_less_sharp = b->cap_less_sharp; o.cap_flat = b->cap_flat;
   o.max_iterations = c->cfg.max_iterations;
   rc |= dalloc(b, &o.blk, (size_t)S * (b->cap_sharp + b->cap_flat) * 9);

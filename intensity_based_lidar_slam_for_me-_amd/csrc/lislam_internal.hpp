@@ -85,7 +85,6 @@ struct OdomArgs {
   int max_iterations;  // ceres max_num_iterations (4, laserOdometry.cpp:707)
   const double* init_state;  // [n_chains][14] = para(7) + pose(7) at the chain start, or null
   double* state;             // [n_chains][16] = para(7), q_w(4), t_w(3)
-  int* counters;             // [n_chains][2] correspondences of the current association
   double* blk;     // [n_chains][cap_sharp + cap_flat][9] residual block records
   int* blk_kind;   // -1 invalid, 0 edge, 1 plane
   // outputs per scan

@@ -25,7 +25,6 @@
 
 namespace lislam {
 
-constexpr int kAssocThreads = 256;
 constexpr int kLmThreads = 512;
 constexpr int kLmWaves = kLmThreads / 64;
 constexpr double kDistSq = 25.0;   // DISTANCE_SQ_THRESHOLD (laserOdometry.cpp:89)
@@ -192,201 +191,376 @@ __device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, cons
   return dx * dx + dy * dy + dz * dz;
 }
 
-// The 16 points of chunk c, loaded with independent loads (clamped to the cloud) so that a whole
-// chunk is in flight at once; the caller masks indices >= n.
-__device__ __forceinline__ void load_chunk(const P4* tgt, int c, int n, P4 (&p)[kChunk]) {
-#pragma unroll
-  for (int k = 0; k < kChunk; k++) p[k] = ld4(tgt + min(c * kChunk + k, n - 1));
+
+// ------------------------------------------------------------------ phase 1: association
+// One wavefront per query.  Every step of a search is one round trip in which the 64 lanes
+// look at 64 candidates at once: super-chunk / chunk bounds, or four 16-point chunks (lane
+// groups g = lane / 16).  Results are combined by wave-wide lexicographic minima, so the visit
+// order of the reference is only needed as a tie-break key:
+//   1-NN         (distance, original index)                 == FLANN's nearest, ties lowest index
+//   line search  (distance, walk rank) with rank = j - closest going up, n + closest - j going
+//                down == the first strict '<' improvement along the reference's walk (:467-520,
+//                :589-646); a chunk is skipped only if its float bound is > the current best.
+constexpr int kAssocWaves = 4;  // queries per 256-thread workgroup
+
+#ifdef LISLAM_PHASE_PROF  // developer statistics of the searches (scripts/phase_prof.py)
+__device__ unsigned long long g_assoc_stats[16];
+#define ASTAT(i) do { if (lane_id() == 0) atomicAdd(&g_assoc_stats[i], 1ull); } while (0)
+extern "C" int lislam_debug_assoc_stats(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assoc_stats), sizeof(g_assoc_stats)) != hipSuccess) return -2;
+  static const unsigned long long zero[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_assoc_stats), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+#else
+#define ASTAT(i)
+#endif
+constexpr int kNone = 0x7fffffff;
+constexpr int kBatch = 8;  // chunks evaluated per round trip: 4 lane groups x 2 slots
+
+__device__ __forceinline__ void lexmin(float& d, int& key, float d2, int k2) {
+  if (d2 < d || (d2 == d && k2 < key)) { d = d2; key = k2; }
 }
 
-// Chunk / super-chunk metadata, either staged in LDS (kLds) or read from global memory; the
-// address space is a template parameter so every access compiles to ds_read / global_load.
-template <bool kLds>
-struct MetaT {
-  const float4* chunk_p;
-  const float4* super_p;
-  __device__ __forceinline__ float4 chunk(int i) const {
-    if constexpr (kLds) return lds4(chunk_p + i);
-    else return ldg(chunk_p + i);
+template <int kCtrl>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_mov_dpp(v, kCtrl, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rdlanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Wave-wide lexicographic minimum, returned uniform: DPP within each 16-lane row (quad xor 1,
+// xor 2, half-row mirror, row mirror), then the four row results by readlane.
+template <int kStep>
+__device__ __forceinline__ void lexmin_dpp_step(float& d, int& key) {
+  const float d2 = __int_as_float(dpp<kStep>(__float_as_int(d)));
+  const int k2 = dpp<kStep>(key);
+  lexmin(d, key, d2, k2);
+}
+__device__ __forceinline__ void wave_lexmin(float& d, int& key) {
+  lexmin_dpp_step<0xB1>(d, key);   // quad_perm [1,0,3,2]
+  lexmin_dpp_step<0x4E>(d, key);   // quad_perm [2,3,0,1]
+  lexmin_dpp_step<0x141>(d, key);  // row_half_mirror
+  lexmin_dpp_step<0x140>(d, key);  // row_mirror
+  float rd = rdlanef(d, 0);
+  int rk = rdlane(key, 0);
+  lexmin(rd, rk, rdlanef(d, 16), rdlane(key, 16));
+  lexmin(rd, rk, rdlanef(d, 32), rdlane(key, 32));
+  lexmin(rd, rk, rdlanef(d, 48), rdlane(key, 48));
+  d = rd;
+  key = rk;
+}
+
+// Take the first (up to) kN pending lanes of mask m: their values of v, -1 where none.
+template <int kN>
+__device__ __forceinline__ void take(uint64_t m, int v, int (&out)[kN]) {
+#pragma unroll
+  for (int g = 0; g < kN; g++) {
+    if (m) {
+      out[g] = rdlane(v, (int)__builtin_ctzll(m));
+      m &= m - 1;
+    } else {
+      out[g] = -1;
+    }
   }
-  __device__ __forceinline__ float4 super(int i) const {
-    if constexpr (kLds) return lds4(super_p + i);
-    else return ldg(super_p + i);
+}
+template <int kN>
+__device__ __forceinline__ bool taken(uint64_t m) {  // is this lane among the first kN of m?
+  const int lane = lane_id();
+  return ((m >> lane) & 1ull) && __popcll(m & lanemask_lt()) < kN;
+}
+__device__ __forceinline__ int sel4(int g, int v0, int v1, int v2, int v3) {
+  return g == 0 ? v0 : g == 1 ? v1 : g == 2 ? v2 : v3;
+}
+// chunk of lane group g (lane / 16) in slot t of a batch
+__device__ __forceinline__ int batch_item(const int (&v)[kBatch], int g, int t) {
+  return t == 0 ? sel4(g, v[0], v[1], v[2], v[3]) : sel4(g, v[4], v[5], v[6], v[7]);
+}
+
+// Evaluate up to eight 16-point chunks of the Morton-ordered cloud against q.
+__device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)[kBatch], const P4& q, float& bd, int& bi) {
+  const int lane = lane_id(), g = lane >> 4;
+  P4 p[2];
+  int j[2];
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const int c = batch_item(ch, g, t);
+    j[t] = c >= 0 ? c * kChunk + (lane & 15) : n;
+    if (j[t] < n) p[t] = ld4(sorted + j[t]);
   }
+  float d = 3.4e38f;
+  int key = kNone;
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    if (j[t] < n) {
+      const float dd = d2f(q, p[t]);
+      if (dd < 25.f) lexmin(d, key, dd, __float_as_int(p[t].i));
+    }
+  }
+  wave_lexmin(d, key);
+  if (key != kNone) lexmin(bd, bi, d, key);
+}
+
+// Exact 1-NN with d < 25 (the reference drops farther neighbours, :455/:577) over the
+// Morton-ordered copy: the 256 points of the super-chunk with the smallest bound first, then the
+// chunk bounds of every other super-chunk whose bound is not above the best (eight super-chunks
+// per round trip), then those chunks (eight per round trip).  Returns the original index of the
+// lexicographically smallest (distance, index), or -1.
+__device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* chm, const float4* sum, const P4& q) {
+  const int lane = lane_id();
+  if (n <= 0) return -1;
+  const int nch = (n + kChunk - 1) / kChunk, nsu = (nch + kChunk - 1) / kChunk;
+  float ulb = 3.4e38f;
+  int uid = kNone;
+  float lb0 = 3.4e38f;  // this lane's bound in the first window of super-chunks
+  for (int u = lane; u < nsu; u += 64) {
+    const float lb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
+    if (u < 64) lb0 = lb;
+    lexmin(ulb, uid, lb, u);
+  }
+  wave_lexmin(ulb, uid);
+  if (!(ulb < 25.f)) return -1;  // every point is at least 25 away
+  const int u0 = uid;
+  ASTAT(0);
+  float bd = 25.f;
+  int bi = kNone;
+  {  // the nearest super-chunk, all 256 points in one round trip
+    float d = 3.4e38f;
+    int key = kNone;
+    P4 p[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) p[t] = ld4(sorted + min(u0 * kChunk * kChunk + lane + 64 * t, n - 1));
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = u0 * kChunk * kChunk + lane + 64 * t;
+      if (j < n) {
+        const float dd = d2f(q, p[t]);
+        if (dd < 25.f) lexmin(d, key, dd, __float_as_int(p[t].i));
+      }
+    }
+    wave_lexmin(d, key);
+    if (key != kNone) lexmin(bd, bi, d, key);
+  }
+  for (int ub = 0; ub < nsu; ub += 64) {
+    const int u = ub + lane;
+    float slb = ub == 0 ? lb0 : 3.4e38f;
+    if (ub > 0 && u < nsu) slb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
+    bool spend = u < nsu && u != u0;
+    for (;;) {
+      const uint64_t um = __ballot(spend && !(slb > bd));
+      if (!um) break;
+      ASTAT(1);
+      int su8[kBatch];
+      take<kBatch>(um, u, su8);
+      if (taken<kBatch>(um)) spend = false;
+      // the 16 chunk bounds of each of those super-chunks: lane group g, slots 0 / 1
+      int c[2];
+      float clb[2];
+      bool cpend[2];
+      float4 lo[2], hi[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int sg = batch_item(su8, lane >> 4, t);
+        c[t] = sg >= 0 ? sg * kChunk + (lane & 15) : -1;
+        cpend[t] = c[t] >= 0 && c[t] < nch;
+        if (cpend[t]) { lo[t] = ldg(chm + 2 * c[t]); hi[t] = ldg(chm + 2 * c[t] + 1); }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; t++) clb[t] = cpend[t] ? box_lb(lo[t], hi[t], q) : 3.4e38f;
+      for (;;) {
+        const uint64_t m0 = __ballot(cpend[0] && !(clb[0] > bd));
+        const uint64_t m1 = __ballot(cpend[1] && !(clb[1] > bd));
+        if (!m0 && !m1) break;
+        ASTAT(2);
+        int c8[kBatch], a0[kBatch], a1[kBatch];
+        take<kBatch>(m0, c[0], a0);
+        take<kBatch>(m1, c[1], a1);
+        const int n0 = min(__popcll(m0), kBatch);
+#pragma unroll
+        for (int e = 0; e < kBatch; e++) c8[e] = e < n0 ? a0[e] : (e - n0 < kBatch ? a1[e - n0 < 0 ? 0 : e - n0] : -1);
+        if (taken<kBatch>(m0)) cpend[0] = false;
+        if (((m1 >> lane) & 1ull) && __popcll(m1 & lanemask_lt()) < kBatch - n0) cpend[1] = false;
+        nn_eval(sorted, n, c8, q, bd, bi);
+      }
+    }
+  }
+  return bi == kNone ? -1 : bi;
+}
+
+// Scan-line searches in the target cloud (scan-line order) around `closest` (label cid).
+// kCorner: the corner's second point (:467-520), best in (b2, k2).
+// else:    the surf's second (same side of the line, :600-612 / :628-640) and third points.
+struct LineSearch {
+  const P4* L;
+  const float4* chm;  // chunk bounds (scan-line order), w = label min / max
+  int n, nch, closest, cid;
+  P4 sel;
+  float b2, b3;  // running bests (25 = none)
+  int k2, k3;    // walk-rank keys
 };
 
-// 1-NN candidates of chunk c of the Morton-ordered cloud: lexicographic (distance, original index).
-__device__ __forceinline__ void nn_chunk(const P4* sorted, int c, int n, const P4& q, float& best, int& bi) {
-  P4 p[kChunk];
-  load_chunk(sorted, c, n, p);
+// Evaluate up to eight chunks (dir: 1 up / 0 down) against the running bests.  brk[t]: the
+// lane group met the walk's 'break' inside its slot-t chunk.
+template <bool kCorner>
+__device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[kBatch], const int (&dir)[kBatch],
+                                        uint64_t* brk_mask = nullptr) {
+  const int lane = lane_id(), g = lane >> 4, l16 = lane & 15;
+  P4 p[2];
+  bool valid[2], up[2];
+  int j[2];
 #pragma unroll
-  for (int k = 0; k < kChunk; k++) {
-    if (c * kChunk + k < n) {
-      const int j = __float_as_int(p[k].i);
-      const float d = d2f(q, p[k]);
-      if (d < best || (d == best && j < bi)) { best = d; bi = j; }
-    }
+  for (int t = 0; t < 2; t++) {
+    const int c = batch_item(ch, g, t);
+    up[t] = batch_item(dir, g, t) != 0;
+    j[t] = c * kChunk + l16;
+    valid[t] = c >= 0 && j[t] < s.n && (up[t] ? j[t] > s.closest : j[t] < s.closest);
+    p[t] = P4{0.f, 0.f, 0.f, 0.f};
+    if (valid[t]) p[t] = ld4(s.L + j[t]);
   }
-}
-
-template <class M>
-__device__ __forceinline__ void nn_super(const P4* sorted, int n, const M& m, int u, const P4& q, float& best, int& bi) {
-  const int nch = (n + kChunk - 1) / kChunk;
-  for (int c = u * kChunk; c < min(nch, u * kChunk + kChunk); c++) {
-    if (box_lb(m.chunk(2 * c), m.chunk(2 * c + 1), q) > best) continue;
-    nn_chunk(sorted, c, n, q, best, bi);
-  }
-}
-
-// Exact 1-NN restricted to d < 25 (the reference discards farther neighbours, :455/:577) over the
-// Morton-ordered copy: the super-chunk nearest the query first (a tight bound), then every other
-// super-chunk / chunk whose box bound does not exceed the best distance.  Returns the
-// lexicographically smallest (float distance, original index), or -1.
-template <class M>
-__device__ __forceinline__ int nn_search(const P4* sorted, int n, const M& m, const P4& q) {
-  float best = 25.0f;
-  int bi = -1;
-  const int nsu = ((n + kChunk - 1) / kChunk + kChunk - 1) / kChunk;
-  int u0 = -1;
-  float lb0 = 3.4e38f;
-  for (int u = 0; u < nsu; u++) {
-    const float lb = box_lb(m.super(2 * u), m.super(2 * u + 1), q);
-    if (lb < lb0) { lb0 = lb; u0 = u; }
-  }
-  if (u0 < 0 || lb0 > best) return -1;
-  nn_super(sorted, n, m, u0, q, best, bi);
-  for (int u = 0; u < nsu; u++) {
-    if (u == u0 || box_lb(m.super(2 * u), m.super(2 * u + 1), q) > best) continue;
-    nn_super(sorted, n, m, u, q, best, bi);
-  }
-  return bi;
-}
-
-__device__ __forceinline__ double line_d2(const P4& p, const P4& sel) {  // laserOdometry.cpp:478-483
-  return (double)((p.x - sel.x) * (p.x - sel.x) + (p.y - sel.y) * (p.y - sel.y) + (p.z - sel.z) * (p.z - sel.z));
-}
-
-// Corner second point (laserOdometry.cpp:464-520): min over scanID in (cid, cid+2.5] going up,
-// then [cid-2.5, cid) going down; strict '<', 'continue' / 'break' on int(intensity).  A chunk is
-// skipped from its metadata only when that cannot change the outcome; otherwise its 16 points
-// are loaded at once and walked in the reference's order.
-template <class M>
-__device__ __forceinline__ int corner_second(const P4* L, int n, const M& m, int closest, int cid, const P4& sel) {
-  double best = kDistSq;
-  int mi = -1;
-  const double hiL = cid + kNearby, loL = cid - kNearby;
-  bool stop = false;
-  for (int c = (closest + 1) / kChunk; !stop && c * kChunk < n; c++) {  // up
-    const int j0 = max(closest + 1, c * kChunk);
-    if (j0 == c * kChunk) {
-      const float4 lo = m.chunk(2 * c), hi = m.chunk(2 * c + 1);
-      if ((double)(int)lo.w > hiL) break;                    // its first point breaks
-      if (!((double)(int)hi.w > hiL)) {                      // no break inside
-        if ((int)hi.w <= cid) continue;                      // every point 'continue's
-        if ((double)box_lb(lo, hi, sel) >= best) continue;   // none can be closer
+  float d2 = 3.4e38f, d3 = 3.4e38f;
+  int q2 = kNone, q3 = kNone;
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const int pid = int(p[t].i);
+    const bool brk = valid[t] && (up[t] ? pid > s.cid + 2 : pid < s.cid - 2);  // the walk's 'break'
+    const uint64_t bm = __ballot(brk);
+    if (brk_mask) brk_mask[t] = bm;
+    const uint32_t gm = (uint32_t)((bm >> (lane & 48)) & 0xffffull);
+    bool v = valid[t];
+    if (gm) v = v && (up[t] ? l16 < (int)__builtin_ctz(gm) : l16 > 31 - (int)__builtin_clz(gm));
+    if (v) {
+      const float d = d2f(s.sel, p[t]);
+      const int key = up[t] ? j[t] - s.closest : s.n + s.closest - j[t];
+      if (d < 25.f) {
+        if (kCorner) {
+          if (up[t] ? pid > s.cid : pid < s.cid) lexmin(d2, q2, d, key);
+        } else {
+          if (up[t] ? pid <= s.cid : pid >= s.cid) lexmin(d2, q2, d, key);
+          else lexmin(d3, q3, d, key);
+        }
       }
     }
-    P4 p[kChunk];
-    load_chunk(L, c, n, p);
-#pragma unroll
-    for (int k = 0; k < kChunk; k++) {
-      const int j = c * kChunk + k;
-      if (stop || j < j0 || j >= n) continue;
-      const int pid = int(p[k].i);
-      if (pid <= cid) continue;
-      if ((double)pid > hiL) { stop = true; continue; }
-      const double d = line_d2(p[k], sel);
-      if (d < best) { best = d; mi = j; }
-    }
   }
-  stop = false;
-  for (int c = (closest - 1) / kChunk; !stop && closest >= 1 && c >= 0; c--) {  // down
-    const int j0 = min(closest - 1, min(n, c * kChunk + kChunk) - 1);
-    if (j0 == min(n, c * kChunk + kChunk) - 1) {
-      const float4 lo = m.chunk(2 * c), hi = m.chunk(2 * c + 1);
-      if ((double)(int)hi.w < loL) break;
-      if (!((double)(int)lo.w < loL)) {
-        if ((int)lo.w >= cid) continue;
-        if ((double)box_lb(lo, hi, sel) >= best) continue;
-      }
-    }
-    P4 p[kChunk];
-    load_chunk(L, c, n, p);
-#pragma unroll
-    for (int k = kChunk - 1; k >= 0; k--) {
-      const int j = c * kChunk + k;
-      if (stop || j > j0) continue;
-      const int pid = int(p[k].i);
-      if (pid >= cid) continue;
-      if ((double)pid < loL) { stop = true; continue; }
-      const double d = line_d2(p[k], sel);
-      if (d < best) { best = d; mi = j; }
-    }
+  wave_lexmin(d2, q2);
+  if (q2 != kNone) lexmin(s.b2, s.k2, d2, q2);
+  if (!kCorner) {
+    wave_lexmin(d3, q3);
+    if (q3 != kNone) lexmin(s.b3, s.k3, d3, q3);
   }
-  return mi;
 }
 
-// Surf second / third points (laserOdometry.cpp:586-646).
-template <class M>
-__device__ __forceinline__ void surf_second_third(const P4* L, int n, const M& m, int closest, int cid, const P4& sel, int* m2,
-                                  int* m3) {
-  double b2 = kDistSq, b3 = kDistSq;
-  int i2 = -1, i3 = -1;
-  const double hiL = cid + kNearby, loL = cid - kNearby;
-  bool stop = false;
-  for (int c = (closest + 1) / kChunk; !stop && c * kChunk < n; c++) {  // up
-    const int j0 = max(closest + 1, c * kChunk);
-    if (j0 == c * kChunk) {
-      const float4 lo = m.chunk(2 * c), hi = m.chunk(2 * c + 1);
-      if ((double)(int)lo.w > hiL) break;
-      if (!((double)(int)hi.w > hiL)) {
-        const double lb = box_lb(lo, hi, sel);
-        const bool need2 = (int)lo.w <= cid && lb < b2;
-        const bool need3 = (int)hi.w > cid && lb < b3;
-        if (!need2 && !need3) continue;
+// Does an up / down chunk with bounds (lo, hi) and bound lb still need a visit?
+template <bool kCorner>
+__device__ __forceinline__ bool ls_need(const LineSearch& s, bool up, const float4& lo, const float4& hi, float lb) {
+  const int lmin = (int)lo.w, lmax = (int)hi.w;
+  if (kCorner) return (up ? lmax > s.cid : lmin < s.cid) && !(lb > s.b2);
+  const bool n2 = (up ? lmin <= s.cid : lmax >= s.cid) && !(lb > s.b2);
+  const bool n3 = (up ? lmax > s.cid : lmin < s.cid) && !(lb > s.b3);
+  return n2 || n3;
+}
+
+template <bool kCorner>
+__device__ __forceinline__ void line_search(LineSearch& s) {
+  const int lane = lane_id();
+  const int hc = s.closest / kChunk;
+  // Round trip 1: the home chunk in both directions and its two neighbours, together with the
+  // bounds of the next 64 chunks each way (window 0).
+  int w = 0;
+  int cu = hc + 2 + lane, cd = hc - 2 - lane;
+  float4 ulo = make_float4(0, 0, 0, 0), uhi = ulo, dlo = ulo, dhi = ulo;
+  bool uin = cu < s.nch, din = cd >= 0;
+  if (uin) { ulo = ldg(s.chm + 2 * cu); uhi = ldg(s.chm + 2 * cu + 1); }
+  if (din) { dlo = ldg(s.chm + 2 * cd); dhi = ldg(s.chm + 2 * cd + 1); }
+  bool up_open, dn_open;  // no 'break' met yet in that direction
+  {
+    const int ch[kBatch] = {hc, hc, hc + 1 < s.nch ? hc + 1 : -1, hc - 1, -1, -1, -1, -1};
+    const int dir[kBatch] = {1, 0, 1, 0, 1, 1, 1, 1};
+    uint64_t bm[2];
+    LineSearch s0 = s;
+    ls_eval<kCorner>(s0, ch, dir, bm);
+    const bool home_up_brk = bm[0] & 0xffffull, home_dn_brk = (bm[0] >> 16) & 0xffffull;
+    if (!home_up_brk && !home_dn_brk) {
+      s = s0;
+    } else {  // rare: the home chunk broke a walk; redo without the neighbour beyond it
+      const int ch2[kBatch] = {hc, hc, home_up_brk ? -1 : ch[2], home_dn_brk ? -1 : ch[3], -1, -1, -1, -1};
+      ls_eval<kCorner>(s, ch2, dir);
+    }
+    up_open = !home_up_brk && !((bm[0] >> 32) & 0xffffull);
+    dn_open = !home_dn_brk && !((bm[0] >> 48) & 0xffffull);
+  }
+  for (;;) {
+    uin = uin && up_open;
+    din = din && dn_open;
+    if (!__ballot(uin) && !__ballot(din)) break;
+    ASTAT(4);
+    // the first chunk holding a label past the nearby range is where that walk breaks
+    const uint64_t ufl = __ballot(uin && (int)uhi.w > s.cid + 2);
+    const uint64_t dfl = __ballot(din && (int)dlo.w < s.cid - 2);
+    const int ulast = ufl ? (int)__builtin_ctzll(ufl) : 63, dlast = dfl ? (int)__builtin_ctzll(dfl) : 63;
+    bool upend = uin && lane <= ulast, dpend = din && lane <= dlast;
+    const float ulb = upend ? box_lb(ulo, uhi, s.sel) : 3.4e38f;
+    const float dlb = dpend ? box_lb(dlo, dhi, s.sel) : 3.4e38f;
+    if (w == 0) {
+      // first batch: around the up and the down chunk with the smallest bound among those that
+      // can still improve a best (chunks i-1 .. i+2 of each), which sets tight bests at once
+      float mu = upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? ulb : 3.4e38f;
+      int iu = mu < 3.4e38f ? lane : kNone;
+      float md = dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dlb : 3.4e38f;
+      int id = md < 3.4e38f ? lane : kNone;
+      wave_lexmin(mu, iu);
+      wave_lexmin(md, id);
+      int ch[kBatch], dir[kBatch];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int lu = (iu != kNone ? iu : 0) - 1 + e, ld = (id != kNone ? id : 0) - 1 + e;
+        const bool okl = iu != kNone && lu >= 0 && lu <= ulast && __builtin_amdgcn_readlane((int)upend, lu & 63);
+        const bool okd = id != kNone && ld >= 0 && ld <= dlast && __builtin_amdgcn_readlane((int)dpend, ld & 63);
+        ch[e] = okl ? hc + 2 + lu : -1;
+        dir[e] = 1;
+        ch[4 + e] = okd ? hc - 2 - ld : -1;
+        dir[4 + e] = 0;
+      }
+      if (iu != kNone || id != kNone) {
+        ASTAT(5);
+        if (iu != kNone && lane >= iu - 1 && lane <= iu + 2) upend = false;
+        if (id != kNone && lane >= id - 1 && lane <= id + 2) dpend = false;
+        ls_eval<kCorner>(s, ch, dir);
       }
     }
-    P4 p[kChunk];
-    load_chunk(L, c, n, p);
+    for (;;) {
+      const uint64_t um = __ballot(upend && ls_need<kCorner>(s, true, ulo, uhi, ulb));
+      const uint64_t dm = __ballot(dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb));
+      if (!um && !dm) break;
+      ASTAT(kCorner ? 6 : 7);
+      int au[kBatch], ad[kBatch], ch[kBatch], dir[kBatch];
+      take<kBatch>(um, cu, au);
+      take<kBatch>(dm, cd, ad);
+      const int nu = min(__popcll(um), kBatch);
 #pragma unroll
-    for (int k = 0; k < kChunk; k++) {
-      const int j = c * kChunk + k;
-      if (stop || j < j0 || j >= n) continue;
-      const int pid = int(p[k].i);
-      if ((double)pid > hiL) { stop = true; continue; }
-      const double d = line_d2(p[k], sel);
-      if (pid <= cid && d < b2) { b2 = d; i2 = j; }
-      else if (pid > cid && d < b3) { b3 = d; i3 = j; }
-    }
-  }
-  stop = false;
-  for (int c = (closest - 1) / kChunk; !stop && closest >= 1 && c >= 0; c--) {  // down
-    const int j0 = min(closest - 1, min(n, c * kChunk + kChunk) - 1);
-    if (j0 == min(n, c * kChunk + kChunk) - 1) {
-      const float4 lo = m.chunk(2 * c), hi = m.chunk(2 * c + 1);
-      if ((double)(int)hi.w < loL) break;
-      if (!((double)(int)lo.w < loL)) {
-        const double lb = box_lb(lo, hi, sel);
-        const bool need2 = (int)hi.w >= cid && lb < b2;
-        const bool need3 = (int)lo.w < cid && lb < b3;
-        if (!need2 && !need3) continue;
+      for (int e = 0; e < kBatch; e++) {
+        ch[e] = e < nu ? au[e] : ad[e - nu < 0 ? 0 : e - nu];
+        dir[e] = e < nu ? 1 : 0;
       }
+      if (taken<kBatch>(um)) upend = false;
+      if (((dm >> lane) & 1ull) && __popcll(dm & lanemask_lt()) < kBatch - nu) dpend = false;
+      ls_eval<kCorner>(s, ch, dir);
     }
-    P4 p[kChunk];
-    load_chunk(L, c, n, p);
-#pragma unroll
-    for (int k = kChunk - 1; k >= 0; k--) {
-      const int j = c * kChunk + k;
-      if (stop || j > j0) continue;
-      const int pid = int(p[k].i);
-      if ((double)pid < loL) { stop = true; continue; }
-      const double d = line_d2(p[k], sel);
-      if (pid >= cid && d < b2) { b2 = d; i2 = j; }
-      else if (pid < cid && d < b3) { b3 = d; i3 = j; }
-    }
+    // next window only where the walk did not break inside this one
+    w++;
+    up_open = up_open && !ufl;
+    dn_open = dn_open && !dfl;
+    cu += 64;
+    cd -= 64;
+    uin = cu < s.nch;
+    din = cd >= 0;
+    if (uin && up_open) { ulo = ldg(s.chm + 2 * cu); uhi = ldg(s.chm + 2 * cu + 1); }
+    if (din && dn_open) { dlo = ldg(s.chm + 2 * cd); dhi = ldg(s.chm + 2 * cd + 1); }
   }
-  *m2 = i2;
-  *m3 = i3;
+}
+
+__device__ __forceinline__ int rank_to_index(const LineSearch& s, int key) {
+  return key < s.n ? s.closest + key : s.closest - (key - s.n);
 }
 
 __device__ __forceinline__ bool pair_of(const OdomArgs& a, int c, int r, int* k) {
@@ -396,98 +570,74 @@ __device__ __forceinline__ bool pair_of(const OdomArgs& a, int c, int r, int* k)
   return *k <= k1;
 }
 
-// ------------------------------------------------------------------ phase 1: association
-// Grid: x = corner blocks (cap_sharp / 256) then surf blocks (cap_flat / 256), y = chain.  A
-// block handles one query kind, so it stages only its target cloud's metadata in LDS.
-constexpr int kMetaCap = 768;  // chunks per structure staged in LDS; larger clouds read global memory
-
-struct AssocShared {
-  float4 chunk[2 * kMetaCap];                // scan-line order
-  float4 super[2 * (kMetaCap / kChunk)];
-  float4 nn_chunk[2 * kMetaCap];             // Morton order
-  float4 nn_super[2 * (kMetaCap / kChunk)];
-};
-
-template <bool kCorner, class M>
-__device__ __forceinline__ void assoc_query(const OdomArgs& a, int c, int k, int q, const M& lm, const M& nm, const P4* L,
-                            const P4* sorted, int nL, bool* found_out) {
-  double x[7];
-  const double* st = a.state + (size_t)c * 16;
-  for (int e = 0; e < 7; e++) x[e] = st[e];
-  double* blk = a.blk + (size_t)c * (a.cap_sharp + a.cap_flat) * 9;
-  int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
-  const P4 cur = kCorner ? ld4(a.sharp + (size_t)k * a.cap_sharp + q) : ld4(a.flat + (size_t)k * a.cap_flat + q);
-  const P4 sel = transform_to_start(cur, x);
-  const int closest = (a.dbg & 1) ? -1 : nn_search(sorted, nL, nm, sel);
-  const int slot = kCorner ? q : a.cap_sharp + q;
-  double* rec = blk + (size_t)slot * 9;
-  bool found = false;
-  if (closest >= 0 && !(a.dbg & 2)) {
-    const P4 pa = ld4(L + closest);
-    const int cid = int(pa.i);
-    if (kCorner) {  // LidarEdgeFactor(curr, a, b)
-      const int m2 = corner_second(L, nL, lm, closest, cid, sel);
-      if (m2 >= 0) {
-        const P4 pb = ld4(L + m2);
-        rec[0] = cur.x; rec[1] = cur.y; rec[2] = cur.z; rec[3] = pa.x; rec[4] = pa.y; rec[5] = pa.z;
-        rec[6] = pb.x; rec[7] = pb.y; rec[8] = pb.z;
-        found = true;
-      }
-    } else {        // LidarPlaneFactor(curr, j, l, m)
-      int m2, m3;
-      surf_second_third(L, nL, lm, closest, cid, sel, &m2, &m3);
-      if (m2 >= 0 && m3 >= 0) {
-        const P4 pl = ld4(L + m2), pm = ld4(L + m3);
-        const D3 j{pa.x, pa.y, pa.z};
-        const D3 nrm = plane_normal(j, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
-        rec[0] = cur.x; rec[1] = cur.y; rec[2] = cur.z; rec[3] = j.x; rec[4] = j.y; rec[5] = j.z;
-        rec[6] = nrm.x; rec[7] = nrm.y; rec[8] = nrm.z;
-        found = true;
-      }
-    }
+// Grid: qblocks = ceil((cap_sharp + cap_flat) / 4) workgroups of 4 waves per chain.  Wave w of
+// pair k takes corner query w (w < n_sharp) or surf query w - n_sharp, in Morton order.  With
+// 8 or more chains, workgroup b serves chain 8 * ((b / 8) / qblocks) + b % 8: workgroups are
+// dealt round-robin over the 8 XCDs, so each XCD's L2 holds the target clouds of only its own
+// chains (placement is a speed matter only).
+__global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int r, int qblocks) {
+  int c, qb;
+  if (a.n_chains >= 8) {
+    const int b = blockIdx.x, x = b & 7, rr = b >> 3;
+    c = 8 * (rr / qblocks) + x;
+    qb = rr % qblocks;
+  } else {
+    c = blockIdx.x / qblocks;
+    qb = blockIdx.x % qblocks;
   }
-  kind[slot] = found ? (kCorner ? 0 : 1) : -1;
-  *found_out = found;
-}
-
-__global__ __launch_bounds__(kAssocThreads) void k_odom_assoc(OdomArgs a, int r) {
-  __shared__ AssocShared sh;
-  const int c = blockIdx.y;
+  if (c >= a.n_chains) return;
   int k;
   if (!pair_of(a, c, r, &k)) return;
-  const int cb = (a.cap_sharp + kAssocThreads - 1) / kAssocThreads;
-  const bool corner = (int)blockIdx.x < cb;
-  const int t = (corner ? blockIdx.x : blockIdx.x - cb) * kAssocThreads + threadIdx.x;
-  const int nq = a.n_feat[k * 4 + (corner ? 0 : 2)];
-  if ((t - (int)threadIdx.x) >= nq) return;  // whole block past the queries
-  const int q = t < nq ? (corner ? a.qperm_sharp[(size_t)k * a.cap_sharp + t] : a.qperm_flat[(size_t)k * a.cap_flat + t]) : nq;
+  const int lane = lane_id();
+  const int w = qb * kAssocWaves + (int)(threadIdx.x >> 6);
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  if (w >= ns + nf) return;  // whole waves leave; nothing below synchronizes the workgroup
+  const bool corner = w < ns;
+  const int t = corner ? w : w - ns;
+  const int q = corner ? a.qperm_sharp[(size_t)k * a.cap_sharp + t] : a.qperm_flat[(size_t)k * a.cap_flat + t];
   const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
   const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
   const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
   const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
-  const int nch = (nL + kChunk - 1) / kChunk, nsu = (nch + kChunk - 1) / kChunk;
   const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
-  const MetaT<false> glm{ix.chunk + mo, ix.super + so}, gnm{ix.nn_chunk + mo, ix.nn_super + so};
-  const bool staged = nch <= kMetaCap;
-  if (staged) {
-    for (int e = threadIdx.x; e < 2 * nch; e += kAssocThreads) { sh.chunk[e] = glm.chunk(e); sh.nn_chunk[e] = gnm.chunk(e); }
-    for (int e = threadIdx.x; e < 2 * nsu; e += kAssocThreads) { sh.super[e] = glm.super(e); sh.nn_super[e] = gnm.super(e); }
-  }
-  __syncthreads();
+  double x[7];
+  const double* st = a.state + (size_t)c * 16;
+  for (int e = 0; e < 7; e++) x[e] = st[e];
+  const P4 cur = corner ? ld4(a.sharp + (size_t)k * a.cap_sharp + q) : ld4(a.flat + (size_t)k * a.cap_flat + q);
+  const P4 sel = transform_to_start(cur, x);
+  const int closest = nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel);
+  const int slot = corner ? q : a.cap_sharp + q;
+  double* rec = a.blk + ((size_t)c * (a.cap_sharp + a.cap_flat) + slot) * 9;
   bool found = false;
-  if (t < nq) {
-    if (staged) {
-      const MetaT<true> lm{sh.chunk, sh.super}, nm{sh.nn_chunk, sh.nn_super};
-      if (corner) assoc_query<true>(a, c, k, q, lm, nm, L, sorted, nL, &found);
-      else assoc_query<false>(a, c, k, q, lm, nm, L, sorted, nL, &found);
-    } else {
-      if (corner) assoc_query<true>(a, c, k, q, glm, gnm, L, sorted, nL, &found);
-      else assoc_query<false>(a, c, k, q, glm, gnm, L, sorted, nL, &found);
+  double v = 0.0;  // this lane's record entry (lanes 0..8)
+  ASTAT(corner ? 8 : 9);
+  if (closest >= 0) {
+    ASTAT(corner ? 10 : 11);
+    const P4 pa = ld4(L + closest);
+    LineSearch s{L, ix.chunk + mo, nL, (nL + kChunk - 1) / kChunk, closest, int(pa.i), sel, 25.f, 25.f, kNone, kNone};
+    if (corner) {  // LidarEdgeFactor(curr, a, b)
+      line_search<true>(s);
+      if (s.k2 != kNone) {
+        const P4 pb = ld4(L + rank_to_index(s, s.k2));
+        const float e9[9] = {cur.x, cur.y, cur.z, pa.x, pa.y, pa.z, pb.x, pb.y, pb.z};
+        for (int e = 0; e < 9; e++) if (lane == e) v = e9[e];
+        found = true;
+      }
+    } else {        // LidarPlaneFactor(curr, j, l, m)
+      line_search<false>(s);
+      if (s.k2 != kNone && s.k3 != kNone) {
+        const P4 pl = ld4(L + rank_to_index(s, s.k2)), pm = ld4(L + rank_to_index(s, s.k3));
+        const D3 j{pa.x, pa.y, pa.z};
+        const D3 nrm = plane_normal(j, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
+        const double e9[9] = {cur.x, cur.y, cur.z, j.x, j.y, j.z, nrm.x, nrm.y, nrm.z};
+        for (int e = 0; e < 9; e++) if (lane == e) v = e9[e];
+        found = true;
+      }
     }
   }
-  // corner_correspondence / plane_correspondence (:562/:685), one atomic per wave
-  const uint64_t mf = __ballot(found);
-  if ((threadIdx.x & 63) == 0 && mf) atomicAdd(&a.counters[c * 2 + (corner ? 0 : 1)], __popcll(mf));
+  if (found && lane < 9) rec[lane] = v;
+  // the LM kernel counts corner_correspondence / plane_correspondence (:562/:685) from the kinds
+  if (lane == 0) a.blk_kind[(size_t)c * (a.cap_sharp + a.cap_flat) + slot] = found ? (corner ? 0 : 1) : -1;
 }
 
 // ------------------------------------------------------------------ phase 2: LM solve
@@ -503,11 +653,52 @@ __device__ __forceinline__ void accum_row(double* acc, const double* J, double r
 }
 
 struct LmShared {
-  double red[kLmWaves][28];
+  double red[kLmWaves * 4][28];  // one partial sum per 16-lane row
   double x[7];
   double acc[28];
+  int cnt[kLmWaves][2];
+  int nc, np;
   int flag;
 };
+
+template <int kCtrl>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, kCtrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), kCtrl, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+// sum over the 16 lanes of each row (every lane of the row gets it)
+__device__ __forceinline__ double row_sum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  return v;
+}
+
+// corner_correspondence / plane_correspondence (:562/:685) of the current association
+__device__ __forceinline__ void count_kinds(LmShared& sh, const int* kind, int ns, int cap_sharp, int nf) {
+  int c0 = 0, c1 = 0;
+  for (int i = threadIdx.x; i < ns + nf; i += kLmThreads) {
+    const int kd = kind[i < ns ? i : cap_sharp + (i - ns)];
+    c0 += kd == 0;
+    c1 += kd == 1;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c0 += __shfl_xor(c0, o);
+    c1 += __shfl_xor(c1, o);
+  }
+  if ((threadIdx.x & 63) == 0) { sh.cnt[threadIdx.x >> 6][0] = c0; sh.cnt[threadIdx.x >> 6][1] = c1; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int a0 = 0, a1 = 0;
+    for (int w = 0; w < kLmWaves; w++) { a0 += sh.cnt[w][0]; a1 += sh.cnt[w][1]; }
+    sh.nc = a0;
+    sh.np = a1;
+  }
+  __syncthreads();
+}
 
 // One evaluation at sh.x: cost, J^T J (upper, row-major), J^T r -> sh.acc
 __device__ __forceinline__ void evaluate(LmShared& sh, const double* blk, const int* kind, int ns, int cap_sharp, int nf) {
@@ -541,17 +732,16 @@ __device__ __forceinline__ void evaluate(LmShared& sh, const double* blk, const 
       accum_row(acc, J, res * sc);
     }
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
 #pragma unroll
   for (int e = 0; e < 28; e++) {
-    double v = acc[e];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane == 0) sh.red[wave][e] = v;
+    const double v = row_sum(acc[e]);
+    if ((lane & 15) == 0) sh.red[row][e] = v;
   }
   __syncthreads();
   if (threadIdx.x < 28) {
     double v = 0;
-    for (int w = 0; w < kLmWaves; w++) v += sh.red[w][threadIdx.x];
+    for (int w = 0; w < kLmWaves * 4; w++) v += sh.red[w][threadIdx.x];
     sh.acc[threadIdx.x] = v;
   }
   __syncthreads();
@@ -684,7 +874,8 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const double* blk = a.blk + (size_t)c * (a.cap_sharp + a.cap_flat) * 9;
   const int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
-  const int nc = a.counters[c * 2 + 0], np = a.counters[c * 2 + 1];
+  count_kinds(sh, kind, ns, a.cap_sharp, nf);
+  const int nc = sh.nc, np = sh.np;
   LM s;
   double mcc = 0;
   bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
@@ -756,8 +947,6 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   so[6 + outer] = (nc + np) > 0 ? s.term : 1;
   if ((nc + np) > 0)
     for (int e = 0; e < 7; e++) st[e] = s.x[e];
-  a.counters[c * 2 + 0] = 0;
-  a.counters[c * 2 + 1] = 0;
   if (outer == 1) {
     // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr
     DQ qw{st[7], st[8], st[9], st[10]};
@@ -781,8 +970,6 @@ __global__ void k_odom_init(OdomArgs a) {
     const double id[14] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0};
     for (int e = 0; e < 14; e++) st[e] = id[e];
   }
-  a.counters[c * 2 + 0] = 0;
-  a.counters[c * 2 + 1] = 0;
   if (c == 0 && !a.init_state) {  // scan 0 of the batch: first frame, initialization only
     for (int e = 0; e < 7; e++) { a.para[e] = st[e]; a.pose[e] = st[7 + e]; }
     for (int e = 0; e < 8; e++) a.stats[e] = 0;
@@ -842,12 +1029,13 @@ void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>*
   };
   mark();
   hipLaunchKernelGGL(k_odom_init, dim3((a.n_chains + 63) / 64), dim3(64), 0, st, a);
-  const int qblocks = (a.cap_sharp + kAssocThreads - 1) / kAssocThreads + (a.cap_flat + kAssocThreads - 1) / kAssocThreads;
+  const int qblocks = (a.cap_sharp + a.cap_flat + kAssocWaves - 1) / kAssocWaves;
   const int rounds = min(a.chain_len, a.S - 1);
   mark();
   for (int r = 0; r < rounds; r++) {
     for (int outer = 0; outer < 2; outer++) {
-      hipLaunchKernelGGL(k_odom_assoc, dim3(qblocks, a.n_chains), dim3(kAssocThreads), 0, st, a, r);
+      hipLaunchKernelGGL(k_odom_assoc, dim3(qblocks * (a.n_chains >= 8 ? (a.n_chains + 7) / 8 * 8 : a.n_chains)),
+                         dim3(64 * kAssocWaves), 0, st, a, r, qblocks);
       mark();
       hipLaunchKernelGGL(k_odom_lm, dim3(a.n_chains), dim3(kLmThreads), 0, st, a, r, outer);
       mark();

@@ -43,4 +43,16 @@ with pkg.Context() as ctx:
     nl = S * 64
     for i, n in enumerate(PHASES):
         print(f"{n:22s} {buf[i] / nl:12.0f} cycles/line  {100 * buf[i] / max(tot, 1):5.1f}%")
+    # association search statistics over one odometry pass
+    b.odometry(S, 10)
+    ctx.synchronize()
+    L.lislam_debug_assoc_stats(buf)
+    b.odometry(S, 10)
+    ctx.synchronize()
+    L.lislam_debug_assoc_stats(buf)
+    names = ["nn queries (>=1 super in range)", "nn extra super batches", "nn chunk batches", "-", "ls windows",
+             "ls first batches", "ls corner batches", "ls surf batches", "corner queries", "surf queries",
+             "corner with closest", "surf with closest"]
+    for i, n in enumerate(names):
+        print(f"{n:34s} {buf[i]}")
     b.close()
