@@ -147,6 +147,75 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
 int lislam_eval_factors(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,
                         const double* t, double* residuals, double* jac);
 
+/* ---------------------------------------------------------------- scan-to-map (a19-a21) */
+/* A device-resident point map with the semantics of the vendored ikd-Tree
+ * (src/ikd-Tree/ikd_Tree.h:256-279): Build, Add_Points with box downsampling, exact k-NN
+ * Nearest_Search, and the mapping stages that consume it.  Points are float32 x, y, z; input
+ * arrays are n points of `stride` floats (3 = PointXYZ packed, 4 = PointXYZ / PointXYZI as PCL
+ * stores them).  Pointers may be host or device memory (copied with hipMemcpyDefault). */
+typedef struct lislam_map lislam_map;
+
+typedef struct {
+  float downsample_size; /* ikd KD_TREE(delete_param, balance_param, box_length): 0.4 ground map,
+                            0.8 corner map (mapOptimization.cpp:504-505) */
+  float cell_size;       /* edge of the hash-grid cells the search walks (0: downsample_size);
+                            a search accelerator only, results do not depend on it */
+} lislam_map_config;
+
+int lislam_map_create(lislam_ctx* ctx, const lislam_map_config* cfg, lislam_map** out);
+int lislam_map_destroy(lislam_map* m);
+/* KD_TREE::Build (ikd_Tree.cpp:470-492): the map holds exactly these points (ids 0..n-1). */
+int lislam_map_build(lislam_map* m, const float* pts, int64_t n, int32_t stride);
+/* KD_TREE::Add_Points (ikd_Tree.cpp:569-706).  downsample_on: per box of edge downsample_size
+ * only the point nearest the box centre survives, as the reference's sequential loop leaves it.
+ * Inputs take ids next_id .. next_id+n-1.  n_added (nullable) = inputs that entered the map. */
+int lislam_map_add_points(lislam_map* m, const float* pts, int64_t n, int32_t stride, int32_t downsample_on,
+                          int64_t* n_added);
+/* KD_TREE::size / validnum. */
+int lislam_map_size(lislam_map* m, int64_t* n);
+/* KD_TREE::flatten / PCL_Storage: live points as (x, y, z, id bits), storage order. */
+int lislam_map_points(lislam_map* m, float* out_xyzi, int64_t cap, int64_t* n);
+/* KD_TREE::Nearest_Search (ikd_Tree.cpp:494-547) for n queries: up to k (<= 8) points with
+ * squared distance <= max_dist^2 (max_dist <= 0: unbounded), ascending (squared float distance,
+ * id).  out_pts[n][k][4] = x, y, z, id bits; out_d2[n][k]; out_found[n] (all nullable). */
+int lislam_map_nearest_search(lislam_map* m, const float* queries, int32_t n, int32_t stride, int32_t k,
+                              float max_dist, float* out_pts, float* out_d2, int32_t* out_found);
+
+#define LISLAM_MATCH_LINE 0  /* laserMapping corner: 5-NN, PCA line, LidarEdgeFactor (laserMapping.cpp:668-723) */
+#define LISLAM_MATCH_PLANE 1 /* 5-NN, QR plane, LidarPlaneNormFactor (laserMapping.cpp:744-796,
+                                mapOptimization.cpp:376-429) */
+/* Associate n sensor-frame points at pose x = (q x,y,z,w, t) against the map: out_rec[n][9]
+ * (line: curr, a, b; plane: curr, n, d, 0, 0) and out_kind[n] (0 edge, 2 plane-norm, -1 none). */
+int lislam_map_associate(lislam_map* m, int32_t kind, const float* pts, int32_t n, int32_t stride, const double* x,
+                         double* out_rec, int32_t* out_kind);
+/* Cost, J^T J (upper, 21) and J^T r (6) = 28 doubles of n records (kinds 0 edge / 1 plane /
+ * 2 plane-norm, -1 skipped) under HuberLoss(0.1) at x (SURVEY.md §8(b) eval_normal_eq). */
+int lislam_normal_equations(lislam_ctx* ctx, const double* rec, const int32_t* kind, int32_t n, const double* x,
+                            double* out28);
+/* ceres::Solve (DENSE_QR, max_iterations) of n records at x (in/out, 7 doubles).
+ * summary[4] (nullable) = iterations, termination (0 no-convergence, 1 convergence, 2 failure),
+ * edge blocks, plane blocks. */
+int lislam_pose_solve(lislam_ctx* ctx, const double* rec, const int32_t* kind, int32_t n, double* x,
+                      int32_t max_iterations, int32_t* summary);
+/* pcl::VoxelGrid (leaf) of n points (x, y, z, intensity, stride 4): per-voxel centroid of all four
+ * fields, output ordered by voxel index; points of a voxel summed in input order.  out holds up
+ * to n points. */
+int lislam_voxel_grid(lislam_ctx* ctx, const float* pts, int32_t n, float leaf, float* out, int32_t* n_out);
+
+/* mapOptimization::mapOptimizationCallback ground-map stage (mapOptimization.cpp:99-479 without
+ * the ORB / keyframe-image logic): ground = GroundPointOut (sensor frame, stride 4), odom =
+ * q_wodom_curr, t_wodom_curr (7); state = q_wmap_wodom, t_wmap_wodom (7, in/out).  Empty map:
+ * Build with the transformed cloud.  Otherwise VoxelGrid(0.8), plane association, Ceres(10 it),
+ * transformUpdate on CONVERGENCE, Add_Points(downsample) at the keyframe pose.
+ * out_pose = q_w_curr, t_w_curr; summary[3] = planes, iterations, termination (-1: built). */
+int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const double* odom, double* state,
+                       double* out_pose, int32_t* summary);
+/* laserMapping::process optimization (laserMapping.cpp:620-850) against a corner map and a surf
+ * map: the downsampled current corner / surf clouds (stride 4), pose x (in/out), two outer
+ * passes of association + Ceres(4 it).  stats[4] = corner / surf blocks of each pass. */
+int lislam_laser_mapping(lislam_map* corner_map, lislam_map* surf_map, const float* corner, int32_t n_corner,
+                         const float* surf, int32_t n_surf, double* x, int32_t* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,18 +11,11 @@
 #include <vector>
 
 #include "../../include/lislam.h"
+#include "lislam_ctx.hpp"
 #include "lislam_internal.hpp"
 
 using namespace lislam;
 
-struct lislam_ctx {
-  lislam_config cfg;
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  std::string err;
-  lislam_batch* single = nullptr;  // 2-scan batch behind lislam_scan_registration / odom_step
-};
 
 struct lislam_batch {
   lislam_ctx* ctx = nullptr;
@@ -132,6 +125,10 @@ int lislam_ctx_destroy(lislam_ctx* c) {
   if (!c) return LISLAM_OK;
   hipSetDevice(c->device);
   if (c->single) lislam_batch_destroy(c->single);
+  if (c->map_scratch) {
+    (void)hipStreamSynchronize(c->stream);
+    lislam_free_map_scratch(c->map_scratch);
+  }
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return LISLAM_OK;

@@ -1,0 +1,1413 @@
+// lislam scan-to-map stages on gfx950 (a19-a21 of SURVEY.md §8(a)): a device-resident point map
+// with the semantics of the vendored ikd-Tree (src/ikd-Tree/ikd_Tree.cpp), exact k-NN, the 5-NN
+// line / plane fits of laserMapping / mapOptimization, the PCL VoxelGrid of whole clouds, and the
+// multi-workgroup Ceres-semantics pose solve.
+//
+// Map layout in HBM.  The ikd-Tree is a pointer-chasing balanced kd-tree; its results (which
+// points a box search returns, which k points are nearest) do not depend on its layout, so the
+// map is stored the way a wide GPU reads best:
+//   pts   float4 [n]  (x, y, z, id bits), sorted by hash-grid cell (CSR), one 16-B load per point
+//   hkey  u64 [hcap]  open-addressing table of occupied cells (21-bit biased ix, iy, iz)
+//   hval  int2 [hcap] (begin, count) of the cell's points in pts
+// Build = cell keys -> radix sort (rocPRIM via hipCUB) -> gather -> run-length cells into the
+// table.  Add_Points rewrites the point array (live points + entering inputs) and rebuilds the
+// table (one sort of the map per call).
+//
+// Search (k_knn).  Sixteen lanes per query (4 queries per wavefront).  The lanes walk the cells of
+// the 3x3x3 block around the query's cell, then of ever larger shells; each lane keeps a sorted
+// k-best list in registers, the group merges the lists with xor-shuffle lexicographic minima of
+// (float squared distance, id).  A shell walk stops when k points are closer than the distance
+// from the query to the faces of the walked block (every unvisited point is farther: the cell
+// index floor(p / cell) is monotone in p) or when the block covers max_dist.  The result is the
+// exact (distance, id)-ordered k-NN, i.e. ikd's Nearest_Search with ties broken by id.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "lislam_ctx.hpp"
+#include "lislam_device.hpp"
+#include "lislam_lm.hpp"
+
+namespace lislam {
+namespace mapk {
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr int kG = 16;          // lanes per query in k_knn
+constexpr int kMaxShell = 24;   // beyond this the search scans the whole map (unbounded max_dist only)
+constexpr float kInf = __builtin_huge_valf();
+
+__host__ __device__ __forceinline__ uint64_t pack_cell(int ix, int iy, int iz) {
+  return ((uint64_t)(uint32_t)((ix + (1 << 20)) & 0x1fffff) << 42) |
+         ((uint64_t)(uint32_t)((iy + (1 << 20)) & 0x1fffff) << 21) | (uint64_t)(uint32_t)((iz + (1 << 20)) & 0x1fffff);
+}
+__device__ __forceinline__ uint32_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+__device__ __forceinline__ int cell_of(float v, float inv) { return (int)floorf(v * inv); }
+
+// ikd_Tree.cpp:2224-2235, left-to-right float sum (no contraction: -ffp-contract=off)
+__device__ __forceinline__ float calc_dist(float ax, float ay, float az, float bx, float by, float bz) {
+  return (ax - bx) * (ax - bx) + (ay - by) * (ay - by) + (az - bz) * (az - bz);
+}
+
+struct MapView {
+  const float4* pts;
+  const uint64_t* hkey;
+  const int2* hval;
+  uint32_t hmask;
+  float cell, inv_cell;
+  int n;
+};
+
+__device__ __forceinline__ int2 cell_lookup(const MapView& m, uint64_t key) {
+  uint32_t h = mix64(key) & m.hmask;
+  while (true) {
+    const uint64_t k = m.hkey[h];
+    if (k == key) return m.hval[h];
+    if (k == kEmptyKey) return make_int2(0, 0);
+    h = (h + 1) & m.hmask;
+  }
+}
+
+// ------------------------------------------------------------------ build
+__global__ void k_cell_keys(const float4* pts, int n, float inv, uint64_t* keys, int* idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[i];
+  keys[i] = pack_cell(cell_of(p.x, inv), cell_of(p.y, inv), cell_of(p.z, inv));
+  idx[i] = i;
+}
+
+__global__ void k_gather(const float4* src, const int* perm, int n, float4* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
+}
+
+__global__ void k_count_runs(const uint64_t* keys, int n, int* count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool start = i < n && (i == 0 || keys[i] != keys[i - 1]);
+  const uint64_t b = __ballot(start);
+  if (lane_id() == 0 && b) atomicAdd(count, __popcll(b));
+}
+
+__global__ void k_insert_runs(const uint64_t* keys, int n, uint64_t* hkey, int2* hval, uint32_t mask) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (i > 0 && keys[i] == keys[i - 1])) return;
+  const uint64_t key = keys[i];
+  int e = i + 1;
+  while (e < n && keys[e] == key) e++;
+  uint32_t h = mix64(key) & mask;
+  while (true) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)kEmptyKey,
+                                              (unsigned long long)key);
+    if (prev == kEmptyKey) break;
+    h = (h + 1) & mask;
+  }
+  hval[h] = make_int2(i, e - i);
+}
+
+// points (stride floats) -> float4 (x, y, z, id = id0 + i)
+__global__ void k_pack_points(const float* src, int n, int stride, int id0, float4* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* p = src + (size_t)i * stride;
+  dst[i] = make_float4(p[0], p[1], p[2], __int_as_float(id0 + i));
+}
+
+// ------------------------------------------------------------------ k-NN
+template <int K>
+struct KBest {
+  float d[K];
+  int id[K];
+  int ix[K];
+};
+
+__device__ __forceinline__ bool lex_less(float d1, int i1, float d2, int i2) {
+  return d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+template <int K>
+__device__ __forceinline__ void kb_clear(KBest<K>& b) {
+#pragma unroll
+  for (int j = 0; j < K; j++) { b.d[j] = kInf; b.id[j] = 0x7fffffff; b.ix[j] = -1; }
+}
+
+template <int K>
+__device__ __forceinline__ void kb_insert(KBest<K>& b, float d, int id, int ix) {
+  if (!lex_less(d, id, b.d[K - 1], b.id[K - 1])) return;
+  bool placed = false;
+#pragma unroll
+  for (int j = K - 1; j >= 0; j--) {
+    if (!placed) {
+      if (j > 0 && lex_less(d, id, b.d[j - 1], b.id[j - 1])) {
+        b.d[j] = b.d[j - 1]; b.id[j] = b.id[j - 1]; b.ix[j] = b.ix[j - 1];
+      } else {
+        b.d[j] = d; b.id[j] = id; b.ix[j] = ix;
+        placed = true;
+      }
+    }
+  }
+}
+
+// Merge the k-best lists of the 16 lanes of each group: afterwards every lane of the group
+// returns the merged list in `out`; the group leader keeps it in b, the others are cleared.
+template <int K>
+__device__ __forceinline__ void group_merge(KBest<K>& b, KBest<K>& out) {
+#pragma unroll
+  for (int r = 0; r < K; r++) {
+    float md = b.d[0];
+    int mi = b.id[0];
+#pragma unroll
+    for (int o = 1; o < kG; o <<= 1) {
+      const float od = __shfl_xor(md, o, kG);
+      const int oi = __shfl_xor(mi, o, kG);
+      if (lex_less(od, oi, md, mi)) { md = od; mi = oi; }
+    }
+    const bool own = b.d[0] == md && b.id[0] == mi && md != kInf;
+    int ox = own ? b.ix[0] : 0;
+#pragma unroll
+    for (int o = 1; o < kG; o <<= 1) ox += __shfl_xor(ox, o, kG);
+    out.d[r] = md; out.id[r] = mi; out.ix[r] = md == kInf ? -1 : ox;
+    if (own) {
+#pragma unroll
+      for (int j = 0; j < K - 1; j++) { b.d[j] = b.d[j + 1]; b.id[j] = b.id[j + 1]; b.ix[j] = b.ix[j + 1]; }
+      b.d[K - 1] = kInf; b.id[K - 1] = 0x7fffffff; b.ix[K - 1] = -1;
+    }
+  }
+  if ((threadIdx.x & (kG - 1)) == 0) b = out;
+  else kb_clear(b);
+}
+
+// pointAssociateToMap (laserMapping.cpp:138-147) / mapOptimization.cpp:385: q * p + t in
+// double, stored as float.
+__device__ __forceinline__ float4 to_world(const double* x, float px, float py, float pz) {
+  const DQ q{x[0], x[1], x[2], x[3]};
+  const D3 w = qrot(q, D3{(double)px, (double)py, (double)pz});
+  return make_float4((float)(w.x + x[4]), (float)(w.y + x[5]), (float)(w.z + x[6]), 0.f);
+}
+
+// distance from q to the faces of the block of cells [c - s, c + s] (per axis), minus the
+// rounding of the face positions; 0 if negative
+__device__ __forceinline__ double block_gap(double q, int c, int s, double cell) {
+  const double lo = (double)(c - s) * cell, hi = (double)(c + s + 1) * cell;
+  const double tol = 1e-6 * (fabs(q) + fabs(lo) + fabs(hi)) + 1e-9;
+  return fmax(0.0, fmin(q - lo, hi - q) - tol);
+}
+
+// queries: n points of `stride` floats (optionally counted on the device: *qcount); pose
+// (device, nullable): queries are sensor-frame points mapped by pointAssociateToMap first.
+template <int K>
+__global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, int stride, const int* qcount, int nq,
+                                             const double* pose, int k, float max_d2, float4* out_pts, float* out_d2,
+                                             int* out_found) {
+  const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / kG;
+  const int gl = threadIdx.x & (kG - 1);
+  const int n = qcount ? min(*qcount, nq) : nq;
+  if (qi >= n) return;  // whole groups leave together
+  const float* qp = queries + (size_t)qi * stride;
+  float4 q = make_float4(qp[0], qp[1], qp[2], 0.f);
+  if (pose) q = to_world(pose, q.x, q.y, q.z);
+  const int cx = cell_of(q.x, m.inv_cell), cy = cell_of(q.y, m.inv_cell), cz = cell_of(q.z, m.inv_cell);
+  KBest<K> b, mg;
+  kb_clear(b);
+  const double maxd = sqrt((double)max_d2);
+  for (int s = 1;; s++) {
+    const int side = 2 * s + 1, plane = side * side, total = plane * side;
+    for (int j = gl; j < total; j += kG) {
+      const int dz = j / plane - s, rem = j % plane, dy = rem / side - s, dx = rem % side - s;
+      if (s > 1 && max(abs(dx), max(abs(dy), abs(dz))) < s) continue;  // inner block already walked
+      const int2 r = cell_lookup(m, pack_cell(cx + dx, cy + dy, cz + dz));
+      for (int p = r.x; p < r.x + r.y; p++) {
+        const float4 v = m.pts[p];
+        const float d = calc_dist(q.x, q.y, q.z, v.x, v.y, v.z);
+        if (d <= max_d2) kb_insert(b, d, __float_as_int(v.w), p);
+      }
+    }
+    group_merge(b, mg);
+    const double gap = fmin(block_gap(q.x, cx, s, m.cell), fmin(block_gap(q.y, cy, s, m.cell), block_gap(q.z, cz, s, m.cell)));
+    if (gap >= maxd * (1.0 + 1e-6)) break;                                  // every point within max_dist seen
+    if (mg.d[k - 1] != kInf && (double)mg.d[k - 1] < gap * gap * (1.0 - 1e-6)) break;  // none closer outside
+    if (s >= kMaxShell) {                                                   // far from the map: scan it all
+      kb_clear(b);
+      for (int p = gl; p < m.n; p += kG) {
+        const float4 v = m.pts[p];
+        const float d = calc_dist(q.x, q.y, q.z, v.x, v.y, v.z);
+        if (d <= max_d2) kb_insert(b, d, __float_as_int(v.w), p);
+      }
+      group_merge(b, mg);
+      break;
+    }
+  }
+  if (gl != 0) return;
+  int found = 0;
+  for (int r = 0; r < k; r++) {
+    const bool ok = mg.d[r] != kInf;
+    found += ok;
+    if (out_pts) out_pts[(size_t)qi * k + r] = ok ? m.pts[mg.ix[r]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (out_d2) out_d2[(size_t)qi * k + r] = mg.d[r];
+  }
+  if (out_found) out_found[qi] = found;
+}
+
+// ------------------------------------------------------------------ fits (fp64, one thread per query)
+// Eigen::ColPivHouseholderQR<Matrix<double,5,3>>::compute + solve(-1): column-pivoted
+// Householder QR with norm downdating, rank from the threshold, R^-1 Q^T b, un-permuted.
+__device__ __forceinline__ void colpiv_qr_solve_5x3(double (&A)[5][3], double* x) {
+  const int R = 5, C = 3;
+  double upd[3], dir[3], tau[3];
+  int trans[3];
+  double maxn = 0;
+  for (int j = 0; j < C; j++) {
+    double s = 0;
+    for (int i = 0; i < R; i++) s += A[i][j] * A[i][j];
+    upd[j] = dir[j] = sqrt(s);
+    maxn = fmax(maxn, upd[j]);
+  }
+  const double eps = 2.220446049250313e-16;
+  const double thr = (maxn * eps) * (maxn * eps) / R;
+  const double downdate = sqrt(eps);
+  int nonzero = C;
+  for (int k = 0; k < C; k++) {
+    int big = k;
+    for (int j = k + 1; j < C; j++)
+      if (upd[j] > upd[big]) big = j;
+    const double bsq = upd[big] * upd[big];
+    if (nonzero == C && bsq < thr * (R - k)) nonzero = k;
+    trans[k] = big;
+    if (k != big) {
+      for (int i = 0; i < R; i++) { const double t = A[i][k]; A[i][k] = A[i][big]; A[i][big] = t; }
+      double t = upd[k]; upd[k] = upd[big]; upd[big] = t;
+      t = dir[k]; dir[k] = dir[big]; dir[big] = t;
+    }
+    const double c0 = A[k][k];
+    double tail = 0;
+    for (int i = k + 1; i < R; i++) tail += A[i][k] * A[i][k];
+    double beta;
+    if (tail <= 2.2250738585072014e-308) {
+      tau[k] = 0;
+      beta = c0;
+      for (int i = k + 1; i < R; i++) A[i][k] = 0;
+    } else {
+      beta = sqrt(c0 * c0 + tail);
+      if (c0 >= 0) beta = -beta;
+      for (int i = k + 1; i < R; i++) A[i][k] = A[i][k] / (c0 - beta);
+      tau[k] = (beta - c0) / beta;
+    }
+    A[k][k] = beta;
+    for (int j = k + 1; j < C; j++) {
+      if (tau[k] == 0) continue;
+      double t = A[k][j];
+      for (int i = k + 1; i < R; i++) t += A[i][k] * A[i][j];
+      A[k][j] -= tau[k] * t;
+      for (int i = k + 1; i < R; i++) A[i][j] -= tau[k] * A[i][k] * t;
+    }
+    for (int j = k + 1; j < C; j++) {
+      if (upd[j] == 0) continue;
+      double t = fabs(A[k][j]) / upd[j];
+      t = (1 + t) * (1 - t);
+      t = t < 0 ? 0 : t;
+      const double t2 = t * (upd[j] / dir[j]) * (upd[j] / dir[j]);
+      if (t2 <= downdate) {
+        double s = 0;
+        for (int i = k + 1; i < R; i++) s += A[i][j] * A[i][j];
+        dir[j] = upd[j] = sqrt(s);
+      } else {
+        upd[j] *= sqrt(t);
+      }
+    }
+  }
+  int perm[3] = {0, 1, 2};
+  for (int k = 0; k < C; k++) { const int t = perm[k]; perm[k] = perm[trans[k]]; perm[trans[k]] = t; }
+  double c[5] = {-1, -1, -1, -1, -1};
+  for (int k = 0; k < nonzero; k++) {
+    if (tau[k] == 0) continue;
+    double t = c[k];
+    for (int i = k + 1; i < R; i++) t += A[i][k] * c[i];
+    c[k] -= tau[k] * t;
+    for (int i = k + 1; i < R; i++) c[i] -= tau[k] * A[i][k] * t;
+  }
+  for (int i = nonzero - 1; i >= 0; i--) {
+    c[i] /= A[i][i];
+    for (int r = 0; r < i; r++) c[r] -= A[r][i] * c[i];
+  }
+  for (int i = 0; i < C; i++) x[perm[i]] = i < nonzero ? c[i] : 0.0;
+}
+
+// laserMapping.cpp:756-788, mapOptimization.cpp:398-420
+__device__ __forceinline__ bool plane_fit(const float4* nb, double* n, double* d) {
+  double A[5][3];
+  for (int j = 0; j < 5; j++) { A[j][0] = nb[j].x; A[j][1] = nb[j].y; A[j][2] = nb[j].z; }
+  colpiv_qr_solve_5x3(A, n);
+  const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+  *d = 1 / nn;
+  if (nn > 0) { n[0] /= nn; n[1] /= nn; n[2] /= nn; }
+  for (int j = 0; j < 5; j++)
+    if (fabs(n[0] * nb[j].x + n[1] * nb[j].y + n[2] * nb[j].z + *d) > 0.2) return false;
+  return true;
+}
+
+// symmetric 3x3 eigen-decomposition, cyclic Jacobi; ascending eigenvalues, V[:, k] vectors
+__device__ __forceinline__ void sym_eig3(double (&a)[3][3], double* w, double (&V)[3][3]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) V[i][j] = i == j ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 32; sweep++) {
+    const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    if (off == 0.0) break;
+    for (int p = 0; p < 2; p++)
+      for (int q = p + 1; q < 3; q++) {
+        if (a[p][q] == 0.0) continue;
+        const double theta = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 3; k++) {
+          const double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - s * akq;
+          a[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 3; k++) {
+          const double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - s * aqk;
+          a[q][k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < 3; k++) {
+          const double vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = c * vkp - s * vkq;
+          V[k][q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  int ord[3] = {0, 1, 2};
+  for (int i = 0; i < 3; i++)
+    for (int j = i + 1; j < 3; j++)
+      if (a[ord[j]][ord[j]] < a[ord[i]][ord[i]]) { const int t = ord[i]; ord[i] = ord[j]; ord[j] = t; }
+  double W[3][3];
+  for (int k = 0; k < 3; k++) {
+    w[k] = a[ord[k]][ord[k]];
+    for (int i = 0; i < 3; i++) W[i][k] = V[i][ord[k]];
+  }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) V[i][j] = W[i][j];
+}
+
+// laserMapping.cpp:681-723
+__device__ __forceinline__ bool line_fit(const float4* nb, double* pa, double* pb) {
+  double c[3] = {0, 0, 0};
+  for (int j = 0; j < 5; j++) { c[0] = c[0] + nb[j].x; c[1] = c[1] + nb[j].y; c[2] = c[2] + nb[j].z; }
+  for (int k = 0; k < 3; k++) c[k] = c[k] / 5.0;
+  double M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+  for (int j = 0; j < 5; j++) {
+    const double z[3] = {nb[j].x - c[0], nb[j].y - c[1], nb[j].z - c[2]};
+    for (int r = 0; r < 3; r++)
+      for (int s = 0; s < 3; s++) M[r][s] = M[r][s] + z[r] * z[s];
+  }
+  double w[3], V[3][3];
+  sym_eig3(M, w, V);
+  if (!(w[2] > 3 * w[1])) return false;
+  for (int k = 0; k < 3; k++) {
+    pa[k] = 0.1 * V[k][2] + c[k];
+    pb[k] = -0.1 * V[k][2] + c[k];
+  }
+  return true;
+}
+
+// One thread per query: the 5 neighbours from k_knn -> residual-block record + kind.
+__global__ void k_fit(int match, const float* queries, int stride, const int* qcount, int nq, const float4* nb,
+                      const float* d2, const int* found, double* rec, int* kind) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = qcount ? min(*qcount, nq) : nq;
+  if (i >= n) return;
+  double r[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int kd = -1;
+  if (found[i] == 5 && d2[(size_t)i * 5 + 4] < 1.0f) {  // pointSearchSqDis[4] < 1.0
+    const float* p = queries + (size_t)i * stride;
+    r[0] = p[0]; r[1] = p[1]; r[2] = p[2];
+    float4 v[5];
+    for (int j = 0; j < 5; j++) v[j] = nb[(size_t)i * 5 + j];
+    if (match == 0) {
+      if (line_fit(v, r + 3, r + 6)) kd = 0;
+    } else {
+      double nn[3], d;
+      if (plane_fit(v, nn, &d)) {
+        r[3] = nn[0]; r[4] = nn[1]; r[5] = nn[2]; r[6] = d;
+        kd = 2;
+      }
+    }
+  }
+  for (int e = 0; e < 9; e++) rec[(size_t)i * 9 + e] = r[e];
+  kind[i] = kd;
+}
+
+// ------------------------------------------------------------------ Add_Points with downsampling
+// Sequential semantics of ikd_Tree.cpp:594-640 per box B (inputs in order n1..nj, stored points
+// S0): after the first input B holds exactly one point, and input n_i replaces the holder m iff
+// dist(n_i, mid) <= dist(m, mid) (a stored point wins only with a strictly smaller distance).
+// So B ends with the lexicographic minimum over [S0 (first strict minimum, ascending id), n1..nj]
+// of (dist, later-wins): the inputs' winner is (min dist, max index); it enters iff its distance
+// is <= that of S0's best; every other stored point of B leaves (all of them if the input wins).
+struct DsArgs {
+  MapView m;
+  const float4* in;  // [nin] inputs (x, y, z, id bits)
+  int nin;
+  float L;
+  uint64_t* bkey;   // [bcap]
+  unsigned long long* bwin;  // [bcap] (dist bits << 32) | ~index
+  uint32_t bmask;
+  int* boxes;       // [nin] claimed slots
+  int* nbox;
+  uint8_t* dead;    // [map n]
+  uint8_t* enter;   // [nin]
+};
+
+__device__ __forceinline__ void ds_box(float L, const float4& p, float* bmin, float* bmax, float* mid) {
+  const float c[3] = {p.x, p.y, p.z};
+  for (int k = 0; k < 3; k++) {
+    bmin[k] = floorf(c[k] / L) * L;
+    bmax[k] = bmin[k] + L;
+    mid[k] = (float)(bmin[k] + (bmax[k] - bmin[k]) / 2.0);
+  }
+}
+
+__global__ void k_ds_claim(DsArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nin) return;
+  const float4 p = a.in[i];
+  float bmin[3], bmax[3], mid[3];
+  ds_box(a.L, p, bmin, bmax, mid);
+  const uint64_t key = pack_cell((int)floorf(p.x / a.L), (int)floorf(p.y / a.L), (int)floorf(p.z / a.L));
+  const float d = calc_dist(p.x, p.y, p.z, mid[0], mid[1], mid[2]);
+  uint32_t h = mix64(key) & a.bmask;
+  while (true) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&a.bkey[h], (unsigned long long)kEmptyKey,
+                                              (unsigned long long)key);
+    if (prev == kEmptyKey) { a.boxes[atomicAdd(a.nbox, 1)] = (int)h; break; }
+    if (prev == key) break;
+    h = (h + 1) & a.bmask;
+  }
+  atomicMin(&a.bwin[h], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)i));
+}
+
+__global__ void k_ds_resolve(DsArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= *a.nbox) return;
+  const unsigned long long wv = a.bwin[a.boxes[t]];
+  const int w = (int)(0xffffffffu - (uint32_t)(wv & 0xffffffffu));
+  const float dw = __uint_as_float((uint32_t)(wv >> 32));
+  const float4 pw = a.in[w];
+  float bmin[3], bmax[3], mid[3];
+  ds_box(a.L, pw, bmin, bmax, mid);
+  const MapView& m = a.m;
+  // Search_by_range: cells [cell(bmin), cell(bmax)] hold every point with bmin <= p < bmax
+  // (floor(p / cell) is monotone in p)
+  const int x0 = cell_of(bmin[0], m.inv_cell), x1 = cell_of(bmax[0], m.inv_cell);
+  const int y0 = cell_of(bmin[1], m.inv_cell), y1 = cell_of(bmax[1], m.inv_cell);
+  const int z0 = cell_of(bmin[2], m.inv_cell), z1 = cell_of(bmax[2], m.inv_cell);
+  int ns = 0, best = -1, best_id = 0x7fffffff;
+  float bd = kInf;
+  for (int pass = 0; pass < 2; pass++) {
+    for (int ix = x0; ix <= x1; ix++)
+      for (int iy = y0; iy <= y1; iy++)
+        for (int iz = z0; iz <= z1; iz++) {
+          if (m.n == 0) continue;
+          const int2 r = cell_lookup(m, pack_cell(ix, iy, iz));
+          for (int p = r.x; p < r.x + r.y; p++) {
+            const float4 v = m.pts[p];
+            if (!(bmin[0] <= v.x && bmax[0] > v.x && bmin[1] <= v.y && bmax[1] > v.y && bmin[2] <= v.z && bmax[2] > v.z))
+              continue;
+            if (pass == 0) {
+              ns++;
+              const float d = calc_dist(v.x, v.y, v.z, mid[0], mid[1], mid[2]);
+              const int id = __float_as_int(v.w);
+              if (d < bd || (d == bd && id < best_id)) { bd = d; best = p; best_id = id; }
+            } else {
+              const bool input_wins = dw <= bd;
+              if (input_wins || (ns > 1 && p != best)) a.dead[p] = 1;
+            }
+          }
+        }
+    if (ns == 0) break;
+  }
+  if (ns == 0 || dw <= bd) a.enter[w] = 1;
+}
+
+__global__ void k_flags_inv(const uint8_t* dead, int n, uint8_t* live) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) live[i] = dead[i] ? 0 : 1;
+}
+
+// ------------------------------------------------------------------ PCL VoxelGrid of a whole cloud
+// pcl::VoxelGrid<PointT>::applyFilter (PCL 1.10): bounds, ijk = floor(p / leaf) - min_b, index
+// i + j*div0 + k*div0*div1, (index, point) pairs sorted by index (stable: points of a voxel in
+// input order), one centroid of all four fields per voxel in index order.  A leaf too small for
+// 32-bit indices returns the input (PCL warns and copies).
+struct VgArgs {
+  const float4* in;
+  int n;
+  float inv;
+  float* bounds;     // [6] min xyz, max xyz (device)
+  uint32_t* keys;    // [n]
+  int* idx;          // [n]
+  int* overflow;     // [1]
+};
+
+__device__ __forceinline__ unsigned ord_f(float f) {  // order-preserving float -> uint
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f(unsigned u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+
+__global__ __launch_bounds__(1024) void k_vg_bounds(VgArgs a) {
+  __shared__ unsigned smn[3][16], smx[3][16];
+  unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+  for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+    const float4 p = a.in[i];
+    const unsigned c[3] = {ord_f(p.x), ord_f(p.y), ord_f(p.z)};
+    for (int k = 0; k < 3; k++) { mn[k] = min(mn[k], c[k]); mx[k] = max(mx[k], c[k]); }
+  }
+  for (int o = 32; o > 0; o >>= 1)
+    for (int k = 0; k < 3; k++) { mn[k] = min(mn[k], (unsigned)__shfl_xor((int)mn[k], o)); mx[k] = max(mx[k], (unsigned)__shfl_xor((int)mx[k], o)); }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 3; k++) { smn[k][w] = mn[k]; smx[k][w] = mx[k]; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) / 64;
+    for (int k = 0; k < 3; k++) {
+      unsigned a0 = smn[k][0], a1 = smx[k][0];
+      for (int j = 1; j < nw; j++) { a0 = min(a0, smn[k][j]); a1 = max(a1, smx[k][j]); }
+      a.bounds[k] = unord_f(a0);
+      a.bounds[3 + k] = unord_f(a1);
+    }
+  }
+}
+
+__global__ void k_vg_keys(VgArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const float inv = a.inv;
+  const float mn[3] = {a.bounds[0], a.bounds[1], a.bounds[2]}, mx[3] = {a.bounds[3], a.bounds[4], a.bounds[5]};
+  const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1, dy = (int64_t)((mx[1] - mn[1]) * inv) + 1,
+                dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+  if (dx * dy * dz > (int64_t)0x7fffffff) {
+    if (i == 0) *a.overflow = 1;
+    return;
+  }
+  if (i >= a.n) return;
+  int min_b[3], div_b[3];
+  for (int k = 0; k < 3; k++) {
+    min_b[k] = (int)floorf(mn[k] * inv);
+    div_b[k] = (int)floorf(mx[k] * inv) - min_b[k] + 1;
+  }
+  const int mul1 = div_b[0], mul2 = div_b[0] * div_b[1];
+  const float4 p = a.in[i];
+  const int i0 = (int)(floorf(p.x * inv) - (float)min_b[0]);
+  const int i1 = (int)(floorf(p.y * inv) - (float)min_b[1]);
+  const int i2 = (int)(floorf(p.z * inv) - (float)min_b[2]);
+  a.keys[i] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+  a.idx[i] = i;
+}
+
+__global__ void k_vg_runs(const uint32_t* skeys, int n, const int* overflow, int* flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flag[i] = (*overflow == 0) && (i == 0 || skeys[i] != skeys[i - 1]) ? 1 : 0;
+}
+
+__global__ void k_vg_centroids(const float4* in, const uint32_t* skeys, const int* sidx, const int* pos, const int* flag,
+                               int n, const int* overflow, float4* out, int* n_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (*overflow) {  // leaf too small: output = input
+    if (i < n) out[i] = in[i];
+    if (i == 0) *n_out = n;
+    return;
+  }
+  if (i == 0) *n_out = n > 0 ? pos[n - 1] + flag[n - 1] : 0;
+  if (i >= n || !flag[i]) return;
+  float4 c = in[sidx[i]];
+  int e = i + 1;
+  for (; e < n && skeys[e] == skeys[i]; e++) {
+    const float4 p = in[sidx[e]];
+    c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
+  }
+  const float cnt = (float)(e - i);
+  c.x /= cnt; c.y /= cnt; c.z /= cnt; c.w /= cnt;
+  out[pos[i]] = c;
+}
+
+// ------------------------------------------------------------------ multi-workgroup pose solve
+constexpr int kEvalThreads = 256;
+constexpr int kMaxParts = 1024;
+constexpr int kPart = kAcc + 2;  // acc + edge / plane block counts
+
+struct LmDev {
+  LM s;
+  double x0[7], xe[7];
+  int flag, phase, nedge, nplane;
+};
+
+__global__ void k_lm_init(LmDev* st, const double* x0) {
+  if (threadIdx.x != 0) return;
+  for (int e = 0; e < 7; e++) { st->x0[e] = x0[e]; st->xe[e] = x0[e]; }
+  st->flag = 1;
+  st->phase = 0;
+  st->nedge = st->nplane = 0;
+  st->s.it = 0;
+  st->s.term = 1;
+}
+
+__global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, const int* kind, const int* ncount, int n,
+                                                          LmDev* st, double* partial) {
+  if (!st->flag) return;
+  __shared__ double red[kEvalThreads / 16][kPart];
+  const int nn = ncount ? min(*ncount, n) : n;
+  double acc[kPart];
+#pragma unroll
+  for (int e = 0; e < kPart; e++) acc[e] = 0;
+  const DQ q{st->xe[0], st->xe[1], st->xe[2], st->xe[3]};
+  const D3 t{st->xe[4], st->xe[5], st->xe[6]};
+  for (int i = blockIdx.x * kEvalThreads + threadIdx.x; i < nn; i += gridDim.x * kEvalThreads) {
+    const int kd = kind[i];
+    if (kd < 0) continue;
+    block_accum(kd, rec + (size_t)i * 9, q, t, acc);
+    acc[kAcc + (kd == 0 ? 0 : 1)] += 1.0;
+  }
+  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
+#pragma unroll
+  for (int e = 0; e < kPart; e++) {
+    const double v = row_sum(acc[e]);
+    if ((lane & 15) == 0) red[row][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kPart) {
+    double v = 0;
+    for (int w = 0; w < kEvalThreads / 16; w++) v += red[w][threadIdx.x];
+    partial[(size_t)blockIdx.x * kPart + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_lm_step(LmDev* st, const double* partial, int nparts, int max_it) {
+  if (!st->flag) return;
+  __shared__ double acc[kPart];
+  if (threadIdx.x < kPart) {
+    double v = 0;
+    for (int p = 0; p < nparts; p++) v += partial[(size_t)p * kPart + threadIdx.x];
+    acc[threadIdx.x] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  LM& s = st->s;
+  bool cont;
+  if (st->phase == 0) {
+    st->nedge = (int)acc[kAcc];
+    st->nplane = (int)acc[kAcc + 1];
+    st->phase = 1;
+    if (st->nedge + st->nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
+      for (int e = 0; e < 7; e++) s.x[e] = st->x0[e];
+      s.it = 0;
+      s.term = 1;
+      cont = false;
+    } else {
+      cont = lm_start(s, st->x0, acc, max_it);
+    }
+  } else {
+    cont = lm_next(s, acc, max_it);
+  }
+  st->flag = cont;
+  if (cont)
+    for (int e = 0; e < 7; e++) st->xe[e] = s.xc[e];
+}
+
+// x_out = solved pose; summary = iterations, termination, edge blocks, plane blocks
+__global__ void k_lm_finish(const LmDev* st, double* x_out, int* summary) {
+  if (threadIdx.x != 0) return;
+  for (int e = 0; e < 7; e++) x_out[e] = st->s.x[e];
+  if (summary) { summary[0] = st->s.it; summary[1] = st->s.term; summary[2] = st->nedge; summary[3] = st->nplane; }
+}
+
+// mapOptimization.cpp:730-746: transformAssociateToMap (mode 0) / transformUpdate on
+// CONVERGENCE + keyframe pose selection (mode 1).  st7 = q_wmap_wodom, t_wmap_wodom; odom =
+// q_wodom_curr, t_wodom_curr; x = q_w_curr, t_w_curr.
+__global__ void k_mapopt_pose(int mode, double* st7, const double* odom, double* x, const LmDev* lm, double* key_pose) {
+  if (threadIdx.x != 0) return;
+  const DQ qm{st7[0], st7[1], st7[2], st7[3]};
+  const DQ qo{odom[0], odom[1], odom[2], odom[3]};
+  const D3 to{odom[4], odom[5], odom[6]};
+  if (mode == 0) {
+    const DQ qw = qmul(qm, qo);
+    const D3 tw = qrot(qm, to) + D3{st7[4], st7[5], st7[6]};
+    x[0] = qw.x; x[1] = qw.y; x[2] = qw.z; x[3] = qw.w; x[4] = tw.x; x[5] = tw.y; x[6] = tw.z;
+    return;
+  }
+  const bool conv = lm->s.term == 1;
+  const double* xs = lm->s.x;
+  if (conv) {
+    const DQ nq = qmul(DQ{xs[0], xs[1], xs[2], xs[3]}, DQ{-odom[0], -odom[1], -odom[2], odom[3]});
+    st7[0] = nq.x; st7[1] = nq.y; st7[2] = nq.z; st7[3] = nq.w;
+    const D3 r = qrot(nq, to);
+    st7[4] = xs[4] - r.x; st7[5] = xs[5] - r.y; st7[6] = xs[6] - r.z;
+  }
+  for (int e = 0; e < 7; e++) key_pose[e] = conv ? xs[e] : x[e];
+  for (int e = 0; e < 7; e++) x[e] = xs[e];
+}
+
+// world points of a cloud at a device pose: pcl::transformPointCloud(cloud, T(q, t))
+__global__ void k_transform(const float* src, int stride, const int* ncount, int n, const double* pose, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nn = ncount ? min(*ncount, n) : n;
+  if (i >= nn) return;
+  const float* p = src + (size_t)i * stride;
+  const float4 w = to_world(pose, p[0], p[1], p[2]);
+  dst[(size_t)i * 4 + 0] = w.x; dst[(size_t)i * 4 + 1] = w.y; dst[(size_t)i * 4 + 2] = w.z; dst[(size_t)i * 4 + 3] = 0.f;
+}
+
+}  // namespace mapk
+}  // namespace lislam
+
+// ================================================================== host side
+using namespace lislam;
+using namespace lislam::mapk;
+
+namespace {
+
+int mfail(lislam_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define MCHK(ctx, x)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) return mfail(ctx, LISLAM_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+#define MRC(x)                    \
+  do {                            \
+    int rc_ = (x);                \
+    if (rc_ != LISLAM_OK) return rc_; \
+  } while (0)
+
+inline int blocks(int64_t n, int t = 256) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// Growable device buffer.
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DBuf() { if (p) (void)hipFree(p); }
+  hipError_t reserve(size_t b) {
+    if (b <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    const size_t nb = std::max<size_t>(b, 256) + b / 4;
+    hipError_t e = hipMalloc(&p, nb);
+    if (e == hipSuccess) bytes = nb;
+    return e;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+uint32_t pow2_at_least(uint64_t v) {
+  uint32_t c = 1024;
+  while (c < v) c <<= 1;
+  return c;
+}
+
+}  // namespace
+
+// Scratch shared by the stateless entry points of a context (voxel grid, solve, association).
+struct MapScratch {
+  DBuf sort_tmp, keys32a, keys32b, idxa, idxb, flag, pos, vin, vout, bounds, counters;
+  DBuf lm, partial, rec, kind, x, nb, d2, found, q, vox, qc, qs;
+};
+
+struct lislam_map {
+  lislam_ctx* ctx = nullptr;
+  float ds = 0.2f, cell = 0.2f;
+  int64_t n = 0;
+  int next_id = 0;
+  DBuf pts, tmp, keys, keys2, idx, idx2, sort_tmp, hkey, hval, counter, dead, live, enter, newp, bkey, bwin, boxes, sel;
+  uint32_t hcap = 0;
+  MapScratch sc;
+  MapView view() const {
+    MapView v;
+    v.pts = pts.as<float4>();
+    v.hkey = hkey.as<uint64_t>();
+    v.hval = hval.as<int2>();
+    v.hmask = hcap ? hcap - 1 : 0;
+    v.cell = cell;
+    v.inv_cell = 1.0f / cell;
+    v.n = (int)n;
+    return v;
+  }
+};
+
+namespace {
+
+hipStream_t stream_of(lislam_ctx* c) { return c->stream; }
+
+// Stable radix sort of (u64 key, int) pairs.
+int sort_pairs_u64(lislam_ctx* c, DBuf& tmp, const uint64_t* ki, uint64_t* ko, const int* vi, int* vo, int n) {
+  size_t tb = 0;
+  MCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ki, ko, vi, vo, n, 0, 64, stream_of(c)));
+  MCHK(c, tmp.reserve(tb));
+  MCHK(c, hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, ki, ko, vi, vo, n, 0, 64, stream_of(c)));
+  return LISLAM_OK;
+}
+int sort_pairs_u32(lislam_ctx* c, DBuf& tmp, const uint32_t* ki, uint32_t* ko, const int* vi, int* vo, int n) {
+  size_t tb = 0;
+  MCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ki, ko, vi, vo, n, 0, 32, stream_of(c)));
+  MCHK(c, tmp.reserve(tb));
+  MCHK(c, hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, ki, ko, vi, vo, n, 0, 32, stream_of(c)));
+  return LISLAM_OK;
+}
+
+// Rebuild the cell index of the n points in m->tmp (unsorted) into m->pts.
+int rebuild(lislam_map* m, int64_t n) {
+  lislam_ctx* c = m->ctx;
+  hipStream_t st = stream_of(c);
+  m->n = n;
+  MCHK(c, m->pts.reserve(std::max<int64_t>(n, 1) * sizeof(float4)));
+  if (n == 0) { m->hcap = 0; return LISLAM_OK; }
+  MCHK(c, m->keys.reserve(n * 8));
+  MCHK(c, m->keys2.reserve(n * 8));
+  MCHK(c, m->idx.reserve(n * 4));
+  MCHK(c, m->idx2.reserve(n * 4));
+  MCHK(c, m->counter.reserve(16));
+  const float inv = 1.0f / m->cell;
+  hipLaunchKernelGGL(k_cell_keys, dim3(blocks(n)), dim3(256), 0, st, m->tmp.as<float4>(), (int)n, inv,
+                     m->keys.as<uint64_t>(), m->idx.as<int>());
+  MRC(sort_pairs_u64(c, m->sort_tmp, m->keys.as<uint64_t>(), m->keys2.as<uint64_t>(), m->idx.as<int>(), m->idx2.as<int>(),
+                     (int)n));
+  hipLaunchKernelGGL(k_gather, dim3(blocks(n)), dim3(256), 0, st, m->tmp.as<float4>(), m->idx2.as<int>(), (int)n,
+                     m->pts.as<float4>());
+  MCHK(c, hipMemsetAsync(m->counter.p, 0, sizeof(int), st));
+  hipLaunchKernelGGL(k_count_runs, dim3(blocks(n)), dim3(256), 0, st, m->keys2.as<uint64_t>(), (int)n, m->counter.as<int>());
+  int ncell = 0;
+  MCHK(c, hipMemcpyAsync(&ncell, m->counter.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  m->hcap = pow2_at_least((uint64_t)ncell * 2);
+  MCHK(c, m->hkey.reserve((size_t)m->hcap * 8));
+  MCHK(c, m->hval.reserve((size_t)m->hcap * 8));
+  MCHK(c, hipMemsetAsync(m->hkey.p, 0xff, (size_t)m->hcap * 8, st));
+  hipLaunchKernelGGL(k_insert_runs, dim3(blocks(n)), dim3(256), 0, st, m->keys2.as<uint64_t>(), (int)n,
+                     m->hkey.as<uint64_t>(), m->hval.as<int2>(), m->hcap - 1);
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// points (host or device, stride floats) -> device float4 with ids id0.. in dst[off..]
+int upload_points(lislam_map* m, const float* pts, int64_t n, int stride, int id0, DBuf& dst, int64_t off) {
+  lislam_ctx* c = m->ctx;
+  hipStream_t st = stream_of(c);
+  if (n == 0) return LISLAM_OK;
+  MCHK(c, m->sc.vin.reserve((size_t)n * stride * 4));
+  MCHK(c, hipMemcpyAsync(m->sc.vin.p, pts, (size_t)n * stride * 4, hipMemcpyDefault, st));
+  hipLaunchKernelGGL(k_pack_points, dim3(blocks(n)), dim3(256), 0, st, m->sc.vin.as<float>(), (int)n, stride, id0,
+                     dst.as<float4>() + off);
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// Add n points already packed (float4 with ids) in m->newp.
+int add_packed(lislam_map* m, int64_t nin, bool downsample, int64_t* n_added) {
+  lislam_ctx* c = m->ctx;
+  hipStream_t st = stream_of(c);
+  const int64_t n0 = m->n;
+  if (!downsample) {
+    MCHK(c, m->tmp.reserve((n0 + nin) * sizeof(float4)));
+    if (n0) MCHK(c, hipMemcpyAsync(m->tmp.p, m->pts.p, n0 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    MCHK(c, hipMemcpyAsync(m->tmp.as<float4>() + n0, m->newp.p, nin * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    if (n_added) *n_added = nin;
+    return rebuild(m, n0 + nin);
+  }
+  const uint32_t bcap = pow2_at_least((uint64_t)nin * 2);
+  MCHK(c, m->bkey.reserve((size_t)bcap * 8));
+  MCHK(c, m->bwin.reserve((size_t)bcap * 8));
+  MCHK(c, m->boxes.reserve(nin * 4));
+  MCHK(c, m->dead.reserve(std::max<int64_t>(n0, 1)));
+  MCHK(c, m->enter.reserve(nin));
+  MCHK(c, m->counter.reserve(16));
+  MCHK(c, hipMemsetAsync(m->bkey.p, 0xff, (size_t)bcap * 8, st));
+  MCHK(c, hipMemsetAsync(m->bwin.p, 0xff, (size_t)bcap * 8, st));
+  MCHK(c, hipMemsetAsync(m->dead.p, 0, std::max<int64_t>(n0, 1), st));
+  MCHK(c, hipMemsetAsync(m->enter.p, 0, nin, st));
+  MCHK(c, hipMemsetAsync(m->counter.p, 0, 16, st));
+  DsArgs a;
+  a.m = m->view();
+  a.in = m->newp.as<float4>();
+  a.nin = (int)nin;
+  a.L = m->ds;
+  a.bkey = m->bkey.as<uint64_t>();
+  a.bwin = m->bwin.as<unsigned long long>();
+  a.bmask = bcap - 1;
+  a.boxes = m->boxes.as<int>();
+  a.nbox = m->counter.as<int>();
+  a.dead = m->dead.as<uint8_t>();
+  a.enter = m->enter.as<uint8_t>();
+  hipLaunchKernelGGL(k_ds_claim, dim3(blocks(nin)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_ds_resolve, dim3(blocks(nin)), dim3(256), 0, st, a);
+  // survivors (stable) + entering inputs (input order) -> tmp
+  MCHK(c, m->tmp.reserve((n0 + nin) * sizeof(float4)));
+  MCHK(c, m->live.reserve(std::max<int64_t>(n0, 1)));
+  int* nsel = m->counter.as<int>() + 1;
+  int* nsel2 = m->counter.as<int>() + 2;
+  size_t tb = 0, tb2 = 0;
+  if (n0) {
+    hipLaunchKernelGGL(k_flags_inv, dim3(blocks(n0)), dim3(256), 0, st, m->dead.as<uint8_t>(), (int)n0, m->live.as<uint8_t>());
+    MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, m->pts.as<float4>(), m->live.as<uint8_t>(), m->tmp.as<float4>(),
+                                          nsel, (int)n0, st));
+  }
+  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb2, m->newp.as<float4>(), m->enter.as<uint8_t>(), m->tmp.as<float4>(),
+                                        nsel2, (int)nin, st));
+  MCHK(c, m->sort_tmp.reserve(std::max(tb, tb2)));
+  if (n0)
+    MCHK(c, hipcub::DeviceSelect::Flagged(m->sort_tmp.p, tb, m->pts.as<float4>(), m->live.as<uint8_t>(),
+                                          m->tmp.as<float4>(), nsel, (int)n0, st));
+  else
+    MCHK(c, hipMemsetAsync(nsel, 0, sizeof(int), st));
+  int h[2] = {0, 0};
+  MCHK(c, hipMemcpyAsync(&h[0], nsel, sizeof(int), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  MCHK(c, hipcub::DeviceSelect::Flagged(m->sort_tmp.p, tb2, m->newp.as<float4>(), m->enter.as<uint8_t>(),
+                                        m->tmp.as<float4>() + h[0], nsel2, (int)nin, st));
+  MCHK(c, hipMemcpyAsync(&h[1], nsel2, sizeof(int), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  if (n_added) *n_added = h[1];
+  return rebuild(m, (int64_t)h[0] + h[1]);
+}
+
+// k-NN of n queries (device buffer, stride floats, optional device count / pose).
+int knn_device(lislam_map* m, const float* q, int stride, const int* qcount, int n, const double* pose, int k, float max_d2,
+               float4* out_pts, float* out_d2, int* out_found) {
+  lislam_ctx* c = m->ctx;
+  if (n <= 0) return LISLAM_OK;
+  const int nb = blocks((int64_t)n * kG);
+  MapView v = m->view();
+  if (k <= 5)
+    hipLaunchKernelGGL(k_knn<5>, dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2, out_pts,
+                       out_d2, out_found);
+  else
+    hipLaunchKernelGGL(k_knn<8>, dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2, out_pts,
+                       out_d2, out_found);
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// association of n device queries at a device pose into device rec / kind
+int associate_device(lislam_map* m, int match, const float* q, int stride, const int* qcount, int n, const double* pose,
+                     double* rec, int* kind) {
+  lislam_ctx* c = m->ctx;
+  if (n <= 0) return LISLAM_OK;
+  MCHK(c, m->sc.nb.reserve((size_t)n * 5 * sizeof(float4)));
+  MCHK(c, m->sc.d2.reserve((size_t)n * 5 * 4));
+  MCHK(c, m->sc.found.reserve((size_t)n * 4));
+  if (m->n == 0) {
+    MCHK(c, hipMemsetAsync(m->sc.found.p, 0, (size_t)n * 4, stream_of(c)));
+  } else {
+    MRC(knn_device(m, q, stride, qcount, n, pose, 5, 1.0f, m->sc.nb.as<float4>(), m->sc.d2.as<float>(),
+                   m->sc.found.as<int>()));
+  }
+  hipLaunchKernelGGL(k_fit, dim3(blocks(n)), dim3(256), 0, stream_of(c), match, q, stride, qcount, n,
+                     m->sc.nb.as<float4>(), m->sc.d2.as<float>(), m->sc.found.as<int>(), rec, kind);
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// ceres::Solve over n device records; result stays in the LmDev (device).
+int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* kind, const int* ncount, int n,
+                 const double* x0_dev, int max_it) {
+  hipStream_t st = stream_of(c);
+  MCHK(c, sc.lm.reserve(sizeof(LmDev)));
+  MCHK(c, sc.partial.reserve((size_t)kMaxParts * kPart * 8));
+  LmDev* lm = sc.lm.as<LmDev>();
+  const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev);
+  for (int e = 0; e <= max_it; e++) {  // initial evaluation + at most one per iteration
+    hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm, sc.partial.as<double>());
+    hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(64), 0, st, lm, sc.partial.as<double>(), parts, max_it);
+  }
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// PCL VoxelGrid of n device float4 points into out (device); n_out device count.
+int voxel_grid_device(lislam_ctx* c, MapScratch& sc, const float4* in, int n, float leaf, float4* out, int* n_out) {
+  hipStream_t st = stream_of(c);
+  if (n == 0) {
+    MCHK(c, hipMemsetAsync(n_out, 0, sizeof(int), st));
+    return LISLAM_OK;
+  }
+  MCHK(c, sc.bounds.reserve(64));
+  MCHK(c, sc.keys32a.reserve((size_t)n * 4));
+  MCHK(c, sc.keys32b.reserve((size_t)n * 4));
+  MCHK(c, sc.idxa.reserve((size_t)n * 4));
+  MCHK(c, sc.idxb.reserve((size_t)n * 4));
+  MCHK(c, sc.flag.reserve((size_t)n * 4));
+  MCHK(c, sc.pos.reserve((size_t)n * 4));
+  VgArgs a;
+  a.in = in;
+  a.n = n;
+  a.inv = 1.0f / leaf;
+  a.bounds = sc.bounds.as<float>();
+  a.overflow = sc.bounds.as<int>() + 8;
+  a.keys = sc.keys32a.as<uint32_t>();
+  a.idx = sc.idxa.as<int>();
+  MCHK(c, hipMemsetAsync(a.overflow, 0, sizeof(int), st));
+  hipLaunchKernelGGL(k_vg_bounds, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(k_vg_keys, dim3(blocks(n)), dim3(256), 0, st, a);
+  MRC(sort_pairs_u32(c, sc.sort_tmp, sc.keys32a.as<uint32_t>(), sc.keys32b.as<uint32_t>(), sc.idxa.as<int>(),
+                     sc.idxb.as<int>(), n));
+  hipLaunchKernelGGL(k_vg_runs, dim3(blocks(n)), dim3(256), 0, st, sc.keys32b.as<uint32_t>(), n, a.overflow, sc.flag.as<int>());
+  size_t tb = 0;
+  MCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sc.flag.as<int>(), sc.pos.as<int>(), n, st));
+  MCHK(c, sc.sort_tmp.reserve(tb));
+  MCHK(c, hipcub::DeviceScan::ExclusiveSum(sc.sort_tmp.p, tb, sc.flag.as<int>(), sc.pos.as<int>(), n, st));
+  hipLaunchKernelGGL(k_vg_centroids, dim3(blocks(n)), dim3(256), 0, st, in, sc.keys32b.as<uint32_t>(), sc.idxb.as<int>(),
+                     sc.pos.as<int>(), sc.flag.as<int>(), n, a.overflow, out, n_out);
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// host-or-device input of n points (stride floats) -> device float4 buffer (intensity = 0 when stride 3)
+int stage_points(lislam_ctx* c, MapScratch& sc, DBuf& dst, const float* pts, int n, int stride) {
+  hipStream_t st = stream_of(c);
+  MCHK(c, dst.reserve((size_t)std::max(n, 1) * sizeof(float4)));
+  if (n == 0) return LISLAM_OK;
+  if (stride == 4) {
+    MCHK(c, hipMemcpyAsync(dst.p, pts, (size_t)n * 16, hipMemcpyDefault, st));
+    return LISLAM_OK;
+  }
+  MCHK(c, sc.vin.reserve((size_t)n * stride * 4));
+  MCHK(c, hipMemcpyAsync(sc.vin.p, pts, (size_t)n * stride * 4, hipMemcpyDefault, st));
+  hipLaunchKernelGGL(k_pack_points, dim3(blocks(n)), dim3(256), 0, st, sc.vin.as<float>(), n, stride, 0, dst.as<float4>());
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+MapScratch& ctx_scratch(lislam_ctx* c) {
+  if (!c->map_scratch) c->map_scratch = new MapScratch();
+  return *static_cast<MapScratch*>(c->map_scratch);
+}
+
+bool valid_stride(int s) { return s >= 3; }
+
+}  // namespace
+
+void lislam_free_map_scratch(void* p) { delete static_cast<MapScratch*>(p); }
+
+extern "C" {
+
+int lislam_map_create(lislam_ctx* c, const lislam_map_config* cfg, lislam_map** out) {
+  if (!c || !cfg || !out) return LISLAM_ERR_ARG;
+  *out = nullptr;
+  if (!(cfg->downsample_size > 0) || cfg->cell_size < 0) return mfail(c, LISLAM_ERR_ARG, "lislam_map_create: bad sizes");
+  hipSetDevice(c->device);
+  lislam_map* m = new lislam_map();
+  m->ctx = c;
+  m->ds = cfg->downsample_size;
+  m->cell = cfg->cell_size > 0 ? cfg->cell_size : cfg->downsample_size;
+  *out = m;
+  return LISLAM_OK;
+}
+
+int lislam_map_destroy(lislam_map* m) {
+  if (!m) return LISLAM_OK;
+  hipSetDevice(m->ctx->device);
+  (void)hipStreamSynchronize(m->ctx->stream);
+  delete m;
+  return LISLAM_OK;
+}
+
+int lislam_map_build(lislam_map* m, const float* pts, int64_t n, int32_t stride) {
+  if (!m || n < 0 || (n > 0 && !pts) || !valid_stride(stride) || n > 0x7fffffff) return LISLAM_ERR_ARG;
+  hipSetDevice(m->ctx->device);
+  MCHK(m->ctx, m->tmp.reserve((size_t)std::max<int64_t>(n, 1) * sizeof(float4)));
+  MRC(upload_points(m, pts, n, stride, 0, m->tmp, 0));
+  m->next_id = (int)n;
+  MRC(rebuild(m, n));
+  MCHK(m->ctx, hipStreamSynchronize(m->ctx->stream));
+  return LISLAM_OK;
+}
+
+int lislam_map_add_points(lislam_map* m, const float* pts, int64_t n, int32_t stride, int32_t downsample_on,
+                          int64_t* n_added) {
+  if (!m || n < 0 || (n > 0 && !pts) || !valid_stride(stride)) return LISLAM_ERR_ARG;
+  if (m->n + n > 0x7fffffff || (int64_t)m->next_id + n > 0x7fffffff) return mfail(m->ctx, LISLAM_ERR_CAPACITY, "map too large");
+  hipSetDevice(m->ctx->device);
+  if (n_added) *n_added = 0;
+  if (n == 0) return LISLAM_OK;
+  MCHK(m->ctx, m->newp.reserve((size_t)n * sizeof(float4)));
+  MRC(upload_points(m, pts, n, stride, m->next_id, m->newp, 0));
+  m->next_id += (int)n;
+  MRC(add_packed(m, n, downsample_on != 0, n_added));
+  MCHK(m->ctx, hipStreamSynchronize(m->ctx->stream));
+  return LISLAM_OK;
+}
+
+int lislam_map_size(lislam_map* m, int64_t* n) {
+  if (!m || !n) return LISLAM_ERR_ARG;
+  *n = m->n;
+  return LISLAM_OK;
+}
+
+int lislam_map_points(lislam_map* m, float* out, int64_t cap, int64_t* n) {
+  if (!m || !n) return LISLAM_ERR_ARG;
+  *n = m->n;
+  if (m->n == 0) return LISLAM_OK;
+  if (!out || cap < m->n) return mfail(m->ctx, LISLAM_ERR_CAPACITY, "lislam_map_points: capacity %lld < %lld",
+                                       (long long)cap, (long long)m->n);
+  hipSetDevice(m->ctx->device);
+  MCHK(m->ctx, hipMemcpyAsync(out, m->pts.p, m->n * sizeof(float4), hipMemcpyDefault, m->ctx->stream));
+  MCHK(m->ctx, hipStreamSynchronize(m->ctx->stream));
+  return LISLAM_OK;
+}
+
+int lislam_map_nearest_search(lislam_map* m, const float* queries, int32_t n, int32_t stride, int32_t k,
+                              float max_dist, float* out_pts, float* out_d2, int32_t* out_found) {
+  if (!m || n < 0 || (n > 0 && !queries) || !valid_stride(stride) || k < 1 || k > 8) return LISLAM_ERR_ARG;
+  if (n == 0) return LISLAM_OK;
+  lislam_ctx* c = m->ctx;
+  hipSetDevice(c->device);
+  MapScratch& sc = m->sc;
+  hipStream_t st = stream_of(c);
+  MCHK(c, sc.q.reserve((size_t)n * stride * 4));
+  MCHK(c, hipMemcpyAsync(sc.q.p, queries, (size_t)n * stride * 4, hipMemcpyDefault, st));
+  MCHK(c, sc.nb.reserve((size_t)n * k * sizeof(float4)));
+  MCHK(c, sc.d2.reserve((size_t)n * k * 4));
+  MCHK(c, sc.found.reserve((size_t)n * 4));
+  const float md2 = max_dist > 0 ? max_dist * max_dist : kInf;
+  if (m->n == 0) {
+    MCHK(c, hipMemsetAsync(sc.nb.p, 0, (size_t)n * k * sizeof(float4), st));
+    std::vector<float> inf((size_t)n * k, kInf);
+    MCHK(c, hipMemcpyAsync(sc.d2.p, inf.data(), inf.size() * 4, hipMemcpyHostToDevice, st));
+    MCHK(c, hipMemsetAsync(sc.found.p, 0, (size_t)n * 4, st));
+    MCHK(c, hipStreamSynchronize(st));
+  } else {
+    MRC(knn_device(m, sc.q.as<float>(), stride, nullptr, n, nullptr, k, md2, sc.nb.as<float4>(), sc.d2.as<float>(),
+                   sc.found.as<int>()));
+  }
+  if (out_pts) MCHK(c, hipMemcpyAsync(out_pts, sc.nb.p, (size_t)n * k * sizeof(float4), hipMemcpyDefault, st));
+  if (out_d2) MCHK(c, hipMemcpyAsync(out_d2, sc.d2.p, (size_t)n * k * 4, hipMemcpyDefault, st));
+  if (out_found) MCHK(c, hipMemcpyAsync(out_found, sc.found.p, (size_t)n * 4, hipMemcpyDefault, st));
+  MCHK(c, hipStreamSynchronize(st));
+  return LISLAM_OK;
+}
+
+int lislam_map_associate(lislam_map* m, int32_t kind, const float* pts, int32_t n, int32_t stride, const double* x,
+                         double* out_rec, int32_t* out_kind) {
+  if (!m || n < 0 || (n > 0 && !pts) || !valid_stride(stride) || !x || (kind != 0 && kind != 1)) return LISLAM_ERR_ARG;
+  if (n == 0) return LISLAM_OK;
+  lislam_ctx* c = m->ctx;
+  hipSetDevice(c->device);
+  MapScratch& sc = m->sc;
+  hipStream_t st = stream_of(c);
+  MCHK(c, sc.q.reserve((size_t)n * stride * 4));
+  MCHK(c, hipMemcpyAsync(sc.q.p, pts, (size_t)n * stride * 4, hipMemcpyDefault, st));
+  MCHK(c, sc.x.reserve(64));
+  MCHK(c, hipMemcpyAsync(sc.x.p, x, 56, hipMemcpyDefault, st));
+  MCHK(c, sc.rec.reserve((size_t)n * 72));
+  MCHK(c, sc.kind.reserve((size_t)n * 4));
+  MRC(associate_device(m, kind, sc.q.as<float>(), stride, nullptr, n, sc.x.as<double>(), sc.rec.as<double>(),
+                       sc.kind.as<int>()));
+  if (out_rec) MCHK(c, hipMemcpyAsync(out_rec, sc.rec.p, (size_t)n * 72, hipMemcpyDefault, st));
+  if (out_kind) MCHK(c, hipMemcpyAsync(out_kind, sc.kind.p, (size_t)n * 4, hipMemcpyDefault, st));
+  MCHK(c, hipStreamSynchronize(st));
+  return LISLAM_OK;
+}
+
+int lislam_normal_equations(lislam_ctx* c, const double* rec, const int32_t* kind, int32_t n, const double* x,
+                            double* out28) {
+  if (!c || n < 0 || (n > 0 && (!rec || !kind)) || !x || !out28) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  MapScratch& sc = ctx_scratch(c);
+  hipStream_t st = stream_of(c);
+  MCHK(c, sc.rec.reserve((size_t)std::max(n, 1) * 72));
+  MCHK(c, sc.kind.reserve((size_t)std::max(n, 1) * 4));
+  MCHK(c, sc.lm.reserve(sizeof(LmDev)));
+  MCHK(c, sc.partial.reserve((size_t)kMaxParts * kPart * 8));
+  MCHK(c, sc.x.reserve(64));
+  if (n) {
+    MCHK(c, hipMemcpyAsync(sc.rec.p, rec, (size_t)n * 72, hipMemcpyDefault, st));
+    MCHK(c, hipMemcpyAsync(sc.kind.p, kind, (size_t)n * 4, hipMemcpyDefault, st));
+  }
+  MCHK(c, hipMemcpyAsync(sc.x.p, x, 56, hipMemcpyDefault, st));
+  LmDev* lm = sc.lm.as<LmDev>();
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, sc.x.as<double>());
+  const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
+  hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, sc.rec.as<double>(), sc.kind.as<int>(), nullptr,
+                     n, lm, sc.partial.as<double>());
+  std::vector<double> part((size_t)parts * kPart);
+  MCHK(c, hipMemcpyAsync(part.data(), sc.partial.p, part.size() * 8, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  for (int e = 0; e < kAcc; e++) {
+    double v = 0;
+    for (int p = 0; p < parts; p++) v += part[(size_t)p * kPart + e];
+    out28[e] = v;
+  }
+  return LISLAM_OK;
+}
+
+int lislam_pose_solve(lislam_ctx* c, const double* rec, const int32_t* kind, int32_t n, double* x, int32_t max_iterations,
+                      int32_t* summary) {
+  if (!c || n < 0 || (n > 0 && (!rec || !kind)) || !x || max_iterations < 0) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  MapScratch& sc = ctx_scratch(c);
+  hipStream_t st = stream_of(c);
+  MCHK(c, sc.rec.reserve((size_t)std::max(n, 1) * 72));
+  MCHK(c, sc.kind.reserve((size_t)std::max(n, 1) * 4));
+  MCHK(c, sc.x.reserve(128));
+  if (n) {
+    MCHK(c, hipMemcpyAsync(sc.rec.p, rec, (size_t)n * 72, hipMemcpyDefault, st));
+    MCHK(c, hipMemcpyAsync(sc.kind.p, kind, (size_t)n * 4, hipMemcpyDefault, st));
+  }
+  MCHK(c, hipMemcpyAsync(sc.x.p, x, 56, hipMemcpyDefault, st));
+  MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, sc.x.as<double>(), max_iterations));
+  int* dsum = reinterpret_cast<int*>(sc.x.as<double>() + 8);
+  hipLaunchKernelGGL(k_lm_finish, dim3(1), dim3(64), 0, st, sc.lm.as<LmDev>(), sc.x.as<double>(), dsum);
+  int hs[4];
+  MCHK(c, hipMemcpyAsync(x, sc.x.p, 56, hipMemcpyDefault, st));
+  MCHK(c, hipMemcpyAsync(hs, dsum, 16, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  if (summary) for (int e = 0; e < 4; e++) summary[e] = hs[e];
+  return LISLAM_OK;
+}
+
+int lislam_voxel_grid(lislam_ctx* c, const float* pts, int32_t n, float leaf, float* out, int32_t* n_out) {
+  if (!c || n < 0 || (n > 0 && (!pts || !out)) || !n_out || !(leaf > 0)) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  MapScratch& sc = ctx_scratch(c);
+  hipStream_t st = stream_of(c);
+  MRC(stage_points(c, sc, sc.q, pts, n, 4));
+  MCHK(c, sc.vout.reserve((size_t)std::max(n, 1) * 16));
+  MCHK(c, sc.counters.reserve(64));
+  MRC(voxel_grid_device(c, sc, sc.q.as<float4>(), n, leaf, sc.vout.as<float4>(), sc.counters.as<int>()));
+  int no = 0;
+  MCHK(c, hipMemcpyAsync(&no, sc.counters.p, 4, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  if (no) MCHK(c, hipMemcpyAsync(out, sc.vout.p, (size_t)no * 16, hipMemcpyDefault, st));
+  MCHK(c, hipStreamSynchronize(st));
+  *n_out = no;
+  return LISLAM_OK;
+}
+
+int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const double* odom, double* state,
+                       double* out_pose, int32_t* summary) {
+  if (!m || n < 0 || (n > 0 && !ground) || !odom || !state) return LISLAM_ERR_ARG;
+  lislam_ctx* c = m->ctx;
+  hipSetDevice(c->device);
+  MapScratch& sc = m->sc;
+  hipStream_t st = stream_of(c);
+  // device pose block: [0,7) state, [8,15) odom, [16,23) x, [24,31) keyframe pose
+  MCHK(c, sc.x.reserve(40 * 8));
+  double* dp = sc.x.as<double>();
+  MCHK(c, hipMemcpyAsync(dp, state, 56, hipMemcpyDefault, st));
+  MCHK(c, hipMemcpyAsync(dp + 8, odom, 56, hipMemcpyDefault, st));
+  hipLaunchKernelGGL(k_mapopt_pose, dim3(1), dim3(64), 0, st, 0, dp, dp + 8, dp + 16, (const LmDev*)nullptr, dp + 24);
+  int32_t summ[3] = {0, 0, -1};
+  MRC(stage_points(c, sc, sc.vout, ground, n, 4));  // sensor-frame ground cloud (float4)
+  if (m->n == 0) {  // first keyframe: Build with the transformed raw cloud (mapOptimization.cpp:185-192)
+    MCHK(c, m->tmp.reserve((size_t)std::max(n, 1) * 16));
+    MCHK(c, sc.vin.reserve((size_t)std::max(n, 1) * 16));
+    hipLaunchKernelGGL(k_transform, dim3(blocks(n)), dim3(256), 0, st, sc.vout.as<float>(), 4, (const int*)nullptr, n,
+                       dp + 16, sc.vin.as<float>());
+    hipLaunchKernelGGL(k_pack_points, dim3(blocks(n)), dim3(256), 0, st, sc.vin.as<float>(), n, 4, 0, m->tmp.as<float4>());
+    m->next_id = n;
+    MRC(rebuild(m, n));
+    MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
+  } else {
+    // VoxelGrid(0.8) (:368-370) of the xyz cloud (PointXYZ: intensity lane zeroed)
+    MCHK(c, sc.flag.reserve((size_t)std::max(n, 1) * 4));
+    MCHK(c, sc.counters.reserve(64));
+    MCHK(c, sc.vin.reserve((size_t)std::max(n, 1) * 16));
+    MCHK(c, hipMemcpy2DAsync(sc.vin.p, 16, sc.vout.p, 16, 12, n, hipMemcpyDeviceToDevice, st));
+    MCHK(c, hipMemset2DAsync(sc.vin.as<char>() + 12, 16, 0, 4, n, st));
+    DBuf& voxbuf = sc.vox;
+    MCHK(c, voxbuf.reserve((size_t)std::max(n, 1) * 16));
+    int* nvox = sc.counters.as<int>();
+    MRC(voxel_grid_device(c, sc, sc.vin.as<float4>(), n, 0.8f, voxbuf.as<float4>(), nvox));
+    MCHK(c, sc.rec.reserve((size_t)std::max(n, 1) * 72));
+    MCHK(c, sc.kind.reserve((size_t)std::max(n, 1) * 4));
+    MRC(associate_device(m, 1, voxbuf.as<float>(), 4, nvox, n, dp + 16, sc.rec.as<double>(), sc.kind.as<int>()));
+    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nvox, n, dp + 16, 10));
+    LmDev* lm = sc.lm.as<LmDev>();
+    hipLaunchKernelGGL(k_mapopt_pose, dim3(1), dim3(64), 0, st, 1, dp, dp + 8, dp + 16, lm, dp + 24);
+    int* dsum = reinterpret_cast<int*>(dp + 32);
+    hipLaunchKernelGGL(k_lm_finish, dim3(1), dim3(64), 0, st, lm, dp + 16, dsum);
+    // Add_Points(downsample) of the voxelized cloud at the keyframe pose (:467-475)
+    MCHK(c, m->newp.reserve((size_t)std::max(n, 1) * 16));
+    hipLaunchKernelGGL(k_transform, dim3(blocks(n)), dim3(256), 0, st, voxbuf.as<float>(), 4, nvox, n, dp + 24,
+                       sc.vin.as<float>());
+    int hn = 0;
+    int hs[4];
+    MCHK(c, hipMemcpyAsync(&hn, nvox, 4, hipMemcpyDeviceToHost, st));
+    MCHK(c, hipMemcpyAsync(hs, dsum, 16, hipMemcpyDeviceToHost, st));
+    MCHK(c, hipStreamSynchronize(st));
+    summ[0] = hs[3];
+    summ[1] = hs[0];
+    summ[2] = hs[1];
+    hipLaunchKernelGGL(k_pack_points, dim3(blocks(hn)), dim3(256), 0, st, sc.vin.as<float>(), hn, 4, m->next_id,
+                       m->newp.as<float4>());
+    m->next_id += hn;
+    MRC(add_packed(m, hn, true, nullptr));
+    MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
+    MCHK(c, hipMemcpyAsync(state, dp, 56, hipMemcpyDefault, st));
+  }
+  MCHK(c, hipStreamSynchronize(st));
+  if (summary) for (int e = 0; e < 3; e++) summary[e] = summ[e];
+  return LISLAM_OK;
+}
+
+int lislam_laser_mapping(lislam_map* mc, lislam_map* ms, const float* corner, int32_t nc, const float* surf, int32_t ns,
+                         double* x, int32_t* stats) {
+  if (!mc || !ms || mc->ctx != ms->ctx || nc < 0 || ns < 0 || (nc && !corner) || (ns && !surf) || !x)
+    return LISLAM_ERR_ARG;
+  lislam_ctx* c = mc->ctx;
+  hipSetDevice(c->device);
+  MapScratch& sc = mc->sc;
+  hipStream_t st = stream_of(c);
+  const int n = nc + ns;
+  MCHK(c, sc.x.reserve(40 * 8));
+  double* dp = sc.x.as<double>();
+  MCHK(c, hipMemcpyAsync(dp, x, 56, hipMemcpyDefault, st));
+  DBuf& qc = sc.qc;
+  DBuf& qs = sc.qs;
+  MRC(stage_points(c, sc, qc, corner, nc, 4));
+  MRC(stage_points(c, sc, qs, surf, ns, 4));
+  MCHK(c, sc.rec.reserve((size_t)std::max(n, 1) * 72));
+  MCHK(c, sc.kind.reserve((size_t)std::max(n, 1) * 4));
+  int hs[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int* dsum = reinterpret_cast<int*>(dp + 32);
+  for (int outer = 0; outer < 2; outer++) {
+    MRC(associate_device(mc, 0, qc.as<float>(), 4, nullptr, nc, dp, sc.rec.as<double>(), sc.kind.as<int>()));
+    MRC(associate_device(ms, 1, qs.as<float>(), 4, nullptr, ns, dp, sc.rec.as<double>() + (size_t)nc * 9,
+                         sc.kind.as<int>() + nc));
+    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, dp, 4));
+    hipLaunchKernelGGL(k_lm_finish, dim3(1), dim3(64), 0, st, sc.lm.as<LmDev>(), dp, dsum + outer * 4);
+  }
+  MCHK(c, hipMemcpyAsync(x, dp, 56, hipMemcpyDefault, st));
+  MCHK(c, hipMemcpyAsync(hs, dsum, 32, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  if (stats)
+    for (int o = 0; o < 2; o++) { stats[o * 2] = hs[o][2]; stats[o * 2 + 1] = hs[o][3]; }
+  return LISLAM_OK;
+}
+
+}  // extern "C"

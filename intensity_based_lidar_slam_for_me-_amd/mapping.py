@@ -1,0 +1,165 @@
+"""Host-side mirror of the reference's scan-to-map interfaces over the lislam C ABI.
+
+``IkdMap`` plays the vendored ``KD_TREE`` (``src/ikd-Tree/ikd_Tree.h:256-279``: ``Build``,
+``Add_Points``, ``Nearest_Search``, ``size``, ``flatten``) on a device-resident map;
+``MapOptimization.callback`` plays the ground-map stage of
+``mapOptimization::mapOptimizationCallback`` (``src/mapOptimization.cpp:99-479``);
+``laser_mapping`` plays the optimization of ``laserMapping::process``
+(``src/laserMapping.cpp:620-850``).  All compute runs in ``liblislam.so`` on the GPU; inputs may
+be numpy arrays (host) or any object exposing a device pointer via ``data_ptr()`` (torch CUDA
+tensors), which the library reads in place.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import native as nat
+
+
+def _as_points(points):
+    """(pointer, n, stride, keepalive) of a float32 (n, 3|4) host array or device tensor."""
+    if hasattr(points, "data_ptr"):  # torch tensor (host or device), float32, contiguous
+        t = points.contiguous()
+        if str(t.dtype) != "torch.float32" or t.dim() != 2 or t.shape[1] < 3:
+            raise ValueError("points must be a float32 (n, 3|4) tensor")
+        return ctypes.c_void_p(t.data_ptr()), t.shape[0], t.shape[1], t
+    a = np.ascontiguousarray(points, np.float32)
+    if a.ndim != 2 or a.shape[1] < 3:
+        raise ValueError("points must be (n, 3|4)")
+    return ctypes.c_void_p(a.ctypes.data), a.shape[0], a.shape[1], a
+
+
+class IkdMap:
+    """Device-resident ikd-Tree point set (lislam_map)."""
+
+    def __init__(self, ctx, downsample_size: float = 0.2, cell_size: float = 0.0):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        cfg = nat.MapConfig(downsample_size, cell_size)
+        nat.check(ctx.lib.lislam_map_create(ctx.h, ctypes.byref(cfg), ctypes.byref(h)), ctx.h, "lislam_map_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lislam_map_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build(self, points):
+        """KD_TREE::Build."""
+        p, n, s, _k = _as_points(points)
+        nat.check(self.ctx.lib.lislam_map_build(self.h, p, n, s), self.ctx.h, "lislam_map_build")
+
+    def add_points(self, points, downsample_on: bool = True) -> int:
+        """KD_TREE::Add_Points; returns the number of inputs that entered the map."""
+        p, n, s, _k = _as_points(points)
+        added = ctypes.c_int64()
+        nat.check(self.ctx.lib.lislam_map_add_points(self.h, p, n, s, int(downsample_on), ctypes.byref(added)),
+                  self.ctx.h, "lislam_map_add_points")
+        return added.value
+
+    def size(self) -> int:
+        n = ctypes.c_int64()
+        nat.check(self.ctx.lib.lislam_map_size(self.h, ctypes.byref(n)), self.ctx.h, "lislam_map_size")
+        return n.value
+
+    def points(self) -> np.ndarray:
+        """KD_TREE::flatten: live points (n, 4) = x, y, z, id bits (storage order)."""
+        n = self.size()
+        out = np.zeros((max(n, 1), 4), np.float32)
+        got = ctypes.c_int64()
+        nat.check(self.ctx.lib.lislam_map_points(self.h, nat.ptr(out), out.shape[0], ctypes.byref(got)), self.ctx.h,
+                  "lislam_map_points")
+        return out[: got.value]
+
+    def nearest_search(self, queries, k: int = 5, max_dist: float = 0.0):
+        """Batched KD_TREE::Nearest_Search: (points (n, k, 4), d2 (n, k), found (n,))."""
+        p, n, s, _k = _as_points(queries)
+        pts = np.zeros((n, k, 4), np.float32)
+        d2 = np.zeros((n, k), np.float32)
+        found = np.zeros(n, np.int32)
+        nat.check(self.ctx.lib.lislam_map_nearest_search(self.h, p, n, s, k, max_dist, nat.ptr(pts), nat.ptr(d2),
+                                                         nat.ptr(found)), self.ctx.h, "lislam_map_nearest_search")
+        return pts, d2, found
+
+    def associate(self, match: int, points, x):
+        """Line (0) / plane (1) association at pose x: (records (n, 9), kinds (n,))."""
+        p, n, s, _k = _as_points(points)
+        rec = np.zeros((n, 9))
+        kind = np.zeros(n, np.int32)
+        xx = np.ascontiguousarray(x, np.float64)
+        nat.check(self.ctx.lib.lislam_map_associate(self.h, match, p, n, s, nat.ptr(xx), nat.ptr(rec), nat.ptr(kind)),
+                  self.ctx.h, "lislam_map_associate")
+        return rec, kind
+
+
+def normal_equations(ctx, records, kinds, x) -> np.ndarray:
+    """cost, J^T J (21), J^T r (6) of residual-block records at x (28 doubles)."""
+    rec = np.ascontiguousarray(records, np.float64).reshape(-1, 9)
+    kd = np.ascontiguousarray(kinds, np.int32)
+    out = np.zeros(28)
+    xx = np.ascontiguousarray(x, np.float64)
+    nat.check(ctx.lib.lislam_normal_equations(ctx.h, nat.ptr(rec), nat.ptr(kd), rec.shape[0], nat.ptr(xx), nat.ptr(out)),
+              ctx.h, "lislam_normal_equations")
+    return out
+
+
+def pose_solve(ctx, records, kinds, x0, max_iterations: int):
+    """ceres::Solve of the records: (x (7,), summary (iterations, termination, edges, planes))."""
+    rec = np.ascontiguousarray(records, np.float64).reshape(-1, 9)
+    kd = np.ascontiguousarray(kinds, np.int32)
+    x = np.array(x0, np.float64)
+    summ = np.zeros(4, np.int32)
+    nat.check(ctx.lib.lislam_pose_solve(ctx.h, nat.ptr(rec), nat.ptr(kd), rec.shape[0], nat.ptr(x), max_iterations,
+                                        nat.ptr(summ)), ctx.h, "lislam_pose_solve")
+    return x, summ
+
+
+def voxel_grid(ctx, points, leaf: float) -> np.ndarray:
+    """pcl::VoxelGrid of (n, 4) float32 points (x, y, z, intensity)."""
+    a = np.ascontiguousarray(points, np.float32).reshape(-1, 4)
+    out = np.zeros((max(a.shape[0], 1), 4), np.float32)
+    n = ctypes.c_int32()
+    nat.check(ctx.lib.lislam_voxel_grid(ctx.h, nat.ptr(a), a.shape[0], leaf, nat.ptr(out), ctypes.byref(n)), ctx.h,
+              "lislam_voxel_grid")
+    return out[: n.value]
+
+
+class MapOptimization:
+    """Ground-map stage of the mapOptimization node (ikd-Tree map of downsample 0.4,
+    mapOptimization.cpp:504)."""
+
+    def __init__(self, ctx, downsample_size: float = 0.4, cell_size: float = 0.0):
+        self.map = IkdMap(ctx, downsample_size, cell_size)
+        self.state = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)  # q_wmap_wodom, t_wmap_wodom
+
+    def callback(self, ground, odom):
+        """One frame: ground = GroundPointOut (sensor frame, (n, 4)), odom = q_wodom_curr, t_wodom_curr.
+        Returns (q_w_curr, t_w_curr (7,), summary (planes, iterations, termination; -1 = built))."""
+        g = np.ascontiguousarray(ground, np.float32).reshape(-1, 4)
+        od = np.ascontiguousarray(odom, np.float64)
+        pose = np.zeros(7)
+        summ = np.zeros(3, np.int32)
+        ctx = self.map.ctx
+        nat.check(ctx.lib.lislam_mapopt_step(self.map.h, nat.ptr(g), g.shape[0], nat.ptr(od), nat.ptr(self.state),
+                                             nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_mapopt_step")
+        return pose, summ
+
+
+def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):
+    """laserMapping optimization: (x (7,), stats (corner / surf blocks of the two passes))."""
+    c = np.ascontiguousarray(corner, np.float32).reshape(-1, 4)
+    s = np.ascontiguousarray(surf, np.float32).reshape(-1, 4)
+    x = np.array(x0, np.float64)
+    st = np.zeros(4, np.int32)
+    ctx = corner_map.ctx
+    nat.check(ctx.lib.lislam_laser_mapping(corner_map.h, surf_map.h, nat.ptr(c), c.shape[0], nat.ptr(s), s.shape[0],
+                                           nat.ptr(x), nat.ptr(st)), ctx.h, "lislam_laser_mapping")
+    return x, st

@@ -30,7 +30,12 @@ EXPORTED_SYMBOLS = (
     "lislam_batch_upload", "lislam_batch_input_device_ptr", "lislam_batch_extract",
     "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
     "lislam_batch_download", "lislam_eval_factors",
+    "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
+    "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
+    "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_laser_mapping",
 )
+
+MATCH_LINE, MATCH_PLANE = 0, 1
 
 
 class Config(ctypes.Structure):
@@ -56,6 +61,10 @@ class ScanOut(ctypes.Structure):
                 ("less_flat", _fp), ("cap_less_flat", _i32), ("n_less_flat", _i32),
                 ("image_range", ctypes.POINTER(ctypes.c_uint8)), ("image_intensity", ctypes.POINTER(ctypes.c_uint8)),
                 ("cloud_track", _fp)]
+
+
+class MapConfig(ctypes.Structure):
+    _fields_ = [("downsample_size", ctypes.c_float), ("cell_size", ctypes.c_float)]
 
 
 class Frame(ctypes.Structure):
@@ -108,6 +117,20 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_kernel_times.argtypes = [vp, _fp, _i32p, _i32p]
     L.lislam_batch_download.argtypes = [vp, _i32, _i32, vp, _i32, _i32p]
     L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
+    i64, i64p = ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)
+    L.lislam_map_create.argtypes = [vp, ctypes.POINTER(MapConfig), ctypes.POINTER(vp)]
+    L.lislam_map_destroy.argtypes = [vp]
+    L.lislam_map_build.argtypes = [vp, vp, i64, _i32]
+    L.lislam_map_add_points.argtypes = [vp, vp, i64, _i32, _i32, i64p]
+    L.lislam_map_size.argtypes = [vp, i64p]
+    L.lislam_map_points.argtypes = [vp, vp, i64, i64p]
+    L.lislam_map_nearest_search.argtypes = [vp, vp, _i32, _i32, _i32, ctypes.c_float, vp, vp, vp]
+    L.lislam_map_associate.argtypes = [vp, _i32, vp, _i32, _i32, vp, vp, vp]
+    L.lislam_normal_equations.argtypes = [vp, vp, vp, _i32, vp, vp]
+    L.lislam_pose_solve.argtypes = [vp, vp, vp, _i32, vp, _i32, vp]
+    L.lislam_voxel_grid.argtypes = [vp, vp, _i32, ctypes.c_float, vp, _i32p]
+    L.lislam_mapopt_step.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
+    L.lislam_laser_mapping.argtypes = [vp, vp, vp, _i32, vp, _i32, vp, vp]
     for name in EXPORTED_SYMBOLS:
         getattr(L, name).restype = getattr(L, name).restype or ctypes.c_int
     L.lislam_last_error.restype = ctypes.c_char_p

@@ -185,3 +185,67 @@ def relative_ground_truth(k: int):
     dx, dy = b.x - a.x, b.y - a.y
     t = np.array([ca * dx + sa * dy, -sa * dx + ca * dy, 0.0])
     return np.array([0.0, 0.0, math.sin(dyaw / 2), math.cos(dyaw / 2)]), t
+
+
+# ------------------------------------------------------------------ maps (config 5, a19-a21)
+def make_corridor_map(n_points: int, spacing: float = 0.05, seed: int = BASE_SEED, x0: float = -10.0,
+                      noise: float = 0.005) -> np.ndarray:
+    """World-frame surface samples of the corridor (floor, ceiling, side walls, pillar faces) on a
+    jittered ``spacing`` grid, extended along +x until ``n_points`` points exist; ``(n, 4)``
+    float32 with w = 0 (PointXYZ as PCL stores it).  SURVEY.md §8(d) config 5: 5 cm sampling."""
+    rng = np.random.default_rng(seed)
+    s = spacing
+    ny = int(round(2 * WALL_Y / s))
+    nz = int(round((CEIL_Z - FLOOR_Z) / s))
+    per_x = 2 * ny + 2 * nz  # floor + ceiling + two walls per x step
+    nx = max(1, int(math.ceil(n_points / per_x)))
+    xs = x0 + s * np.arange(nx)
+    parts = []
+    gy = -WALL_Y + s * (np.arange(ny) + 0.5)
+    gz = FLOOR_Z + s * (np.arange(nz) + 0.5)
+    X, Y = np.meshgrid(xs, gy, indexing="ij")
+    for zc in (FLOOR_Z, CEIL_Z):
+        parts.append(np.stack([X.ravel(), Y.ravel(), np.full(X.size, zc)], axis=1))
+    X, Z = np.meshgrid(xs, gz, indexing="ij")
+    for yc in (-WALL_Y, WALL_Y):
+        parts.append(np.stack([X.ravel(), np.full(X.size, yc), Z.ravel()], axis=1))
+    P = np.concatenate(parts)
+    # in-plane jitter (no exact distance ties) and normal noise
+    P += rng.uniform(-0.25 * s, 0.25 * s, size=P.shape) + rng.normal(0.0, noise, size=P.shape)
+    P = P[:n_points]
+    out = np.zeros((P.shape[0], 4), np.float32)
+    out[:, :3] = P
+    return out
+
+
+def make_edge_map(n_lines: int = 40, spacing: float = 0.05, seed: int = BASE_SEED + 7, x0: float = 0.0) -> np.ndarray:
+    """Vertical pillar edges (corner map of laserMapping): points every ``spacing`` along the four
+    vertical edges of the first ``n_lines / 4`` pillars, jittered 5 mm.  ``(n, 4)`` float32."""
+    rng = np.random.default_rng(seed)
+    pts = []
+    for i, (xl, xh, yl, yh) in enumerate(_PILLARS[: max(1, n_lines // 4)]):
+        for ex, ey in ((xl, yl), (xl, yh), (xh, yl), (xh, yh)):
+            z = np.arange(FLOOR_Z, CEIL_Z, spacing)
+            e = np.stack([np.full(z.size, ex + x0), np.full(z.size, ey), z], axis=1)
+            pts.append(e + rng.normal(0.0, 0.005, size=e.shape))
+    P = np.concatenate(pts)
+    out = np.zeros((P.shape[0], 4), np.float32)
+    out[:, :3] = P
+    return out
+
+
+def perturb_pose(q, t, dt: float = 0.05, drot_deg: float = 0.5, seed: int = 1):
+    """(q, t) perturbed by a random translation of |dt| and rotation of drot about a random axis;
+    returned as x = (qx, qy, qz, qw, tx, ty, tz)."""
+    rng = np.random.default_rng(seed)
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    h = 0.5 * math.radians(drot_deg)
+    dq = np.array([*(math.sin(h) * ax), math.cos(h)])
+    x1, y1, z1, w1 = dq
+    x2, y2, z2, w2 = q
+    qq = np.array([w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2, w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                   w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2, w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2])
+    dtv = rng.normal(size=3)
+    dtv *= dt / np.linalg.norm(dtv)
+    return np.concatenate([qq, np.asarray(t, np.float64) + dtv])

@@ -39,6 +39,20 @@ def lib():
             ctypes.c_int, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f64p, _f64p, _i32p]
         L.oracle_nn1.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, _i32p, _f32p]
         L.oracle_eval_factor.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, _f64p, _f64p]
+        vp = ctypes.c_void_p
+        L.oracle_map_create.argtypes = [ctypes.c_float]
+        L.oracle_map_create.restype = vp
+        L.oracle_map_destroy.argtypes = [vp]
+        L.oracle_map_build.argtypes = [vp, _f32p, ctypes.c_int, ctypes.c_int]
+        L.oracle_map_add_points.argtypes = [vp, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_map_size.argtypes = [vp]
+        L.oracle_map_points.argtypes = [vp, _f32p]
+        L.oracle_map_knn.argtypes = [vp, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _f32p,
+                                     _f32p, _i32p]
+        L.oracle_map_associate.argtypes = [vp, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f64p, _f64p, _i32p]
+        L.oracle_map_solve.argtypes = [_f64p, _i32p, ctypes.c_int, _f64p, ctypes.c_int, _i32p]
+        L.oracle_mapopt_step.argtypes = [vp, _f32p, ctypes.c_int, _f64p, _f64p, _f64p, _i32p]
+        L.oracle_laser_mapping.argtypes = [vp, vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _i32p]
         _LIB = L
     return _LIB
 
@@ -135,3 +149,86 @@ def eval_factor(kind: int, pts: np.ndarray, q: np.ndarray, t: np.ndarray):
                              np.ascontiguousarray(q, np.float64), np.ascontiguousarray(t, np.float64), r,
                              J.reshape(-1))
     return r, J
+
+
+def _xyz4(points) -> np.ndarray:
+    p = np.ascontiguousarray(points, np.float32).reshape(-1, points.shape[-1])
+    if p.shape[1] == 4:
+        return p
+    out = np.zeros((p.shape[0], 4), np.float32)
+    out[:, :3] = p[:, :3]
+    return out
+
+
+class IkdMap:
+    """Restated ikd-Tree point set (oracle_map.cpp): Build / Add_Points / Nearest_Search."""
+
+    def __init__(self, downsample_size: float = 0.2):
+        self.h = lib().oracle_map_create(downsample_size)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_map_destroy(self.h)
+            self.h = None
+
+    def build(self, points):
+        p = _xyz4(points)
+        lib().oracle_map_build(self.h, p.reshape(-1), p.shape[0], 4)
+
+    def add_points(self, points, downsample: bool = True) -> int:
+        p = _xyz4(points)
+        return lib().oracle_map_add_points(self.h, p.reshape(-1), p.shape[0], 4, int(downsample))
+
+    def size(self) -> int:
+        return lib().oracle_map_size(self.h)
+
+    def points(self) -> np.ndarray:
+        """Live points (n, 4) = x, y, z, id (int32 bits in column 3) in ascending id."""
+        out = np.zeros((max(self.size(), 1), 4), np.float32)
+        n = lib().oracle_map_points(self.h, out.reshape(-1))
+        return out[:n]
+
+    def knn(self, queries, k: int = 5, max_dist: float = float("inf")):
+        q = _xyz4(queries)
+        n = q.shape[0]
+        pts = np.zeros((n, k, 4), np.float32)
+        d2 = np.zeros((n, k), np.float32)
+        found = np.zeros(n, np.int32)
+        lib().oracle_map_knn(self.h, q.reshape(-1), n, 4, k, max_dist, pts.reshape(-1), d2.reshape(-1), found)
+        return pts, d2, found
+
+    def associate(self, kind: int, points, x):
+        """kind 0 corner line / 1 surf plane: (records (n, 9), block kinds (n,): 0 edge, 2 plane-norm, -1)."""
+        p = _xyz4(points)
+        n = p.shape[0]
+        rec = np.zeros((n, 9))
+        valid = np.zeros(n, np.int32)
+        lib().oracle_map_associate(self.h, kind, p.reshape(-1), n, 4, np.ascontiguousarray(x, np.float64), rec.reshape(-1),
+                                   valid)
+        return rec, valid
+
+
+def map_solve(records: np.ndarray, kinds: np.ndarray, x0, max_iterations: int):
+    x = np.array(x0, np.float64)
+    summ = np.zeros(2, np.int32)
+    rec = np.ascontiguousarray(records, np.float64)
+    lib().oracle_map_solve(rec.reshape(-1), np.ascontiguousarray(kinds, np.int32), rec.shape[0], x, max_iterations, summ)
+    return x, summ
+
+
+def mapopt_step(m: IkdMap, ground, odom, state):
+    """One mapOptimization ground step; returns (pose (7,), new state (7,), summary (3,))."""
+    g = _xyz4(ground)
+    st = np.array(state, np.float64)
+    pose = np.zeros(7)
+    summ = np.zeros(3, np.int32)
+    lib().oracle_mapopt_step(m.h, g.reshape(-1), g.shape[0], np.ascontiguousarray(odom, np.float64), st, pose, summ)
+    return pose, st, summ
+
+
+def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):
+    c, s = _xyz4(corner), _xyz4(surf)
+    x = np.array(x0, np.float64)
+    stats = np.zeros(4, np.int32)
+    lib().oracle_laser_mapping(corner_map.h, surf_map.h, c.reshape(-1), c.shape[0], s.reshape(-1), s.shape[0], x, stats)
+    return x, stats

@@ -1,0 +1,256 @@
+"""GPU parity of the scan-to-map path (a19-a21) through the C ABI against the CPU oracle.
+
+k-NN results (point ids, squared distances), Add_Points' surviving point sets and the VoxelGrid
+are integer / index / float-copy work and must be bit-exact; residual-block records are fp64
+fits written with the same operation order on both sides (compared bit-exact, with a 1e-12
+relative fallback reported); poses within the north-star tolerance 1e-4 m / 1e-4 rad.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4  # BASELINE.json north_star
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(n_scans=64, width=1024)
+    yield c
+    c.close()
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def _by_id(p):
+    ids = p[:, 3].view(np.int32)
+    o = np.argsort(ids, kind="stable")
+    return p[o]
+
+
+def _knn_equal(g, r, k):
+    gp, gd, gf = g
+    rp, rd, rf = r
+    assert np.array_equal(gf, rf)
+    for i in range(len(gf)):
+        f = gf[i]
+        assert np.array_equal(gp[i, :f], rp[i, :f]), i
+        assert np.array_equal(gd[i, :f], rd[i, :f]), i
+
+
+@pytest.mark.parametrize("cell", [0.0, 0.1, 1.0])
+def test_knn_random_bit_exact(pkg, oracle, ctx, cell):
+    rng = np.random.default_rng(21)
+    P = _f32(rng.uniform(-6, 6, (50000, 3)))
+    Q = _f32(rng.uniform(-8, 8, (4000, 3)))  # includes queries outside the map's box
+    g = pkg.mapping.IkdMap(ctx, 0.4, cell)
+    g.build(P)
+    o = oracle.IkdMap(0.4)
+    o.build(P)
+    for k in (1, 5, 8):
+        _knn_equal(g.nearest_search(Q, k), o.knn(Q, k), k)
+    for md in (0.05, 0.3, 1.0):
+        _knn_equal(g.nearest_search(Q, 5, md), o.knn(Q, 5, md), 5)
+    g.close()
+
+
+def test_knn_corridor_and_far_queries(pkg, oracle, ctx, synth):
+    M = synth.make_corridor_map(300_000, spacing=0.05)
+    g = pkg.mapping.IkdMap(ctx, 0.4, 0.1)
+    g.build(M)
+    o = oracle.IkdMap(0.4)
+    o.build(M)
+    rng = np.random.default_rng(4)
+    Q = M[rng.choice(len(M), 3000, replace=False), :3] + rng.normal(0, 0.03, (3000, 3))
+    far = _f32(np.array([[500.0, 30.0, 9.0], [-50.0, 0.0, 0.0], [2.0, 0.0, 40.0]]))  # full-scan fallback
+    Q = _f32(np.concatenate([Q, far]))
+    _knn_equal(g.nearest_search(Q, 5), o.knn(Q, 5), 5)
+    g.close()
+
+
+def test_knn_small_and_empty_maps(pkg, oracle, ctx):
+    g = pkg.mapping.IkdMap(ctx, 0.2)
+    Q = _f32([[0.1, 0, 0], [5, 5, 5]])
+    pts, d2, found = g.nearest_search(Q, 5)
+    assert (found == 0).all() and np.isinf(d2).all()
+    P = _f32([[0, 0, 0], [1, 0, 0], [0, 2, 0]])
+    g.build(P)
+    o = oracle.IkdMap(0.2)
+    o.build(P)
+    _knn_equal(g.nearest_search(Q, 5), o.knn(Q, 5), 5)
+    _knn_equal(g.nearest_search(Q, 5, 1.0), o.knn(Q, 5, 1.0), 5)
+    g.close()
+
+
+@pytest.mark.parametrize("L,cell", [(0.4, 0.0), (0.4, 0.1), (0.8, 0.3)])
+def test_add_points_downsample_bit_exact(pkg, oracle, ctx, L, cell):
+    rng = np.random.default_rng(8)
+    base = _f32(rng.uniform(0, 6, (20000, 3)))
+    g = pkg.mapping.IkdMap(ctx, L, cell)
+    o = oracle.IkdMap(L)
+    g.build(base)
+    o.build(base)
+    for batch in range(4):
+        new = _f32(rng.uniform(-1, 7, (6000, 3)))
+        g.add_points(new, True)
+        o.add_points(new, True)
+        gp, op = _by_id(g.points()), o.points()
+        assert g.size() == o.size() == len(op)
+        assert np.array_equal(gp, op), batch
+    g.close()
+
+
+def test_add_points_no_downsample_and_empty_start(pkg, oracle, ctx):
+    rng = np.random.default_rng(9)
+    g = pkg.mapping.IkdMap(ctx, 0.4)
+    o = oracle.IkdMap(0.4)
+    a = _f32(rng.uniform(0, 3, (3000, 3)))
+    g.add_points(a, True)  # downsampled insert into an empty map
+    o.add_points(a, True)
+    assert np.array_equal(_by_id(g.points()), o.points())
+    b = _f32(rng.uniform(0, 3, (1000, 3)))
+    g.add_points(b, False)
+    o.add_points(b, False)
+    assert np.array_equal(_by_id(g.points()), o.points())
+    Q = _f32(rng.uniform(0, 3, (500, 3)))
+    _knn_equal(g.nearest_search(Q, 5), o.knn(Q, 5), 5)
+    g.close()
+
+
+@pytest.mark.parametrize("leaf", [0.2, 0.8])
+def test_voxel_grid_bit_exact(pkg, oracle, ctx, synth, leaf):
+    scan = synth.make_scan(3)
+    pts = _f32(scan.reshape(-1, 4))
+    pts = pts[np.abs(pts[:, :3]).sum(1) > 0]
+    g = pkg.mapping.voxel_grid(ctx, pts, leaf)
+    r = oracle.voxel_grid(pts, leaf, canonical=True)
+    assert np.array_equal(g, r)
+
+
+def _records_equal(ga, ra):
+    grec, gk = ga
+    rrec, rk = ra
+    assert np.array_equal(gk, rk)
+    v = gk >= 0
+    if not np.array_equal(grec[v], rrec[v]):
+        assert np.allclose(grec[v], rrec[v], rtol=1e-12, atol=1e-12)
+
+
+def test_associate_plane_and_line(pkg, oracle, ctx, synth):
+    M = synth.make_corridor_map(300_000, spacing=0.05)
+    E = synth.make_edge_map(40)
+    rng = np.random.default_rng(6)
+    truth = np.array([0, 0, 0, 1, 5.0, 0.1, 0.0])
+    x0 = synth.perturb_pose(truth[:4], truth[4:], 0.05, 0.5, seed=2)
+    gs, os_ = pkg.mapping.IkdMap(ctx, 0.4, 0.1), oracle.IkdMap(0.4)
+    gs.build(M)
+    os_.build(M)
+    Qs = M[rng.choice(len(M), 4000, replace=False)].copy()
+    Qs[:, :3] -= truth[4:7].astype(np.float32)
+    _records_equal(gs.associate(1, Qs, x0), os_.associate(1, Qs, x0))
+    gc, oc = pkg.mapping.IkdMap(ctx, 0.8, 0.2), oracle.IkdMap(0.8)
+    gc.build(E)
+    oc.build(E)
+    Qc = E[rng.choice(len(E), 600, replace=False)].copy()
+    Qc[:, :3] += rng.normal(0, 0.02, (600, 3)).astype(np.float32) - truth[4:7].astype(np.float32)
+    _records_equal(gc.associate(0, Qc, x0), oc.associate(0, Qc, x0))
+    gs.close()
+    gc.close()
+
+
+def test_normal_equations_and_solve(pkg, oracle, ctx, synth):
+    M = synth.make_corridor_map(300_000, spacing=0.05)
+    E = synth.make_edge_map(40)
+    rng = np.random.default_rng(7)
+    truth = np.array([0, 0, 0, 1, 5.0, 0.1, 0.0])
+    x0 = synth.perturb_pose(truth[:4], truth[4:], 0.05, 0.5, seed=4)
+    os_, oc = oracle.IkdMap(0.4), oracle.IkdMap(0.8)
+    os_.build(M)
+    oc.build(E)
+    Qs = M[rng.choice(len(M), 3000, replace=False)].copy()
+    Qs[:, :3] -= truth[4:7].astype(np.float32)
+    Qc = E[rng.choice(len(E), 500, replace=False)].copy()
+    Qc[:, :3] -= truth[4:7].astype(np.float32)
+    rs, ks = os_.associate(1, Qs, x0)
+    rc, kc = oc.associate(0, Qc, x0)
+    rec = np.concatenate([rc, rs])
+    kind = np.concatenate([kc, ks])
+    # normal equations vs the oracle's autodiff functors (same Huber corrector)
+    ne = pkg.mapping.normal_equations(ctx, rec, kind, x0)
+    acc = np.zeros(28)
+    for r9, kd in zip(rec, kind):
+        if kd < 0:
+            continue
+        if kd == 0:
+            r, J = oracle.eval_factor(0, r9, x0[:4], x0[4:])
+        else:
+            r, J = oracle.eval_factor(2, np.concatenate([r9[:7], np.zeros(5)]), x0[:4], x0[4:])
+        # local parameterization: d/d delta = J_q(4) * P(4x3)
+        q = x0[:4]
+        P = np.array([[q[3], q[2], -q[1]], [-q[2], q[3], q[0]], [q[1], -q[0], q[3]], [-q[0], -q[1], -q[2]]])
+        Jl = np.concatenate([J[:, :4] @ P, J[:, 4:]], axis=1)
+        s = float(r @ r)
+        if s > 0.01:
+            rr = np.sqrt(s)
+            acc[0] += 0.5 * (2 * 0.1 * rr - 0.01)
+            sc = np.sqrt(0.1 / rr)
+        else:
+            acc[0] += 0.5 * s
+            sc = 1.0
+        Jl, r = Jl * sc, r * sc
+        A = Jl.T @ Jl
+        acc[1:22] += A[np.triu_indices(6)]
+        acc[22:28] += Jl.T @ r
+    assert np.allclose(ne, acc, rtol=1e-9, atol=1e-12)
+    # the full solve (10 iterations, mapOptimization) vs the oracle's Ceres restatement
+    xg, sg = pkg.mapping.pose_solve(ctx, rec, kind, x0, 10)
+    xo, so = oracle.map_solve(rec, kind, x0, 10)
+    assert np.max(np.abs(xg - xo)) < POSE_TOL, (xg, xo)
+    assert sg[0] == so[0] and sg[1] == so[1]
+    assert sg[2] == (kind == 0).sum() and sg[3] == (kind == 2).sum()
+
+
+def test_mapopt_sequence(pkg, oracle, ctx, synth):
+    """mapOptimization ground-map stage over a short drive: Build on the first frame, then
+    VoxelGrid(0.8) + plane association + Ceres(10) + transformUpdate + Add_Points(0.4)."""
+    go = pkg.mapping.MapOptimization(ctx, 0.4, 0.2)
+    om = oracle.IkdMap(0.4)
+    ostate = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    for k in range(5):
+        scan = synth.make_scan(k).reshape(-1, 4)
+        ground = _f32(scan[np.abs(scan[:, :3]).sum(1) > 0])
+        q, t = synth.ground_truth_pose(k).as_qt()
+        odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=10 + k)  # drifting odometry
+        pg, sg = go.callback(ground, odom)
+        po, ostate, so = oracle.mapopt_step(om, ground, odom, ostate)
+        assert np.max(np.abs(pg - po)) < POSE_TOL, (k, pg, po)
+        assert np.max(np.abs(go.state - ostate)) < POSE_TOL, k
+        assert list(sg) == list(so), (k, sg, so)
+        assert go.map.size() == om.size(), k
+    go.map.close()
+
+
+def test_laser_mapping(pkg, oracle, ctx, synth):
+    M = synth.make_corridor_map(300_000, spacing=0.05)
+    E = synth.make_edge_map(40)
+    rng = np.random.default_rng(13)
+    truth = np.array([0, 0, 0, 1, 5.0, 0.1, 0.0])
+    x0 = synth.perturb_pose(truth[:4], truth[4:], 0.05, 0.5, seed=5)
+    gs, gc = pkg.mapping.IkdMap(ctx, 0.4, 0.1), pkg.mapping.IkdMap(ctx, 0.8, 0.2)
+    os_, oc = oracle.IkdMap(0.4), oracle.IkdMap(0.8)
+    for a, b, P in ((gs, os_, M), (gc, oc, E)):
+        a.build(P)
+        b.build(P)
+    Qs = M[rng.choice(len(M), 3000, replace=False)].copy()
+    Qs[:, :3] -= truth[4:7].astype(np.float32)
+    Qc = E[rng.choice(len(E), 400, replace=False)].copy()
+    Qc[:, :3] -= truth[4:7].astype(np.float32)
+    xg, stg = pkg.mapping.laser_mapping(gc, gs, Qc, Qs, x0)
+    xo, sto = oracle.laser_mapping(oc, os_, Qc, Qs, x0)
+    assert np.max(np.abs(xg - xo)) < POSE_TOL, (xg, xo)
+    assert list(stg) == list(sto)
+    assert np.linalg.norm(xg[4:] - truth[4:]) < np.linalg.norm(x0[4:] - truth[4:])
+    gs.close()
+    gc.close()
