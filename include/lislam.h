@@ -18,6 +18,18 @@
  *   lislam_eval_factors       <- ceres::CostFunction::Evaluate of LidarEdgeFactor /
  *                                LidarPlaneFactor / LidarPlaneNormFactor
  *                                                                      src/lidarFeaturePointsFunction.hpp:143-293
+ *   lislam_map_*              <- KD_TREE Build / Add_Points / Nearest_Search / size / flatten
+ *                                                                      src/ikd-Tree/ikd_Tree.h:256-279
+ *   lislam_map_associate      <- 5-NN line / plane association        src/laserMapping.cpp:668-796,
+ *                                                                      src/mapOptimization.cpp:376-429
+ *   lislam_normal_equations / lislam_pose_solve
+ *                             <- ceres::Solve(DENSE_QR) of those blocks (laserMapping.cpp:836-845,
+ *                                mapOptimization.cpp:433-442)
+ *   lislam_voxel_grid         <- pcl::VoxelGrid::filter                (scanRegistration.cpp:583-586,
+ *                                laserMapping.cpp:608-616, mapOptimization.cpp:368-370)
+ *   lislam_mapopt_step        <- mapOptimization::mapOptimizationCallback ground-map stage
+ *                                                                      src/mapOptimization.cpp:99-479
+ *   lislam_laser_mapping      <- laserMapping::process optimization    src/laserMapping.cpp:620-850
  */
 #ifndef LISLAM_H_
 #define LISLAM_H_
@@ -215,6 +227,15 @@ int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const doub
  * passes of association + Ceres(4 it).  stats[4] = corner / surf blocks of each pass. */
 int lislam_laser_mapping(lislam_map* corner_map, lislam_map* surf_map, const float* corner, int32_t n_corner,
                          const float* surf, int32_t n_surf, double* x, int32_t* stats);
+
+/* HIP-event timing of the mapping kernels of a context (recorded on its stream, no host sync
+ * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
+ * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
+ * clears the record. */
+#define LISLAM_MAP_NUM_KERNELS 6 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+                                    gather + cell table), Add_Points downsample (claim + resolve) */
+int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
+int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 
 #ifdef __cplusplus
 }

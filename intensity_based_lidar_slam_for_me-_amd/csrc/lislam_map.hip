@@ -39,7 +39,7 @@ namespace lislam {
 namespace mapk {
 
 constexpr uint64_t kEmptyKey = ~0ull;
-constexpr int kG = 16;          // lanes per query in k_knn
+constexpr int kG = 64;          // lanes per query in k_knn (one wavefront)
 constexpr int kMaxShell = 24;   // beyond this the search scans the whole map (unbounded max_dist only)
 constexpr float kInf = __builtin_huge_valf();
 
@@ -95,11 +95,17 @@ __global__ void k_gather(const float4* src, const int* perm, int n, float4* dst)
   if (i < n) dst[i] = src[perm[i]];
 }
 
-__global__ void k_count_runs(const uint64_t* keys, int n, int* count) {
+__global__ __launch_bounds__(256) void k_count_runs(const uint64_t* keys, int n, int* count) {
+  __shared__ int wsum[4];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool start = i < n && (i == 0 || keys[i] != keys[i - 1]);
   const uint64_t b = __ballot(start);
-  if (lane_id() == 0 && b) atomicAdd(count, __popcll(b));
+  if (lane_id() == 0) wsum[threadIdx.x >> 6] = __popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic per workgroup
+    const int t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(count, t);
+  }
 }
 
 __global__ void k_insert_runs(const uint64_t* keys, int n, uint64_t* hkey, int2* hval, uint32_t mask) {
@@ -206,42 +212,150 @@ __device__ __forceinline__ double block_gap(double q, int c, int s, double cell)
   return fmax(0.0, fmin(q - lo, hi - q) - tol);
 }
 
+// Cell (dx, dy, dz) number j of pass s: s == 1 the whole 3x3x3 block, s > 1 the 24 s^2 + 2
+// cells at Chebyshev distance s (two z faces, then the square rings of the z layers between).
+__device__ __forceinline__ void shell_cell(int s, int j, int& dx, int& dy, int& dz) {
+  if (s == 1) {
+    dz = j / 9 - 1;
+    dy = (j / 3) % 3 - 1;
+    dx = j % 3 - 1;
+    return;
+  }
+  const int side = 2 * s + 1, face = side * side;
+  if (j < 2 * face) {
+    dz = j < face ? -s : s;
+    const int r = j % face;
+    dx = r % side - s;
+    dy = r / side - s;
+    return;
+  }
+  const int jj = j - 2 * face, ring = 8 * s;
+  dz = jj / ring - (s - 1);
+  const int r = jj % ring, e = r / (2 * s), o = r % (2 * s);
+  if (e == 0) { dx = -s + o; dy = -s; }
+  else if (e == 1) { dx = s; dy = -s + o; }
+  else if (e == 2) { dx = s - o; dy = s; }
+  else { dx = -s; dy = s - o; }
+}
+
+// lower bound of the squared distance from q to any point stored in cell (ix, iy, iz): the box
+// [i c, (i+1) c] widened by the rounding of floor(p / c), squared in double, shrunk by 1e-6
+__device__ __forceinline__ double cell_lb2(const float4& q, int ix, int iy, int iz, float cell) {
+  const double c = cell;
+  const double qs[3] = {q.x, q.y, q.z};
+  const int is[3] = {ix, iy, iz};
+  double s2 = 0;
+  for (int a = 0; a < 3; a++) {
+    const double lo = (double)is[a] * c, hi = lo + c;
+    const double tol = 1e-6 * (fabs(qs[a]) + fabs(lo) + c) + 1e-9;
+    const double g = fmax(0.0, fmax((lo - tol) - qs[a], qs[a] - (hi + tol)));
+    s2 += g * g;
+  }
+  return s2 * (1.0 - 1e-6);
+}
+
+// mg.d[k - 1] without a dynamic register index
+template <int K>
+__device__ __forceinline__ float kth_of(const KBest<K>& mg, int k) {
+  float v = kInf;
+#pragma unroll
+  for (int r = 0; r < K; r++) v = r == k - 1 ? mg.d[r] : v;
+  return v;
+}
+
+// Block b of a grid of nblk is dealt to XCD b % 8; give each XCD one contiguous range of
+// (spatially ordered) queries so the cells it walks stay in its own L2.  Bijective for any nblk.
+__device__ __forceinline__ int xcd_block(int b, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7, x = b & 7;
+  return x * q + min(x, r) + (b >> 3);
+}
+
+// One pass over `total` cells (the 3x3x3 block for s == 1, else the shell at radius s): lanes
+// probe one cell each (skipping cells whose box cannot beat `bound`), then the points of the
+// probed cells are dealt evenly over the 64 lanes (exclusive prefix of the counts + a 6-step
+// binary search per point), four loads in flight per lane.
+template <int K>
+__device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int cx, int cy, int cz, int s, float bound,
+                                         float max_d2, KBest<K>& b) {
+  const int lane = threadIdx.x & 63;
+  const int total = s == 1 ? 27 : 24 * s * s + 2;
+  for (int j0 = 0; j0 < total; j0 += 64) {
+    const int j = j0 + lane;
+    int cnt = 0, beg = 0;
+    if (j < total) {
+      int dx, dy, dz;
+      shell_cell(s, j, dx, dy, dz);
+      if (s == 1 || cell_lb2(q, cx + dx, cy + dy, cz + dz, m.cell) <= (double)bound) {
+        const int2 r = cell_lookup(m, pack_cell(cx + dx, cy + dy, cz + dz));
+        beg = r.x;
+        cnt = r.y;
+      }
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int T = __shfl(incl, 63, 64);
+    const int excl = incl - cnt;
+    for (int t0 = 0; t0 < T; t0 += 4 * 64) {
+      int pi[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int t = t0 + u * 64 + lane;
+        int lo = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const int e = __shfl(excl, lo + st, 64);
+          if (e <= t) lo += st;
+        }
+        const int bb = __shfl(beg, lo, 64), ee = __shfl(excl, lo, 64);
+        pi[u] = t < T ? bb + (t - ee) : -1;
+      }
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[u] = pi[u] >= 0 ? m.pts[pi[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (pi[u] < 0) continue;
+        const float d = calc_dist(q.x, q.y, q.z, v[u].x, v[u].y, v[u].z);
+        if (d <= max_d2) kb_insert(b, d, __float_as_int(v[u].w), pi[u]);
+      }
+    }
+  }
+}
+
 // queries: n points of `stride` floats (optionally counted on the device: *qcount); pose
 // (device, nullable): queries are sensor-frame points mapped by pointAssociateToMap first.
 template <int K>
 __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, int stride, const int* qcount, int nq,
                                              const double* pose, int k, float max_d2, float4* out_pts, float* out_d2,
                                              int* out_found) {
-  const int qi = (blockIdx.x * blockDim.x + threadIdx.x) / kG;
-  const int gl = threadIdx.x & (kG - 1);
+  const int qi = xcd_block(blockIdx.x, gridDim.x) * (256 / kG) + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int n = qcount ? min(*qcount, nq) : nq;
-  if (qi >= n) return;  // whole groups leave together
+  if (qi >= n) return;  // whole waves leave
   const float* qp = queries + (size_t)qi * stride;
   float4 q = make_float4(qp[0], qp[1], qp[2], 0.f);
   if (pose) q = to_world(pose, q.x, q.y, q.z);
   const int cx = cell_of(q.x, m.inv_cell), cy = cell_of(q.y, m.inv_cell), cz = cell_of(q.z, m.inv_cell);
   KBest<K> b, mg;
   kb_clear(b);
+  kb_clear(mg);
   const double maxd = sqrt((double)max_d2);
   for (int s = 1;; s++) {
-    const int side = 2 * s + 1, plane = side * side, total = plane * side;
-    for (int j = gl; j < total; j += kG) {
-      const int dz = j / plane - s, rem = j % plane, dy = rem / side - s, dx = rem % side - s;
-      if (s > 1 && max(abs(dx), max(abs(dy), abs(dz))) < s) continue;  // inner block already walked
-      const int2 r = cell_lookup(m, pack_cell(cx + dx, cy + dy, cz + dz));
-      for (int p = r.x; p < r.x + r.y; p++) {
-        const float4 v = m.pts[p];
-        const float d = calc_dist(q.x, q.y, q.z, v.x, v.y, v.z);
-        if (d <= max_d2) kb_insert(b, d, __float_as_int(v.w), p);
-      }
-    }
+    // a cell is probed only if its (conservative) box distance can beat the current k-th best
+    const float bound = fminf(max_d2, s == 1 ? kInf : kth_of(mg, k));
+    knn_pass(m, q, cx, cy, cz, s, bound, max_d2, b);
     group_merge(b, mg);
+    const float kth = kth_of(mg, k);
     const double gap = fmin(block_gap(q.x, cx, s, m.cell), fmin(block_gap(q.y, cy, s, m.cell), block_gap(q.z, cz, s, m.cell)));
     if (gap >= maxd * (1.0 + 1e-6)) break;                                  // every point within max_dist seen
-    if (mg.d[k - 1] != kInf && (double)mg.d[k - 1] < gap * gap * (1.0 - 1e-6)) break;  // none closer outside
+    if (kth != kInf && (double)kth < gap * gap * (1.0 - 1e-6)) break;  // none closer outside
     if (s >= kMaxShell) {                                                   // far from the map: scan it all
       kb_clear(b);
-      for (int p = gl; p < m.n; p += kG) {
+      for (int p = lane; p < m.n; p += 64) {
         const float4 v = m.pts[p];
         const float d = calc_dist(q.x, q.y, q.z, v.x, v.y, v.z);
         if (d <= max_d2) kb_insert(b, d, __float_as_int(v.w), p);
@@ -250,15 +364,17 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
       break;
     }
   }
-  if (gl != 0) return;
   int found = 0;
-  for (int r = 0; r < k; r++) {
+#pragma unroll
+  for (int r = 0; r < K; r++) found += (r < k && mg.d[r] != kInf);
+#pragma unroll
+  for (int r = 0; r < K; r++) {
+    if (r >= k || lane != r) continue;
     const bool ok = mg.d[r] != kInf;
-    found += ok;
     if (out_pts) out_pts[(size_t)qi * k + r] = ok ? m.pts[mg.ix[r]] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (out_d2) out_d2[(size_t)qi * k + r] = mg.d[r];
   }
-  if (out_found) out_found[qi] = found;
+  if (out_found && lane == 0) out_found[qi] = found;
 }
 
 // ------------------------------------------------------------------ fits (fp64, one thread per query)
@@ -646,7 +762,7 @@ __global__ void k_vg_centroids(const float4* in, const uint32_t* skeys, const in
 
 // ------------------------------------------------------------------ multi-workgroup pose solve
 constexpr int kEvalThreads = 256;
-constexpr int kMaxParts = 1024;
+constexpr int kMaxParts = 256;
 constexpr int kPart = kAcc + 2;  // acc + edge / plane block counts
 
 struct LmDev {
@@ -665,11 +781,10 @@ __global__ void k_lm_init(LmDev* st, const double* x0) {
   st->s.term = 1;
 }
 
-__global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, const int* kind, const int* ncount, int n,
-                                                          LmDev* st, double* partial) {
-  if (!st->flag) return;
+// This workgroup's partial (acc + block counts) of the evaluation at st->xe.
+__device__ __forceinline__ void lm_eval_partial(const double* rec, const int* kind, int nn, const LmDev* st,
+                                                double* partial) {
   __shared__ double red[kEvalThreads / 16][kPart];
-  const int nn = ncount ? min(*ncount, n) : n;
   double acc[kPart];
 #pragma unroll
   for (int e = 0; e < kPart; e++) acc[e] = 0;
@@ -695,17 +810,35 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, con
   }
 }
 
+__global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, const int* kind, const int* ncount, int n,
+                                                          LmDev* st, double* partial) {
+  if (!st->flag) return;
+  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
+}
+
+// The trust-region step after an evaluation: sums the workgroup partials in order
+// (deterministic), then one thread advances the LM state (held in registers for the step).
 __global__ __launch_bounds__(64) void k_lm_step(LmDev* st, const double* partial, int nparts, int max_it) {
   if (!st->flag) return;
   __shared__ double acc[kPart];
-  if (threadIdx.x < kPart) {
-    double v = 0;
-    for (int p = 0; p < nparts; p++) v += partial[(size_t)p * kPart + threadIdx.x];
-    acc[threadIdx.x] = v;
+  // thread t sums parts t, t+64, ... (all loads in flight), then a fixed xor tree over the wave
+  double v[kPart];
+#pragma unroll
+  for (int e = 0; e < kPart; e++) v[e] = 0;
+  for (int p = threadIdx.x; p < nparts; p += 64) {
+#pragma unroll
+    for (int e = 0; e < kPart; e++) v[e] += partial[(size_t)p * kPart + e];
+  }
+#pragma unroll
+  for (int e = 0; e < kPart; e++) {
+    double x = v[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (threadIdx.x == 0) acc[e] = x;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  LM& s = st->s;
+  LM s = st->s;
   bool cont;
   if (st->phase == 0) {
     st->nedge = (int)acc[kAcc];
@@ -717,11 +850,14 @@ __global__ __launch_bounds__(64) void k_lm_step(LmDev* st, const double* partial
       s.term = 1;
       cont = false;
     } else {
-      cont = lm_start(s, st->x0, acc, max_it);
+      double x0[7];
+      for (int e = 0; e < 7; e++) x0[e] = st->x0[e];
+      cont = lm_start(s, x0, acc, max_it);
     }
   } else {
     cont = lm_next(s, acc, max_it);
   }
+  st->s = s;
   st->flag = cont;
   if (cont)
     for (int e = 0; e < 7; e++) st->xe[e] = s.xc[e];
@@ -802,6 +938,24 @@ int mfail(lislam_ctx* c, int code, const char* fmt, ...) {
     int rc_ = (x);                \
     if (rc_ != LISLAM_OK) return rc_; \
   } while (0)
+
+// kernel ids of lislam_map_kernel_times
+enum { kT_knn = 0, kT_fit, kT_lm_eval, kT_lm_step, kT_rebuild, kT_downsample, kT_count };
+
+struct TimedScope {
+  lislam_ctx* c;
+  int id;
+  hipEvent_t b = nullptr;
+  TimedScope(lislam_ctx* c_, int id_) : c(c_), id(id_) {
+    if (c->mtimer.on) { b = c->mtimer.get(); (void)hipEventRecord(b, c->stream); }
+  }
+  ~TimedScope() {
+    if (!b) return;
+    hipEvent_t e = c->mtimer.get();
+    (void)hipEventRecord(e, c->stream);
+    c->mtimer.rec.push_back({id, {b, e}});
+  }
+};
 
 inline int blocks(int64_t n, int t = 256) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
 
@@ -892,6 +1046,7 @@ int rebuild(lislam_map* m, int64_t n) {
   MCHK(c, m->idx2.reserve(n * 4));
   MCHK(c, m->counter.reserve(16));
   const float inv = 1.0f / m->cell;
+  TimedScope ts(c, kT_rebuild);
   hipLaunchKernelGGL(k_cell_keys, dim3(blocks(n)), dim3(256), 0, st, m->tmp.as<float4>(), (int)n, inv,
                      m->keys.as<uint64_t>(), m->idx.as<int>());
   MRC(sort_pairs_u64(c, m->sort_tmp, m->keys.as<uint64_t>(), m->keys2.as<uint64_t>(), m->idx.as<int>(), m->idx2.as<int>(),
@@ -962,8 +1117,11 @@ int add_packed(lislam_map* m, int64_t nin, bool downsample, int64_t* n_added) {
   a.nbox = m->counter.as<int>();
   a.dead = m->dead.as<uint8_t>();
   a.enter = m->enter.as<uint8_t>();
-  hipLaunchKernelGGL(k_ds_claim, dim3(blocks(nin)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_ds_resolve, dim3(blocks(nin)), dim3(256), 0, st, a);
+  {
+    TimedScope ts(c, kT_downsample);
+    hipLaunchKernelGGL(k_ds_claim, dim3(blocks(nin)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_ds_resolve, dim3(blocks(nin)), dim3(256), 0, st, a);
+  }
   // survivors (stable) + entering inputs (input order) -> tmp
   MCHK(c, m->tmp.reserve((n0 + nin) * sizeof(float4)));
   MCHK(c, m->live.reserve(std::max<int64_t>(n0, 1)));
@@ -999,8 +1157,9 @@ int knn_device(lislam_map* m, const float* q, int stride, const int* qcount, int
                float4* out_pts, float* out_d2, int* out_found) {
   lislam_ctx* c = m->ctx;
   if (n <= 0) return LISLAM_OK;
-  const int nb = blocks((int64_t)n * kG);
+  const int nb = blocks((int64_t)n * kG);  // one wavefront per query
   MapView v = m->view();
+  TimedScope ts(c, kT_knn);
   if (k <= 5)
     hipLaunchKernelGGL(k_knn<5>, dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2, out_pts,
                        out_d2, out_found);
@@ -1025,8 +1184,11 @@ int associate_device(lislam_map* m, int match, const float* q, int stride, const
     MRC(knn_device(m, q, stride, qcount, n, pose, 5, 1.0f, m->sc.nb.as<float4>(), m->sc.d2.as<float>(),
                    m->sc.found.as<int>()));
   }
-  hipLaunchKernelGGL(k_fit, dim3(blocks(n)), dim3(256), 0, stream_of(c), match, q, stride, qcount, n,
-                     m->sc.nb.as<float4>(), m->sc.d2.as<float>(), m->sc.found.as<int>(), rec, kind);
+  {
+    TimedScope ts(c, kT_fit);
+    hipLaunchKernelGGL(k_fit, dim3(blocks(n)), dim3(256), 0, stream_of(c), match, q, stride, qcount, n,
+                       m->sc.nb.as<float4>(), m->sc.d2.as<float>(), m->sc.found.as<int>(), rec, kind);
+  }
   MCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -1041,7 +1203,12 @@ int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* ki
   const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
   hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev);
   for (int e = 0; e <= max_it; e++) {  // initial evaluation + at most one per iteration
-    hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm, sc.partial.as<double>());
+    {
+      TimedScope ts(c, kT_lm_eval);
+      hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
+                         sc.partial.as<double>());
+    }
+    TimedScope ts(c, kT_lm_step);
     hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(64), 0, st, lm, sc.partial.as<double>(), parts, max_it);
   }
   MCHK(c, hipGetLastError());
@@ -1125,6 +1292,29 @@ int lislam_map_create(lislam_ctx* c, const lislam_map_config* cfg, lislam_map** 
   m->ds = cfg->downsample_size;
   m->cell = cfg->cell_size > 0 ? cfg->cell_size : cfg->downsample_size;
   *out = m;
+  return LISLAM_OK;
+}
+
+int lislam_map_set_timing(lislam_ctx* c, int32_t enable) {
+  if (!c) return LISLAM_ERR_ARG;
+  c->mtimer.on = enable != 0;
+  return LISLAM_OK;
+}
+
+int lislam_map_kernel_times(lislam_ctx* c, float* ms, int32_t* launches) {
+  if (!c || !ms) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  MCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < kT_count; k++) { ms[k] = 0; if (launches) launches[k] = 0; }
+  for (auto& r : c->mtimer.rec) {
+    float t = 0;
+    MCHK(c, hipEventElapsedTime(&t, r.second.first, r.second.second));
+    ms[r.first] += t;
+    if (launches) launches[r.first]++;
+    c->mtimer.pool.push_back(r.second.first);
+    c->mtimer.pool.push_back(r.second.second);
+  }
+  c->mtimer.rec.clear();
   return LISLAM_OK;
 }
 

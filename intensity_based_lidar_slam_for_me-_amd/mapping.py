@@ -26,7 +26,7 @@ def _as_points(points):
             raise ValueError("points must be a float32 (n, 3|4) tensor")
         return ctypes.c_void_p(t.data_ptr()), t.shape[0], t.shape[1], t
     a = np.ascontiguousarray(points, np.float32)
-    if a.ndim != 2 or a.shape[1] < 3:
+    if a.ndim != 2 or (a.shape[1] < 3 and a.shape[0] > 0):
         raise ValueError("points must be (n, 3|4)")
     return ctypes.c_void_p(a.ctypes.data), a.shape[0], a.shape[1], a
 
@@ -154,12 +154,28 @@ class MapOptimization:
 
 
 def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):
-    """laserMapping optimization: (x (7,), stats (corner / surf blocks of the two passes))."""
-    c = np.ascontiguousarray(corner, np.float32).reshape(-1, 4)
-    s = np.ascontiguousarray(surf, np.float32).reshape(-1, 4)
+    """laserMapping optimization: (x (7,), stats (corner / surf blocks of the two passes)).
+    corner / surf: (n, 4) float32 host arrays or device tensors (read in place)."""
+    cp, nc, cs, _kc = _as_points(corner if len(corner) else np.zeros((0, 4), np.float32))
+    sp, ns, ss, _ks = _as_points(surf if len(surf) else np.zeros((0, 4), np.float32))
+    if (nc and cs != 4) or (ns and ss != 4):
+        raise ValueError("laser_mapping expects (n, 4) point arrays")
     x = np.array(x0, np.float64)
     st = np.zeros(4, np.int32)
     ctx = corner_map.ctx
-    nat.check(ctx.lib.lislam_laser_mapping(corner_map.h, surf_map.h, nat.ptr(c), c.shape[0], nat.ptr(s), s.shape[0],
-                                           nat.ptr(x), nat.ptr(st)), ctx.h, "lislam_laser_mapping")
+    nat.check(ctx.lib.lislam_laser_mapping(corner_map.h, surf_map.h, cp, nc, sp, ns, nat.ptr(x), nat.ptr(st)), ctx.h,
+              "lislam_laser_mapping")
     return x, st
+
+def set_timing(ctx, on: bool):
+    nat.check(ctx.lib.lislam_map_set_timing(ctx.h, int(on)), ctx.h, "lislam_map_set_timing")
+
+
+def kernel_times(ctx):
+    """{kernel: (total ms, launches)} of the mapping kernels since the previous read."""
+    ms = np.zeros(len(nat.MAP_KERNELS), np.float32)
+    n = np.zeros(len(nat.MAP_KERNELS), np.int32)
+    nat.check(ctx.lib.lislam_map_kernel_times(ctx.h, ms.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                              n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), ctx.h,
+              "lislam_map_kernel_times")
+    return {k: (float(a), int(b)) for k, a, b in zip(nat.MAP_KERNELS, ms, n)}

@@ -33,7 +33,10 @@ EXPORTED_SYMBOLS = (
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
     "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_laser_mapping",
+    "lislam_map_set_timing", "lislam_map_kernel_times",
 )
+
+MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample")
 
 MATCH_LINE, MATCH_PLANE = 0, 1
 
@@ -131,6 +134,8 @@ def load(path: str = LIB_PATH):
     L.lislam_voxel_grid.argtypes = [vp, vp, _i32, ctypes.c_float, vp, _i32p]
     L.lislam_mapopt_step.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
     L.lislam_laser_mapping.argtypes = [vp, vp, vp, _i32, vp, _i32, vp, vp]
+    L.lislam_map_set_timing.argtypes = [vp, _i32]
+    L.lislam_map_kernel_times.argtypes = [vp, _fp, _i32p]
     for name in EXPORTED_SYMBOLS:
         getattr(L, name).restype = getattr(L, name).restype or ctypes.c_int
     L.lislam_last_error.restype = ctypes.c_char_p
