@@ -148,6 +148,11 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
 #define LISLAM_OUT_PARA 11           /* double [7]   */
 #define LISLAM_OUT_POSE 12           /* double [7]   */
 #define LISLAM_OUT_STATS 13          /* int32  [8]   */
+#define LISLAM_OUT_ORB_T 14          /* double [7]   T_s2s of pair (scan-1, scan) (q x,y,z,w, t) */
+#define LISLAM_OUT_ORB_STATS 15      /* int32  [8]   see lislam_intensity_tracker_step */
+#define LISLAM_OUT_ORB_KEYPOINTS 16  /* float  [n][6] of the nfeatures detection */
+#define LISLAM_OUT_ORB_POINTS 17     /* float4 [n]   their cloud_track points */
+#define LISLAM_OUT_ORB_DESCRIPTORS 18 /* uint8 [n][32] */
 /* Copy one output of one scan to host memory; cap/n count elements of the listed type. */
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n);
 
@@ -158,6 +163,32 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
  * parameterization Jacobians jac[3n x 6] (d/d delta-theta, d/d t), both optional. */
 int lislam_eval_factors(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,
                         const double* t, double* residuals, double* jac);
+
+/* ---------------------------------------------------------------- ORB intensity front end (a8-a11) */
+/* cv::ORB::create(nfeatures, 1.2f, 8, 1) detect (with the feature_tracker MASK, H x W u8, 0 =
+ * blocked; null = none) + extractPointsAndFilterZeroValue + compute on one intensity image
+ * (intensity_feature_tracker.cpp:609-628, :1071-1099).  kp[n][6] = x, y, size, angle (deg),
+ * response, octave; desc[n][32]; p3d[n][4] = the cloud_track point (x, y, z, 0).  cloud_track is
+ * the organized H*W float4 cloud of ImageHandler::cloud_handler.  Host or device pointers. */
+int lislam_orb_detect(lislam_ctx* ctx, const uint8_t* image, const float* cloud_track, const uint8_t* mask, int32_t H,
+                      int32_t W, int32_t nfeatures, float* kp, uint8_t* desc, float* p3d, int32_t cap, int32_t* n);
+/* BFMatcher(NORM_HAMMING, crossCheck=true).match(query, train) (:631): matches[m][3] = query,
+ * train, distance in query order (capacity nq). */
+int lislam_orb_match(lislam_ctx* ctx, const uint8_t* qdesc, int32_t nq, const uint8_t* tdesc, int32_t nt,
+                     int32_t* matches, int32_t* n_matches);
+/* feature_tracker::detectfeatures (intensity_feature_tracker.cpp:597-738): one frame per step,
+ * state = the previous frame.  T_s2s[7] = (q x,y,z,w, t) of p2p_calculateRandT (identity when
+ * the frame is skipped); stats[8] = good (1) / skipped (0) / first frame (-1), re-detected,
+ * keypoints, matches, good matches, LM iterations, LM termination, previous keypoints. */
+typedef struct lislam_intensity_tracker lislam_intensity_tracker;
+int lislam_intensity_tracker_create(lislam_ctx* ctx, int32_t H, int32_t W, int32_t nfeatures, const uint8_t* mask,
+                                    lislam_intensity_tracker** out);
+int lislam_intensity_tracker_destroy(lislam_intensity_tracker* t);
+int lislam_intensity_tracker_step(lislam_intensity_tracker* t, const uint8_t* image, const float* cloud_track,
+                                  double* T_s2s, int32_t* stats);
+/* detectfeatures over scans [0, n_scans) of a batch (its a1 images, want_images = 1): scan k is
+ * matched against scan k-1 exactly as the tracker would; outputs LISLAM_OUT_ORB_*. */
+int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask);
 
 /* ---------------------------------------------------------------- scan-to-map (a19-a21) */
 /* A device-resident point map with the semantics of the vendored ikd-Tree
@@ -232,8 +263,10 @@ int lislam_laser_mapping(lislam_map* corner_map, lislam_map* surf_map, const flo
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
  * clears the record. */
-#define LISLAM_MAP_NUM_KERNELS 6 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
-                                    gather + cell table), Add_Points downsample (claim + resolve) */
+#define LISLAM_MAP_NUM_KERNELS 14 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+                                     gather + cell table), Add_Points downsample (claim + resolve),
+                                     k_orb_pyramid, k_orb_fast, k_orb_select, k_orb_finish,
+                                     k_orb_blur, k_orb_desc, k_orb_match, k_orb_lm */
 int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
 int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 

@@ -4,7 +4,7 @@ Import with ``importlib.import_module("intensity_based_lidar_slam_for_me-_amd")`
 name is not a Python identifier).  The compute path is the HIP library ``liblislam.so`` built by
 ``__graft_entry__.build()``; there is no CPU fallback.
 """
-from . import mapping, native, synth  # noqa: F401
+from . import intensity, mapping, native, synth  # noqa: F401
 from .frontend import Batch, Context, Features, LaserOdometry, ScanRegistration, eval_factors  # noqa: F401
 
-__all__ = ["mapping", "native", "synth", "Batch", "Context", "Features", "LaserOdometry", "ScanRegistration", "eval_factors"]
+__all__ = ["intensity", "mapping", "native", "synth", "Batch", "Context", "Features", "LaserOdometry", "ScanRegistration", "eval_factors"]

@@ -11,41 +11,12 @@
 #include <vector>
 
 #include "../../include/lislam.h"
+#include "lislam_batch.hpp"
 #include "lislam_ctx.hpp"
 #include "lislam_internal.hpp"
 
 using namespace lislam;
 
-
-struct lislam_batch {
-  lislam_ctx* ctx = nullptr;
-  int max_scans = 0, H = 0, W = 0, N = 0;
-  int cap_sharp = 0, cap_less_sharp = 0, cap_flat = 0;
-  std::vector<void*> allocs;
-  FeatureArgs fa{};
-  OdomArgs oa{};
-  double* d_init = nullptr;
-  bool timing = false;
-  // per-call event sets recorded on the stream while timing is on; read back (and released)
-  // by lislam_batch_kernel_times, so the timed region never blocks on the host.
-  std::vector<std::vector<hipEvent_t>> ext_ev, odo_ev;
-  std::vector<hipEvent_t> pool;
-  int extracted = 0;
-  hipEvent_t get_event() {
-    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
-    hipEvent_t e = nullptr;
-    hipEventCreate(&e);
-    return e;
-  }
-  static hipEvent_t event_cb(void* self) { return static_cast<lislam_batch*>(self)->get_event(); }
-};
-
-struct lislam_odom {
-  lislam_ctx* ctx = nullptr;
-  bool have_last = false;
-  double state[14] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0};
-  int frames = 0;
-};
 
 namespace {
 
@@ -245,6 +216,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   for (auto& v : b->ext_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (auto& v : b->odo_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
+  if (b->orb) lislam_free_orb(b->orb);
   delete b;
   return LISLAM_OK;
 }
@@ -413,6 +385,15 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
     case LISLAM_OUT_PARA: src = o.para + (size_t)scan * 7; cnt = 7; esz = 8; break;
     case LISLAM_OUT_POSE: src = o.pose + (size_t)scan * 7; cnt = 7; esz = 8; break;
     case LISLAM_OUT_STATS: src = o.stats + (size_t)scan * 8; cnt = 8; esz = 4; break;
+    case LISLAM_OUT_ORB_T:
+    case LISLAM_OUT_ORB_STATS:
+    case LISLAM_OUT_ORB_KEYPOINTS:
+    case LISLAM_OUT_ORB_POINTS:
+    case LISLAM_OUT_ORB_DESCRIPTORS: {
+      const int rc = lislam_orb_batch_output(b, what, scan, &src, &cnt, &esz);
+      if (rc) return fail(c, rc, "ORB output %d unavailable (run lislam_batch_intensity_odometry first)", what);
+      break;
+    }
     default: return fail(c, LISLAM_ERR_ARG, "unknown output %d", what);
   }
   if (!src) return fail(c, LISLAM_ERR_STATE, "output %d not materialized (want_images=0?)", what);

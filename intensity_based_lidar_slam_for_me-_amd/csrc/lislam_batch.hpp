@@ -1,0 +1,49 @@
+// The device-resident batch and laserOdometry node objects behind the lislam C ABI, shared by
+// the ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/lislam.h"
+#include "lislam_internal.hpp"
+
+using lislam::FeatureArgs;
+using lislam::OdomArgs;
+
+struct lislam_batch {
+  lislam_ctx* ctx = nullptr;
+  int max_scans = 0, H = 0, W = 0, N = 0;
+  int cap_sharp = 0, cap_less_sharp = 0, cap_flat = 0;
+  std::vector<void*> allocs;
+  FeatureArgs fa{};
+  OdomArgs oa{};
+  double* d_init = nullptr;
+  bool timing = false;
+  // per-call event sets recorded on the stream while timing is on; read back (and released)
+  // by lislam_batch_kernel_times, so the timed region never blocks on the host.
+  std::vector<std::vector<hipEvent_t>> ext_ev, odo_ev;
+  std::vector<hipEvent_t> pool;
+  int extracted = 0;
+  void* orb = nullptr;  // ORB engine of lislam_batch_intensity_odometry (lislam_orb.hip)
+  hipEvent_t get_event() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+  }
+  static hipEvent_t event_cb(void* self) { return static_cast<lislam_batch*>(self)->get_event(); }
+};
+
+struct lislam_odom {
+  lislam_ctx* ctx = nullptr;
+  bool have_last = false;
+  double state[14] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0};
+  int frames = 0;
+};
+
+
+// Frees lislam_batch::orb (lislam_orb.hip).
+void lislam_free_orb(void* p);
+// Device source of the ORB outputs (LISLAM_OUT_ORB_*) of one scan (lislam_orb.hip).
+int lislam_orb_batch_output(lislam_batch* b, int what, int scan, const void** src, int* cnt, size_t* esz);

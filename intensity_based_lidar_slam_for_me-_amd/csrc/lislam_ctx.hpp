@@ -38,5 +38,28 @@ struct lislam_ctx {
   lislam_ktimer mtimer;            // mapping-kernel timing
 };
 
+// kernel ids of lislam_map_kernel_times (LISLAM_CTX_NUM_KERNELS in include/lislam.h)
+enum {
+  kT_knn = 0, kT_fit, kT_lm_eval, kT_lm_step, kT_rebuild, kT_downsample,
+  kT_orb_pyramid, kT_orb_fast, kT_orb_select, kT_orb_finish, kT_orb_blur, kT_orb_desc, kT_orb_match, kT_orb_lm,
+  kT_count
+};
+
+// Records HIP events around the launches of its scope when the context's timer is on.
+struct TimedScope {
+  lislam_ctx* c;
+  int id;
+  hipEvent_t b = nullptr;
+  TimedScope(lislam_ctx* c_, int id_) : c(c_), id(id_) {
+    if (c->mtimer.on) { b = c->mtimer.get(); (void)hipEventRecord(b, c->stream); }
+  }
+  ~TimedScope() {
+    if (!b) return;
+    hipEvent_t e = c->mtimer.get();
+    (void)hipEventRecord(e, c->stream);
+    c->mtimer.rec.push_back({id, {b, e}});
+  }
+};
+
 // Frees lislam_ctx::map_scratch (lislam_map.hip).
 void lislam_free_map_scratch(void* p);

@@ -53,6 +53,18 @@ __device__ __forceinline__ void plane_norm_factor(const DQ& q, const D3& t, cons
   J[3] = n.x; J[4] = n.y; J[5] = n.z;
 }
 
+// front_end_residual (hpp:21-58): r = q c + t - dst (3 residuals).
+__device__ __forceinline__ void p2p_factor(const DQ& q, const D3& t, const D3& c, const D3& dst, double* r,
+                                           double (*J)[6]) {
+  const D3 p = qrot(q, c);
+  const D3 w = p + t;
+  r[0] = w.x - dst.x; r[1] = w.y - dst.y; r[2] = w.z - dst.z;
+  if (!J) return;
+  const double P[3][3] = {{0, 2 * p.z, -2 * p.y}, {-2 * p.z, 0, 2 * p.x}, {2 * p.y, -2 * p.x, 0}};  // -2[p]x
+  for (int i = 0; i < 3; i++)
+    for (int cc = 0; cc < 3; cc++) { J[i][cc] = P[i][cc]; J[i][3 + cc] = i == cc ? 1.0 : 0.0; }
+}
+
 // LidarPlaneFactor constructor: ljm_norm = normalize((j - l) x (j - m)) (Eigen normalize()).
 __device__ __forceinline__ D3 plane_normal(const D3& j, const D3& l, const D3& m) {
   D3 n = cross(j - l, j - m);

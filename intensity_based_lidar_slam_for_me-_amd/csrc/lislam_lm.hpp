@@ -8,6 +8,7 @@
 //   0 LidarEdgeFactor(curr, a, b, s=1)         rec = curr, a, b
 //   1 LidarPlaneFactor(curr, j, l, m, s=1)     rec = curr, j, unit normal of the constructor
 //   2 LidarPlaneNormFactor(curr, n, d)         rec = curr, n, d, -, -
+//   3 front_end_residual(src, dst)             rec = src, dst, -, -, -
 // every one under the same HuberLoss(0.1) (laserOdometry.cpp:424, laserMapping.cpp:646,
 // mapOptimization.cpp:233).  One evaluation = cost, J^T J (21, upper) and J^T r (6) of the
 // loss-corrected residuals in the local parameterization = 28 doubles ("acc").  The step logic
@@ -39,9 +40,12 @@ __device__ __forceinline__ void accum_row(double* acc, const double* J, double r
 __device__ __forceinline__ void block_accum(int kd, const double* r9, const DQ& q, const D3& t, double* acc) {
   const double ha = 0.1;  // HuberLoss(0.1)
   const D3 c{r9[0], r9[1], r9[2]};
-  if (kd == 0) {
+  if (kd == 0 || kd == 3) {
     double res[3], J[3][6];
-    edge_factor(q, t, c, D3{r9[3], r9[4], r9[5]}, D3{r9[6], r9[7], r9[8]}, res, J);
+    if (kd == 0)
+      edge_factor(q, t, c, D3{r9[3], r9[4], r9[5]}, D3{r9[6], r9[7], r9[8]}, res, J);
+    else
+      p2p_factor(q, t, c, D3{r9[3], r9[4], r9[5]}, res, J);
     const double sc = huber_scale(ha, res[0] * res[0] + res[1] * res[1] + res[2] * res[2], &acc[0]);
     for (int k = 0; k < 3; k++) {
       double Js[6];

@@ -939,24 +939,6 @@ int mfail(lislam_ctx* c, int code, const char* fmt, ...) {
     if (rc_ != LISLAM_OK) return rc_; \
   } while (0)
 
-// kernel ids of lislam_map_kernel_times
-enum { kT_knn = 0, kT_fit, kT_lm_eval, kT_lm_step, kT_rebuild, kT_downsample, kT_count };
-
-struct TimedScope {
-  lislam_ctx* c;
-  int id;
-  hipEvent_t b = nullptr;
-  TimedScope(lislam_ctx* c_, int id_) : c(c_), id(id_) {
-    if (c->mtimer.on) { b = c->mtimer.get(); (void)hipEventRecord(b, c->stream); }
-  }
-  ~TimedScope() {
-    if (!b) return;
-    hipEvent_t e = c->mtimer.get();
-    (void)hipEventRecord(e, c->stream);
-    c->mtimer.rec.push_back({id, {b, e}});
-  }
-};
-
 inline int blocks(int64_t n, int t = 256) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
 
 // Growable device buffer.

@@ -1,0 +1,1412 @@
+// lislam ORB intensity front end on gfx950 (a8-a11 of SURVEY.md §8(a)): per-scan ORB detect +
+// describe on the intensity image, cloud-track lookup, Hamming cross-check matching of
+// consecutive scans, match selection and the front_end_residual pose solve
+// (src/intensity_feature_tracker.cpp:597-941, src/lidarFeaturePointsFunction.hpp:21-58).
+//
+// Layout in HBM (per scan): the 8-level pyramid as OpenCV lays it out level by level — each level
+// its own (h + 46) x (w + 46) byte image with a 23-pixel reflect-101 border — once unblurred
+// (FAST, Harris, intensity centroid) and once with the blurred interior (descriptors sample the
+// blurred interior and the unblurred border, as OpenCV's in-place GaussianBlur of the level ROI
+// leaves them); FAST scores per level pixel; keypoints as float x, y, size, angle, response,
+// octave; descriptors 32 B; cloud points float4.
+//
+// Kernels (the semantics are those of oracle/oracle_orb.cpp, which restates OpenCV 4.x):
+//   k_orb_pyramid   1 WG per scan: level 0 copy, levels 1..7 by the bit-exact fixed-point
+//                   INTER_LINEAR_EXACT resize of the previous level, borders
+//   k_orb_blur      1 thread per padded pixel: 7x7 sigma-2 separable float Gaussian (row sums
+//                   then the symmetric column sum, the FilterEngine order) on the ROI, border copy
+//   k_orb_fast      1 thread per level pixel: FAST-9/16 segment test + cornerScore<16>
+//   k_orb_select    1 WG per (scan, level): 3x3 non-max suppression, mask, ordered compaction,
+//                   retainBest(2n) on the FAST score (256-bin histogram), Harris responses,
+//                   retainBest(n) on them (radix select of the n-th largest), intensity-centroid
+//                   angle; detection order is kept (OpenCV's set, canonical order)
+//   k_orb_finish    1 WG per scan: levels concatenated, coordinates scaled to level 0,
+//                   cloud-track lookup + |x| < 0.01 filter (extractPointsAndFilterZeroValue)
+//   k_orb_desc      32 threads per keypoint: steered rBRIEF-256 bytes
+//   k_orb_match     1 WG per scan pair: XOR-popcount distances, batchDistance's cross-check,
+//                   stable counting selection of the first ceil(frac M) matches, good-frame
+//                   test, front_end_residual records
+//   k_orb_lm        1 WG per scan pair: Ceres-semantics LM (20 iterations) of those records
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "lislam_batch.hpp"
+#include "lislam_ctx.hpp"
+#include "lislam_device.hpp"
+#include "lislam_lm.hpp"
+
+namespace lislam {
+namespace orbk {
+
+constexpr int kB = 23;  // pyramid border: max(edgeThreshold 1, max(22, 4)) + 1
+constexpr int kL = 8;   // nlevels
+constexpr int kHalf = 15;
+constexpr int kFastT = 20;
+constexpr int kSelThreads = 1024;
+constexpr int kPairThreads = 1024;
+constexpr int kLmThreads = 256;
+
+__constant__ int c_pattern[256 * 4] = {
+#include "lislam_orb_pattern.inc"
+};
+
+struct Geom {
+  int W, H;
+  int w[kL], h[kL], stride[kL];
+  int off[kL];      // byte offset of padded level l in a scan's pyramid
+  int pix[kL + 1];  // prefix of w*h (flattened level pixels)
+  int pad[kL + 1];  // prefix of padded sizes
+  int bytes;        // per scan
+  float scale[kL];
+  int nper[kL];     // nfeaturesPerLevel
+  int lcap[kL];     // keypoint capacity per level
+  int lofs[kL + 1]; // prefix of lcap
+  int cap;          // per scan keypoints (sum lcap)
+  float gk[7];      // Gaussian taps
+  int umax[kHalf + 2];
+};
+
+struct Tabs {  // resize coefficients of level l from level l-1 (l >= 1), per axis
+  const int* xo; const uint16_t* xc; const int* yo; const uint16_t* yc;
+  const int* lim;  // [kL][4] xmin, xmax, ymin, ymax
+  int xs, ys;      // row strides of the x / y tables
+};
+
+struct Args {
+  Geom g;
+  Tabs t;
+  int S;
+  const uint8_t* img;     // [S][H*W]
+  const float4* track;    // [S][H*W]
+  uint8_t* pyr;           // [S][bytes]
+  uint8_t* blur;          // [S][bytes]
+  const uint8_t* mpyr;    // [bytes] mask pyramid or null
+  uint8_t* score;         // [S][pix[kL]]
+  int* cand;              // [S][pix[kL]] candidate pixel indices
+  float* cresp;           // [S][pix[kL]]
+  float* lkp;             // [S][cap][6] per-level staging (level l at lofs[l])
+  int* lcnt;              // [S][kL]
+  float* kp;              // [S][cap][6] x, y, size, angle, response, octave
+  float4* p3d;            // [S][cap]
+  uint8_t* desc;          // [S][cap][32]
+  int* nkp;               // [S]
+  int* overflow;          // [1]
+};
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+  if ((unsigned)p < (unsigned)len) return p;
+  if (len == 1) return 0;
+  do {
+    if (p < 0) p = -p;
+    else p = 2 * len - p - 2;
+  } while ((unsigned)p >= (unsigned)len);
+  return p;
+}
+
+// pixel (r, c) of level l (r, c relative to the ROI origin; may reach into the border)
+__device__ __forceinline__ uint8_t& px(uint8_t* base, const Geom& g, int l, int r, int c) {
+  return base[g.off[l] + (r + kB) * g.stride[l] + (c + kB)];
+}
+__device__ __forceinline__ uint8_t pxc(const uint8_t* base, const Geom& g, int l, int r, int c) {
+  return base[g.off[l] + (r + kB) * g.stride[l] + (c + kB)];
+}
+
+// ------------------------------------------------------------------ pyramid
+__device__ __forceinline__ uint32_t hval(const uint8_t* base, const Geom& g, const Tabs& t, int l, int row, int x) {
+  const int* lim = t.lim + l * 4;
+  if (x < lim[0]) return (uint32_t)pxc(base, g, l - 1, row, 0) << 8;
+  if (x < lim[1]) {
+    const int o = t.xo[l * t.xs + x];
+    const uint32_t c1 = t.xc[l * t.xs + x];
+    return (256u - c1) * pxc(base, g, l - 1, row, o) + c1 * pxc(base, g, l - 1, row, o + 1);
+  }
+  return (uint32_t)pxc(base, g, l - 1, row, t.xo[l * t.xs + g.w[l] - 1]) << 8;
+}
+
+// mode 0: image pyramids of scans; mode 1: the mask pyramid (constant-0 border, threshold 254)
+__global__ __launch_bounds__(1024) void k_orb_pyramid(Args a, int mode) {
+  const int s = blockIdx.x;
+  const Geom& g = a.g;
+  uint8_t* base = mode ? const_cast<uint8_t*>(a.mpyr) : a.pyr + (size_t)s * g.bytes;
+  const uint8_t* src = a.img + (size_t)s * g.W * g.H;
+  for (int l = 0; l < kL; l++) {
+    const int w = g.w[l], h = g.h[l];
+    for (int i = threadIdx.x; i < w * h; i += blockDim.x) {
+      const int y = i / w, x = i % w;
+      uint8_t v;
+      if (l == 0) {
+        v = src[y * g.W + x];
+      } else {
+        const int* lim = a.t.lim + l * 4;
+        if (y < lim[2] || y >= lim[3]) {
+          const uint32_t hv = hval(base, g, a.t, l, y < lim[2] ? 0 : g.h[l - 1] - 1, x);
+          v = (uint8_t)min(255u, (hv + 128u) >> 8);
+        } else {
+          const int yo = a.t.yo[l * a.t.ys + y];
+          const uint32_t c1 = a.t.yc[l * a.t.ys + y];
+          const uint32_t r = hval(base, g, a.t, l, yo, x) * (256u - c1) + hval(base, g, a.t, l, yo + 1, x) * c1;
+          v = (uint8_t)min(255u, (r + 32768u) >> 16);
+        }
+        if (mode && v <= 254) v = 0;  // threshold(254, THRESH_TOZERO)
+      }
+      px(base, g, l, y, x) = v;
+    }
+    __syncthreads();
+    const int pw = w + 2 * kB, ph = h + 2 * kB;
+    for (int i = threadIdx.x; i < pw * ph; i += blockDim.x) {
+      const int r = i / pw - kB, c = i % pw - kB;
+      if (r >= 0 && r < h && c >= 0 && c < w) continue;
+      px(base, g, l, r, c) = mode ? 0 : pxc(base, g, l, reflect101(r, h), reflect101(c, w));
+    }
+    __syncthreads();
+  }
+}
+
+// GaussianBlur(level ROI, 7x7, 2, 2, BORDER_REFLECT_101): row sums then symmetric column sum
+__global__ __launch_bounds__(256) void k_orb_blur(Args a) {
+  const Geom& g = a.g;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  if (i >= g.pad[kL]) return;
+  int l = 0;
+  while (i >= g.pad[l + 1]) l++;
+  const int j = i - g.pad[l], pw = g.stride[l];
+  const int r = j / pw - kB, c = j % pw - kB;
+  const uint8_t* src = a.pyr + (size_t)s * g.bytes;
+  uint8_t* dst = a.blur + (size_t)s * g.bytes;
+  if (r < 0 || r >= g.h[l] || c < 0 || c >= g.w[l]) {
+    px(dst, g, l, r, c) = pxc(src, g, l, r, c);
+    return;
+  }
+  float rs[7];
+#pragma unroll
+  for (int dy = 0; dy < 7; dy++) {
+    float v = g.gk[0] * (float)pxc(src, g, l, r - 3 + dy, c - 3);
+#pragma unroll
+    for (int t = 1; t < 7; t++) v += g.gk[t] * (float)pxc(src, g, l, r - 3 + dy, c - 3 + t);
+    rs[dy] = v;
+  }
+  float v = g.gk[3] * rs[3];
+#pragma unroll
+  for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t] + rs[3 - t]);
+  const int iv = (int)rintf(v);
+  px(dst, g, l, r, c) = (uint8_t)min(255, max(0, iv));
+}
+
+// ------------------------------------------------------------------ FAST
+__constant__ int c_fast[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                                  {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+__device__ int corner_score(const int* d, int threshold) {
+  int a0 = threshold;
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    if (a <= a0) continue;
+    a = min(a, d[k + 4]);
+    a = min(a, d[k + 5]);
+    a = min(a, d[k + 6]);
+    a = min(a, d[k + 7]);
+    a = min(a, d[k + 8]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+    b = max(b, d[k + 3]);
+    b = max(b, d[k + 4]);
+    b = max(b, d[k + 5]);
+    if (b >= b0) continue;
+    b = max(b, d[k + 6]);
+    b = max(b, d[k + 7]);
+    b = max(b, d[k + 8]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+__global__ __launch_bounds__(256) void k_orb_fast(Args a) {
+  const Geom& g = a.g;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  if (i >= g.pix[kL]) return;
+  int l = 0;
+  while (i >= g.pix[l + 1]) l++;
+  const int j = i - g.pix[l];
+  const int r = j / g.w[l], c = j % g.w[l];
+  const uint8_t* base = a.pyr + (size_t)s * g.bytes;
+  int score = 0;
+  if (r >= 3 && r < g.h[l] - 3 && c >= 3 && c < g.w[l] - 3) {
+    const int v = pxc(base, g, l, r, c);
+    int x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = pxc(base, g, l, r + c_fast[k][1], c + c_fast[k][0]);
+    auto tab = [&](int k) { const int dd = x[k] - v; return dd < -kFastT ? 1 : dd > kFastT ? 2 : 0; };
+    int d = tab(0) | tab(8);
+    if (d) {
+      d &= tab(2) | tab(10);
+      d &= tab(4) | tab(12);
+      d &= tab(6) | tab(14);
+    }
+    if (d) {
+      d &= tab(1) | tab(9);
+      d &= tab(3) | tab(11);
+      d &= tab(5) | tab(13);
+      d &= tab(7) | tab(15);
+    }
+    bool corner = false;
+    if (d & 1) {
+      const int vt = v - kFastT;
+      int count = 0;
+      for (int k = 0; k < 25; k++) {
+        if (x[k & 15] < vt) {
+          if (++count > 8) { corner = true; break; }
+        } else {
+          count = 0;
+        }
+      }
+    }
+    if (!corner && (d & 2)) {
+      const int vt = v + kFastT;
+      int count = 0;
+      for (int k = 0; k < 25; k++) {
+        if (x[k & 15] > vt) {
+          if (++count > 8) { corner = true; break; }
+        } else {
+          count = 0;
+        }
+      }
+    }
+    if (corner) {
+      int dd[25];
+#pragma unroll
+      for (int k = 0; k < 25; k++) dd[k] = v - x[k & 15];
+      score = corner_score(dd, kFastT);
+    }
+  }
+  a.score[(size_t)s * g.pix[kL] + i] = (uint8_t)score;
+}
+
+// ------------------------------------------------------------------ selection (1 WG per scan, level)
+struct SelShared {
+  int wsum[kSelThreads / 64];
+  int hist[256];
+  int total;
+  uint32_t prefix;  // radix-select prefix
+  int want;
+};
+
+// Ordered compaction helper: block-wide exclusive prefix of flag; returns the rank, *tot the sum.
+__device__ __forceinline__ int block_rank(SelShared& sh, bool flag, int* tot) {
+  const uint64_t b = __ballot(flag);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int inwave = __popcll(b & lanemask_lt());
+  if (lane == 0) sh.wsum[w] = __popcll(b);
+  __syncthreads();
+  int before = 0, all = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+    const int v = sh.wsum[k];
+    if (k < w) before += v;
+    all += v;
+  }
+  __syncthreads();
+  *tot = all;
+  return before + inwave;
+}
+
+__device__ __forceinline__ int score_at(const uint8_t* sc, const Geom& g, int l, int r, int c) {
+  if (r < 0 || r >= g.h[l] || c < 0 || c >= g.w[l]) return 0;
+  return sc[g.pix[l] + r * g.w[l] + c];
+}
+
+__device__ __forceinline__ uint32_t ord_key(float f) {  // larger float -> larger key
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ float harris_at(const uint8_t* base, const Geom& g, int l, int x0, int y0) {
+  const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+  const float sq = scale * scale * scale * scale;
+  int A = 0, B = 0, C = 0;
+  for (int i = 0; i < 7; i++)
+    for (int j = 0; j < 7; j++) {
+      const int y = y0 - 3 + i, x = x0 - 3 + j;
+      const int Ix = (pxc(base, g, l, y, x + 1) - pxc(base, g, l, y, x - 1)) * 2 +
+                     (pxc(base, g, l, y - 1, x + 1) - pxc(base, g, l, y - 1, x - 1)) +
+                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y + 1, x - 1));
+      const int Iy = (pxc(base, g, l, y + 1, x) - pxc(base, g, l, y - 1, x)) * 2 +
+                     (pxc(base, g, l, y + 1, x - 1) - pxc(base, g, l, y - 1, x - 1)) +
+                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y - 1, x + 1));
+      A += Ix * Ix;
+      B += Iy * Iy;
+      C += Ix * Iy;
+    }
+  return ((float)A * B - (float)C * C - 0.04f * ((float)A + B) * ((float)A + B)) * sq;
+}
+
+// cv::fastAtan2 (degrees)
+__device__ float fast_atan2(float y, float x) {
+  const float k = (float)(180 / kPi);
+  const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k, p5 = 0.1555786518463281f * k,
+              p7 = -0.04432655554792128f * k;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)2.220446049250313e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)2.220446049250313e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__device__ float ic_angle(const uint8_t* base, const Geom& g, int l, int cx, int cy) {
+  int m01 = 0, m10 = 0;
+  for (int u = -kHalf; u <= kHalf; ++u) m10 += u * pxc(base, g, l, cy, cx + u);
+  for (int v = 1; v <= kHalf; ++v) {
+    int vsum = 0;
+    const int d = g.umax[v];
+    for (int u = -d; u <= d; ++u) {
+      const int vp = pxc(base, g, l, cy + v, cx + u), vm = pxc(base, g, l, cy - v, cx + u);
+      vsum += vp - vm;
+      m10 += u * (vp + vm);
+    }
+    m01 += v * vsum;
+  }
+  return fast_atan2((float)m01, (float)m10);
+}
+
+// n-th largest key among cnt keys (radix select, 4 x 8 bits); all threads get it
+__device__ uint32_t nth_largest(SelShared& sh, const float* resp, int cnt, int n) {
+  if (threadIdx.x == 0) { sh.prefix = 0; sh.want = n; }
+  __syncthreads();
+  for (int pass = 3; pass >= 0; pass--) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) sh.hist[b] = 0;
+    __syncthreads();
+    const uint32_t prefix = sh.prefix;
+    const uint32_t hmask = pass == 3 ? 0u : (0xffffffffu << ((pass + 1) * 8));
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const uint32_t k = ord_key(resp[i]);
+      if ((k & hmask) == prefix) atomicAdd(&sh.hist[(k >> (pass * 8)) & 255], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int want = sh.want;
+      for (int b = 255; b >= 0; b--) {
+        if (sh.hist[b] >= want) { sh.prefix = prefix | ((uint32_t)b << (pass * 8)); break; }
+        want -= sh.hist[b];
+      }
+      sh.want = want;
+    }
+    __syncthreads();
+  }
+  return sh.prefix;
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
+  __shared__ SelShared sh;
+  const Geom& g = a.g;
+  const int s = blockIdx.x / kL, l = blockIdx.x % kL;
+  const int w = g.w[l], h = g.h[l];
+  const uint8_t* base = a.pyr + (size_t)s * g.bytes;
+  const uint8_t* sc = a.score + (size_t)s * g.pix[kL];
+  int* cand = a.cand + (size_t)s * g.pix[kL] + g.pix[l];
+  float* resp = a.cresp + (size_t)s * g.pix[kL] + g.pix[l];
+  // 1. FAST keypoints in row-major order: non-max suppression over the 8 neighbours, pixel mask,
+  //    image border (edgeThreshold 1)
+  int n = 0;
+  for (int b0 = 0; b0 < w * h; b0 += blockDim.x) {
+    const int i = b0 + threadIdx.x;
+    bool keep = false;
+    if (i < w * h) {
+      const int r = i / w, c = i % w;
+      const int v = sc[g.pix[l] + i];
+      if (v && r >= 3 && r < h - 3) {
+        keep = v > score_at(sc, g, l, r, c + 1) && v > score_at(sc, g, l, r, c - 1) &&
+               v > score_at(sc, g, l, r - 1, c - 1) && v > score_at(sc, g, l, r - 1, c) &&
+               v > score_at(sc, g, l, r - 1, c + 1) && v > score_at(sc, g, l, r + 1, c - 1) &&
+               v > score_at(sc, g, l, r + 1, c) && v > score_at(sc, g, l, r + 1, c + 1);
+        if (keep && a.mpyr && pxc(a.mpyr, g, l, r, c) == 0) keep = false;
+        if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
+      }
+    }
+    int tot;
+    const int rank = block_rank(sh, keep, &tot);
+    if (keep) cand[n + rank] = i;
+    n += tot;
+  }
+  // 2. retainBest(2 n_l) on the FAST score: keep every score >= the (2 n_l)-th largest
+  const int n2 = 2 * g.nper[l];
+  if (n > n2) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) sh.hist[b] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&sh.hist[sc[g.pix[l] + cand[i]]], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int cum = 0, t = 0;
+      for (int b = 255; b >= 0; b--) {
+        cum += sh.hist[b];
+        if (n2 > 0 && cum >= n2) { t = b; break; }
+      }
+      sh.total = n2 > 0 ? t : 256;
+    }
+    __syncthreads();
+    const int thr = sh.total;
+    int m = 0;
+    for (int b0 = 0; b0 < n; b0 += blockDim.x) {
+      const int i = b0 + threadIdx.x;
+      const int ci = i < n ? cand[i] : 0;
+      const bool keep = i < n && sc[g.pix[l] + ci] >= thr;
+      __syncthreads();
+      int tot;
+      const int rank = block_rank(sh, keep, &tot);
+      if (keep) cand[m + rank] = ci;
+      m += tot;
+    }
+    n = m;
+  }
+  // 3. Harris responses, retainBest(n_l)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) resp[i] = harris_at(base, g, l, cand[i] % w, cand[i] / w);
+  __syncthreads();
+  const int n1 = g.nper[l];
+  if (n > n1) {
+    const uint32_t thr = n1 > 0 ? nth_largest(sh, resp, n, n1) : 0xffffffffu;
+    int m = 0;
+    for (int b0 = 0; b0 < n; b0 += blockDim.x) {
+      const int i = b0 + threadIdx.x;
+      const bool keep = i < n && n1 > 0 && ord_key(resp[i]) >= thr;
+      const int ci = i < n ? cand[i] : 0;
+      const float rv = i < n ? resp[i] : 0.f;
+      __syncthreads();
+      int tot;
+      const int rank = block_rank(sh, keep, &tot);
+      if (keep) { cand[m + rank] = ci; resp[m + rank] = rv; }
+      m += tot;
+    }
+    n = m;
+  }
+  __syncthreads();
+  // 4. angles; per-level staging (level coordinates scaled to level 0 in k_orb_finish)
+  if (n > g.lcap[l]) {
+    if (threadIdx.x == 0) atomicOr(a.overflow, 1);
+    n = g.lcap[l];
+  }
+  float* out = a.lkp + ((size_t)s * g.cap + g.lofs[l]) * 6;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int x = cand[i] % w, y = cand[i] / w;
+    float* o = out + (size_t)i * 6;
+    o[0] = (float)x; o[1] = (float)y; o[2] = 31 * g.scale[l];
+    o[3] = ic_angle(base, g, l, x, y);
+    o[4] = resp[i];
+    o[5] = (float)l;
+  }
+  if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
+}
+
+// levels in order, level-0 coordinates, cloud-track lookup and zero filter (a9)
+__global__ __launch_bounds__(256) void k_orb_finish(Args a) {
+  __shared__ SelShared sh;
+  const Geom& g = a.g;
+  const int s = blockIdx.x;
+  int n = 0;
+  for (int l = 0; l < kL; l++) {
+    const int cnt = a.lcnt[s * kL + l];
+    const float* in = a.lkp + ((size_t)s * g.cap + g.lofs[l]) * 6;
+    for (int b0 = 0; b0 < cnt; b0 += blockDim.x) {
+      const int i = b0 + threadIdx.x;
+      bool keep = false;
+      float o[6];
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < cnt) {
+        for (int e = 0; e < 6; e++) o[e] = in[(size_t)i * 6 + e];
+        o[0] *= g.scale[l];
+        o[1] *= g.scale[l];
+        const int col = (int)rintf(o[0]), row = (int)rintf(o[1]);
+        p = a.track[(size_t)s * g.W * g.H + row * g.W + col];
+        keep = !(fabsf(p.x) < 0.01f);
+      }
+      int tot;
+      const int rank = block_rank(sh, keep, &tot);
+      if (keep) {
+        float* d = a.kp + ((size_t)s * g.cap + n + rank) * 6;
+        for (int e = 0; e < 6; e++) d[e] = o[e];
+        a.p3d[(size_t)s * g.cap + n + rank] = make_float4(p.x, p.y, p.z, 0.f);
+      }
+      n += tot;
+    }
+  }
+  if (threadIdx.x == 0) a.nkp[s] = n;
+}
+
+// steered rBRIEF: 32 threads per keypoint, one descriptor byte each
+__global__ __launch_bounds__(256) void k_orb_desc(Args a) {
+  const Geom& g = a.g;
+  const int s = blockIdx.y;
+  const int k = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int byte = threadIdx.x & 31;
+  if (k >= a.nkp[s]) return;
+  const float* kp = a.kp + ((size_t)s * g.cap + k) * 6;
+  const int l = (int)kp[5];
+  const float scale = 1.f / g.scale[l];
+  const float ang = kp[3] * (float)(kPi / 180.f);
+  const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+  const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
+  const uint8_t* base = a.blur + (size_t)s * g.bytes;
+  int v = 0;
+#pragma unroll
+  for (int bit = 0; bit < 8; bit++) {
+    const int p = (byte * 8 + bit) * 2;
+    int t[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const float qx = (float)c_pattern[(p + e) * 2], qy = (float)c_pattern[(p + e) * 2 + 1];
+      const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
+      t[e] = pxc(base, g, l, cy + (int)rintf(y), cx + (int)rintf(x));
+    }
+    v |= (t[0] < t[1]) << bit;
+  }
+  a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)v;
+}
+
+// ------------------------------------------------------------------ matching (a10) + records
+struct PairArgs {
+  int npairs;
+  const int* qscan;   // [npairs] cur scan (query)
+  const int* tscan;   // [npairs] prev scan (train)
+  const uint8_t* qdesc; const uint8_t* tdesc;  // descriptor arrays ([scan][cap][32])
+  const float4* qp3d; const float4* tp3d;
+  const int* qn; const int* tn;                // keypoint counts per scan
+  int qcap, tcap;                              // descriptor / point strides per scan
+  int bstride;                                 // per-pair stride of the buffers below (>= qcap)
+  double frac;                                 // 0.3 / 0.2
+  int* mscratch;      // [npairs][qcap] packed (dist << 16 | train)
+  int* mout;          // [npairs][qcap][3] all matches (query, train, distance) in query order, or null
+  double* rec;        // [npairs][qcap][9]
+  int* kind;          // [npairs][qcap]
+  int* stats;         // [npairs][8]: ok, -, nq, matches, good, iterations, termination, nt
+  double* T;          // [npairs][7]
+};
+
+__device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
+  int d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
+  return d;
+}
+
+__global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
+  __shared__ SelShared sh;
+  __shared__ int hist[257];
+  __shared__ int sM, sG;
+  const int pr = blockIdx.x;
+  const int qs = p.qscan[pr], ts = p.tscan[pr];
+  const int nq = p.qn[qs], nt = p.tn[ts];
+  const uint32_t* Q = reinterpret_cast<const uint32_t*>(p.qdesc + (size_t)qs * p.qcap * 32);
+  const uint32_t* T = reinterpret_cast<const uint32_t*>(p.tdesc + (size_t)ts * p.tcap * 32);
+  int* best = p.mscratch + (size_t)pr * p.bstride;
+  for (int j = threadIdx.x; j < nq; j += blockDim.x) best[j] = 0x7fffffff;
+  __syncthreads();
+  // batchDistance cross-check: train i -> nearest query (first minimum); query keeps the nearest
+  // train among those that chose it (first minimum) = atomicMin of (distance, train)
+  for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+    uint32_t td[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) td[e] = T[(size_t)i * 8 + e];
+    int bd = 0x7fffffff, bj = -1;
+    for (int j = 0; j < nq; j++) {
+      const int d = hamming32(td, Q + (size_t)j * 8);
+      if (d < bd) { bd = d; bj = j; }
+    }
+    if (bj >= 0) atomicMin(&best[bj], (bd << 16) | i);
+  }
+  __syncthreads();
+  // std::sort by distance (stable, query order) + the first ceil(frac M)
+  for (int b = threadIdx.x; b < 257; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (int j = threadIdx.x; j < nq; j += blockDim.x)
+    if (best[j] != 0x7fffffff) atomicAdd(&hist[best[j] >> 16], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int M = 0;
+    for (int b = 0; b < 257; b++) M += hist[b];
+    int G = 0;
+    while ((double)G < (double)M * p.frac) G++;
+    int cum = 0, dstar = 257, before = 0;
+    for (int b = 0; b < 257 && G > 0; b++) {
+      if (cum + hist[b] >= G) { dstar = b; before = cum; break; }
+      cum += hist[b];
+    }
+    sM = M;
+    sG = G;
+    sh.total = dstar;
+    sh.want = G - before;  // matches of distance d* to take, in query order
+  }
+  __syncthreads();
+  const int M = sM, G = sG, dstar = sh.total, take = sh.want;
+  int n = 0, neq = 0, nm = 0;
+  for (int b0 = 0; b0 < nq; b0 += blockDim.x) {
+    const int j = b0 + threadIdx.x;
+    const int v = j < nq ? best[j] : 0x7fffffff;
+    const int d = v >> 16;
+    if (p.mout) {
+      int tm;
+      const int rm = block_rank(sh, v != 0x7fffffff, &tm);
+      if (v != 0x7fffffff) {
+        int* o = p.mout + ((size_t)pr * p.bstride + nm + rm) * 3;
+        o[0] = j; o[1] = v & 0xffff; o[2] = d;
+      }
+      nm += tm;
+    }
+    const bool eq = v != 0x7fffffff && d == dstar;
+    int te;
+    const int req = block_rank(sh, eq, &te);
+    const bool keep = v != 0x7fffffff && (d < dstar || (eq && neq + req < take));
+    neq += te;
+    int tot;
+    const int rank = block_rank(sh, keep, &tot);
+    if (keep) {
+      const int i = v & 0xffff;
+      const float4 a = p.qp3d[(size_t)qs * p.qcap + j], b = p.tp3d[(size_t)ts * p.tcap + i];
+      double* r = p.rec + ((size_t)pr * p.bstride + n + rank) * 9;
+      r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = b.x; r[4] = b.y; r[5] = b.z; r[6] = r[7] = r[8] = 0;
+      p.kind[(size_t)pr * p.bstride + n + rank] = 3;
+    }
+    n += tot;
+  }
+  if (threadIdx.x == 0) {
+    int* st = p.stats + pr * 8;
+    st[0] = (nt != nq && G >= 4 && G != M) ? 1 : 0;
+    st[1] = 0;
+    st[2] = nq;
+    st[3] = M;
+    st[4] = G;
+    st[5] = 0;
+    st[6] = -1;
+    st[7] = nt;
+  }
+}
+
+// front_end_residual solve per pair (p2p_calculateRandT): identity start, 20 iterations
+struct LmSh {
+  double red[kLmThreads / 16][kAcc];
+  double x[7];
+  double acc[kAcc];
+  int flag;
+};
+
+__device__ void pair_eval(LmSh& sh, const double* rec, int n) {
+  double acc[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) acc[e] = 0;
+  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
+  const D3 t{sh.x[4], sh.x[5], sh.x[6]};
+  for (int i = threadIdx.x; i < n; i += kLmThreads) block_accum(3, rec + (size_t)i * 9, q, t, acc);
+  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) {
+    const double v = row_sum(acc[e]);
+    if ((lane & 15) == 0) sh.red[row][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kAcc) {
+    double v = 0;
+    for (int w = 0; w < kLmThreads / 16; w++) v += sh.red[w][threadIdx.x];
+    sh.acc[threadIdx.x] = v;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
+  __shared__ LmSh sh;
+  const int pr = blockIdx.x;
+  int* st = p.stats + pr * 8;
+  double* T = p.T + pr * 7;
+  const bool good = st[0] == 1;
+  const int n = st[4];
+  const double* rec = p.rec + (size_t)pr * p.bstride * 9;
+  if (!good) {
+    if (threadIdx.x == 0) {
+      const double I[7] = {0, 0, 0, 1, 0, 0, 0};
+      for (int e = 0; e < 7; e++) T[e] = I[e];
+    }
+    return;
+  }
+  LM s;
+  if (threadIdx.x == 0) {
+    const double I[7] = {0, 0, 0, 1, 0, 0, 0};
+    for (int e = 0; e < 7; e++) sh.x[e] = I[e];
+  }
+  __syncthreads();
+  pair_eval(sh, rec, n);
+  if (threadIdx.x == 0) {
+    const bool cont = lm_start(s, sh.x, sh.acc, max_it);
+    sh.flag = cont;
+    if (cont)
+      for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+  }
+  __syncthreads();
+  bool go = sh.flag;
+  while (go) {
+    pair_eval(sh, rec, n);
+    if (threadIdx.x == 0) {
+      const bool cont = lm_next(s, sh.acc, max_it);
+      sh.flag = cont;
+      if (cont)
+        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+    }
+    __syncthreads();
+    go = sh.flag;
+  }
+  if (threadIdx.x == 0) {
+    for (int e = 0; e < 7; e++) T[e] = s.x[e];
+    st[5] = s.it;
+    st[6] = s.term;
+  }
+}
+
+}  // namespace orbk
+}  // namespace lislam
+
+// ================================================================== host side
+using namespace lislam;
+using namespace lislam::orbk;
+
+namespace {
+
+int ofail(lislam_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define OCHK(ctx, x)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) return ofail(ctx, LISLAM_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+#define ORC(x)                        \
+  do {                                \
+    int rc_ = (x);                    \
+    if (rc_ != LISLAM_OK) return rc_; \
+  } while (0)
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+int cv_round(float v) { return (int)std::nearbyint(v); }
+
+// nfeaturesPerLevel of computeKeyPoints (orb.cpp)
+void features_per_level(int nfeatures, int* n) {
+  const float factor = (float)(1.0 / (double)1.2f);
+  float nd = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)kL));
+  int sum = 0;
+  for (int l = 0; l < kL - 1; l++) {
+    n[l] = cv_round(nd);
+    sum += n[l];
+    nd *= factor;
+  }
+  n[kL - 1] = std::max(nfeatures - sum, 0);
+}
+
+}  // namespace
+
+// One ORB engine: geometry, resize tables, mask pyramid, per-scan buffers for up to max_scans
+// scans of one image size and feature budget.
+struct OrbEngine {
+  lislam_ctx* ctx = nullptr;
+  int H = 0, W = 0, max_scans = 0, nfeatures = 0;
+  Geom g{};
+  std::vector<void*> allocs;
+  int *xo = nullptr, *yo = nullptr, *lim = nullptr;
+  uint16_t *xc = nullptr, *yc = nullptr;
+  int xs = 0, ys = 0;
+  uint8_t* mpyr = nullptr;
+  uint8_t *pyr = nullptr, *blur = nullptr, *score = nullptr, *desc = nullptr;
+  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr;
+  float *cresp = nullptr, *lkp = nullptr, *kp = nullptr;
+  float4* p3d = nullptr;
+  ~OrbEngine() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+  template <typename T>
+  int alloc(T** p, size_t count) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+    if (e != hipSuccess) return ofail(ctx, LISLAM_ERR_DEVICE, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return LISLAM_OK;
+  }
+  Args args(const uint8_t* img, const float4* track) const {
+    Args a{};
+    a.g = g;
+    a.t.xo = xo; a.t.xc = xc; a.t.yo = yo; a.t.yc = yc; a.t.lim = lim; a.t.xs = xs; a.t.ys = ys;
+    a.S = max_scans;
+    a.img = img; a.track = track;
+    a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.score = score; a.cand = cand; a.cresp = cresp;
+    a.lkp = lkp; a.lcnt = lcnt; a.kp = kp; a.p3d = p3d; a.desc = desc; a.nkp = nkp; a.overflow = overflow;
+    return a;
+  }
+};
+
+namespace {
+
+int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nfeatures, const uint8_t* mask) {
+  e->ctx = c; e->H = H; e->W = W; e->max_scans = max_scans; e->nfeatures = nfeatures;
+  Geom& g = e->g;
+  g.W = W; g.H = H;
+  int off = 0;
+  g.pix[0] = 0;
+  g.pad[0] = 0;
+  features_per_level(nfeatures, g.nper);
+  g.lofs[0] = 0;
+  for (int l = 0; l < kL; l++) {
+    const float scale = (float)std::pow((double)1.2f, (double)l);
+    const float inv = 1.0f / scale;
+    g.scale[l] = scale;
+    g.w[l] = cv_round((float)W * inv);
+    g.h[l] = cv_round((float)H * inv);
+    if (g.w[l] < 1 || g.h[l] < 1) return ofail(c, LISLAM_ERR_ARG, "image %dx%d too small for 8 ORB levels", W, H);
+    g.stride[l] = g.w[l] + 2 * kB;
+    g.off[l] = off;
+    off += g.stride[l] * (g.h[l] + 2 * kB);
+    g.pix[l + 1] = g.pix[l] + g.w[l] * g.h[l];
+    g.pad[l + 1] = g.pad[l] + g.stride[l] * (g.h[l] + 2 * kB);
+    g.lcap[l] = 2 * g.nper[l] + 64;
+    g.lofs[l + 1] = g.lofs[l] + g.lcap[l];
+  }
+  g.bytes = (off + 255) & ~255;
+  g.cap = g.lofs[kL];
+  // Gaussian taps (getGaussianKernel(7, 2, CV_32F))
+  double sum = 0;
+  for (int i = 0; i < 7; i++) {
+    const double x = i - 3.0;
+    g.gk[i] = (float)std::exp(-0.5 / 4.0 * x * x);
+    sum += g.gk[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) g.gk[i] = (float)(g.gk[i] * sum);
+  // umax of the circular patch
+  {
+    int* umax = g.umax;
+    const int vmax = (int)std::floor(kHalf * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(kHalf * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) umax[v] = (int)std::nearbyint(std::sqrt((double)kHalf * kHalf - v * v));
+    for (int v = kHalf, v0 = 0; v >= vmin; --v) {
+      while (umax[v0] == umax[v0 + 1]) ++v0;
+      umax[v] = v0;
+      ++v0;
+    }
+  }
+  // resize tables (INTER_LINEAR_EXACT of level l from level l-1)
+  e->xs = g.w[0];
+  e->ys = g.h[0];
+  std::vector<int> hxo((size_t)kL * e->xs, 0), hyo((size_t)kL * e->ys, 0), hlim(kL * 4, 0);
+  std::vector<uint16_t> hxc((size_t)kL * e->xs, 0), hyc((size_t)kL * e->ys, 0);
+  for (int l = 1; l < kL; l++) {
+    for (int axis = 0; axis < 2; axis++) {
+      const int src = axis == 0 ? g.w[l - 1] : g.h[l - 1], dst = axis == 0 ? g.w[l] : g.h[l];
+      int* o = axis == 0 ? &hxo[(size_t)l * e->xs] : &hyo[(size_t)l * e->ys];
+      uint16_t* cc = axis == 0 ? &hxc[(size_t)l * e->xs] : &hyc[(size_t)l * e->ys];
+      int mn = 0, mx = dst;
+      const double inv_scale = (double)dst / src;
+      const double scale = 1.0 / inv_scale;
+      for (int v = 0; v < dst; v++) {
+        const double fval = scale * ((double)v + 0.5) - 0.5;
+        const int ival = (int)std::floor(fval);
+        if (ival >= 0 && src > 1) {
+          if (ival < src - 1) {
+            o[v] = ival;
+            cc[v] = (uint16_t)std::nearbyint((fval - (double)ival) * 256.0);
+          } else {
+            o[v] = src - 1;
+            mx = std::min(mx, v);
+          }
+        } else {
+          mn = std::max(mn, v + 1);
+        }
+      }
+      hlim[l * 4 + axis * 2] = mn;
+      hlim[l * 4 + axis * 2 + 1] = mx;
+    }
+  }
+  hipStream_t st = c->stream;
+  ORC(e->alloc(&e->xo, hxo.size()));
+  ORC(e->alloc(&e->yo, hyo.size()));
+  ORC(e->alloc(&e->xc, hxc.size()));
+  ORC(e->alloc(&e->yc, hyc.size()));
+  ORC(e->alloc(&e->lim, hlim.size()));
+  OCHK(c, hipMemcpyAsync(e->xo, hxo.data(), hxo.size() * 4, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(e->yo, hyo.data(), hyo.size() * 4, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(e->xc, hxc.data(), hxc.size() * 2, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(e->yc, hyc.data(), hyc.size() * 2, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(e->lim, hlim.data(), hlim.size() * 4, hipMemcpyHostToDevice, st));
+  const size_t S = max_scans;
+  ORC(e->alloc(&e->pyr, S * g.bytes));
+  ORC(e->alloc(&e->blur, S * g.bytes));
+  ORC(e->alloc(&e->score, S * g.pix[kL]));
+  ORC(e->alloc(&e->cand, S * g.pix[kL]));
+  ORC(e->alloc(&e->cresp, S * g.pix[kL]));
+  ORC(e->alloc(&e->lkp, S * g.cap * 6));
+  ORC(e->alloc(&e->lcnt, S * kL));
+  ORC(e->alloc(&e->kp, S * g.cap * 6));
+  ORC(e->alloc(&e->p3d, S * g.cap));
+  ORC(e->alloc(&e->desc, S * g.cap * 32));
+  ORC(e->alloc(&e->nkp, S));
+  ORC(e->alloc(&e->overflow, 1));
+  OCHK(c, hipMemsetAsync(e->overflow, 0, 4, st));
+  if (mask) {  // mask pyramid, once
+    uint8_t* dmask = nullptr;
+    ORC(e->alloc(&dmask, (size_t)H * W));
+    ORC(e->alloc(&e->mpyr, g.bytes));
+    OCHK(c, hipMemcpyAsync(dmask, mask, (size_t)H * W, hipMemcpyDefault, st));
+    Args a = e->args(dmask, nullptr);
+    hipLaunchKernelGGL(k_orb_pyramid, dim3(1), dim3(1024), 0, st, a, 1);
+    OCHK(c, hipGetLastError());
+  }
+  return LISLAM_OK;
+}
+
+// a8 + a9 for scans [0, n) of device images / tracks
+int engine_detect(OrbEngine* e, const uint8_t* d_img, const float4* d_track, int n) {
+  lislam_ctx* c = e->ctx;
+  hipStream_t st = c->stream;
+  if (n <= 0) return LISLAM_OK;
+  Args a = e->args(d_img, d_track);
+  a.S = n;
+  const Geom& g = e->g;
+  hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(1024), 0, st, a, 0);
+  hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a);
+  hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_orb_blur, dim3(cdiv(g.pad[kL], 256), n), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a);
+  OCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+}  // namespace
+
+namespace {
+
+Args args_slot(const OrbEngine* e, const uint8_t* img, const float4* track, int slot) {
+  Args a = e->args(img, track);
+  const Geom& g = e->g;
+  const size_t s = slot;
+  a.img = img ? img + s * g.W * g.H : nullptr;
+  a.track = track ? track + s * g.W * g.H : nullptr;
+  a.pyr = e->pyr + s * g.bytes;
+  a.blur = e->blur + s * g.bytes;
+  a.score = e->score + s * g.pix[kL];
+  a.cand = e->cand + s * g.pix[kL];
+  a.cresp = e->cresp + s * g.pix[kL];
+  a.lkp = e->lkp + s * g.cap * 6;
+  a.lcnt = e->lcnt + s * kL;
+  a.kp = e->kp + s * g.cap * 6;
+  a.p3d = e->p3d + s * g.cap;
+  a.desc = e->desc + s * g.cap * 32;
+  a.nkp = e->nkp + s;
+  return a;
+}
+
+// a8 + a9 for scans [slot0, slot0 + n) of the engine (device images / tracks indexed by scan)
+int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_track, int slot0, int n) {
+  lislam_ctx* c = e->ctx;
+  hipStream_t st = c->stream;
+  if (n <= 0) return LISLAM_OK;
+  Args a = args_slot(e, d_img, d_track, slot0);
+  a.S = n;
+  const Geom& g = e->g;
+  { TimedScope t(c, kT_orb_pyramid); hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(1024), 0, st, a, 0); }
+  { TimedScope t(c, kT_orb_fast); hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_blur); hipLaunchKernelGGL(k_orb_blur, dim3(cdiv(g.pad[kL], 256), n), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a); }
+  OCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// Device buffers of up to `maxp` scan pairs with queries of up to qcap keypoints.
+struct PairBufs {
+  lislam_ctx* ctx = nullptr;
+  int maxp = 0, qcap = 0;
+  std::vector<void*> allocs;
+  int *qscan = nullptr, *tscan = nullptr, *mscratch = nullptr, *mout = nullptr, *kind = nullptr, *stats = nullptr;
+  double *rec = nullptr, *T = nullptr;
+  ~PairBufs() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+  template <typename T_>
+  int alloc(T_** p, size_t count) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T_));
+    if (e != hipSuccess) return ofail(ctx, LISLAM_ERR_DEVICE, "hipMalloc(%zu): %s", count * sizeof(T_), hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = static_cast<T_*>(q);
+    return LISLAM_OK;
+  }
+  int init(lislam_ctx* c, int maxp_, int qcap_, bool raw) {
+    ctx = c; maxp = maxp_; qcap = qcap_;
+    ORC(alloc(&qscan, maxp));
+    ORC(alloc(&tscan, maxp));
+    ORC(alloc(&mscratch, (size_t)maxp * qcap));
+    if (raw) ORC(alloc(&mout, (size_t)maxp * qcap * 3));
+    ORC(alloc(&kind, (size_t)maxp * qcap));
+    ORC(alloc(&stats, (size_t)maxp * 8));
+    ORC(alloc(&rec, (size_t)maxp * qcap * 9));
+    ORC(alloc(&T, (size_t)maxp * 7));
+    return LISLAM_OK;
+  }
+};
+
+// Match pairs (query scan qs[i] of engine qe, train scan ts[i] of te), select frac, test, and
+// (lm) solve; results in pb slots [p0, p0 + n).
+int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int* qs, const int* ts, int n, double frac,
+              PairBufs& pb, int p0, bool lm) {
+  hipStream_t st = c->stream;
+  if (n <= 0) return LISLAM_OK;
+  if (qe->g.cap > pb.qcap || p0 + n > pb.maxp) return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
+  OCHK(c, hipMemcpyAsync(pb.qscan + p0, qs, n * 4, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(pb.tscan + p0, ts, n * 4, hipMemcpyHostToDevice, st));
+  PairArgs p;
+  p.npairs = n;
+  p.qscan = pb.qscan + p0; p.tscan = pb.tscan + p0;
+  p.qdesc = qe->desc; p.tdesc = te->desc;
+  p.qp3d = qe->p3d; p.tp3d = te->p3d;
+  p.qn = qe->nkp; p.tn = te->nkp;
+  p.qcap = qe->g.cap; p.tcap = te->g.cap;
+  p.bstride = pb.qcap;
+  p.frac = frac;
+  p.mscratch = pb.mscratch + (size_t)p0 * pb.qcap;
+  p.mout = pb.mout ? pb.mout + (size_t)p0 * pb.qcap * 3 : nullptr;
+  p.rec = pb.rec + (size_t)p0 * pb.qcap * 9;
+  p.kind = pb.kind + (size_t)p0 * pb.qcap;
+  p.stats = pb.stats + p0 * 8;
+  p.T = pb.T + p0 * 7;
+  { TimedScope t(c, kT_orb_match); hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p); }
+  if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(n), dim3(kLmThreads), 0, st, p, 20); }
+  OCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- batch intensity odometry
+struct OrbBatch {
+  lislam_ctx* ctx = nullptr;
+  int nfeatures = 0;
+  bool has_mask = false;
+  OrbEngine* e1 = nullptr;
+  OrbEngine* e2 = nullptr;  // 2 * nfeatures, re-detection
+  PairBufs pb;
+  std::vector<void*> allocs;
+  double* outT = nullptr;   // [S][7]
+  int* outS = nullptr;      // [S][8]
+  ~OrbBatch() {
+    delete e1;
+    delete e2;
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+void lislam_free_orb(void* p) { delete static_cast<OrbBatch*>(p); }
+
+namespace {
+
+int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch** out) {
+  lislam_ctx* c = b->ctx;
+  OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
+  if (ob && (ob->nfeatures != nfeatures || ob->has_mask != (mask != nullptr))) {
+    (void)hipStreamSynchronize(c->stream);
+    delete ob;
+    ob = nullptr;
+    b->orb = nullptr;
+  }
+  if (!ob) {
+    ob = new OrbBatch();
+    b->orb = ob;
+    ob->ctx = c;
+    ob->nfeatures = nfeatures;
+    ob->has_mask = mask != nullptr;
+    ob->e1 = new OrbEngine();
+    ob->e2 = new OrbEngine();
+    ORC(engine_init(ob->e1, c, b->H, b->W, b->max_scans, nfeatures, mask));
+    ORC(engine_init(ob->e2, c, b->H, b->W, b->max_scans, 2 * nfeatures, mask));
+    ORC(ob->pb.init(c, b->max_scans, std::max(ob->e1->g.cap, ob->e2->g.cap), false));
+    void* q = nullptr;
+    OCHK(c, hipMalloc(&q, (size_t)b->max_scans * 7 * 8));
+    ob->allocs.push_back(q);
+    ob->outT = static_cast<double*>(q);
+    OCHK(c, hipMalloc(&q, (size_t)b->max_scans * 8 * 4));
+    ob->allocs.push_back(q);
+    ob->outS = static_cast<int*>(q);
+  }
+  *out = ob;
+  return LISLAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask) {
+  if (!b || n_scans < 1 || n_scans > b->max_scans || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  if (!b->fa.img_int || !b->fa.track)
+    return ofail(c, LISLAM_ERR_STATE, "lislam_batch_intensity_odometry needs want_images (the a1 images)");
+  hipSetDevice(c->device);
+  hipStream_t st = c->stream;
+  OrbBatch* ob = nullptr;
+  ORC(orb_batch_get(b, nfeatures, mask, &ob));
+  const uint8_t* img = b->fa.img_int;
+  const float4* trk = reinterpret_cast<const float4*>(b->fa.track);
+  ORC(engine_detect_slots(ob->e1, img, trk, 0, n_scans));
+  const int np = n_scans - 1;
+  std::vector<int> qs(std::max(np, 1)), ts(std::max(np, 1));
+  for (int k = 1; k < n_scans; k++) { qs[k - 1] = k; ts[k - 1] = k - 1; }
+  ORC(run_pairs(c, ob->e1, ob->e1, qs.data(), ts.data(), np, 0.3, ob->pb, 0, true));
+  std::vector<int> hs((size_t)std::max(np, 1) * 8);
+  if (np > 0) OCHK(c, hipMemcpyAsync(hs.data(), ob->pb.stats, (size_t)np * 8 * 4, hipMemcpyDeviceToHost, st));
+  OCHK(c, hipStreamSynchronize(st));
+  // outputs: scan 0 = first frame; scan k = pair (k-1, k)
+  {
+    std::vector<int> s0 = {-1, 0, 0, 0, 0, 0, 0, 0};
+    const double I[7] = {0, 0, 0, 1, 0, 0, 0};
+    OCHK(c, hipMemcpyAsync(ob->outS, s0.data(), 32, hipMemcpyHostToDevice, st));
+    OCHK(c, hipMemcpyAsync(ob->outT, I, 56, hipMemcpyHostToDevice, st));
+    OCHK(c, hipMemcpyAsync(ob->outS + 2, ob->e1->nkp, 4, hipMemcpyDeviceToDevice, st));
+    if (np > 0) {
+      OCHK(c, hipMemcpyAsync(ob->outS + 8, ob->pb.stats, (size_t)np * 32, hipMemcpyDeviceToDevice, st));
+      OCHK(c, hipMemcpyAsync(ob->outT + 7, ob->pb.T, (size_t)np * 56, hipMemcpyDeviceToDevice, st));
+    }
+  }
+  // the rare sequential cases: a frame whose previous frame was re-detected, or a failed test
+  // (feature_tracker::detectfeatures re-detects both frames with 2 * nfeatures)
+  bool prev2 = false;
+  std::vector<char> have2(n_scans, 0);
+  for (int k = 1; k < n_scans; k++) {
+    const int* s = &hs[(size_t)(k - 1) * 8];
+    bool ok = s[0] == 1;
+    bool redone = false;
+    const int slot = k - 1;  // the pair's own buffer slot
+    if (prev2) {
+      const int q = k, t = k - 1;
+      ORC(run_pairs(c, ob->e1, ob->e2, &q, &t, 1, 0.3, ob->pb, slot, true));
+      int h8[8];
+      OCHK(c, hipMemcpyAsync(h8, ob->pb.stats + slot * 8, 32, hipMemcpyDeviceToHost, st));
+      OCHK(c, hipStreamSynchronize(st));
+      ok = h8[0] == 1;
+      redone = true;
+    }
+    bool cur2 = false;
+    if (!ok) {
+      for (int sc : {k - 1, k})
+        if (!have2[sc]) { ORC(engine_detect_slots(ob->e2, img, trk, sc, 1)); have2[sc] = 1; }
+      const int q = k, t = k - 1;
+      ORC(run_pairs(c, ob->e2, ob->e2, &q, &t, 1, 0.2, ob->pb, slot, true));
+      cur2 = true;
+      redone = true;
+    }
+    if (redone) {
+      if (cur2) {  // mark re-detection
+        int one = 1;
+        OCHK(c, hipMemcpyAsync(ob->pb.stats + slot * 8 + 1, &one, 4, hipMemcpyHostToDevice, st));
+      }
+      OCHK(c, hipMemcpyAsync(ob->outS + (size_t)k * 8, ob->pb.stats + slot * 8, 32, hipMemcpyDeviceToDevice, st));
+      OCHK(c, hipMemcpyAsync(ob->outT + (size_t)k * 7, ob->pb.T + slot * 7, 56, hipMemcpyDeviceToDevice, st));
+      OCHK(c, hipStreamSynchronize(st));
+    }
+    prev2 = cur2;
+  }
+  return LISLAM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- single frame drop-in
+struct lislam_intensity_tracker {
+  lislam_ctx* ctx = nullptr;
+  int H = 0, W = 0, nfeatures = 0;
+  OrbEngine e1, e2;
+  PairBufs pb;
+  uint8_t* img = nullptr;   // [2][H*W]
+  float4* trk = nullptr;    // [2][H*W]
+  int cur = 0;
+  bool have_prev = false, prev2 = false;
+};
+
+extern "C" {
+
+int lislam_intensity_tracker_create(lislam_ctx* c, int32_t H, int32_t W, int32_t nfeatures, const uint8_t* mask,
+                                    lislam_intensity_tracker** out) {
+  if (!c || !out || H < 8 || W < 8 || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
+  *out = nullptr;
+  hipSetDevice(c->device);
+  lislam_intensity_tracker* t = new lislam_intensity_tracker();
+  t->ctx = c; t->H = H; t->W = W; t->nfeatures = nfeatures;
+  int rc = engine_init(&t->e1, c, H, W, 2, nfeatures, mask);
+  if (!rc) rc = engine_init(&t->e2, c, H, W, 2, 2 * nfeatures, mask);
+  if (!rc) rc = t->pb.init(c, 1, std::max(t->e1.g.cap, t->e2.g.cap), false);
+  if (!rc) rc = t->e1.alloc(&t->img, (size_t)2 * H * W);
+  if (!rc) rc = t->e1.alloc(&t->trk, (size_t)2 * H * W);
+  if (rc) { delete t; return rc; }
+  *out = t;
+  return LISLAM_OK;
+}
+
+int lislam_intensity_tracker_destroy(lislam_intensity_tracker* t) {
+  if (!t) return LISLAM_OK;
+  hipSetDevice(t->ctx->device);
+  (void)hipStreamSynchronize(t->ctx->stream);
+  delete t;
+  return LISLAM_OK;
+}
+
+int lislam_intensity_tracker_step(lislam_intensity_tracker* t, const uint8_t* image, const float* cloud_track,
+                                  double* T_out, int32_t* stats_out) {
+  if (!t || !image || !cloud_track) return LISLAM_ERR_ARG;
+  lislam_ctx* c = t->ctx;
+  hipSetDevice(c->device);
+  hipStream_t st = c->stream;
+  const size_t N = (size_t)t->H * t->W;
+  const int cs = t->cur, ps = 1 - t->cur;
+  OCHK(c, hipMemcpyAsync(t->img + cs * N, image, N, hipMemcpyDefault, st));
+  OCHK(c, hipMemcpyAsync(t->trk + cs * N, cloud_track, N * 16, hipMemcpyDefault, st));
+  ORC(engine_detect_slots(&t->e1, t->img, t->trk, cs, 1));
+  int h8[8] = {-1, 0, 0, 0, 0, 0, 0, 0};
+  double T[7] = {0, 0, 0, 1, 0, 0, 0};
+  bool cur2 = false;
+  if (!t->have_prev) {
+    OCHK(c, hipMemcpyAsync(&h8[2], t->e1.nkp + cs, 4, hipMemcpyDeviceToHost, st));
+    OCHK(c, hipStreamSynchronize(st));
+  } else {
+    ORC(run_pairs(c, &t->e1, t->prev2 ? &t->e2 : &t->e1, &cs, &ps, 1, 0.3, t->pb, 0, true));
+    OCHK(c, hipMemcpyAsync(h8, t->pb.stats, 32, hipMemcpyDeviceToHost, st));
+    OCHK(c, hipStreamSynchronize(st));
+    if (h8[0] != 1) {  // re-detect both frames with 2 * nfeatures (intensity_feature_tracker.cpp:652-687)
+      ORC(engine_detect_slots(&t->e2, t->img, t->trk, cs, 1));
+      if (!t->prev2) ORC(engine_detect_slots(&t->e2, t->img, t->trk, ps, 1));
+      ORC(run_pairs(c, &t->e2, &t->e2, &cs, &ps, 1, 0.2, t->pb, 0, true));
+      OCHK(c, hipMemcpyAsync(h8, t->pb.stats, 32, hipMemcpyDeviceToHost, st));
+      OCHK(c, hipStreamSynchronize(st));
+      h8[1] = 1;
+      cur2 = true;
+    }
+    OCHK(c, hipMemcpyAsync(T, t->pb.T, 56, hipMemcpyDeviceToHost, st));
+    OCHK(c, hipStreamSynchronize(st));
+  }
+  t->have_prev = true;
+  t->prev2 = cur2;
+  t->cur = ps;
+  if (T_out) std::memcpy(T_out, T, 56);
+  if (stats_out) std::memcpy(stats_out, h8, 32);
+  return LISLAM_OK;
+}
+
+// ---------------------------------------------------------------- building blocks
+int lislam_orb_detect(lislam_ctx* c, const uint8_t* image, const float* cloud_track, const uint8_t* mask, int32_t H,
+                      int32_t W, int32_t nfeatures, float* kp, uint8_t* desc, float* p3d, int32_t cap, int32_t* n) {
+  if (!c || !image || !cloud_track || !n || H < 8 || W < 8 || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  hipStream_t st = c->stream;
+  OrbEngine e;
+  ORC(engine_init(&e, c, H, W, 1, nfeatures, mask));
+  uint8_t* dimg = nullptr;
+  float4* dtrk = nullptr;
+  ORC(e.alloc(&dimg, (size_t)H * W));
+  ORC(e.alloc(&dtrk, (size_t)H * W));
+  OCHK(c, hipMemcpyAsync(dimg, image, (size_t)H * W, hipMemcpyDefault, st));
+  OCHK(c, hipMemcpyAsync(dtrk, cloud_track, (size_t)H * W * 16, hipMemcpyDefault, st));
+  ORC(engine_detect_slots(&e, dimg, dtrk, 0, 1));
+  int cnt = 0, ovf = 0;
+  OCHK(c, hipMemcpyAsync(&cnt, e.nkp, 4, hipMemcpyDeviceToHost, st));
+  OCHK(c, hipMemcpyAsync(&ovf, e.overflow, 4, hipMemcpyDeviceToHost, st));
+  OCHK(c, hipStreamSynchronize(st));
+  *n = cnt;
+  if (ovf) return ofail(c, LISLAM_ERR_CAPACITY, "ORB level keypoint capacity exceeded");
+  if (cnt > cap) return ofail(c, LISLAM_ERR_CAPACITY, "lislam_orb_detect: %d keypoints > cap %d", cnt, cap);
+  if (kp) OCHK(c, hipMemcpyAsync(kp, e.kp, (size_t)cnt * 24, hipMemcpyDefault, st));
+  if (desc) OCHK(c, hipMemcpyAsync(desc, e.desc, (size_t)cnt * 32, hipMemcpyDefault, st));
+  if (p3d) OCHK(c, hipMemcpyAsync(p3d, e.p3d, (size_t)cnt * 16, hipMemcpyDefault, st));
+  OCHK(c, hipStreamSynchronize(st));
+  return LISLAM_OK;
+}
+
+int lislam_orb_match(lislam_ctx* c, const uint8_t* qdesc, int32_t nq, const uint8_t* tdesc, int32_t nt, int32_t* matches,
+                     int32_t* n_matches) {
+  if (!c || nq < 0 || nt < 0 || nq > 65535 || nt > 65535 || !n_matches || (nq && !qdesc) || (nt && !tdesc))
+    return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  hipStream_t st = c->stream;
+  // a minimal engine-shaped view: descriptors with cap = max(nq, nt, 1) per "scan"
+  OrbEngine e;
+  e.ctx = c;
+  const int cap = std::max(std::max(nq, nt), 1);
+  e.g.cap = cap;
+  ORC(e.alloc(&e.desc, (size_t)2 * cap * 32));
+  ORC(e.alloc(&e.p3d, (size_t)2 * cap));
+  ORC(e.alloc(&e.nkp, 2));
+  const int cnts[2] = {nq, nt};
+  OCHK(c, hipMemcpyAsync(e.nkp, cnts, 8, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemsetAsync(e.p3d, 0, (size_t)2 * cap * 16, st));
+  if (nq) OCHK(c, hipMemcpyAsync(e.desc, qdesc, (size_t)nq * 32, hipMemcpyDefault, st));
+  if (nt) OCHK(c, hipMemcpyAsync(e.desc + (size_t)cap * 32, tdesc, (size_t)nt * 32, hipMemcpyDefault, st));
+  PairBufs pb;
+  ORC(pb.init(c, 1, cap, true));
+  const int q = 0, t = 1;
+  ORC(run_pairs(c, &e, &e, &q, &t, 1, 0.3, pb, 0, false));
+  int h8[8];
+  OCHK(c, hipMemcpyAsync(h8, pb.stats, 32, hipMemcpyDeviceToHost, st));
+  OCHK(c, hipStreamSynchronize(st));
+  *n_matches = h8[3];
+  if (matches && h8[3]) OCHK(c, hipMemcpyAsync(matches, pb.mout, (size_t)h8[3] * 12, hipMemcpyDefault, st));
+  OCHK(c, hipStreamSynchronize(st));
+  return LISLAM_OK;
+}
+
+}  // extern "C"
+
+// Outputs of lislam_batch_intensity_odometry for lislam_batch_download.
+int lislam_orb_batch_output(lislam_batch* b, int what, int scan, const void** src, int* cnt, size_t* esz) {
+  OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
+  if (!ob) return LISLAM_ERR_STATE;
+  const Geom& g = ob->e1->g;
+  switch (what) {
+    case LISLAM_OUT_ORB_T: *src = ob->outT + (size_t)scan * 7; *cnt = 7; *esz = 8; return LISLAM_OK;
+    case LISLAM_OUT_ORB_STATS: *src = ob->outS + (size_t)scan * 8; *cnt = 8; *esz = 4; return LISLAM_OK;
+    case LISLAM_OUT_ORB_KEYPOINTS:
+    case LISLAM_OUT_ORB_POINTS:
+    case LISLAM_OUT_ORB_DESCRIPTORS: {
+      int n = 0;
+      hipStream_t st = b->ctx->stream;
+      if (hipMemcpyAsync(&n, ob->e1->nkp + scan, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return LISLAM_ERR_DEVICE;
+      *cnt = n;
+      if (what == LISLAM_OUT_ORB_KEYPOINTS) { *src = ob->e1->kp + (size_t)scan * g.cap * 6; *esz = 24; }
+      else if (what == LISLAM_OUT_ORB_POINTS) { *src = ob->e1->p3d + (size_t)scan * g.cap; *esz = 16; }
+      else { *src = ob->e1->desc + (size_t)scan * g.cap * 32; *esz = 32; }
+      return LISLAM_OK;
+    }
+  }
+  return LISLAM_ERR_ARG;
+}

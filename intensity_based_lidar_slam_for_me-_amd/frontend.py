@@ -149,6 +149,14 @@ class Batch:
     def odometry(self, n: int, chain_len: int):
         nat.check(self.ctx.lib.lislam_batch_odometry(self.h, n, chain_len), self.ctx.h, "lislam_batch_odometry")
 
+    def intensity_odometry(self, n: int, nfeatures: int = 1000, mask=None):
+        """feature_tracker::detectfeatures over scans [0, n) of the batch (ORB path a8-a11)."""
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        rc = self.ctx.lib.lislam_batch_intensity_odometry(self.h, n, nfeatures,
+                                                          None if m is None else ctypes.c_void_p(m.ctypes.data))
+        nat.check(rc, self.ctx.h, "lislam_batch_intensity_odometry")
+        self._mask_keep = m
+
     def set_timing(self, on: bool):
         nat.check(self.ctx.lib.lislam_batch_set_timing(self.h, int(on)), self.ctx.h, "lislam_batch_set_timing")
 
@@ -168,7 +176,9 @@ class Batch:
            nat.OUT_LASER_CLOUD: (np.float32, 4), nat.OUT_CURVATURE: (np.float32, 1), nat.OUT_LABEL: (np.int8, 1),
            nat.OUT_LINE_OFFSETS: (np.int32, 1), nat.OUT_SHARP: (np.float32, 4), nat.OUT_LESS_SHARP: (np.float32, 4),
            nat.OUT_FLAT: (np.float32, 4), nat.OUT_LESS_FLAT: (np.float32, 4), nat.OUT_PARA: (np.float64, 1),
-           nat.OUT_POSE: (np.float64, 1), nat.OUT_STATS: (np.int32, 1)}
+           nat.OUT_POSE: (np.float64, 1), nat.OUT_STATS: (np.int32, 1), nat.OUT_ORB_T: (np.float64, 1),
+           nat.OUT_ORB_STATS: (np.int32, 1), nat.OUT_ORB_KEYPOINTS: (np.float32, 6), nat.OUT_ORB_POINTS: (np.float32, 4),
+           nat.OUT_ORB_DESCRIPTORS: (np.uint8, 32)}
 
     def download(self, what: int, scan: int) -> np.ndarray:
         dt, w = self._DT[what]

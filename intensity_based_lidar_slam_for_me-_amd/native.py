@@ -20,6 +20,7 @@ OUT_IMAGE_RANGE, OUT_IMAGE_INTENSITY, OUT_CLOUD_TRACK, OUT_LASER_CLOUD = 0, 1, 2
 OUT_CURVATURE, OUT_LABEL, OUT_LINE_OFFSETS = 4, 5, 6
 OUT_SHARP, OUT_LESS_SHARP, OUT_FLAT, OUT_LESS_FLAT = 7, 8, 9, 10
 OUT_PARA, OUT_POSE, OUT_STATS = 11, 12, 13
+OUT_ORB_T, OUT_ORB_STATS, OUT_ORB_KEYPOINTS, OUT_ORB_POINTS, OUT_ORB_DESCRIPTORS = 14, 15, 16, 17, 18
 
 KERNELS = ("k_scan_front", "k_scan_lines", "k_scan_compact", "k_target_index", "k_odom_assoc", "k_odom_lm")
 
@@ -34,9 +35,12 @@ EXPORTED_SYMBOLS = (
     "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_laser_mapping",
     "lislam_map_set_timing", "lislam_map_kernel_times",
+    "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
+    "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry",
 )
 
-MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample")
+MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
+               "k_orb_fast", "k_orb_select", "k_orb_finish", "k_orb_blur", "k_orb_desc", "k_orb_match", "k_orb_lm")
 
 MATCH_LINE, MATCH_PLANE = 0, 1
 
@@ -134,6 +138,12 @@ def load(path: str = LIB_PATH):
     L.lislam_voxel_grid.argtypes = [vp, vp, _i32, ctypes.c_float, vp, _i32p]
     L.lislam_mapopt_step.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
     L.lislam_laser_mapping.argtypes = [vp, vp, vp, _i32, vp, _i32, vp, vp]
+    L.lislam_orb_detect.argtypes = [vp, vp, vp, vp, _i32, _i32, _i32, vp, vp, vp, _i32, _i32p]
+    L.lislam_orb_match.argtypes = [vp, vp, _i32, vp, _i32, vp, _i32p]
+    L.lislam_intensity_tracker_create.argtypes = [vp, _i32, _i32, _i32, vp, ctypes.POINTER(vp)]
+    L.lislam_intensity_tracker_destroy.argtypes = [vp]
+    L.lislam_intensity_tracker_step.argtypes = [vp, vp, vp, vp, vp]
+    L.lislam_batch_intensity_odometry.argtypes = [vp, _i32, _i32, vp]
     L.lislam_map_set_timing.argtypes = [vp, _i32]
     L.lislam_map_kernel_times.argtypes = [vp, _fp, _i32p]
     for name in EXPORTED_SYMBOLS:

@@ -53,6 +53,12 @@ def lib():
         L.oracle_map_solve.argtypes = [_f64p, _i32p, ctypes.c_int, _f64p, ctypes.c_int, _i32p]
         L.oracle_mapopt_step.argtypes = [vp, _f32p, ctypes.c_int, _f64p, _f64p, _f64p, _i32p]
         L.oracle_laser_mapping.argtypes = [vp, vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _i32p]
+        L.oracle_orb_detect.argtypes = [_u8p, vp, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _u8p, _f32p,
+                                        ctypes.c_int]
+        L.oracle_orb_level.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _i32p, _i32p]
+        L.oracle_orb_match.argtypes = [_u8p, ctypes.c_int, _u8p, ctypes.c_int, _i32p]
+        L.oracle_intensity_odometry.argtypes = [ctypes.c_int, _u8p, _f32p, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                _i32p, _f64p]
         _LIB = L
     return _LIB
 
@@ -232,3 +238,63 @@ def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):
     stats = np.zeros(4, np.int32)
     lib().oracle_laser_mapping(corner_map.h, surf_map.h, c.reshape(-1), c.shape[0], s.reshape(-1), s.shape[0], x, stats)
     return x, stats
+
+
+def hand_held_mask(H: int = 64, W: int = 1024, crop: int = 3) -> np.ndarray:
+    """feature_tracker::setMask (intensity_feature_tracker.cpp:1126-1136): 0 where j < crop or j > W - crop."""
+    m = np.full((H, W), 255, np.uint8)
+    j = np.arange(W)
+    m[:, (j < crop) | (j > W - crop)] = 0
+    return m
+
+
+def _mask_ptr(mask):
+    if mask is None:
+        return None, None
+    m = np.ascontiguousarray(mask, np.uint8)
+    return ctypes.c_void_p(m.ctypes.data), m
+
+
+def orb_detect(img: np.ndarray, track: np.ndarray, nfeatures: int = 1000, mask=None):
+    """ORB detect + zero filter + compute: (keypoints (n, 6) = x, y, size, angle, response, octave,
+    descriptors (n, 32) u8, points (n, 3))."""
+    im = np.ascontiguousarray(img, np.uint8)
+    H, W = im.shape
+    tr = np.ascontiguousarray(track, np.float32).reshape(-1)
+    cap = 8 * nfeatures + 64
+    kp = np.zeros((cap, 6), np.float32)
+    de = np.zeros((cap, 32), np.uint8)
+    p3 = np.zeros((cap, 3), np.float32)
+    mp, _keep = _mask_ptr(mask)
+    n = lib().oracle_orb_detect(im.reshape(-1), mp, tr, W, H, nfeatures, kp.reshape(-1), de.reshape(-1), p3.reshape(-1), cap)
+    return kp[:n], de[:n], p3[:n]
+
+
+def orb_level(img: np.ndarray, level: int, blurred: bool = False) -> np.ndarray:
+    im = np.ascontiguousarray(img, np.uint8)
+    H, W = im.shape
+    out = np.zeros(H * W, np.uint8)
+    w = np.zeros(1, np.int32)
+    h = np.zeros(1, np.int32)
+    lib().oracle_orb_level(im.reshape(-1), W, H, level, int(blurred), out, w, h)
+    return out[: w[0] * h[0]].reshape(h[0], w[0])
+
+
+def orb_match(qdesc: np.ndarray, tdesc: np.ndarray) -> np.ndarray:
+    q = np.ascontiguousarray(qdesc, np.uint8)
+    t = np.ascontiguousarray(tdesc, np.uint8)
+    out = np.zeros((max(q.shape[0], 1), 3), np.int32)
+    m = lib().oracle_orb_match(q.reshape(-1), q.shape[0], t.reshape(-1), t.shape[0], out.reshape(-1))
+    return out[:m]
+
+
+def intensity_odometry(imgs: np.ndarray, tracks: np.ndarray, nfeatures: int = 1000, mask=None):
+    """feature_tracker::detectfeatures over frames: (stats (n, 8), T_s2s (n, 7))."""
+    im = np.ascontiguousarray(imgs, np.uint8)
+    n, H, W = im.shape
+    tr = np.ascontiguousarray(tracks, np.float32).reshape(-1)
+    st = np.zeros((n, 8), np.int32)
+    T = np.zeros((n, 7))
+    mp, _keep = _mask_ptr(mask)
+    lib().oracle_intensity_odometry(n, im.reshape(-1), tr, mp, W, H, nfeatures, st.reshape(-1), T.reshape(-1))
+    return st, T

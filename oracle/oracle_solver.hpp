@@ -78,6 +78,21 @@ struct PlaneNormFactor {  // LidarPlaneNormFactor, lidarFeaturePointsFunction.hp
   }
 };
 
+struct P2PFactor {  // front_end_residual, lidarFeaturePointsFunction.hpp:21-58
+  double src[3], dst[3];
+  static constexpr int kResiduals = 3;
+  template <typename T>
+  bool operator()(const T* q, const T* t, T* residual) const {
+    Q4<T> qq{q[0], q[1], q[2], q[3]};
+    V3<T> cp{T(src[0]), T(src[1]), T(src[2])};
+    V3<T> p = rotate(qq, cp) + V3<T>{t[0], t[1], t[2]};
+    residual[0] = p.x - T(dst[0]);
+    residual[1] = p.y - T(dst[1]);
+    residual[2] = p.z - T(dst[2]);
+    return true;
+  }
+};
+
 // AutoDiffCostFunction<F, R, 4, 3>::Evaluate: residuals, and the 7-column global Jacobian.
 template <typename F>
 static void autodiff_eval(const F& f, const double* q, const double* t, double* r, double* J /*R x 7 or null*/) {
@@ -120,11 +135,12 @@ static void quat_plus(const double* x, const double* d, double* xp) {
 
 // ------------------------------------------------------------------ residual blocks + evaluator
 struct Block {
-  int kind;  // 0 edge, 1 plane, 2 plane-norm
+  int kind;  // 0 edge, 1 plane, 2 plane-norm, 3 point-to-point (front_end_residual)
   EdgeFactor e;
   PlaneFactor p;
   PlaneNormFactor pn;
-  int nres() const { return kind == 0 ? 3 : 1; }
+  P2PFactor pp;
+  int nres() const { return (kind == 0 || kind == 3) ? 3 : 1; }
 };
 
 // ceres::HuberLoss(a).Evaluate(s, rho)
@@ -165,7 +181,8 @@ struct Problem {
       double* jp = J ? Jg : nullptr;
       if (b.kind == 0) autodiff_eval(b.e, q, t, r, jp);
       else if (b.kind == 1) autodiff_eval(b.p, q, t, r, jp);
-      else autodiff_eval(b.pn, q, t, r, jp);
+      else if (b.kind == 2) autodiff_eval(b.pn, q, t, r, jp);
+      else autodiff_eval(b.pp, q, t, r, jp);
       double sq = 0;
       for (int i = 0; i < R; i++) sq += r[i] * r[i];
       double rho[3];

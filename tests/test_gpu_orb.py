@@ -1,0 +1,126 @@
+"""GPU parity of the ORB intensity front end (a8-a11) through the C ABI against the CPU oracle.
+
+Keypoints (positions, angles, responses, octaves), descriptors, cloud points and matches are
+integer / byte / same-order float work and must be bit-exact; T_s2s within the north-star pose
+tolerance 1e-4 (measured agreement ~1e-15).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(n_scans=64, width=1024)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def frames(oracle, synth):
+    scans = synth.make_sequence(6, start=20)
+    feats = [oracle.scan_registration(s) for s in scans]
+    imgs = np.stack([f.img_intensity for f in feats])
+    tracks = np.stack([f.cloud_track for f in feats])
+    return scans, imgs, tracks
+
+
+@pytest.mark.parametrize("nfeatures,masked", [(1000, True), (2000, True), (500, False)])
+def test_orb_detect_bit_exact(pkg, oracle, ctx, frames, nfeatures, masked):
+    _, imgs, tracks = frames
+    mask = oracle.hand_held_mask() if masked else None
+    for k in (0, 3):
+        kp, de, p3 = pkg.intensity.orb_detect(ctx, imgs[k], tracks[k], nfeatures, mask)
+        rkp, rde, rp3 = oracle.orb_detect(imgs[k], tracks[k], nfeatures, mask)
+        assert kp.shape == rkp.shape, (k, kp.shape, rkp.shape)
+        assert np.array_equal(kp, rkp), k
+        assert np.array_equal(de, rde), k
+        assert np.array_equal(p3[:, :3], rp3), k
+
+
+def test_orb_detect_128_lines(pkg, oracle, synth):
+    c = pkg.Context(n_scans=128, width=2048)
+    scan = synth.make_scan(5, 128, 2048)
+    f = oracle.scan_registration(scan)
+    kp, de, p3 = pkg.intensity.orb_detect(c, f.img_intensity, f.cloud_track, 1000, oracle.hand_held_mask(128, 2048))
+    rkp, rde, rp3 = oracle.orb_detect(f.img_intensity, f.cloud_track, 1000, oracle.hand_held_mask(128, 2048))
+    assert np.array_equal(kp, rkp) and np.array_equal(de, rde)
+    c.close()
+
+
+def test_orb_match_bit_exact(pkg, oracle, ctx, frames):
+    _, imgs, tracks = frames
+    mask = oracle.hand_held_mask()
+    _, d0, _ = oracle.orb_detect(imgs[0], tracks[0], 1000, mask)
+    _, d1, _ = oracle.orb_detect(imgs[1], tracks[1], 1000, mask)
+    g = pkg.intensity.orb_match(ctx, d1, d0)
+    r = oracle.orb_match(d1, d0)
+    assert np.array_equal(g, r)
+    rng = np.random.default_rng(3)  # random descriptors: many distance ties
+    a = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (900, 32), dtype=np.uint8)
+    b[:50] = a[:50]
+    assert np.array_equal(pkg.intensity.orb_match(ctx, a, b), oracle.orb_match(a, b))
+    assert pkg.intensity.orb_match(ctx, a[:0], b).shape[0] == 0
+
+
+def test_intensity_tracker_sequence(pkg, oracle, ctx, frames):
+    _, imgs, tracks = frames
+    mask = oracle.hand_held_mask()
+    tr = pkg.intensity.IntensityTracker(ctx, 64, 1024, 1000, mask)
+    rst, rT = oracle.intensity_odometry(imgs, tracks, 1000, mask)
+    for k in range(len(imgs)):
+        T, st = tr.detectfeatures(imgs[k], tracks[k])
+        assert list(st[:5]) == list(rst[k, :5]) and st[7] == rst[k, 7], (k, st, rst[k])
+        if st[0] == 1:
+            assert st[5] == rst[k, 5] and st[6] == rst[k, 6]
+        assert np.max(np.abs(T - rT[k])) < POSE_TOL, (k, T, rT[k])
+    tr.close()
+
+
+def test_intensity_tracker_redetect_path(pkg, oracle, ctx, frames):
+    """Identical consecutive frames give equal keypoint counts, so the good-frame test fails and
+    both frames are re-detected with 2 * nfeatures (intensity_feature_tracker.cpp:652-687)."""
+    _, imgs, tracks = frames
+    seq_i = np.stack([imgs[0], imgs[0], imgs[1], imgs[2]])
+    seq_t = np.stack([tracks[0], tracks[0], tracks[1], tracks[2]])
+    mask = oracle.hand_held_mask()
+    tr = pkg.intensity.IntensityTracker(ctx, 64, 1024, 1000, mask)
+    rst, rT = oracle.intensity_odometry(seq_i, seq_t, 1000, mask)
+    assert rst[1, 1] == 1  # the oracle re-detected
+    for k in range(len(seq_i)):
+        T, st = tr.detectfeatures(seq_i[k], seq_t[k])
+        assert list(st[:5]) == list(rst[k, :5]) and st[7] == rst[k, 7], (k, st, rst[k])
+        assert np.max(np.abs(T - rT[k])) < POSE_TOL, (k, T, rT[k])
+    tr.close()
+
+
+def test_batch_intensity_odometry_matches_tracker(pkg, oracle, ctx, frames):
+    scans, imgs, tracks = frames
+    seq = np.concatenate([scans[:2], scans[1:2], scans[2:]])  # a repeated frame forces re-detection
+    n = seq.shape[0]
+    feats = [oracle.scan_registration(s) for s in seq]
+    si = np.stack([f.img_intensity for f in feats])
+    stt = np.stack([f.cloud_track for f in feats])
+    mask = oracle.hand_held_mask()
+    rst, rT = oracle.intensity_odometry(si, stt, 1000, mask)
+    b = pkg.Batch(ctx, n)
+    b.upload(seq)
+    b.extract(n)
+    b.intensity_odometry(n, 1000, mask)
+    nat = pkg.native
+    for k in range(n):
+        st = b.download(nat.OUT_ORB_STATS, k)
+        T = b.download(nat.OUT_ORB_T, k)
+        if k == 0:
+            assert st[0] == -1
+            continue
+        assert list(st[:5]) == list(rst[k, :5]) and st[7] == rst[k, 7], (k, st, rst[k])
+        assert np.max(np.abs(T - rT[k])) < POSE_TOL, (k, T, rT[k])
+    kp = b.download(nat.OUT_ORB_KEYPOINTS, 2)
+    rkp, _, _ = oracle.orb_detect(si[2], stt[2], 1000, mask)
+    assert np.array_equal(kp, rkp)
+    b.close()
