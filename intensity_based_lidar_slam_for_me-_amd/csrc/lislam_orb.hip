@@ -11,19 +11,23 @@
 // octave; descriptors 32 B; cloud points float4.
 //
 // Kernels (the semantics are those of oracle/oracle_orb.cpp, which restates OpenCV 4.x):
-//   k_orb_pyramid   1 WG per scan: level 0 copy, levels 1..7 by the bit-exact fixed-point
-//                   INTER_LINEAR_EXACT resize of the previous level, borders
+//   k_orb_level     per level (in order), 1 thread per padded pixel: level 0 copy, levels 1..7 by
+//                   the bit-exact fixed-point INTER_LINEAR_EXACT resize of the previous level;
+//                   border pixels evaluate their reflect-101 source directly
 //   k_orb_blur      1 thread per padded pixel: 7x7 sigma-2 separable float Gaussian (row sums
 //                   then the symmetric column sum, the FilterEngine order) on the ROI, border copy
 //   k_orb_fast      1 thread per level pixel: FAST-9/16 segment test + cornerScore<16>
-//   k_orb_select    1 WG per (scan, level): 3x3 non-max suppression, mask, ordered compaction,
-//                   retainBest(2n) on the FAST score (256-bin histogram), Harris responses,
-//                   retainBest(n) on them (radix select of the n-th largest), intensity-centroid
-//                   angle; detection order is kept (OpenCV's set, canonical order)
+//   k_orb_nms       1 thread per level pixel: 3x3 non-max suppression, mask, border
+//   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
+//                   thread), retainBest(2n) on the FAST score (256-bin histogram), Harris responses
+//                   (a wavefront per candidate), retainBest(n) on them (radix select of the n-th
+//                   largest), intensity-centroid angle (a wavefront per keypoint); detection order
+//                   is kept (OpenCV's set, canonical order)
 //   k_orb_finish    1 WG per scan: levels concatenated, coordinates scaled to level 0,
 //                   cloud-track lookup + |x| < 0.01 filter (extractPointsAndFilterZeroValue)
 //   k_orb_desc      32 threads per keypoint: steered rBRIEF-256 bytes
-//   k_orb_match     1 WG per scan pair: XOR-popcount distances, batchDistance's cross-check,
+//   k_orb_match     1 WG per scan pair: XOR-popcount distances against LDS query tiles (wave-
+//                   broadcast reads), batchDistance's cross-check,
 //                   stable counting selection of the first ceil(frac M) matches, good-frame
 //                   test, front_end_residual records
 //   k_orb_lm        1 WG per scan pair: Ceres-semantics LM (20 iterations) of those records
@@ -51,6 +55,12 @@ constexpr int kFastT = 20;
 constexpr int kSelThreads = 1024;
 constexpr int kPairThreads = 1024;
 constexpr int kLmThreads = 256;
+constexpr int kQTile = 1024;  // queries per LDS tile in k_orb_xdist (32 KiB)
+constexpr int kNoMatch = 0x7f7f7f7f;  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
+
+constexpr int kNPatch = 749;  // pixels of the ICAngles circular patch (half size 15; checked on the host)
+constexpr int kPatchIters = (kNPatch + 63) / 64;
+__constant__ short2 c_patch[1024];  // (du, dv) of every pixel of the ICAngles patch (host-filled)
 
 __constant__ int c_pattern[256 * 4] = {
 #include "lislam_orb_pattern.inc"
@@ -58,6 +68,7 @@ __constant__ int c_pattern[256 * 4] = {
 
 struct Geom {
   int W, H;
+  int npatch;            // pixels of the circular intensity-centroid patch (c_patch)
   int w[kL], h[kL], stride[kL];
   int off[kL];      // byte offset of padded level l in a scan's pyramid
   int pix[kL + 1];  // prefix of w*h (flattened level pixels)
@@ -88,6 +99,7 @@ struct Args {
   uint8_t* blur;          // [S][bytes]
   const uint8_t* mpyr;    // [bytes] mask pyramid or null
   uint8_t* score;         // [S][pix[kL]]
+  uint8_t* nms;           // [S][pix[kL]] FAST score of a keypoint (non-max, mask, border), else 0
   int* cand;              // [S][pix[kL]] candidate pixel indices
   float* cresp;           // [S][pix[kL]]
   float* lkp;             // [S][cap][6] per-level staging (level l at lofs[l])
@@ -97,6 +109,7 @@ struct Args {
   uint8_t* desc;          // [S][cap][32]
   int* nkp;               // [S]
   int* overflow;          // [1]
+  const int* smap;        // scan of each grid scan index (null: identity from the slot base)
 };
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -129,50 +142,45 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* base, const Geom& g, con
   return (uint32_t)pxc(base, g, l - 1, row, t.xo[l * t.xs + g.w[l] - 1]) << 8;
 }
 
-// mode 0: image pyramids of scans; mode 1: the mask pyramid (constant-0 border, threshold 254)
-__global__ __launch_bounds__(1024) void k_orb_pyramid(Args a, int mode) {
-  const int s = blockIdx.x;
+// Level l of the pyramid (one thread per padded pixel, levels launched in order): a border pixel
+// takes the value of its reflect-101 image (mode 0) or 0 (mode 1, the mask pyramid); a ROI pixel
+// is level 0's image or the INTER_LINEAR_EXACT resize of level l-1 (mask: threshold 254 to 0).
+__global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
   const Geom& g = a.g;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
+  const int w = g.w[l], h = g.h[l], pw = g.stride[l];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= pw * (h + 2 * kB)) return;
   uint8_t* base = mode ? const_cast<uint8_t*>(a.mpyr) : a.pyr + (size_t)s * g.bytes;
-  const uint8_t* src = a.img + (size_t)s * g.W * g.H;
-  for (int l = 0; l < kL; l++) {
-    const int w = g.w[l], h = g.h[l];
-    for (int i = threadIdx.x; i < w * h; i += blockDim.x) {
-      const int y = i / w, x = i % w;
-      uint8_t v;
-      if (l == 0) {
-        v = src[y * g.W + x];
+  const int r = i / pw - kB, c = i % pw - kB;
+  const bool roi = r >= 0 && r < h && c >= 0 && c < w;
+  uint8_t v = 0;
+  if (roi || !mode) {
+    const int y = reflect101(r, h), x = reflect101(c, w);
+    if (l == 0) {
+      v = a.img[(size_t)s * g.W * g.H + y * g.W + x];
+    } else {
+      const int* lim = a.t.lim + l * 4;
+      if (y < lim[2] || y >= lim[3]) {
+        const uint32_t hv = hval(base, g, a.t, l, y < lim[2] ? 0 : g.h[l - 1] - 1, x);
+        v = (uint8_t)min(255u, (hv + 128u) >> 8);
       } else {
-        const int* lim = a.t.lim + l * 4;
-        if (y < lim[2] || y >= lim[3]) {
-          const uint32_t hv = hval(base, g, a.t, l, y < lim[2] ? 0 : g.h[l - 1] - 1, x);
-          v = (uint8_t)min(255u, (hv + 128u) >> 8);
-        } else {
-          const int yo = a.t.yo[l * a.t.ys + y];
-          const uint32_t c1 = a.t.yc[l * a.t.ys + y];
-          const uint32_t r = hval(base, g, a.t, l, yo, x) * (256u - c1) + hval(base, g, a.t, l, yo + 1, x) * c1;
-          v = (uint8_t)min(255u, (r + 32768u) >> 16);
-        }
-        if (mode && v <= 254) v = 0;  // threshold(254, THRESH_TOZERO)
+        const int yo = a.t.yo[l * a.t.ys + y];
+        const uint32_t c1 = a.t.yc[l * a.t.ys + y];
+        const uint32_t rr = hval(base, g, a.t, l, yo, x) * (256u - c1) + hval(base, g, a.t, l, yo + 1, x) * c1;
+        v = (uint8_t)min(255u, (rr + 32768u) >> 16);
       }
-      px(base, g, l, y, x) = v;
+      if (mode && v <= 254) v = 0;  // threshold(254, THRESH_TOZERO)
     }
-    __syncthreads();
-    const int pw = w + 2 * kB, ph = h + 2 * kB;
-    for (int i = threadIdx.x; i < pw * ph; i += blockDim.x) {
-      const int r = i / pw - kB, c = i % pw - kB;
-      if (r >= 0 && r < h && c >= 0 && c < w) continue;
-      px(base, g, l, r, c) = mode ? 0 : pxc(base, g, l, reflect101(r, h), reflect101(c, w));
-    }
-    __syncthreads();
   }
+  base[g.off[l] + i] = v;
 }
 
 // GaussianBlur(level ROI, 7x7, 2, 2, BORDER_REFLECT_101): row sums then symmetric column sum
 __global__ __launch_bounds__(256) void k_orb_blur(Args a) {
   const Geom& g = a.g;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = blockIdx.y;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
   if (i >= g.pad[kL]) return;
   int l = 0;
   while (i >= g.pad[l + 1]) l++;
@@ -236,7 +244,7 @@ __device__ int corner_score(const int* d, int threshold) {
 __global__ __launch_bounds__(256) void k_orb_fast(Args a) {
   const Geom& g = a.g;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = blockIdx.y;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
   if (i >= g.pix[kL]) return;
   int l = 0;
   while (i >= g.pix[l + 1]) l++;
@@ -332,26 +340,6 @@ __device__ __forceinline__ uint32_t ord_key(float f) {  // larger float -> large
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__device__ float harris_at(const uint8_t* base, const Geom& g, int l, int x0, int y0) {
-  const float scale = 1.f / ((1 << 2) * 7 * 255.f);
-  const float sq = scale * scale * scale * scale;
-  int A = 0, B = 0, C = 0;
-  for (int i = 0; i < 7; i++)
-    for (int j = 0; j < 7; j++) {
-      const int y = y0 - 3 + i, x = x0 - 3 + j;
-      const int Ix = (pxc(base, g, l, y, x + 1) - pxc(base, g, l, y, x - 1)) * 2 +
-                     (pxc(base, g, l, y - 1, x + 1) - pxc(base, g, l, y - 1, x - 1)) +
-                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y + 1, x - 1));
-      const int Iy = (pxc(base, g, l, y + 1, x) - pxc(base, g, l, y - 1, x)) * 2 +
-                     (pxc(base, g, l, y + 1, x - 1) - pxc(base, g, l, y - 1, x - 1)) +
-                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y - 1, x + 1));
-      A += Ix * Ix;
-      B += Iy * Iy;
-      C += Ix * Iy;
-    }
-  return ((float)A * B - (float)C * C - 0.04f * ((float)A + B) * ((float)A + B)) * sq;
-}
-
 // cv::fastAtan2 (degrees)
 __device__ float fast_atan2(float y, float x) {
   const float k = (float)(180 / kPi);
@@ -371,22 +359,6 @@ __device__ float fast_atan2(float y, float x) {
   if (x < 0) a = 180.f - a;
   if (y < 0) a = 360.f - a;
   return a;
-}
-
-__device__ float ic_angle(const uint8_t* base, const Geom& g, int l, int cx, int cy) {
-  int m01 = 0, m10 = 0;
-  for (int u = -kHalf; u <= kHalf; ++u) m10 += u * pxc(base, g, l, cy, cx + u);
-  for (int v = 1; v <= kHalf; ++v) {
-    int vsum = 0;
-    const int d = g.umax[v];
-    for (int u = -d; u <= d; ++u) {
-      const int vp = pxc(base, g, l, cy + v, cx + u), vm = pxc(base, g, l, cy - v, cx + u);
-      vsum += vp - vm;
-      m10 += u * (vp + vm);
-    }
-    m01 += v * vsum;
-  }
-  return fast_atan2((float)m01, (float)m10);
 }
 
 // n-th largest key among cnt keys (radix select, 4 x 8 bits); all threads get it
@@ -416,44 +388,90 @@ __device__ uint32_t nth_largest(SelShared& sh, const float* resp, int cnt, int n
   return sh.prefix;
 }
 
+// FAST keypoints of every level pixel: score if it beats its 8 neighbours (non-max suppression
+// of FAST_t), passes the pixel mask (runByPixelsMask) and the image border (edgeThreshold 1)
+__global__ __launch_bounds__(256) void k_orb_nms(Args a) {
+  const Geom& g = a.g;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
+  if (i >= g.pix[kL]) return;
+  int l = 0;
+  while (i >= g.pix[l + 1]) l++;
+  const int j = i - g.pix[l], w = g.w[l], h = g.h[l];
+  const int r = j / w, c = j % w;
+  const uint8_t* sc = a.score + (size_t)s * g.pix[kL];
+  const int v = sc[i];
+  bool keep = false;
+  if (v && r >= 3 && r < h - 3) {
+    keep = v > score_at(sc, g, l, r, c + 1) && v > score_at(sc, g, l, r, c - 1) &&
+           v > score_at(sc, g, l, r - 1, c - 1) && v > score_at(sc, g, l, r - 1, c) &&
+           v > score_at(sc, g, l, r - 1, c + 1) && v > score_at(sc, g, l, r + 1, c - 1) &&
+           v > score_at(sc, g, l, r + 1, c) && v > score_at(sc, g, l, r + 1, c + 1);
+    if (keep && a.mpyr && pxc(a.mpyr, g, l, r, c) == 0) keep = false;
+    if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
+  }
+  a.nms[(size_t)s * g.pix[kL] + i] = keep ? (uint8_t)v : 0;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide exclusive prefix of an int per thread; *tot = the sum
+__device__ __forceinline__ int block_excl(SelShared& sh, int v, int* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) sh.wsum[w] = incl;
+  __syncthreads();
+  int before = 0, all = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+    const int x = sh.wsum[k];
+    if (k < w) before += x;
+    all += x;
+  }
+  __syncthreads();
+  *tot = all;
+  return before + incl - v;
+}
+
 __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   __shared__ SelShared sh;
   const Geom& g = a.g;
-  const int s = blockIdx.x / kL, l = blockIdx.x % kL;
+  // level-major blocks: consecutive blocks (dealt round-robin to the 8 XCDs) are different scans
+  // of one level, so the heavy level-0 workgroups spread over every XCD
+  const int S = gridDim.x / kL;
+  const int l = blockIdx.x / S, s = a.smap ? a.smap[blockIdx.x % S] : blockIdx.x % S;
   const int w = g.w[l], h = g.h[l];
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
-  const uint8_t* sc = a.score + (size_t)s * g.pix[kL];
+  const uint8_t* sc = a.score + (size_t)s * g.pix[kL] + g.pix[l];
+  const uint8_t* kf = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
   int* cand = a.cand + (size_t)s * g.pix[kL] + g.pix[l];
   float* resp = a.cresp + (size_t)s * g.pix[kL] + g.pix[l];
-  // 1. FAST keypoints in row-major order: non-max suppression over the 8 neighbours, pixel mask,
-  //    image border (edgeThreshold 1)
-  int n = 0;
-  for (int b0 = 0; b0 < w * h; b0 += blockDim.x) {
-    const int i = b0 + threadIdx.x;
-    bool keep = false;
-    if (i < w * h) {
-      const int r = i / w, c = i % w;
-      const int v = sc[g.pix[l] + i];
-      if (v && r >= 3 && r < h - 3) {
-        keep = v > score_at(sc, g, l, r, c + 1) && v > score_at(sc, g, l, r, c - 1) &&
-               v > score_at(sc, g, l, r - 1, c - 1) && v > score_at(sc, g, l, r - 1, c) &&
-               v > score_at(sc, g, l, r - 1, c + 1) && v > score_at(sc, g, l, r + 1, c - 1) &&
-               v > score_at(sc, g, l, r + 1, c) && v > score_at(sc, g, l, r + 1, c + 1);
-        if (keep && a.mpyr && pxc(a.mpyr, g, l, r, c) == 0) keep = false;
-        if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
-      }
-    }
-    int tot;
-    const int rank = block_rank(sh, keep, &tot);
-    if (keep) cand[n + rank] = i;
-    n += tot;
-  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // 1. FAST keypoints in row-major order: each thread compacts one contiguous pixel segment
+  const int npx = w * h, seg = (npx + blockDim.x - 1) / blockDim.x;
+  const int p0 = min(npx, (int)threadIdx.x * seg), p1 = min(npx, p0 + seg);
+  int mine = 0;
+#pragma unroll 8
+  for (int p = p0; p < p1; p++) mine += kf[p] != 0;
+  int n;
+  int at = block_excl(sh, mine, &n);
+  for (int p = p0; p < p1; p++)
+    if (kf[p]) cand[at++] = p;
+  __syncthreads();
   // 2. retainBest(2 n_l) on the FAST score: keep every score >= the (2 n_l)-th largest
   const int n2 = 2 * g.nper[l];
   if (n > n2) {
     for (int b = threadIdx.x; b < 256; b += blockDim.x) sh.hist[b] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&sh.hist[sc[g.pix[l] + cand[i]]], 1);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&sh.hist[sc[cand[i]]], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
       int cum = 0, t = 0;
@@ -469,8 +487,7 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     for (int b0 = 0; b0 < n; b0 += blockDim.x) {
       const int i = b0 + threadIdx.x;
       const int ci = i < n ? cand[i] : 0;
-      const bool keep = i < n && sc[g.pix[l] + ci] >= thr;
-      __syncthreads();
+      const bool keep = i < n && sc[ci] >= thr;
       int tot;
       const int rank = block_rank(sh, keep, &tot);
       if (keep) cand[m + rank] = ci;
@@ -478,9 +495,31 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     }
     n = m;
   }
-  // 3. Harris responses, retainBest(n_l)
-  for (int i = threadIdx.x; i < n; i += blockDim.x) resp[i] = harris_at(base, g, l, cand[i] % w, cand[i] / w);
   __syncthreads();
+  // 3. Harris responses: one wavefront per candidate, lane = one of the 7x7 block pixels (the
+  //    integer sums are order-free, so the float formula sees OpenCV's exact a, b, c)
+  for (int i = wv; i < n; i += nw) {
+    const int x0 = cand[i] % w, y0 = cand[i] / w;
+    int A = 0, B = 0, C = 0;
+    if (lane < 49) {
+      const int y = y0 - 3 + lane / 7, x = x0 - 3 + lane % 7;
+      const int Ix = (pxc(base, g, l, y, x + 1) - pxc(base, g, l, y, x - 1)) * 2 +
+                     (pxc(base, g, l, y - 1, x + 1) - pxc(base, g, l, y - 1, x - 1)) +
+                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y + 1, x - 1));
+      const int Iy = (pxc(base, g, l, y + 1, x) - pxc(base, g, l, y - 1, x)) * 2 +
+                     (pxc(base, g, l, y + 1, x - 1) - pxc(base, g, l, y - 1, x - 1)) +
+                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y - 1, x + 1));
+      A = Ix * Ix; B = Iy * Iy; C = Ix * Iy;
+    }
+    A = wave_sum(A); B = wave_sum(B); C = wave_sum(C);
+    if (lane == 0) {
+      const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+      const float sq = scale * scale * scale * scale;
+      resp[i] = ((float)A * B - (float)C * C - 0.04f * ((float)A + B) * ((float)A + B)) * sq;
+    }
+  }
+  __syncthreads();
+  // 4. retainBest(n_l) on the Harris response
   const int n1 = g.nper[l];
   if (n > n1) {
     const uint32_t thr = n1 > 0 ? nth_largest(sh, resp, n, n1) : 0xffffffffu;
@@ -499,19 +538,39 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     n = m;
   }
   __syncthreads();
-  // 4. angles; per-level staging (level coordinates scaled to level 0 in k_orb_finish)
   if (n > g.lcap[l]) {
     if (threadIdx.x == 0) atomicOr(a.overflow, 1);
     n = g.lcap[l];
   }
+  // 5. intensity-centroid angle: one wavefront per keypoint over the circular patch (integer
+  //    moments, order-free), fastAtan2 on lane 0; per-level staging
   float* out = a.lkp + ((size_t)s * g.cap + g.lofs[l]) * 6;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  for (int i = wv; i < n; i += nw) {
     const int x = cand[i] % w, y = cand[i] / w;
-    float* o = out + (size_t)i * 6;
-    o[0] = (float)x; o[1] = (float)y; o[2] = 31 * g.scale[l];
-    o[3] = ic_angle(base, g, l, x, y);
-    o[4] = resp[i];
-    o[5] = (float)l;
+    int m01 = 0, m10 = 0;
+    int v[kPatchIters];
+#pragma unroll
+    for (int u = 0; u < kPatchIters; u++) {  // all loads in flight, then the integer moments
+      const int t = u * 64 + lane;
+      const short2 d = c_patch[t < kNPatch ? t : 0];
+      v[u] = t < kNPatch ? pxc(base, g, l, y + d.y, x + d.x) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPatchIters; u++) {
+      const int t = u * 64 + lane;
+      const short2 d = c_patch[t < kNPatch ? t : 0];
+      m10 += d.x * v[u];
+      m01 += d.y * v[u];
+    }
+    m01 = wave_sum(m01);
+    m10 = wave_sum(m10);
+    if (lane == 0) {
+      float* o = out + (size_t)i * 6;
+      o[0] = (float)x; o[1] = (float)y; o[2] = 31 * g.scale[l];
+      o[3] = fast_atan2((float)m01, (float)m10);
+      o[4] = resp[i];
+      o[5] = (float)l;
+    }
   }
   if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
 }
@@ -520,7 +579,7 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
 __global__ __launch_bounds__(256) void k_orb_finish(Args a) {
   __shared__ SelShared sh;
   const Geom& g = a.g;
-  const int s = blockIdx.x;
+  const int s = a.smap ? a.smap[blockIdx.x] : blockIdx.x;
   int n = 0;
   for (int l = 0; l < kL; l++) {
     const int cnt = a.lcnt[s * kL + l];
@@ -554,7 +613,7 @@ __global__ __launch_bounds__(256) void k_orb_finish(Args a) {
 // steered rBRIEF: 32 threads per keypoint, one descriptor byte each
 __global__ __launch_bounds__(256) void k_orb_desc(Args a) {
   const Geom& g = a.g;
-  const int s = blockIdx.y;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
   const int k = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int byte = threadIdx.x & 31;
   if (k >= a.nkp[s]) return;
@@ -584,6 +643,7 @@ __global__ __launch_bounds__(256) void k_orb_desc(Args a) {
 // ------------------------------------------------------------------ matching (a10) + records
 struct PairArgs {
   int npairs;
+  const int* pslot;   // [npairs] buffer slot of pair pr (null: pr)
   const int* qscan;   // [npairs] cur scan (query)
   const int* tscan;   // [npairs] prev scan (train)
   const uint8_t* qdesc; const uint8_t* tdesc;  // descriptor arrays ([scan][cap][32])
@@ -607,37 +667,71 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
   return d;
 }
 
+// batchDistance cross-check, distance part: train i -> its nearest query (first minimum); each
+// query keeps the nearest train among those that chose it (first minimum) = atomicMin of the
+// packed (distance << 16 | train) (best[] preset to 0x7f7f7f7f).  Grid (pairs, train blocks of
+// 2 x 256): each thread owns two trains; queries are staged in LDS tiles and every lane of a
+// wavefront reads the same query (broadcast).
+constexpr int kXdThreads = 256;
+constexpr int kXdTrains = 2 * kXdThreads;
+
+__global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
+  __shared__ uint4 qt[kQTile * 2];
+  const int pi = blockIdx.x;
+  const int pr = p.pslot ? p.pslot[pi] : pi;
+  const int qs = p.qscan[pi], ts = p.tscan[pi];
+  const int nq = p.qn[qs], nt = p.tn[ts];
+  const int i0 = blockIdx.y * kXdTrains;
+  if (i0 >= nt) return;
+  const uint32_t* Q = reinterpret_cast<const uint32_t*>(p.qdesc + (size_t)qs * p.qcap * 32);
+  const uint32_t* T = reinterpret_cast<const uint32_t*>(p.tdesc + (size_t)ts * p.tcap * 32);
+  int* best = p.mscratch + (size_t)pr * p.bstride;
+  const int ia = i0 + threadIdx.x, ib = ia + kXdThreads;
+  uint32_t ta[8], tb[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    ta[e] = ia < nt ? T[(size_t)ia * 8 + e] : 0u;
+    tb[e] = ib < nt ? T[(size_t)ib * 8 + e] : 0u;
+  }
+  int bda = 0x7fffffff, bja = -1, bdb = 0x7fffffff, bjb = -1;
+  for (int q0 = 0; q0 < nq; q0 += kQTile) {
+    const int tn = min(kQTile, nq - q0);
+    __syncthreads();
+    const uint4* Qv = reinterpret_cast<const uint4*>(Q + (size_t)q0 * 8);
+    for (int e = threadIdx.x; e < tn * 2; e += blockDim.x) qt[e] = Qv[e];
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < tn; j++) {
+      const uint4 a0 = qt[2 * j], a1 = qt[2 * j + 1];
+      const int da = __popc(ta[0] ^ a0.x) + __popc(ta[1] ^ a0.y) + __popc(ta[2] ^ a0.z) + __popc(ta[3] ^ a0.w) +
+                     __popc(ta[4] ^ a1.x) + __popc(ta[5] ^ a1.y) + __popc(ta[6] ^ a1.z) + __popc(ta[7] ^ a1.w);
+      const int db = __popc(tb[0] ^ a0.x) + __popc(tb[1] ^ a0.y) + __popc(tb[2] ^ a0.z) + __popc(tb[3] ^ a0.w) +
+                     __popc(tb[4] ^ a1.x) + __popc(tb[5] ^ a1.y) + __popc(tb[6] ^ a1.z) + __popc(tb[7] ^ a1.w);
+      if (da < bda) { bda = da; bja = q0 + j; }
+      if (db < bdb) { bdb = db; bjb = q0 + j; }
+    }
+  }
+  if (ia < nt && bja >= 0) atomicMin(&best[bja], (bda << 16) | ia);
+  if (ib < nt && bjb >= 0) atomicMin(&best[bjb], (bdb << 16) | ib);
+}
+
+// Selection part: std::sort by distance (stable, query order), the first ceil(frac M), the
+// good-frame test and the front_end_residual records.
 __global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
   __shared__ SelShared sh;
   __shared__ int hist[257];
   __shared__ int sM, sG;
-  const int pr = blockIdx.x;
-  const int qs = p.qscan[pr], ts = p.tscan[pr];
+  const int pi = blockIdx.x;
+  const int pr = p.pslot ? p.pslot[pi] : pi;
+  const int qs = p.qscan[pi], ts = p.tscan[pi];
   const int nq = p.qn[qs], nt = p.tn[ts];
-  const uint32_t* Q = reinterpret_cast<const uint32_t*>(p.qdesc + (size_t)qs * p.qcap * 32);
-  const uint32_t* T = reinterpret_cast<const uint32_t*>(p.tdesc + (size_t)ts * p.tcap * 32);
   int* best = p.mscratch + (size_t)pr * p.bstride;
-  for (int j = threadIdx.x; j < nq; j += blockDim.x) best[j] = 0x7fffffff;
-  __syncthreads();
-  // batchDistance cross-check: train i -> nearest query (first minimum); query keeps the nearest
-  // train among those that chose it (first minimum) = atomicMin of (distance, train)
-  for (int i = threadIdx.x; i < nt; i += blockDim.x) {
-    uint32_t td[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) td[e] = T[(size_t)i * 8 + e];
-    int bd = 0x7fffffff, bj = -1;
-    for (int j = 0; j < nq; j++) {
-      const int d = hamming32(td, Q + (size_t)j * 8);
-      if (d < bd) { bd = d; bj = j; }
-    }
-    if (bj >= 0) atomicMin(&best[bj], (bd << 16) | i);
-  }
   __syncthreads();
   // std::sort by distance (stable, query order) + the first ceil(frac M)
   for (int b = threadIdx.x; b < 257; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   for (int j = threadIdx.x; j < nq; j += blockDim.x)
-    if (best[j] != 0x7fffffff) atomicAdd(&hist[best[j] >> 16], 1);
+    if (best[j] != kNoMatch) atomicAdd(&hist[best[j] >> 16], 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     int M = 0;
@@ -659,21 +753,21 @@ __global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
   int n = 0, neq = 0, nm = 0;
   for (int b0 = 0; b0 < nq; b0 += blockDim.x) {
     const int j = b0 + threadIdx.x;
-    const int v = j < nq ? best[j] : 0x7fffffff;
+    const int v = j < nq ? best[j] : kNoMatch;
     const int d = v >> 16;
     if (p.mout) {
       int tm;
-      const int rm = block_rank(sh, v != 0x7fffffff, &tm);
-      if (v != 0x7fffffff) {
+      const int rm = block_rank(sh, v != kNoMatch, &tm);
+      if (v != kNoMatch) {
         int* o = p.mout + ((size_t)pr * p.bstride + nm + rm) * 3;
         o[0] = j; o[1] = v & 0xffff; o[2] = d;
       }
       nm += tm;
     }
-    const bool eq = v != 0x7fffffff && d == dstar;
+    const bool eq = v != kNoMatch && d == dstar;
     int te;
     const int req = block_rank(sh, eq, &te);
-    const bool keep = v != 0x7fffffff && (d < dstar || (eq && neq + req < take));
+    const bool keep = v != kNoMatch && (d < dstar || (eq && neq + req < take));
     neq += te;
     int tot;
     const int rank = block_rank(sh, keep, &tot);
@@ -731,7 +825,7 @@ __device__ void pair_eval(LmSh& sh, const double* rec, int n) {
 
 __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
   __shared__ LmSh sh;
-  const int pr = blockIdx.x;
+  const int pr = p.pslot ? p.pslot[blockIdx.x] : blockIdx.x;
   int* st = p.stats + pr * 8;
   double* T = p.T + pr * 7;
   const bool good = st[0] == 1;
@@ -839,8 +933,8 @@ struct OrbEngine {
   uint16_t *xc = nullptr, *yc = nullptr;
   int xs = 0, ys = 0;
   uint8_t* mpyr = nullptr;
-  uint8_t *pyr = nullptr, *blur = nullptr, *score = nullptr, *desc = nullptr;
-  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr;
+  uint8_t *pyr = nullptr, *blur = nullptr, *score = nullptr, *nms = nullptr, *desc = nullptr;
+  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr;
   float *cresp = nullptr, *lkp = nullptr, *kp = nullptr;
   float4* p3d = nullptr;
   ~OrbEngine() {
@@ -861,8 +955,9 @@ struct OrbEngine {
     a.t.xo = xo; a.t.xc = xc; a.t.yo = yo; a.t.yc = yc; a.t.lim = lim; a.t.xs = xs; a.t.ys = ys;
     a.S = max_scans;
     a.img = img; a.track = track;
-    a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.score = score; a.cand = cand; a.cresp = cresp;
+    a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.score = score; a.nms = nms; a.cand = cand; a.cresp = cresp;
     a.lkp = lkp; a.lcnt = lcnt; a.kp = kp; a.p3d = p3d; a.desc = desc; a.nkp = nkp; a.overflow = overflow;
+    a.smap = nullptr;
     return a;
   }
 };
@@ -915,6 +1010,13 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
       umax[v] = v0;
       ++v0;
     }
+    std::vector<short2> patch;  // the circular patch of ICAngles: rows -15..15, |u| <= umax[|v|]
+    for (int v = -kHalf; v <= kHalf; v++)
+      for (int u = -umax[std::abs(v)]; u <= umax[std::abs(v)]; u++) patch.push_back(make_short2((short)u, (short)v));
+    g.npatch = (int)patch.size();
+    if (g.npatch != kNPatch) return ofail(c, LISLAM_ERR_STATE, "ICAngles patch has %d pixels", g.npatch);
+    OCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(c_patch), patch.data(), patch.size() * sizeof(short2), 0,
+                                   hipMemcpyHostToDevice, c->stream));
   }
   // resize tables (INTER_LINEAR_EXACT of level l from level l-1)
   e->xs = g.w[0];
@@ -963,6 +1065,7 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   ORC(e->alloc(&e->pyr, S * g.bytes));
   ORC(e->alloc(&e->blur, S * g.bytes));
   ORC(e->alloc(&e->score, S * g.pix[kL]));
+  ORC(e->alloc(&e->nms, S * g.pix[kL]));
   ORC(e->alloc(&e->cand, S * g.pix[kL]));
   ORC(e->alloc(&e->cresp, S * g.pix[kL]));
   ORC(e->alloc(&e->lkp, S * g.cap * 6));
@@ -972,6 +1075,7 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   ORC(e->alloc(&e->desc, S * g.cap * 32));
   ORC(e->alloc(&e->nkp, S));
   ORC(e->alloc(&e->overflow, 1));
+  ORC(e->alloc(&e->smap, S));
   OCHK(c, hipMemsetAsync(e->overflow, 0, 4, st));
   if (mask) {  // mask pyramid, once
     uint8_t* dmask = nullptr;
@@ -979,27 +1083,10 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
     ORC(e->alloc(&e->mpyr, g.bytes));
     OCHK(c, hipMemcpyAsync(dmask, mask, (size_t)H * W, hipMemcpyDefault, st));
     Args a = e->args(dmask, nullptr);
-    hipLaunchKernelGGL(k_orb_pyramid, dim3(1), dim3(1024), 0, st, a, 1);
+    for (int l = 0; l < kL; l++)
+      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256), 1), dim3(256), 0, st, a, l, 1);
     OCHK(c, hipGetLastError());
   }
-  return LISLAM_OK;
-}
-
-// a8 + a9 for scans [0, n) of device images / tracks
-int engine_detect(OrbEngine* e, const uint8_t* d_img, const float4* d_track, int n) {
-  lislam_ctx* c = e->ctx;
-  hipStream_t st = c->stream;
-  if (n <= 0) return LISLAM_OK;
-  Args a = e->args(d_img, d_track);
-  a.S = n;
-  const Geom& g = e->g;
-  hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(1024), 0, st, a, 0);
-  hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a);
-  hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_orb_blur, dim3(cdiv(g.pad[kL], 256), n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a);
-  OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
 
@@ -1016,6 +1103,7 @@ Args args_slot(const OrbEngine* e, const uint8_t* img, const float4* track, int 
   a.pyr = e->pyr + s * g.bytes;
   a.blur = e->blur + s * g.bytes;
   a.score = e->score + s * g.pix[kL];
+  a.nms = e->nms + s * g.pix[kL];
   a.cand = e->cand + s * g.pix[kL];
   a.cresp = e->cresp + s * g.pix[kL];
   a.lkp = e->lkp + s * g.cap * 6;
@@ -1027,16 +1115,30 @@ Args args_slot(const OrbEngine* e, const uint8_t* img, const float4* track, int 
   return a;
 }
 
-// a8 + a9 for scans [slot0, slot0 + n) of the engine (device images / tracks indexed by scan)
-int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_track, int slot0, int n) {
+// a8 + a9 for scans [slot0, slot0 + n) of the engine (device images / tracks indexed by scan),
+// or for the scans of `list` (host, n entries) when given
+int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_track, int slot0, int n,
+                        const int* list = nullptr) {
   lislam_ctx* c = e->ctx;
   hipStream_t st = c->stream;
   if (n <= 0) return LISLAM_OK;
-  Args a = args_slot(e, d_img, d_track, slot0);
+  Args a = list ? e->args(d_img, d_track) : args_slot(e, d_img, d_track, slot0);
   a.S = n;
+  if (list) {
+    OCHK(c, hipMemcpyAsync(e->smap, list, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    a.smap = e->smap;
+  }
   const Geom& g = e->g;
-  { TimedScope t(c, kT_orb_pyramid); hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(1024), 0, st, a, 0); }
-  { TimedScope t(c, kT_orb_fast); hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a); }
+  {
+    TimedScope t(c, kT_orb_pyramid);
+    for (int l = 0; l < kL; l++)
+      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256), n), dim3(256), 0, st, a, l, 0);
+  }
+  {
+    TimedScope t(c, kT_orb_fast);
+    hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_orb_nms, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
+  }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
   { TimedScope t(c, kT_orb_blur); hipLaunchKernelGGL(k_orb_blur, dim3(cdiv(g.pad[kL], 256), n), dim3(256), 0, st, a); }
@@ -1050,7 +1152,8 @@ struct PairBufs {
   lislam_ctx* ctx = nullptr;
   int maxp = 0, qcap = 0;
   std::vector<void*> allocs;
-  int *qscan = nullptr, *tscan = nullptr, *mscratch = nullptr, *mout = nullptr, *kind = nullptr, *stats = nullptr;
+  int *qscan = nullptr, *tscan = nullptr, *pslot = nullptr, *mscratch = nullptr, *mout = nullptr, *kind = nullptr,
+      *stats = nullptr;
   double *rec = nullptr, *T = nullptr;
   ~PairBufs() {
     for (void* p : allocs) (void)hipFree(p);
@@ -1068,6 +1171,7 @@ struct PairBufs {
     ctx = c; maxp = maxp_; qcap = qcap_;
     ORC(alloc(&qscan, maxp));
     ORC(alloc(&tscan, maxp));
+    ORC(alloc(&pslot, maxp));
     ORC(alloc(&mscratch, (size_t)maxp * qcap));
     if (raw) ORC(alloc(&mout, (size_t)maxp * qcap * 3));
     ORC(alloc(&kind, (size_t)maxp * qcap));
@@ -1079,30 +1183,44 @@ struct PairBufs {
 };
 
 // Match pairs (query scan qs[i] of engine qe, train scan ts[i] of te), select frac, test, and
-// (lm) solve; results in pb slots [p0, p0 + n).
+// (lm) solve; pair i writes buffer slot slots[i] (null: p0 + i).
 int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int* qs, const int* ts, int n, double frac,
-              PairBufs& pb, int p0, bool lm) {
+              PairBufs& pb, int p0, bool lm, const int* slots = nullptr) {
   hipStream_t st = c->stream;
   if (n <= 0) return LISLAM_OK;
-  if (qe->g.cap > pb.qcap || p0 + n > pb.maxp) return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
-  OCHK(c, hipMemcpyAsync(pb.qscan + p0, qs, n * 4, hipMemcpyHostToDevice, st));
-  OCHK(c, hipMemcpyAsync(pb.tscan + p0, ts, n * 4, hipMemcpyHostToDevice, st));
+  if (qe->g.cap > pb.qcap || (!slots && p0 + n > pb.maxp) || n > pb.maxp)
+    return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
+  const int a0 = slots ? 0 : p0;  // argument arrays: where the scan / slot lists are staged
+  OCHK(c, hipMemcpyAsync(pb.qscan + a0, qs, n * 4, hipMemcpyHostToDevice, st));
+  OCHK(c, hipMemcpyAsync(pb.tscan + a0, ts, n * 4, hipMemcpyHostToDevice, st));
+  if (slots) OCHK(c, hipMemcpyAsync(pb.pslot, slots, n * 4, hipMemcpyHostToDevice, st));
   PairArgs p;
   p.npairs = n;
-  p.qscan = pb.qscan + p0; p.tscan = pb.tscan + p0;
+  p.pslot = slots ? pb.pslot : nullptr;
+  p.qscan = pb.qscan + a0; p.tscan = pb.tscan + a0;
   p.qdesc = qe->desc; p.tdesc = te->desc;
   p.qp3d = qe->p3d; p.tp3d = te->p3d;
   p.qn = qe->nkp; p.tn = te->nkp;
   p.qcap = qe->g.cap; p.tcap = te->g.cap;
   p.bstride = pb.qcap;
   p.frac = frac;
-  p.mscratch = pb.mscratch + (size_t)p0 * pb.qcap;
-  p.mout = pb.mout ? pb.mout + (size_t)p0 * pb.qcap * 3 : nullptr;
-  p.rec = pb.rec + (size_t)p0 * pb.qcap * 9;
-  p.kind = pb.kind + (size_t)p0 * pb.qcap;
-  p.stats = pb.stats + p0 * 8;
-  p.T = pb.T + p0 * 7;
-  { TimedScope t(c, kT_orb_match); hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p); }
+  const int b0 = slots ? 0 : p0;  // buffer base (slots index from buffer 0)
+  p.mscratch = pb.mscratch + (size_t)b0 * pb.qcap;
+  p.mout = pb.mout ? pb.mout + (size_t)b0 * pb.qcap * 3 : nullptr;
+  p.rec = pb.rec + (size_t)b0 * pb.qcap * 9;
+  p.kind = pb.kind + (size_t)b0 * pb.qcap;
+  p.stats = pb.stats + b0 * 8;
+  p.T = pb.T + b0 * 7;
+  {
+    TimedScope t(c, kT_orb_match);
+    if (slots) {
+      for (int i = 0; i < n; i++) OCHK(c, hipMemsetAsync(p.mscratch + (size_t)slots[i] * pb.qcap, 0x7f, (size_t)pb.qcap * 4, st));
+    } else {
+      OCHK(c, hipMemsetAsync(p.mscratch, 0x7f, (size_t)n * pb.qcap * 4, st));
+    }
+    hipLaunchKernelGGL(k_orb_xdist, dim3(n, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
+    hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p);
+  }
   if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(n), dim3(kLmThreads), 0, st, p, 20); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
@@ -1199,44 +1317,64 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
       OCHK(c, hipMemcpyAsync(ob->outT + 7, ob->pb.T, (size_t)np * 56, hipMemcpyDeviceToDevice, st));
     }
   }
-  // the rare sequential cases: a frame whose previous frame was re-detected, or a failed test
-  // (feature_tracker::detectfeatures re-detects both frames with 2 * nfeatures)
-  bool prev2 = false;
+  // The sequential rule of detectfeatures: pair k re-detects both frames (2 * nfeatures, 20 %)
+  // when its first attempt fails, and frame k then keeps the 2n set, against which pair k+1's
+  // first attempt is made.  Resolved as a fixed point in batched rounds: cur2[k] follows from the
+  // first attempt of pair k made against the right previous set (pset[k] == cur2[k-1]); pairs whose
+  // attempt used the wrong set are redone together; finally every re-detecting pair is matched
+  // 2n-against-2n in one batch.
+  std::vector<int> pset(n_scans, 0), cur2(n_scans, 0), ok1(n_scans, 1);
   std::vector<char> have2(n_scans, 0);
-  for (int k = 1; k < n_scans; k++) {
-    const int* s = &hs[(size_t)(k - 1) * 8];
-    bool ok = s[0] == 1;
-    bool redone = false;
-    const int slot = k - 1;  // the pair's own buffer slot
-    if (prev2) {
-      const int q = k, t = k - 1;
-      ORC(run_pairs(c, ob->e1, ob->e2, &q, &t, 1, 0.3, ob->pb, slot, true));
-      int h8[8];
-      OCHK(c, hipMemcpyAsync(h8, ob->pb.stats + slot * 8, 32, hipMemcpyDeviceToHost, st));
-      OCHK(c, hipStreamSynchronize(st));
-      ok = h8[0] == 1;
-      redone = true;
+  for (int k = 1; k < n_scans; k++) ok1[k] = hs[(size_t)(k - 1) * 8] == 1;
+  auto detect2 = [&](std::vector<int> need) -> int {  // 2n detection of scans not done yet
+    std::vector<int> todo;
+    for (int sc : need)
+      if (!have2[sc]) { have2[sc] = 1; todo.push_back(sc); }
+    std::sort(todo.begin(), todo.end());
+    todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
+    if (!todo.empty()) ORC(engine_detect_slots(ob->e2, img, trk, 0, (int)todo.size(), todo.data()));
+    return LISLAM_OK;
+  };
+  for (int round = 0; round < n_scans; round++) {
+    for (int k = 1; k < n_scans; k++) cur2[k] = (pset[k] == cur2[k - 1]) ? !ok1[k] : cur2[k];
+    std::vector<int> dirty[2];
+    for (int k = 1; k < n_scans; k++)
+      if (pset[k] != cur2[k - 1]) dirty[cur2[k - 1]].push_back(k);
+    if (dirty[0].empty() && dirty[1].empty()) break;
+    std::vector<int> need;
+    for (int k : dirty[1]) need.push_back(k - 1);
+    ORC(detect2(need));
+    for (int g2 = 0; g2 < 2; g2++) {
+      const std::vector<int>& d = dirty[g2];
+      if (d.empty()) continue;
+      std::vector<int> q, t, sl;
+      for (int k : d) { q.push_back(k); t.push_back(k - 1); sl.push_back(k - 1); pset[k] = g2; }
+      ORC(run_pairs(c, ob->e1, g2 ? ob->e2 : ob->e1, q.data(), t.data(), (int)d.size(), 0.3, ob->pb, 0, true, sl.data()));
+      for (int k : d) OCHK(c, hipMemcpyAsync(&hs[(size_t)(k - 1) * 8], ob->pb.stats + (k - 1) * 8, 32, hipMemcpyDeviceToHost, st));
     }
-    bool cur2 = false;
-    if (!ok) {
-      for (int sc : {k - 1, k})
-        if (!have2[sc]) { ORC(engine_detect_slots(ob->e2, img, trk, sc, 1)); have2[sc] = 1; }
-      const int q = k, t = k - 1;
-      ORC(run_pairs(c, ob->e2, ob->e2, &q, &t, 1, 0.2, ob->pb, slot, true));
-      cur2 = true;
-      redone = true;
-    }
-    if (redone) {
-      if (cur2) {  // mark re-detection
-        int one = 1;
-        OCHK(c, hipMemcpyAsync(ob->pb.stats + slot * 8 + 1, &one, 4, hipMemcpyHostToDevice, st));
-      }
-      OCHK(c, hipMemcpyAsync(ob->outS + (size_t)k * 8, ob->pb.stats + slot * 8, 32, hipMemcpyDeviceToDevice, st));
-      OCHK(c, hipMemcpyAsync(ob->outT + (size_t)k * 7, ob->pb.T + slot * 7, 56, hipMemcpyDeviceToDevice, st));
-      OCHK(c, hipStreamSynchronize(st));
-    }
-    prev2 = cur2;
+    OCHK(c, hipStreamSynchronize(st));
+    for (int g2 = 0; g2 < 2; g2++)
+      for (int k : dirty[g2]) ok1[k] = hs[(size_t)(k - 1) * 8] == 1;
   }
+  std::vector<int> redet, changed;
+  for (int k = 1; k < n_scans; k++) {
+    if (cur2[k]) redet.push_back(k);
+    if (cur2[k] || pset[k]) changed.push_back(k);
+  }
+  if (!redet.empty()) {
+    std::vector<int> need, q, t, sl;
+    for (int k : redet) { need.push_back(k - 1); need.push_back(k); q.push_back(k); t.push_back(k - 1); sl.push_back(k - 1); }
+    ORC(detect2(need));
+    ORC(run_pairs(c, ob->e2, ob->e2, q.data(), t.data(), (int)redet.size(), 0.2, ob->pb, 0, true, sl.data()));
+    std::vector<int> one(redet.size(), 1);
+    for (size_t i = 0; i < redet.size(); i++)
+      OCHK(c, hipMemcpyAsync(ob->pb.stats + (redet[i] - 1) * 8 + 1, &one[i], 4, hipMemcpyHostToDevice, st));
+  }
+  for (int k : changed) {
+    OCHK(c, hipMemcpyAsync(ob->outS + (size_t)k * 8, ob->pb.stats + (k - 1) * 8, 32, hipMemcpyDeviceToDevice, st));
+    OCHK(c, hipMemcpyAsync(ob->outT + (size_t)k * 7, ob->pb.T + (k - 1) * 7, 56, hipMemcpyDeviceToDevice, st));
+  }
+  OCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
 }
 

@@ -57,6 +57,7 @@ def lib():
                                         ctypes.c_int]
         L.oracle_orb_level.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, _i32p, _i32p]
         L.oracle_orb_match.argtypes = [_u8p, ctypes.c_int, _u8p, ctypes.c_int, _i32p]
+        L.oracle_orb_fast.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i32p]
         L.oracle_intensity_odometry.argtypes = [ctypes.c_int, _u8p, _f32p, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 _i32p, _f64p]
         _LIB = L
@@ -298,3 +299,13 @@ def intensity_odometry(imgs: np.ndarray, tracks: np.ndarray, nfeatures: int = 10
     mp, _keep = _mask_ptr(mask)
     lib().oracle_intensity_odometry(n, im.reshape(-1), tr, mp, W, H, nfeatures, st.reshape(-1), T.reshape(-1))
     return st, T
+
+
+def orb_fast(img: np.ndarray, level: int = 0) -> np.ndarray:
+    im = np.ascontiguousarray(img, np.uint8)
+    H, W = im.shape
+    out = np.zeros(H * W, np.int32)
+    w = np.zeros(1, np.int32)
+    h = np.zeros(1, np.int32)
+    lib().oracle_orb_fast(im.reshape(-1), W, H, level, out, w, h)
+    return out[: w[0] * h[0]].reshape(h[0], w[0])

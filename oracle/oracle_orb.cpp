@@ -579,6 +579,19 @@ int oracle_orb_level(const uint8_t* img, int W, int H, int level, int blurred, u
   return 0;
 }
 
+// FAST scores (0 = no corner) of level `level`: out[h][w].
+int oracle_orb_fast(const uint8_t* img, int W, int H, int level, int* out, int* w, int* h) {
+  Pyramid P;
+  build_pyramid(img, nullptr, W, H, P);
+  const Level& L = P.img[level];
+  *w = L.w;
+  *h = L.h;
+  for (int r = 0; r < L.h; r++)
+    for (int c = 0; c < L.w; c++)
+      out[r * L.w + c] = (r >= 3 && r < L.h - 3 && c >= 3 && c < L.w - 3) ? fast_pixel(L, r, c, kFastThreshold) : 0;
+  return 0;
+}
+
 // BFMatcher cross-check match of descriptor sets: out[m][3] = query, train, distance.
 int oracle_orb_match(const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt, int* out) {
   Frame Q, T;

@@ -1,0 +1,28 @@
+"""Time the ORB batch path (a8-a11) on a 300-scan synthetic batch, per kernel (GPU box)."""
+import sys, time
+import os; _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, _R); sys.path.insert(0, os.path.join(_R, 'oracle'))
+import numpy as np
+import __graft_entry__ as g
+pkg = g.package()
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+scans = np.load('/tmp/lislam_scans.r0.npy')[:S] if len(sys.argv) > 2 else pkg.synth.make_sequence(S)
+ctx = pkg.Context()
+b = pkg.Batch(ctx, S)
+b.upload(scans)
+b.extract(S)
+mask = pkg.intensity.set_mask()
+b.intensity_odometry(S, 1000, mask)
+ctx.synchronize()
+pkg.mapping.kernel_times(ctx)
+pkg.mapping.set_timing(ctx, True)
+t = time.perf_counter()
+for _ in range(3):
+    b.intensity_odometry(S, 1000, mask)
+ctx.synchronize()
+el = (time.perf_counter() - t) / 3
+kt = pkg.mapping.kernel_times(ctx)
+print(f'S={S} intensity odometry {el*1e3:.2f} ms/batch -> {S/el:.0f} scans/s', flush=True)
+for k, (ms, n) in kt.items():
+    if n: print(f'  {k:16s} {ms/3:9.3f} ms/batch {n/3:6.1f} launches', flush=True)
+st = np.stack([b.download(pkg.native.OUT_ORB_STATS, k) for k in range(S)])
+print('good', (st[:, 0] == 1).sum(), 'redetect', st[:, 1].sum(), 'kp mean', st[:, 2].mean(), 'good matches', st[1:, 4].mean())
