@@ -132,6 +132,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   hipSetDevice(c->device);
   lislam_batch* b = new lislam_batch();
   b->ctx = c;
+  hipEventCreateWithFlags(&b->ev_extracted, hipEventDisableTiming);
   const int S = max_scans, H = c->cfg.n_scans, W = c->cfg.width, N = H * W;
   b->max_scans = S; b->H = H; b->W = W; b->N = N;
   b->cap_sharp = kCapSharpPerLine * H;
@@ -217,6 +218,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   for (auto& v : b->odo_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
+  if (b->ev_extracted) hipEventDestroy(b->ev_extracted);
   delete b;
   return LISLAM_OK;
 }
@@ -267,6 +269,7 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   launch_features(f, c->stream, ev);
   launch_target_index(b->oa, n_scans, c->stream);  // spatial index of the clouds odometry searches
   if (ev) HIPCHK(c, hipEventRecord(ev[4], c->stream));
+  HIPCHK(c, hipEventRecord(b->ev_extracted, c->stream));
   HIPCHK(c, hipGetLastError());
   b->extracted = n_scans;
   return LISLAM_OK;

@@ -218,39 +218,41 @@ extern "C" int lislam_debug_assoc_stats(unsigned long long* out) {
 constexpr int kNone = 0x7fffffff;
 constexpr int kBatch = 8;  // chunks evaluated per round trip: 4 lane groups x 2 slots
 
-__device__ __forceinline__ void lexmin(float& d, int& key, float d2, int k2) {
-  if (d2 < d || (d2 == d && k2 < key)) { d = d2; key = k2; }
-}
-
-template <int kCtrl>
-__device__ __forceinline__ int dpp(int v) {
-  return __builtin_amdgcn_mov_dpp(v, kCtrl, 0xf, 0xf, false);
-}
 __device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rdlanef(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 
-// Wave-wide lexicographic minimum, returned uniform: DPP within each 16-lane row (quad xor 1,
-// xor 2, half-row mirror, row mirror), then the four row results by readlane.
-template <int kStep>
-__device__ __forceinline__ void lexmin_dpp_step(float& d, int& key) {
-  const float d2 = __int_as_float(dpp<kStep>(__float_as_int(d)));
-  const int k2 = dpp<kStep>(key);
-  lexmin(d, key, d2, k2);
+// (distance, key) pairs packed as one 64-bit integer, distance bits high: distances are
+// non-negative floats, whose bit patterns order like their values, so the lexicographic minimum
+// of the pairs is the integer minimum (one 64-bit compare instead of three 32-bit ones).
+typedef unsigned long long dkey;
+__device__ __forceinline__ dkey dk(float d, int key) {
+  return ((dkey)__float_as_uint(d) << 32) | (uint32_t)key;
 }
-__device__ __forceinline__ void wave_lexmin(float& d, int& key) {
-  lexmin_dpp_step<0xB1>(d, key);   // quad_perm [1,0,3,2]
-  lexmin_dpp_step<0x4E>(d, key);   // quad_perm [2,3,0,1]
-  lexmin_dpp_step<0x141>(d, key);  // row_half_mirror
-  lexmin_dpp_step<0x140>(d, key);  // row_mirror
-  float rd = rdlanef(d, 0);
-  int rk = rdlane(key, 0);
-  lexmin(rd, rk, rdlanef(d, 16), rdlane(key, 16));
-  lexmin(rd, rk, rdlanef(d, 32), rdlane(key, 32));
-  lexmin(rd, rk, rdlanef(d, 48), rdlane(key, 48));
-  d = rd;
-  key = rk;
+__device__ __forceinline__ float dk_d(dkey v) { return __uint_as_float((uint32_t)(v >> 32)); }
+__device__ __forceinline__ int dk_key(dkey v) { return (int)(uint32_t)v; }
+__device__ __forceinline__ dkey dmin(dkey a, dkey b) { return b < a ? b : a; }
+#define kIdent dk(3.4e38f, kNone)  // identity of the minima (no candidate)
+
+// Wave-wide unsigned minimum, returned uniform: DPP within each 16-lane row (quad xor 1, xor 2,
+// half-row mirror, row mirror; each folds into one v_min_u32_dpp), then row_bcast:15 /
+// row_bcast:31 carry the row minima up to lane 63.
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, true));  // row_half_mirror
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, true));  // row_mirror
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)rdlane((int)v, 63);
+}
+// Wave-wide minimum of the pairs: the minimum distance, then the smallest key among the lanes
+// holding it (one lane in the common case: read directly).
+__device__ __forceinline__ dkey wave_min(dkey v) {
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  const uint32_t m = wave_umin(hi);
+  const uint64_t tie = __ballot(hi == m);
+  const uint32_t key = __popcll(tie) == 1 ? (uint32_t)rdlane((int)lo, (int)__builtin_ctzll(tie))
+                                          : wave_umin(hi == m ? lo : 0xffffffffu);
+  return ((dkey)m << 32) | key;
 }
 
 // Take the first (up to) kN pending lanes of mask m: their values of v, -1 where none.
@@ -280,27 +282,24 @@ __device__ __forceinline__ int batch_item(const int (&v)[kBatch], int g, int t) 
 }
 
 // Evaluate up to eight 16-point chunks of the Morton-ordered cloud against q.
-__device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)[kBatch], const P4& q, float& bd, int& bi) {
+__device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)[kBatch], const P4& q, dkey& best) {
   const int lane = lane_id(), g = lane >> 4;
   P4 p[2];
-  int j[2];
+  bool ok[2];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
     const int c = batch_item(ch, g, t);
-    j[t] = c >= 0 ? c * kChunk + (lane & 15) : n;
-    if (j[t] < n) p[t] = ld4(sorted + j[t]);
+    const int j = c * kChunk + (lane & 15);
+    ok[t] = c >= 0 && j < n;
+    p[t] = ld4(sorted + (ok[t] ? j : 0));  // unpredicated load (point 0 always exists)
   }
-  float d = 3.4e38f;
-  int key = kNone;
+  dkey v = kIdent;
 #pragma unroll
   for (int t = 0; t < 2; t++) {
-    if (j[t] < n) {
-      const float dd = d2f(q, p[t]);
-      if (dd < 25.f) lexmin(d, key, dd, __float_as_int(p[t].i));
-    }
+    const float dd = d2f(q, p[t]);
+    if (ok[t] && dd < 25.f) v = dmin(v, dk(dd, __float_as_int(p[t].i)));
   }
-  wave_lexmin(d, key);
-  if (key != kNone) lexmin(bd, bi, d, key);
+  best = dmin(best, wave_min(v));
 }
 
 // Exact 1-NN with d < 25 (the reference drops farther neighbours, :455/:577) over the
@@ -312,36 +311,30 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
   const int lane = lane_id();
   if (n <= 0) return -1;
   const int nch = (n + kChunk - 1) / kChunk, nsu = (nch + kChunk - 1) / kChunk;
-  float ulb = 3.4e38f;
-  int uid = kNone;
+  dkey ub = kIdent;
   float lb0 = 3.4e38f;  // this lane's bound in the first window of super-chunks
   for (int u = lane; u < nsu; u += 64) {
     const float lb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
     if (u < 64) lb0 = lb;
-    lexmin(ulb, uid, lb, u);
+    ub = dmin(ub, dk(lb, u));
   }
-  wave_lexmin(ulb, uid);
-  if (!(ulb < 25.f)) return -1;  // every point is at least 25 away
-  const int u0 = uid;
+  ub = wave_min(ub);
+  if (!(dk_d(ub) < 25.f)) return -1;  // every point is at least 25 away
+  const int u0 = dk_key(ub);
   ASTAT(0);
-  float bd = 25.f;
-  int bi = kNone;
+  dkey best = dk(25.f, kNone);
   {  // the nearest super-chunk, all 256 points in one round trip
-    float d = 3.4e38f;
-    int key = kNone;
+    dkey v = kIdent;
     P4 p[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) p[t] = ld4(sorted + min(u0 * kChunk * kChunk + lane + 64 * t, n - 1));
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const int j = u0 * kChunk * kChunk + lane + 64 * t;
-      if (j < n) {
-        const float dd = d2f(q, p[t]);
-        if (dd < 25.f) lexmin(d, key, dd, __float_as_int(p[t].i));
-      }
+      const float dd = d2f(q, p[t]);
+      if (j < n && dd < 25.f) v = dmin(v, dk(dd, __float_as_int(p[t].i)));
     }
-    wave_lexmin(d, key);
-    if (key != kNone) lexmin(bd, bi, d, key);
+    best = dmin(best, wave_min(v));
   }
   for (int ub = 0; ub < nsu; ub += 64) {
     const int u = ub + lane;
@@ -349,6 +342,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
     if (ub > 0 && u < nsu) slb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
     bool spend = u < nsu && u != u0;
     for (;;) {
+      const float bd = dk_d(best);
       const uint64_t um = __ballot(spend && !(slb > bd));
       if (!um) break;
       ASTAT(1);
@@ -370,8 +364,9 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
 #pragma unroll
       for (int t = 0; t < 2; t++) clb[t] = cpend[t] ? box_lb(lo[t], hi[t], q) : 3.4e38f;
       for (;;) {
-        const uint64_t m0 = __ballot(cpend[0] && !(clb[0] > bd));
-        const uint64_t m1 = __ballot(cpend[1] && !(clb[1] > bd));
+        const float bd2 = dk_d(best);
+        const uint64_t m0 = __ballot(cpend[0] && !(clb[0] > bd2));
+        const uint64_t m1 = __ballot(cpend[1] && !(clb[1] > bd2));
         if (!m0 && !m1) break;
         ASTAT(2);
         int c8[kBatch], a0[kBatch], a1[kBatch];
@@ -382,10 +377,11 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
         for (int e = 0; e < kBatch; e++) c8[e] = e < n0 ? a0[e] : (e - n0 < kBatch ? a1[e - n0 < 0 ? 0 : e - n0] : -1);
         if (taken<kBatch>(m0)) cpend[0] = false;
         if (((m1 >> lane) & 1ull) && __popcll(m1 & lanemask_lt()) < kBatch - n0) cpend[1] = false;
-        nn_eval(sorted, n, c8, q, bd, bi);
+        nn_eval(sorted, n, c8, q, best);
       }
     }
   }
+  const int bi = dk_key(best);
   return bi == kNone ? -1 : bi;
 }
 
@@ -397,8 +393,7 @@ struct LineSearch {
   const float4* chm;  // chunk bounds (scan-line order), w = label min / max
   int n, nch, closest, cid;
   P4 sel;
-  float b2, b3;  // running bests (25 = none)
-  int k2, k3;    // walk-rank keys
+  dkey b2, b3;  // running bests (distance, walk-rank key); (25, kNone) = none
 };
 
 // Evaluate up to eight chunks (dir: 1 up / 0 down) against the running bests.  brk[t]: the
@@ -416,11 +411,9 @@ __device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[kBatch], 
     up[t] = batch_item(dir, g, t) != 0;
     j[t] = c * kChunk + l16;
     valid[t] = c >= 0 && j[t] < s.n && (up[t] ? j[t] > s.closest : j[t] < s.closest);
-    p[t] = P4{0.f, 0.f, 0.f, 0.f};
-    if (valid[t]) p[t] = ld4(s.L + j[t]);
+    p[t] = ld4(s.L + (valid[t] ? j[t] : s.closest));  // unpredicated load
   }
-  float d2 = 3.4e38f, d3 = 3.4e38f;
-  int q2 = kNone, q3 = kNone;
+  dkey v2 = kIdent, v3 = kIdent;
 #pragma unroll
   for (int t = 0; t < 2; t++) {
     const int pid = int(p[t].i);
@@ -435,29 +428,25 @@ __device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[kBatch], 
       const int key = up[t] ? j[t] - s.closest : s.n + s.closest - j[t];
       if (d < 25.f) {
         if (kCorner) {
-          if (up[t] ? pid > s.cid : pid < s.cid) lexmin(d2, q2, d, key);
+          if (up[t] ? pid > s.cid : pid < s.cid) v2 = dmin(v2, dk(d, key));
         } else {
-          if (up[t] ? pid <= s.cid : pid >= s.cid) lexmin(d2, q2, d, key);
-          else lexmin(d3, q3, d, key);
+          if (up[t] ? pid <= s.cid : pid >= s.cid) v2 = dmin(v2, dk(d, key));
+          else v3 = dmin(v3, dk(d, key));
         }
       }
     }
   }
-  wave_lexmin(d2, q2);
-  if (q2 != kNone) lexmin(s.b2, s.k2, d2, q2);
-  if (!kCorner) {
-    wave_lexmin(d3, q3);
-    if (q3 != kNone) lexmin(s.b3, s.k3, d3, q3);
-  }
+  s.b2 = dmin(s.b2, wave_min(v2));
+  if (!kCorner) s.b3 = dmin(s.b3, wave_min(v3));
 }
 
 // Does an up / down chunk with bounds (lo, hi) and bound lb still need a visit?
 template <bool kCorner>
 __device__ __forceinline__ bool ls_need(const LineSearch& s, bool up, const float4& lo, const float4& hi, float lb) {
   const int lmin = (int)lo.w, lmax = (int)hi.w;
-  if (kCorner) return (up ? lmax > s.cid : lmin < s.cid) && !(lb > s.b2);
-  const bool n2 = (up ? lmin <= s.cid : lmax >= s.cid) && !(lb > s.b2);
-  const bool n3 = (up ? lmax > s.cid : lmin < s.cid) && !(lb > s.b3);
+  if (kCorner) return (up ? lmax > s.cid : lmin < s.cid) && !(lb > dk_d(s.b2));
+  const bool n2 = (up ? lmin <= s.cid : lmax >= s.cid) && !(lb > dk_d(s.b2));
+  const bool n3 = (up ? lmax > s.cid : lmin < s.cid) && !(lb > dk_d(s.b3));
   return n2 || n3;
 }
 
@@ -505,12 +494,9 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
     if (w == 0) {
       // first batch: around the up and the down chunk with the smallest bound among those that
       // can still improve a best (chunks i-1 .. i+2 of each), which sets tight bests at once
-      float mu = upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? ulb : 3.4e38f;
-      int iu = mu < 3.4e38f ? lane : kNone;
-      float md = dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dlb : 3.4e38f;
-      int id = md < 3.4e38f ? lane : kNone;
-      wave_lexmin(mu, iu);
-      wave_lexmin(md, id);
+      const dkey mu = wave_min(upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? dk(ulb, lane) : kIdent);
+      const dkey md = wave_min(dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dk(dlb, lane) : kIdent);
+      const int iu = dk_key(mu), id = dk_key(md);
       int ch[kBatch], dir[kBatch];
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -615,19 +601,19 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   if (closest >= 0) {
     ASTAT(corner ? 10 : 11);
     const P4 pa = ld4(L + closest);
-    LineSearch s{L, ix.chunk + mo, nL, (nL + kChunk - 1) / kChunk, closest, int(pa.i), sel, 25.f, 25.f, kNone, kNone};
+    LineSearch s{L, ix.chunk + mo, nL, (nL + kChunk - 1) / kChunk, closest, int(pa.i), sel, dk(25.f, kNone), dk(25.f, kNone)};
     if (corner) {  // LidarEdgeFactor(curr, a, b)
       line_search<true>(s);
-      if (s.k2 != kNone) {
-        const P4 pb = ld4(L + rank_to_index(s, s.k2));
+      if (dk_key(s.b2) != kNone) {
+        const P4 pb = ld4(L + rank_to_index(s, dk_key(s.b2)));
         const float e9[9] = {cur.x, cur.y, cur.z, pa.x, pa.y, pa.z, pb.x, pb.y, pb.z};
         for (int e = 0; e < 9; e++) if (lane == e) v = e9[e];
         found = true;
       }
     } else {        // LidarPlaneFactor(curr, j, l, m)
       line_search<false>(s);
-      if (s.k2 != kNone && s.k3 != kNone) {
-        const P4 pl = ld4(L + rank_to_index(s, s.k2)), pm = ld4(L + rank_to_index(s, s.k3));
+      if (dk_key(s.b2) != kNone && dk_key(s.b3) != kNone) {
+        const P4 pl = ld4(L + rank_to_index(s, dk_key(s.b2))), pm = ld4(L + rank_to_index(s, dk_key(s.b3)));
         const D3 j{pa.x, pa.y, pa.z};
         const D3 nrm = plane_normal(j, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
         const double e9[9] = {cur.x, cur.y, cur.z, j.x, j.y, j.z, nrm.x, nrm.y, nrm.z};
@@ -714,7 +700,9 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   const int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
   count_kinds(sh, kind, ns, a.cap_sharp, nf);
   const int nc = sh.nc, np = sh.np;
-  LM s;
+  // The solver state lives in LDS and is in registers only inside thread 0's step, so it does not
+  // stack on the evaluation's registers (which spilled to scratch when it was held across).
+  __shared__ LM lm;
   bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
   if (go) {
     if (threadIdx.x == 0)
@@ -722,10 +710,10 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
     __syncthreads();
     evaluate(sh, blk, kind, ns, a.cap_sharp, nf);
     if (threadIdx.x == 0) {
-      const bool cont = lm_start(s, sh.x, sh.acc, a.max_iterations);
+      const bool cont = lm_start(lm, sh.x, sh.acc, a.max_iterations);
       sh.flag = cont;
       if (cont)
-        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
     go = sh.flag;
@@ -733,10 +721,10 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   while (go) {
     evaluate(sh, blk, kind, ns, a.cap_sharp, nf);  // cost + J^T J + J^T r at the candidate
     if (threadIdx.x == 0) {
-      const bool cont = lm_next(s, sh.acc, a.max_iterations);
+      const bool cont = lm_next(lm, sh.acc, a.max_iterations);
       sh.flag = cont;
       if (cont)
-        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
     go = sh.flag;
@@ -745,10 +733,10 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   int* so = a.stats + (size_t)k * 8;
   so[outer * 2 + 0] = nc;
   so[outer * 2 + 1] = np;
-  so[4 + outer] = (nc + np) > 0 ? s.it : 0;
-  so[6 + outer] = (nc + np) > 0 ? s.term : 1;
+  so[4 + outer] = (nc + np) > 0 ? lm.it : 0;
+  so[6 + outer] = (nc + np) > 0 ? lm.term : 1;
   if ((nc + np) > 0)
-    for (int e = 0; e < 7; e++) st[e] = s.x[e];
+    for (int e = 0; e < 7; e++) st[e] = lm.x[e];
   if (outer == 1) {
     // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr
     DQ qw{st[7], st[8], st[9], st[10]};

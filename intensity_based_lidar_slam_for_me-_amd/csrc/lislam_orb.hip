@@ -838,7 +838,7 @@ __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
     }
     return;
   }
-  LM s;
+  __shared__ LM lm;  // in registers only inside thread 0's step (see k_odom_lm)
   if (threadIdx.x == 0) {
     const double I[7] = {0, 0, 0, 1, 0, 0, 0};
     for (int e = 0; e < 7; e++) sh.x[e] = I[e];
@@ -846,28 +846,28 @@ __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
   __syncthreads();
   pair_eval(sh, rec, n);
   if (threadIdx.x == 0) {
-    const bool cont = lm_start(s, sh.x, sh.acc, max_it);
+    const bool cont = lm_start(lm, sh.x, sh.acc, max_it);
     sh.flag = cont;
     if (cont)
-      for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+      for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
   }
   __syncthreads();
   bool go = sh.flag;
   while (go) {
     pair_eval(sh, rec, n);
     if (threadIdx.x == 0) {
-      const bool cont = lm_next(s, sh.acc, max_it);
+      const bool cont = lm_next(lm, sh.acc, max_it);
       sh.flag = cont;
       if (cont)
-        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
     go = sh.flag;
   }
   if (threadIdx.x == 0) {
-    for (int e = 0; e < 7; e++) T[e] = s.x[e];
-    st[5] = s.it;
-    st[6] = s.term;
+    for (int e = 0; e < 7; e++) T[e] = lm.x[e];
+    st[5] = lm.it;
+    st[6] = lm.term;
   }
 }
 
@@ -1239,7 +1239,12 @@ struct OrbBatch {
   std::vector<void*> allocs;
   double* outT = nullptr;   // [S][7]
   int* outS = nullptr;      // [S][8]
+  hipStream_t side = nullptr;  // the batch front end runs here, concurrently with the odometry chain
+  hipEvent_t done = nullptr;
   ~OrbBatch() {
+    if (side) (void)hipStreamSynchronize(side);
+    if (side) (void)hipStreamDestroy(side);
+    if (done) (void)hipEventDestroy(done);
     delete e1;
     delete e2;
     for (void* p : allocs) (void)hipFree(p);
@@ -1277,6 +1282,8 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     OCHK(c, hipMalloc(&q, (size_t)b->max_scans * 8 * 4));
     ob->allocs.push_back(q);
     ob->outS = static_cast<int*>(q);
+    OCHK(c, hipStreamCreateWithFlags(&ob->side, hipStreamNonBlocking));
+    OCHK(c, hipEventCreateWithFlags(&ob->done, hipEventDisableTiming));
   }
   *out = ob;
   return LISLAM_OK;
@@ -1284,17 +1291,13 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
 
 }  // namespace
 
-extern "C" {
 
-int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask) {
-  if (!b || n_scans < 1 || n_scans > b->max_scans || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
+namespace {
+
+// Body of lislam_batch_intensity_odometry; runs with c->stream switched to the batch's side stream.
+int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
   lislam_ctx* c = b->ctx;
-  if (!b->fa.img_int || !b->fa.track)
-    return ofail(c, LISLAM_ERR_STATE, "lislam_batch_intensity_odometry needs want_images (the a1 images)");
-  hipSetDevice(c->device);
   hipStream_t st = c->stream;
-  OrbBatch* ob = nullptr;
-  ORC(orb_batch_get(b, nfeatures, mask, &ob));
   const uint8_t* img = b->fa.img_int;
   const float4* trk = reinterpret_cast<const float4*>(b->fa.track);
   ORC(engine_detect_slots(ob->e1, img, trk, 0, n_scans));
@@ -1376,6 +1379,33 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
   }
   OCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// The ORB front end of every scan pair.  It runs on its own stream, ordered after the last
+// lislam_batch_extract only, so it overlaps the odometry chain the caller may already have
+// queued on the context stream; on return all of its work is done and the context stream is
+// ordered after it.
+int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask) {
+  if (!b || n_scans < 1 || n_scans > b->max_scans || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  if (!b->fa.img_int || !b->fa.track)
+    return ofail(c, LISLAM_ERR_STATE, "lislam_batch_intensity_odometry needs want_images (the a1 images)");
+  if (b->extracted < n_scans) return ofail(c, LISLAM_ERR_STATE, "extract %d scans before intensity odometry", n_scans);
+  hipSetDevice(c->device);
+  OrbBatch* ob = nullptr;
+  ORC(orb_batch_get(b, nfeatures, mask, &ob));
+  const hipStream_t main_stream = c->stream;
+  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_extracted, 0));
+  c->stream = ob->side;
+  const int rc = batch_intensity_odometry(b, ob, n_scans);
+  c->stream = main_stream;
+  OCHK(c, hipEventRecord(ob->done, ob->side));
+  OCHK(c, hipStreamWaitEvent(main_stream, ob->done, 0));
+  return rc;
 }
 
 }  // extern "C"

@@ -1,5 +1,6 @@
-import sys, time
-sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import numpy as np
 import __graft_entry__ as g
 pkg = g.package()
