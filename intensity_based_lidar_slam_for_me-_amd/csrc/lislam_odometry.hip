@@ -244,6 +244,24 @@ __device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
   return (uint32_t)rdlane((int)v, 63);
 }
+// Two independent minima interleaved step by step (each step's DPP read waits on the previous
+// step's write; the other reduction fills those wait states).
+__device__ __forceinline__ void wave_umin2(uint32_t& a, uint32_t& b) {
+#define LISLAM_UMIN2_STEP(ctrl) \
+  a = min(a, (uint32_t)__builtin_amdgcn_mov_dpp((int)a, ctrl, 0xf, 0xf, true)); \
+  b = min(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, ctrl, 0xf, 0xf, true));
+  LISLAM_UMIN2_STEP(0xB1)
+  LISLAM_UMIN2_STEP(0x4E)
+  LISLAM_UMIN2_STEP(0x141)
+  LISLAM_UMIN2_STEP(0x140)
+#undef LISLAM_UMIN2_STEP
+  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x142, 0xa, 0xf, false));
+  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x142, 0xa, 0xf, false));
+  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x143, 0xc, 0xf, false));
+  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x143, 0xc, 0xf, false));
+  a = (uint32_t)rdlane((int)a, 63);
+  b = (uint32_t)rdlane((int)b, 63);
+}
 // Wave-wide minimum of the pairs: the minimum distance, then the smallest key among the lanes
 // holding it (one lane in the common case: read directly).
 __device__ __forceinline__ dkey wave_min(dkey v) {
@@ -254,41 +272,71 @@ __device__ __forceinline__ dkey wave_min(dkey v) {
                                           : wave_umin(hi == m ? lo : 0xffffffffu);
   return ((dkey)m << 32) | key;
 }
-
-// Take the first (up to) kN pending lanes of mask m: their values of v, -1 where none.
-template <int kN>
-__device__ __forceinline__ void take(uint64_t m, int v, int (&out)[kN]) {
-#pragma unroll
-  for (int g = 0; g < kN; g++) {
-    if (m) {
-      out[g] = rdlane(v, (int)__builtin_ctzll(m));
-      m &= m - 1;
-    } else {
-      out[g] = -1;
-    }
+__device__ __forceinline__ void wave_min2(dkey& va, dkey& vb) {
+  const uint32_t ha = (uint32_t)(va >> 32), la = (uint32_t)va, hb = (uint32_t)(vb >> 32), lb = (uint32_t)vb;
+  uint32_t ma = ha, mb = hb;
+  wave_umin2(ma, mb);
+  const uint64_t ta = __ballot(ha == ma), tb = __ballot(hb == mb);
+  uint32_t ka, kb;
+  if (__popcll(ta) == 1 && __popcll(tb) == 1) {
+    ka = (uint32_t)rdlane((int)la, (int)__builtin_ctzll(ta));
+    kb = (uint32_t)rdlane((int)lb, (int)__builtin_ctzll(tb));
+  } else {
+    ka = ha == ma ? la : 0xffffffffu;
+    kb = hb == mb ? lb : 0xffffffffu;
+    wave_umin2(ka, kb);
   }
+  va = ((dkey)ma << 32) | ka;
+  vb = ((dkey)mb << 32) | kb;
 }
-template <int kN>
-__device__ __forceinline__ bool taken(uint64_t m) {  // is this lane among the first kN of m?
+
+__device__ __forceinline__ int mbcnt(uint64_t m) {  // set bits of m below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One batch: the first kBatch pending lanes of m0, then of m1 (lane order), numbered 0..7;
+// lane group g = lane / 16 takes items g (slot 0) and 4 + g (slot 1).  Item lanes push
+// (value << 1 | list) to lane `item` with ds_permute and every lane pulls its two items with
+// ds_bpermute: four crossbar operations instead of a scalar read-lane loop per item.
+struct Picked {
+  int v[2];       // item values of slots 0 / 1, -1 past the end of the batch
+  int list[2];    // which mask the item came from
+  bool took0, took1;  // this lane's m0 / m1 entry is in the batch
+};
+__device__ __forceinline__ Picked pick(uint64_t m0, int v0, uint64_t m1, int v1) {
   const int lane = lane_id();
-  return ((m >> lane) & 1ull) && __popcll(m & lanemask_lt()) < kN;
+  const int n0 = min(__popcll(m0), kBatch), ntot = min(n0 + __popcll(m1), kBatch);
+  const int r0 = mbcnt(m0), r1 = n0 + mbcnt(m1);
+  Picked p;
+  p.took0 = ((m0 >> lane) & 1ull) && r0 < kBatch;
+  p.took1 = ((m1 >> lane) & 1ull) && r1 < kBatch;
+  // lanes outside the batch all push to lane 63, which is never read
+  const int q0 = __builtin_amdgcn_ds_permute((p.took0 ? r0 : 63) << 2, v0 << 1);
+  const int q1 = __builtin_amdgcn_ds_permute((p.took1 ? r1 : 63) << 2, (v1 << 1) | 1);
+  const int items = lane < n0 ? q0 : q1;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const int e = g + 4 * t;
+    const int it = __builtin_amdgcn_ds_bpermute(e << 2, items);
+    p.v[t] = e < ntot ? (it >> 1) : -1;
+    p.list[t] = it & 1;
+  }
+  return p;
 }
 __device__ __forceinline__ int sel4(int g, int v0, int v1, int v2, int v3) {
   return g == 0 ? v0 : g == 1 ? v1 : g == 2 ? v2 : v3;
 }
-// chunk of lane group g (lane / 16) in slot t of a batch
-__device__ __forceinline__ int batch_item(const int (&v)[kBatch], int g, int t) {
-  return t == 0 ? sel4(g, v[0], v[1], v[2], v[3]) : sel4(g, v[4], v[5], v[6], v[7]);
-}
 
 // Evaluate up to eight 16-point chunks of the Morton-ordered cloud against q.
-__device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)[kBatch], const P4& q, dkey& best) {
-  const int lane = lane_id(), g = lane >> 4;
+// ch[t]: this lane group's chunk in slot t (-1 = none).
+__device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)[2], const P4& q, dkey& best) {
+  const int lane = lane_id();
   P4 p[2];
   bool ok[2];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
-    const int c = batch_item(ch, g, t);
+    const int c = ch[t];
     const int j = c * kChunk + (lane & 15);
     ok[t] = c >= 0 && j < n;
     p[t] = ld4(sorted + (ok[t] ? j : 0));  // unpredicated load (point 0 always exists)
@@ -346,9 +394,8 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
       const uint64_t um = __ballot(spend && !(slb > bd));
       if (!um) break;
       ASTAT(1);
-      int su8[kBatch];
-      take<kBatch>(um, u, su8);
-      if (taken<kBatch>(um)) spend = false;
+      const Picked su = pick(um, u, 0ull, 0);
+      if (su.took0) spend = false;
       // the 16 chunk bounds of each of those super-chunks: lane group g, slots 0 / 1
       int c[2];
       float clb[2];
@@ -356,7 +403,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
       float4 lo[2], hi[2];
 #pragma unroll
       for (int t = 0; t < 2; t++) {
-        const int sg = batch_item(su8, lane >> 4, t);
+        const int sg = su.v[t];
         c[t] = sg >= 0 ? sg * kChunk + (lane & 15) : -1;
         cpend[t] = c[t] >= 0 && c[t] < nch;
         if (cpend[t]) { lo[t] = ldg(chm + 2 * c[t]); hi[t] = ldg(chm + 2 * c[t] + 1); }
@@ -369,15 +416,10 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
         const uint64_t m1 = __ballot(cpend[1] && !(clb[1] > bd2));
         if (!m0 && !m1) break;
         ASTAT(2);
-        int c8[kBatch], a0[kBatch], a1[kBatch];
-        take<kBatch>(m0, c[0], a0);
-        take<kBatch>(m1, c[1], a1);
-        const int n0 = min(__popcll(m0), kBatch);
-#pragma unroll
-        for (int e = 0; e < kBatch; e++) c8[e] = e < n0 ? a0[e] : (e - n0 < kBatch ? a1[e - n0 < 0 ? 0 : e - n0] : -1);
-        if (taken<kBatch>(m0)) cpend[0] = false;
-        if (((m1 >> lane) & 1ull) && __popcll(m1 & lanemask_lt()) < kBatch - n0) cpend[1] = false;
-        nn_eval(sorted, n, c8, q, best);
+        const Picked pk = pick(m0, c[0], m1, c[1]);
+        if (pk.took0) cpend[0] = false;
+        if (pk.took1) cpend[1] = false;
+        nn_eval(sorted, n, pk.v, q, best);
       }
     }
   }
@@ -398,17 +440,18 @@ struct LineSearch {
 
 // Evaluate up to eight chunks (dir: 1 up / 0 down) against the running bests.  brk[t]: the
 // lane group met the walk's 'break' inside its slot-t chunk.
+// ch[t] / upd[t]: this lane group's chunk and direction in slot t (-1 = none).
 template <bool kCorner>
-__device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[kBatch], const int (&dir)[kBatch],
+__device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[2], const bool (&upd)[2],
                                         uint64_t* brk_mask = nullptr) {
-  const int lane = lane_id(), g = lane >> 4, l16 = lane & 15;
+  const int lane = lane_id(), l16 = lane & 15;
   P4 p[2];
   bool valid[2], up[2];
   int j[2];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
-    const int c = batch_item(ch, g, t);
-    up[t] = batch_item(dir, g, t) != 0;
+    const int c = ch[t];
+    up[t] = upd[t];
     j[t] = c * kChunk + l16;
     valid[t] = c >= 0 && j[t] < s.n && (up[t] ? j[t] > s.closest : j[t] < s.closest);
     p[t] = ld4(s.L + (valid[t] ? j[t] : s.closest));  // unpredicated load
@@ -436,8 +479,13 @@ __device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[kBatch], 
       }
     }
   }
-  s.b2 = dmin(s.b2, wave_min(v2));
-  if (!kCorner) s.b3 = dmin(s.b3, wave_min(v3));
+  if (kCorner) {
+    s.b2 = dmin(s.b2, wave_min(v2));
+  } else {
+    wave_min2(v2, v3);
+    s.b2 = dmin(s.b2, v2);
+    s.b3 = dmin(s.b3, v3);
+  }
 }
 
 // Does an up / down chunk with bounds (lo, hi) and bound lb still need a visit?
@@ -464,8 +512,10 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
   if (din) { dlo = ldg(s.chm + 2 * cd); dhi = ldg(s.chm + 2 * cd + 1); }
   bool up_open, dn_open;  // no 'break' met yet in that direction
   {
-    const int ch[kBatch] = {hc, hc, hc + 1 < s.nch ? hc + 1 : -1, hc - 1, -1, -1, -1, -1};
-    const int dir[kBatch] = {1, 0, 1, 0, 1, 1, 1, 1};
+    // lane groups: home up, home down, hc + 1 up, hc - 1 down
+    const int g = lane >> 4;
+    const int ch[2] = {sel4(g, hc, hc, hc + 1 < s.nch ? hc + 1 : -1, hc - 1), -1};
+    const bool dir[2] = {(g & 1) == 0, true};
     uint64_t bm[2];
     LineSearch s0 = s;
     ls_eval<kCorner>(s0, ch, dir, bm);
@@ -473,7 +523,7 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
     if (!home_up_brk && !home_dn_brk) {
       s = s0;
     } else {  // rare: the home chunk broke a walk; redo without the neighbour beyond it
-      const int ch2[kBatch] = {hc, hc, home_up_brk ? -1 : ch[2], home_dn_brk ? -1 : ch[3], -1, -1, -1, -1};
+      const int ch2[2] = {(g == 2 && home_up_brk) || (g == 3 && home_dn_brk) ? -1 : ch[0], -1};
       ls_eval<kCorner>(s, ch2, dir);
     }
     up_open = !home_up_brk && !((bm[0] >> 32) & 0xffffull);
@@ -494,20 +544,19 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
     if (w == 0) {
       // first batch: around the up and the down chunk with the smallest bound among those that
       // can still improve a best (chunks i-1 .. i+2 of each), which sets tight bests at once
-      const dkey mu = wave_min(upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? dk(ulb, lane) : kIdent);
-      const dkey md = wave_min(dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dk(dlb, lane) : kIdent);
+      dkey mu = upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? dk(ulb, lane) : kIdent;
+      dkey md = dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dk(dlb, lane) : kIdent;
+      wave_min2(mu, md);
       const int iu = dk_key(mu), id = dk_key(md);
-      int ch[kBatch], dir[kBatch];
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int lu = (iu != kNone ? iu : 0) - 1 + e, ld = (id != kNone ? id : 0) - 1 + e;
-        const bool okl = iu != kNone && lu >= 0 && lu <= ulast && __builtin_amdgcn_readlane((int)upend, lu & 63);
-        const bool okd = id != kNone && ld >= 0 && ld <= dlast && __builtin_amdgcn_readlane((int)dpend, ld & 63);
-        ch[e] = okl ? hc + 2 + lu : -1;
-        dir[e] = 1;
-        ch[4 + e] = okd ? hc - 2 - ld : -1;
-        dir[4 + e] = 0;
-      }
+      // lane group g: up chunk iu - 1 + g (slot 0), down chunk id - 1 + g (slot 1)
+      const int g = lane >> 4;
+      const int lu = (iu != kNone ? iu : 0) - 1 + g, ld = (id != kNone ? id : 0) - 1 + g;
+      const int pu = __builtin_amdgcn_ds_bpermute((lu & 63) << 2, (int)upend);
+      const int pd = __builtin_amdgcn_ds_bpermute((ld & 63) << 2, (int)dpend);
+      const bool okl = iu != kNone && lu >= 0 && lu <= ulast && pu;
+      const bool okd = id != kNone && ld >= 0 && ld <= dlast && pd;
+      const int ch[2] = {okl ? hc + 2 + lu : -1, okd ? hc - 2 - ld : -1};
+      const bool dir[2] = {true, false};
       if (iu != kNone || id != kNone) {
         ASTAT(5);
         if (iu != kNone && lane >= iu - 1 && lane <= iu + 2) upend = false;
@@ -520,18 +569,11 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
       const uint64_t dm = __ballot(dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb));
       if (!um && !dm) break;
       ASTAT(kCorner ? 6 : 7);
-      int au[kBatch], ad[kBatch], ch[kBatch], dir[kBatch];
-      take<kBatch>(um, cu, au);
-      take<kBatch>(dm, cd, ad);
-      const int nu = min(__popcll(um), kBatch);
-#pragma unroll
-      for (int e = 0; e < kBatch; e++) {
-        ch[e] = e < nu ? au[e] : ad[e - nu < 0 ? 0 : e - nu];
-        dir[e] = e < nu ? 1 : 0;
-      }
-      if (taken<kBatch>(um)) upend = false;
-      if (((dm >> lane) & 1ull) && __popcll(dm & lanemask_lt()) < kBatch - nu) dpend = false;
-      ls_eval<kCorner>(s, ch, dir);
+      const Picked pk = pick(um, cu, dm, cd);
+      if (pk.took0) upend = false;
+      if (pk.took1) dpend = false;
+      const bool dir[2] = {pk.list[0] == 0, pk.list[1] == 0};
+      ls_eval<kCorner>(s, pk.v, dir);
     }
     // next window only where the walk did not break inside this one
     w++;
