@@ -132,7 +132,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   hipSetDevice(c->device);
   lislam_batch* b = new lislam_batch();
   b->ctx = c;
-  hipEventCreateWithFlags(&b->ev_extracted, hipEventDisableTiming);
+  hipEventCreateWithFlags(&b->ev_images, hipEventDisableTiming);
   const int S = max_scans, H = c->cfg.n_scans, W = c->cfg.width, N = H * W;
   b->max_scans = S; b->H = H; b->W = W; b->N = N;
   b->cap_sharp = kCapSharpPerLine * H;
@@ -218,7 +218,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   for (auto& v : b->odo_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
-  if (b->ev_extracted) hipEventDestroy(b->ev_extracted);
+  if (b->ev_images) hipEventDestroy(b->ev_images);
   delete b;
   return LISLAM_OK;
 }
@@ -266,10 +266,9 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
     for (int i = 0; i < 5; i++) b->ext_ev.back().push_back(b->get_event());
     ev = b->ext_ev.back().data();
   }
-  launch_features(f, c->stream, ev);
+  launch_features(f, c->stream, ev, b->ev_images);
   launch_target_index(b->oa, n_scans, c->stream);  // spatial index of the clouds odometry searches
   if (ev) HIPCHK(c, hipEventRecord(ev[4], c->stream));
-  HIPCHK(c, hipEventRecord(b->ev_extracted, c->stream));
   HIPCHK(c, hipGetLastError());
   b->extracted = n_scans;
   return LISLAM_OK;

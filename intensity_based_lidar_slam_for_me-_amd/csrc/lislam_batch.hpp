@@ -25,9 +25,10 @@ struct lislam_batch {
   std::vector<std::vector<hipEvent_t>> ext_ev, odo_ev;
   std::vector<hipEvent_t> pool;
   int extracted = 0;
-  // recorded after every lislam_batch_extract: the ORB front end waits on it from its own stream,
-  // so it overlaps whatever the caller queued on the context stream after the extraction.
-  hipEvent_t ev_extracted = nullptr;
+  // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
+  // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
+  // queued on the context stream after it.
+  hipEvent_t ev_images = nullptr;
   void* orb = nullptr;  // ORB engine of lislam_batch_intensity_odometry (lislam_orb.hip)
   hipEvent_t get_event() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }

@@ -642,11 +642,12 @@ __global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
   }
 }
 
-void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev) {
+void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEvent_t images_ready) {
   // ev (nullable): 4 events bracketing k_scan_front, k_scan_lines, k_scan_compact
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(k_scan_front, dim3(a.S), dim3(kFrontThreads), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
+  if (images_ready) (void)hipEventRecord(images_ready, st);  // the a1 images are complete here
   hipLaunchKernelGGL(k_scan_lines, dim3(a.S * a.H), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(k_scan_compact, dim3(a.S), dim3(256), 0, st, a);

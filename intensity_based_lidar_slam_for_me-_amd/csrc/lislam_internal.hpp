@@ -104,7 +104,9 @@ struct FactorArgs {
   double* jac;         // [n][3][6] or null
 };
 
-void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/);
+// images_ready (nullable): recorded once k_scan_front has written the range / intensity images and
+// cloud_track, which is all the ORB front end reads.
+void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/, hipEvent_t images_ready);
 void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st);
 // Issues the whole round/phase schedule; ev (nullable) receives the boundaries of every launch.
 void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>* ev,

@@ -1385,9 +1385,9 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
 
 extern "C" {
 
-// The ORB front end of every scan pair.  It runs on its own stream, ordered after the last
-// lislam_batch_extract only, so it overlaps the odometry chain the caller may already have
-// queued on the context stream; on return all of its work is done and the context stream is
+// The ORB front end of every scan pair.  It runs on its own stream, ordered only after the
+// images of the last lislam_batch_extract, so it overlaps the rest of the extraction and the
+// odometry chain the caller may already have queued on the context stream; on return all of its work is done and the context stream is
 // ordered after it.
 int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask) {
   if (!b || n_scans < 1 || n_scans > b->max_scans || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
@@ -1399,7 +1399,7 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
   OrbBatch* ob = nullptr;
   ORC(orb_batch_get(b, nfeatures, mask, &ob));
   const hipStream_t main_stream = c->stream;
-  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_extracted, 0));
+  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_images, 0));
   c->stream = ob->side;
   const int rc = batch_intensity_odometry(b, ob, n_scans);
   c->stream = main_stream;
