@@ -72,6 +72,56 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// ---------------------------------------------------------------- wave reductions (DPP)
+// Wave-wide unsigned minimum / maximum, returned uniform: DPP within each 16-lane row (quad xor 1,
+// xor 2, half-row mirror, row mirror; each folds into one v_min/max_u32_dpp), then row_bcast:15 /
+// row_bcast:31 carry the row results up to lane 63.  Every lane of the wave must be active.
+#define LISLAM_WAVE_RED(op, v)                                                                          \
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));  /* quad_perm [1,0,3,2] */ \
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));  /* quad_perm [2,3,0,1] */ \
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, true)); /* row_half_mirror */     \
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, true)); /* row_mirror */          \
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false)); /* bcast15 */  \
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false)); /* bcast31 */
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+  LISLAM_WAVE_RED(min, v)
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
+  LISLAM_WAVE_RED(max, v)
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+#undef LISLAM_WAVE_RED
+// Two independent minima interleaved step by step (each step's DPP read waits on the previous
+// step's write; the other reduction fills those wait states).
+__device__ __forceinline__ void wave_umin2(uint32_t& a, uint32_t& b) {
+#define LISLAM_UMIN2_STEP(ctrl)                                                   \
+  a = min(a, (uint32_t)__builtin_amdgcn_mov_dpp((int)a, ctrl, 0xf, 0xf, true)); \
+  b = min(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, ctrl, 0xf, 0xf, true));
+  LISLAM_UMIN2_STEP(0xB1)
+  LISLAM_UMIN2_STEP(0x4E)
+  LISLAM_UMIN2_STEP(0x141)
+  LISLAM_UMIN2_STEP(0x140)
+#undef LISLAM_UMIN2_STEP
+  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x142, 0xa, 0xf, false));
+  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x142, 0xa, 0xf, false));
+  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x143, 0xc, 0xf, false));
+  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x143, 0xc, 0xf, false));
+  a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+  b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
+}
+// 64-bit minimum: the minimum high word, then the minimum low word among the lanes holding it
+// (one lane in the common case: read directly).
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  const uint32_t m = wave_umin(hi);
+  const uint64_t tie = __ballot(hi == m);
+  const uint32_t l = __popcll(tie) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)__builtin_ctzll(tie))
+                                        : wave_umin(hi == m ? lo : 0xffffffffu);
+  return ((uint64_t)m << 32) | l;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { return ~wave_min_u64(~v); }
+
 // ---------------------------------------------------------------- double 3-vectors / quats
 struct D3 {
   double x, y, z;

@@ -269,20 +269,6 @@ __device__ __forceinline__ void bitonic_sort(KeyPtr keys, int P) {
 
 __device__ __forceinline__ uint64_t first_lane(uint64_t m) { return (uint64_t)__builtin_ctzll(m); }
 
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t w = __shfl_xor(v, o);
-    v = w > v ? w : v;
-  }
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t w = __shfl_xor(v, o);
-    v = w < v ? w : v;
-  }
-  return v;
-}
 
 struct LineCounts {
   int sharp, less_sharp, flat, less_flat;
@@ -584,20 +570,395 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
   }
 }
 
+// ------------------------------------------------------------------ register-resident line
+// The line kernel's fast path keeps the whole line in registers: lane l holds points l + 64 t in
+// slot t (t < kS), with per-lane bitmasks over the slots for the picked / label flags.  Only the
+// link masks (uniform, for the suppression), the pick lists and a 64-point centroid window live
+// in LDS (about 2 KiB), so occupancy is set by registers, not by a line-sized LDS footprint.
+
+// Compare-exchange of one bitonic stage of the register layout i = 64 t + lane.
+template <int kS, int kJJ>  // partner i ^ (64 kJJ): slot t ^ kJJ of the same lane
+__device__ __forceinline__ void bx_slots(uint64_t (&key)[kS], int k) {
+  if constexpr (kJJ < kS) {
+#pragma unroll
+    for (int t = 0; t < kS; t++) {
+      if (t & kJJ) continue;
+      const int u = t | kJJ;
+      const bool up = ((t * 64) & k) == 0;
+      const uint64_t x = key[t], y = key[u];
+      const bool sw = (x > y) == up;
+      key[t] = sw ? y : x;
+      key[u] = sw ? x : y;
+    }
+  }
+}
+template <int kJ>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+  if constexpr (kJ == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+  else if constexpr (kJ == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true);  // [2,3,0,1]
+  else if constexpr (kJ < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (kJ << 10) | 0x1f);  // xor mask
+  else return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ 32) << 2, (int)v);
+}
+template <int kS, int kJ>  // partner i ^ kJ: lane ^ kJ, same slot
+__device__ __forceinline__ void bx_lanes(uint64_t (&key)[kS], int k) {
+  const int lane = lane_id();
+  const bool lower = (lane & kJ) == 0;
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    const uint64_t x = key[t];
+    const uint64_t y = ((uint64_t)xor_lane32<kJ>((uint32_t)(x >> 32)) << 32) | xor_lane32<kJ>((uint32_t)x);
+    const bool up = k < 64 ? (lane & k) == 0 : ((t * 64) & k) == 0;
+    key[t] = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
+    if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // four slots' exchanges in flight (registers)
+  }
+}
+// Ascending bitonic sort of the 64 kS keys (every slot: a runtime slot bound doubled the
+// registers the exchanges hold).
+template <int kS>
+__device__ __forceinline__ void reg_bitonic(uint64_t (&key)[kS]) {
+  constexpr int P = 64 * kS;
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      switch (j) {
+        case 1: bx_lanes<kS, 1>(key, k); break;
+        case 2: bx_lanes<kS, 2>(key, k); break;
+        case 4: bx_lanes<kS, 4>(key, k); break;
+        case 8: bx_lanes<kS, 8>(key, k); break;
+        case 16: bx_lanes<kS, 16>(key, k); break;
+        case 32: bx_lanes<kS, 32>(key, k); break;
+        case 64: bx_slots<kS, 1>(key, k); break;
+        case 128: bx_slots<kS, 2>(key, k); break;
+        case 256: bx_slots<kS, 4>(key, k); break;
+        case 512: bx_slots<kS, 8>(key, k); break;
+        default: bx_slots<kS, 16>(key, k); break;
+      }
+    }
+  }
+}
+
+// Same results as line_body (which documents the reference semantics); the differences are only
+// where the state lives.
+template <int kS>
+__device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int line, LineLists& ll, uint64_t* lmask,
+                                              P4* stage) {
+  const int lane = lane_id();
+  const int N = a.N, H = a.H;
+  const int* lo = a.line_off + (size_t)s * (H + 1);
+  const int off = lo[line];
+  const int len = lo[line + 1] - off;
+  const int total = lo[H];
+  const int nsl = (len + 63) >> 6;  // slots in use
+  const P4* cloud = a.cloud + (size_t)s * N;
+  float* curv = a.curv + (size_t)s * N;
+  int8_t* glabel = a.label + (size_t)s * N;
+  PHASE_BEGIN;
+
+  // curvature (scanRegistration.cpp:397-412) and neighbour links (suppress)
+  float cr[kS];
+  uint32_t linkb = 0;
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    cr[t] = 0.f;
+    if (t >= nsl) continue;
+    const int k = lane + 64 * t;
+    if (k < len) {
+      const int i = off + k;
+      float c = 0.f;
+      if (i >= 5 && i < total - 5) {
+        P4 q[11];
+        for (int d = 0; d < 11; d++) q[d] = ld4(cloud + i - 5 + d);
+        const float dX = q[0].x + q[1].x + q[2].x + q[3].x + q[4].x - 10 * q[5].x + q[6].x + q[7].x + q[8].x + q[9].x + q[10].x;
+        const float dY = q[0].y + q[1].y + q[2].y + q[3].y + q[4].y - 10 * q[5].y + q[6].y + q[7].y + q[8].y + q[9].y + q[10].y;
+        const float dZ = q[0].z + q[1].z + q[2].z + q[3].z + q[4].z - 10 * q[5].z + q[6].z + q[7].z + q[8].z + q[9].z + q[10].z;
+        c = dX * dX + dY * dY + dZ * dZ;
+      }
+      curv[i] = c;
+      cr[t] = c;
+      if (k + 1 < len) {
+        const P4 p0 = ld4(cloud + i), p1 = ld4(cloud + i + 1);
+        const float dx = p1.x - p0.x, dy = p1.y - p0.y, dz = p1.z - p0.z;
+        if (!((double)(dx * dx + dy * dy + dz * dz) > 0.05)) linkb |= 1u << t;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one slot's 13 loads in flight at a time (registers)
+  }
+  // lmask[1 + t]: link bits of points 64 t .. 64 t + 63; lmask[0] / lmask[kS + 1] stay zero
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    const uint64_t m = t < nsl ? __ballot((linkb >> t) & 1u) : 0ull;
+    if (lane == 0) lmask[1 + t] = m;
+  }
+  if (lane == 0) { lmask[0] = 0; lmask[kS + 1] = 0; }
+  wave_sync<true>();
+  PHASE(0);
+
+  // Suppression (scanRegistration.cpp:481-504) of pick ind, ind itself included: forward marks
+  // ind+1.. while link[ind], link[ind+1], ... hold (at most 5), backward ind-1.. while
+  // link[ind-1], ... hold.
+  uint32_t pick = 0, lsh = 0, shp = 0, flt = 0;  // per-lane slot bitmasks
+  auto mark = [&](int ind) {
+    const int ti = ind >> 6, b = ind & 63;
+    const uint64_t Wm = lmask[ti], W0 = lmask[ti + 1], W1 = lmask[ti + 2];
+    const uint32_t fwd5 = (uint32_t)((b == 0 ? W0 : ((W0 >> b) | (W1 << (64 - b)))) & 31u);       // link[ind .. ind+4]
+    const uint32_t bwd5 = (uint32_t)((b >= 5 ? (W0 >> (b - 5)) : ((W0 << (5 - b)) | (Wm >> (59 + b)))) & 31u);  // link[ind-5 .. ind-1]
+    const uint32_t fz = ~fwd5 & 31u, bz = ~bwd5 & 31u;
+    const int nf = fz ? (int)__builtin_ctz(fz) : 5;
+    const int nb = bz ? 4 - (31 - (int)__builtin_clz(bz)) : 5;
+    const int k0 = ind - nb, k1 = ind + nf;
+#pragma unroll
+    for (int t = 0; t < kS; t++) {
+      if (t < (k0 >> 6) || t > (k1 >> 6)) continue;
+      const int k = lane + 64 * t;
+      if (k >= k0 && k <= k1) pick |= 1u << t;
+    }
+  };
+
+  int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+  const int sI = 5, eI = len - 6;  // scanStartInd / scanEndInd relative to off
+  const bool segs = eI - sI >= 6;
+  if (segs) {
+    for (int j = 0; j < 6; j++) {
+      const int sp = sI + (eI - sI) * j / 6;
+      const int ep = sI + (eI - sI) * (j + 1) / 6 - 1;
+      const int t0 = sp >> 6, t1 = ep >> 6;
+      // ---- sharp picks: largest (curvature, index) first (:450-506); at most 20 per segment
+      for (int largest = 1; largest <= 20; largest++) {
+        uint64_t best = 0;
+#pragma unroll
+        for (int t = 0; t < kS; t++) {
+          if (t < t0 || t > t1) continue;
+          const int k = lane + 64 * t;
+          if (k >= sp && k <= ep && !((pick >> t) & 1u) && (double)cr[t] > 0.1) {
+            const uint64_t key = ((uint64_t)__float_as_uint(cr[t]) << 32) | (uint32_t)k;
+            best = key > best ? key : best;
+          }
+        }
+        best = wave_max_u64(best);
+        if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
+        const int ind = (int)(uint32_t)best;
+        if (lane == 0) {
+          if (largest <= 2) ll.sharp[n_sharp] = ind;
+          ll.less_sharp[n_lsharp] = ind;
+        }
+        if (lane == (ind & 63)) {
+          lsh |= 1u << (ind >> 6);
+          if (largest <= 2) shp |= 1u << (ind >> 6);
+        }
+        if (largest <= 2) n_sharp++;
+        n_lsharp++;
+        mark(ind);
+      }
+      PHASE(2);
+      // ---- flat picks: smallest (curvature, index) first (:511-568); the 4th pick ends the walk
+      // unmarked
+      for (int smallest = 1; smallest <= 4; smallest++) {
+        uint64_t best = ~0ull;
+#pragma unroll
+        for (int t = 0; t < kS; t++) {
+          if (t < t0 || t > t1) continue;
+          const int k = lane + 64 * t;
+          if (k >= sp && k <= ep && !((pick >> t) & 1u) && (double)cr[t] < 0.1) {
+            const uint64_t key = ((uint64_t)__float_as_uint(cr[t]) << 32) | (uint32_t)k;
+            best = key < best ? key : best;
+          }
+        }
+        best = wave_min_u64(best);
+        if (best == ~0ull) break;
+        const int ind = (int)(uint32_t)best;
+        if (lane == 0) ll.flat[n_flat] = ind;
+        if (lane == (ind & 63)) flt |= 1u << (ind >> 6);
+        n_flat++;
+        if (smallest == 4) break;
+        mark(ind);
+      }
+      PHASE(3);
+    }
+  }
+  // labels (parity tests) and the picked points in pick order
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    const int k = lane + 64 * t;
+    if (t < nsl && k < len) {
+      const uint32_t bit = 1u << t;
+      glabel[off + k] = (shp & bit) ? 2 : (lsh & bit) ? 1 : (flt & bit) ? -1 : 0;
+    }
+  }
+  wave_sync<true>();  // the pick lists
+  P4* o_sharp = a.stg_sharp + ((size_t)s * H + line) * kCapSharpPerLine;
+  P4* o_lsharp = a.stg_less_sharp + ((size_t)s * H + line) * kCapLessSharpPerLine;
+  P4* o_flat = a.stg_flat + ((size_t)s * H + line) * kCapFlatPerLine;
+  P4* o_lflat = a.stg_less_flat + (size_t)s * N + off;
+  for (int k = lane; k < n_sharp; k += 64) st4(o_sharp + k, ld4(cloud + off + ll.sharp[k]));
+  for (int k = lane; k < n_lsharp; k += 64) st4(o_lsharp + k, ld4(cloud + off + ll.less_sharp[k]));
+  for (int k = lane; k < n_flat; k += 64) st4(o_flat + k, ld4(cloud + off + ll.flat[k]));
+  // less-flat points (:570-577): label <= 0 inside the six segments, in index order
+  uint32_t lfl = 0;
+  int nlist = 0;
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    const int k = lane + 64 * t;
+    const bool f = t < nsl && segs && k >= sI && k < eI && !((lsh >> t) & 1u);
+    if (f) lfl |= 1u << t;
+    if (t < nsl) nlist += __popcll(__ballot(f));
+  }
+  PHASE(5);
+
+  // ---- VoxelGrid(0.2) of the line's less-flat points (PCL VoxelGrid::applyFilter semantics)
+  int n_lflat = 0;
+  if (nlist > 0) {
+    const float inv = 1.0f / 0.2f;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+#pragma unroll
+    for (int t = 0; t < kS; t++) {
+      if (!((lfl >> t) & 1u)) continue;
+      const P4 p = ld4(cloud + off + lane + 64 * t);
+      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+    }
+    for (int d = 0; d < 3; d++) {
+      for (int o = 32; o > 0; o >>= 1) {
+        mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+        mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+      }
+    }
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)2147483647) {  // PCL: leaf too small -> copy the input
+      int base = 0;
+#pragma unroll
+      for (int t = 0; t < kS; t++) {
+        if (t >= nsl) continue;
+        const bool f = (lfl >> t) & 1u;
+        const uint64_t m = __ballot(f);
+        if (f) st4(o_lflat + base + __popcll(m & lanemask_lt()), ld4(cloud + off + lane + 64 * t));
+        base += __popcll(m);
+      }
+      n_lflat = nlist;
+    } else {
+      int minb[3], divb[3];
+      for (int d = 0; d < 3; d++) {
+        minb[d] = (int)floorf(mn[d] * inv);
+        divb[d] = (int)floorf(mx[d] * inv) - minb[d] + 1;
+      }
+      const int mul1 = divb[0], mul2 = divb[0] * divb[1];
+      // keys (voxel index, point index): the point index orders like the list position
+      uint64_t key[kS];
+#pragma unroll
+      for (int t = 0; t < kS; t++) {
+        key[t] = ~0ull;
+        if ((lfl >> t) & 1u) {
+          const int k = lane + 64 * t;
+          const P4 p = ld4(cloud + off + k);
+          const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+          const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+          const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+          const uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+          key[t] = ((uint64_t)idx << 32) | (uint32_t)k;
+        }
+      }
+      PHASE(6);
+      reg_bitonic<kS>(key);
+      PHASE(7);
+      // centroids in sorted order (sums in input order within a voxel): window t = sorted
+      // positions 64 t .. 64 t + 63, staged in LDS; the voxel still open at the end of a window
+      // carries over.
+      int nout = 0;
+      P4 carry{0.f, 0.f, 0.f, 0.f};
+      int carry_n = 0;
+      uint32_t prev_hi = 0xffffffffu;  // voxel of sorted position 64 t - 1
+#pragma unroll
+      for (int t = 0; t < kS; t++) {
+        const int b = 64 * t;
+        if (b >= nlist) continue;
+        const int k = b + lane;
+        const int wl = min(64, nlist - b);  // window length
+        const bool valid = k < nlist;
+        const uint32_t v = (uint32_t)(key[t] >> 32);
+        const uint32_t up1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, (int)v);  // lane - 1
+        const uint32_t vprev = lane == 0 ? prev_hi : up1;
+        prev_hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+        if (valid) stage[lane] = ld4(cloud + off + (int)(uint32_t)key[t]);
+        const bool start = valid && (k == 0 || v != vprev);
+        const uint64_t m = __ballot(start);
+        wave_sync<true>();
+        const bool last = b + 64 >= nlist;
+        const bool cont = carry_n > 0 && !(m & 1ull);  // window opens inside the carried voxel
+        int extra = 0;
+        if (carry_n > 0 && (m & 1ull)) {  // the carried voxel closed exactly at the window edge
+          if (lane == 0) {
+            const float n = (float)carry_n;
+            P4 c = carry;
+            c.x /= n; c.y /= n; c.z /= n; c.i /= n;
+            st4(o_lflat + nout, c);
+          }
+          extra = 1;
+        }
+        const bool head = start || (lane == 0 && cont);
+        const uint64_t after = lane == 63 ? 0ull : (m >> (lane + 1)) << (lane + 1);
+        const int end = after ? (int)__builtin_ctzll(after) : wl;
+        const bool closed = head && (end < wl || last);
+        P4 c{0.f, 0.f, 0.f, 0.f};
+        int n = 0;
+        if (head) {
+          int e = lane;
+          if (start) {
+            c = stage[lane];
+            e = lane + 1;
+            n = 1;
+          } else {
+            c = carry;
+            n = carry_n;
+          }
+          for (; e < end; e++) {
+            const P4 p = stage[e];
+            c.x += p.x; c.y += p.y; c.z += p.z; c.i += p.i;
+            n++;
+          }
+        }
+        const uint64_t cm = __ballot(closed);
+        if (closed) {
+          const float fn = (float)n;
+          P4 o = c;
+          o.x /= fn; o.y /= fn; o.z /= fn; o.i /= fn;
+          st4(o_lflat + nout + extra + __popcll(cm & lanemask_lt()), o);
+        }
+        nout += extra + __popcll(cm);
+        // the open voxel (a head that reached the window end) becomes the carry
+        const uint64_t om = __ballot(head && !closed);
+        if (om) {
+          const int src = (int)__builtin_ctzll(om);
+          carry.x = __shfl(c.x, src); carry.y = __shfl(c.y, src);
+          carry.z = __shfl(c.z, src); carry.i = __shfl(c.i, src);
+          carry_n = __shfl(n, src);
+        } else {
+          carry_n = 0;
+        }
+        wave_sync<true>();
+      }
+      n_lflat = nout;
+      PHASE(8);
+    }
+  }
+  if (lane == 0) {
+    int* c = a.line_counts + ((size_t)s * H + line) * 4;
+    c[0] = n_sharp; c[1] = n_lsharp; c[2] = n_flat; c[3] = n_lflat;
+  }
+}
+
+// kS: register slots per lane of the fast path (lines up to 64 kS points); longer lines (input
+// that is not ring-ordered) run line_body on global scratch.
+template <int kS>
 __global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
-  __shared__ uint8_t picked[kLineCap];
-  __shared__ int8_t label[kLineCap];
-  __shared__ uint64_t keys[kLineCap];
-  __shared__ int list[kLineCap];
-  __shared__ uint8_t link[kLineCap];
   __shared__ LineLists ll;
   __shared__ P4 stage[64];
+  __shared__ uint64_t lmask[kS + 2];
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
-  if (len <= kLineCap)
-    line_body<true>(a, s, line, picked, label, keys, list, link, ll, stage);
-  else  // a line longer than the LDS fast path (non ring-ordered input): global scratch
+  if (len <= 64 * kS)
+    line_body_reg<kS>(a, s, line, ll, lmask, stage);
+  else
     line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, ll, stage);
 }
 
@@ -648,7 +1009,12 @@ void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEv
   hipLaunchKernelGGL(k_scan_front, dim3(a.S), dim3(kFrontThreads), 0, st, a);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (images_ready) (void)hipEventRecord(images_ready, st);  // the a1 images are complete here
-  hipLaunchKernelGGL(k_scan_lines, dim3(a.S * a.H), dim3(64), 0, st, a);
+  if (a.W <= 512)
+    hipLaunchKernelGGL(k_scan_lines<8>, dim3(a.S * a.H), dim3(64), 0, st, a);
+  else if (a.W <= 1024)
+    hipLaunchKernelGGL(k_scan_lines<16>, dim3(a.S * a.H), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_scan_lines<32>, dim3(a.S * a.H), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(k_scan_compact, dim3(a.S), dim3(256), 0, st, a);
   if (ev) (void)hipEventRecord(ev[3], st);

@@ -232,46 +232,9 @@ __device__ __forceinline__ int dk_key(dkey v) { return (int)(uint32_t)v; }
 __device__ __forceinline__ dkey dmin(dkey a, dkey b) { return b < a ? b : a; }
 #define kIdent dk(3.4e38f, kNone)  // identity of the minima (no candidate)
 
-// Wave-wide unsigned minimum, returned uniform: DPP within each 16-lane row (quad xor 1, xor 2,
-// half-row mirror, row mirror; each folds into one v_min_u32_dpp), then row_bcast:15 /
-// row_bcast:31 carry the row minima up to lane 63.
-__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, true));  // row_half_mirror
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, true));  // row_mirror
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return (uint32_t)rdlane((int)v, 63);
-}
-// Two independent minima interleaved step by step (each step's DPP read waits on the previous
-// step's write; the other reduction fills those wait states).
-__device__ __forceinline__ void wave_umin2(uint32_t& a, uint32_t& b) {
-#define LISLAM_UMIN2_STEP(ctrl) \
-  a = min(a, (uint32_t)__builtin_amdgcn_mov_dpp((int)a, ctrl, 0xf, 0xf, true)); \
-  b = min(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, ctrl, 0xf, 0xf, true));
-  LISLAM_UMIN2_STEP(0xB1)
-  LISLAM_UMIN2_STEP(0x4E)
-  LISLAM_UMIN2_STEP(0x141)
-  LISLAM_UMIN2_STEP(0x140)
-#undef LISLAM_UMIN2_STEP
-  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x142, 0xa, 0xf, false));
-  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x142, 0xa, 0xf, false));
-  a = min(a, (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)a, 0x143, 0xc, 0xf, false));
-  b = min(b, (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)b, 0x143, 0xc, 0xf, false));
-  a = (uint32_t)rdlane((int)a, 63);
-  b = (uint32_t)rdlane((int)b, 63);
-}
-// Wave-wide minimum of the pairs: the minimum distance, then the smallest key among the lanes
-// holding it (one lane in the common case: read directly).
-__device__ __forceinline__ dkey wave_min(dkey v) {
-  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-  const uint32_t m = wave_umin(hi);
-  const uint64_t tie = __ballot(hi == m);
-  const uint32_t key = __popcll(tie) == 1 ? (uint32_t)rdlane((int)lo, (int)__builtin_ctzll(tie))
-                                          : wave_umin(hi == m ? lo : 0xffffffffu);
-  return ((dkey)m << 32) | key;
-}
+// Wave-wide minimum of the pairs (lislam_device.hpp: the minimum distance, then the smallest key
+// among the lanes holding it).
+__device__ __forceinline__ dkey wave_min(dkey v) { return wave_min_u64(v); }
 __device__ __forceinline__ void wave_min2(dkey& va, dkey& vb) {
   const uint32_t ha = (uint32_t)(va >> 32), la = (uint32_t)va, hb = (uint32_t)(vb >> 32), lb = (uint32_t)vb;
   uint32_t ma = ha, mb = hb;
