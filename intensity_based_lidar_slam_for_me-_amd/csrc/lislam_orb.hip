@@ -14,10 +14,12 @@
 //   k_orb_level     per level (in order), 1 thread per padded pixel: level 0 copy, levels 1..7 by
 //                   the bit-exact fixed-point INTER_LINEAR_EXACT resize of the previous level;
 //                   border pixels evaluate their reflect-101 source directly
-//   k_orb_blur      1 thread per padded pixel: 7x7 sigma-2 separable float Gaussian (row sums
-//                   then the symmetric column sum, the FilterEngine order) on the ROI, border copy
-//   k_orb_fast      1 thread per level pixel: FAST-9/16 segment test + cornerScore<16>
-//   k_orb_nms       1 thread per level pixel: 3x3 non-max suppression, mask, border
+//   k_orb_blur      1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2 separable float
+//                   Gaussian (row sums then the symmetric column sum, the FilterEngine order) on
+//                   the ROI, border copy
+//   k_orb_fastnms   1 WG per band of 8 level rows, staged in LDS: FAST-9/16 segment test +
+//                   cornerScore<16> into an LDS score tile, then 3x3 non-max suppression, mask,
+//                   border
 //   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
 //                   thread), retainBest(2n) on the FAST score (256-bin histogram), Harris responses
 //                   (a wavefront per candidate), retainBest(n) on them (radix select of the n-th
@@ -56,7 +58,9 @@ constexpr int kSelThreads = 1024;
 constexpr int kPairThreads = 1024;
 constexpr int kLmThreads = 256;
 constexpr int kQTile = 1024;  // queries per LDS tile in k_orb_xdist (32 KiB)
-constexpr int kNoMatch = 0x7f7f7f7f;  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
+constexpr int kNoMatch = 0x7f7f7f7f;
+constexpr int kFastBand = 8;   // ROI rows per k_orb_fastnms workgroup
+constexpr int kBlurBand = 8;   // padded rows per k_orb_blur workgroup  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
 
 constexpr int kNPatch = 749;  // pixels of the ICAngles circular patch (half size 15; checked on the host)
 constexpr int kPatchIters = (kNPatch + 63) / 64;
@@ -81,6 +85,8 @@ struct Geom {
   int cap;          // per scan keypoints (sum lcap)
   float gk[7];      // Gaussian taps
   int umax[kHalf + 2];
+  int fband[kL + 1];  // prefix of FAST bands (kFastBand ROI rows) per level
+  int bband[kL + 1];  // prefix of blur bands (kBlurBand padded rows) per level
 };
 
 struct Tabs {  // resize coefficients of level l from level l-1 (l >= 1), per axis
@@ -98,7 +104,6 @@ struct Args {
   uint8_t* pyr;           // [S][bytes]
   uint8_t* blur;          // [S][bytes]
   const uint8_t* mpyr;    // [bytes] mask pyramid or null
-  uint8_t* score;         // [S][pix[kL]]
   uint8_t* nms;           // [S][pix[kL]] FAST score of a keypoint (non-max, mask, border), else 0
   int* cand;              // [S][pix[kL]] candidate pixel indices
   float* cresp;           // [S][pix[kL]]
@@ -176,35 +181,82 @@ __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
   base[g.off[l] + i] = v;
 }
 
-// GaussianBlur(level ROI, 7x7, 2, 2, BORDER_REFLECT_101): row sums then symmetric column sum
+// Stage `rows` (<= kMaxRows) rows of nd dwords (source rows 4-byte aligned, sstride bytes apart)
+// into LDS rows of nd dwords: every load of a thread is issued before its first store.
+template <int kMaxRows>
+__device__ __forceinline__ void stage_rows(uint32_t* dst, const uint8_t* src, int sstride, int rows, int nd) {
+  for (int j0 = 0; j0 < nd; j0 += 3 * 256) {
+    uint32_t v[kMaxRows][3];
+#pragma unroll
+    for (int r = 0; r < kMaxRows; r++)
+#pragma unroll
+      for (int u = 0; u < 3; u++) {
+        const int d = j0 + u * 256 + (int)threadIdx.x;
+        if (r < rows && d < nd)
+          v[r][u] = *(const __attribute__((address_space(1))) uint32_t*)(src + (size_t)r * sstride + 4 * d);
+      }
+#pragma unroll
+    for (int r = 0; r < kMaxRows; r++)
+#pragma unroll
+      for (int u = 0; u < 3; u++) {
+        const int d = j0 + u * 256 + (int)threadIdx.x;
+        if (r < rows && d < nd) dst[r * nd + d] = v[r][u];
+      }
+  }
+}
+
+// GaussianBlur(level ROI, 7x7, 2, 2, BORDER_REFLECT_101): row sums then symmetric column sum.
+// One workgroup per band of kBlurBand padded rows of a level: the band's rows +-3 staged in LDS
+// (row-coalesced byte loads), then one thread per column keeps the band's row sums in registers;
+// border rows / columns are copies.
 __global__ __launch_bounds__(256) void k_orb_blur(Args a) {
+  extern __shared__ uint8_t btile[];  // (kBlurBand + 6) x stride[l]
   const Geom& g = a.g;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
-  if (i >= g.pad[kL]) return;
   int l = 0;
-  while (i >= g.pad[l + 1]) l++;
-  const int j = i - g.pad[l], pw = g.stride[l];
-  const int r = j / pw - kB, c = j % pw - kB;
-  const uint8_t* src = a.pyr + (size_t)s * g.bytes;
-  uint8_t* dst = a.blur + (size_t)s * g.bytes;
-  if (r < 0 || r >= g.h[l] || c < 0 || c >= g.w[l]) {
-    px(dst, g, l, r, c) = pxc(src, g, l, r, c);
-    return;
+  while ((int)blockIdx.x >= g.bband[l + 1]) l++;
+  const int w = g.w[l], h = g.h[l], pw = g.stride[l];
+  const int p0 = ((int)blockIdx.x - g.bband[l]) * kBlurBand;  // first padded row of the band
+  const int nr = min(kBlurBand, h + 2 * kB - p0);
+  const uint8_t* src = a.pyr + (size_t)s * g.bytes + g.off[l];
+  uint8_t* dst = a.blur + (size_t)s * g.bytes + g.off[l];
+  // staged rows: padded rows p0 - 3 .. p0 + nr + 2, clamped to the level's buffer
+  const int t0 = max(0, p0 - 3), t1 = min(h + 2 * kB, p0 + nr + 3);
+  stage_rows<kBlurBand + 6>(reinterpret_cast<uint32_t*>(btile + (t0 - (p0 - 3)) * pw), src + (size_t)t0 * pw, pw,
+                            t1 - t0, pw >> 2);
+  __syncthreads();
+  for (int c = threadIdx.x; c < pw; c += blockDim.x) {
+    const int cr = c - kB;  // ROI column
+    const bool roi_c = cr >= 0 && cr < w;
+    float rs[kBlurBand + 6];
+    if (roi_c) {
+#pragma unroll
+      for (int k = 0; k < kBlurBand + 6; k++) {
+        const int pr = p0 - 3 + k;
+        rs[k] = 0.f;
+        if (pr >= kB - 3 && pr < h + kB + 3 && k < nr + 6) {  // rows some ROI output of the band reads
+          const uint8_t* row = btile + k * pw + c - 3;
+          float v = g.gk[0] * (float)row[0];
+#pragma unroll
+          for (int t = 1; t < 7; t++) v += g.gk[t] * (float)row[t];
+          rs[k] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kBlurBand; k++) {
+      if (k >= nr) break;
+      const int pr = p0 + k, r = pr - kB;
+      uint8_t o = btile[(k + 3) * pw + c];
+      if (roi_c && r >= 0 && r < h) {
+        float v = g.gk[3] * rs[k + 3];
+#pragma unroll
+        for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[k + 3 + t] + rs[k + 3 - t]);
+        o = (uint8_t)min(255, max(0, (int)rintf(v)));
+      }
+      dst[pr * pw + c] = o;
+    }
   }
-  float rs[7];
-#pragma unroll
-  for (int dy = 0; dy < 7; dy++) {
-    float v = g.gk[0] * (float)pxc(src, g, l, r - 3 + dy, c - 3);
-#pragma unroll
-    for (int t = 1; t < 7; t++) v += g.gk[t] * (float)pxc(src, g, l, r - 3 + dy, c - 3 + t);
-    rs[dy] = v;
-  }
-  float v = g.gk[3] * rs[3];
-#pragma unroll
-  for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t] + rs[3 - t]);
-  const int iv = (int)rintf(v);
-  px(dst, g, l, r, c) = (uint8_t)min(255, max(0, iv));
 }
 
 // ------------------------------------------------------------------ FAST
@@ -241,66 +293,115 @@ __device__ int corner_score(const int* d, int threshold) {
   return -b0 - 1;
 }
 
-__global__ __launch_bounds__(256) void k_orb_fast(Args a) {
+// Is there a run of 9 set bits in the circular 16-bit mask m (FAST's "count > 8" over the
+// 25-step doubled walk)?
+__device__ __forceinline__ bool has_run9(uint32_t m) {
+  m |= m << 16;
+  uint32_t r = m & (m >> 1);  // runs of 2 starting at each bit
+  r &= r >> 2;                // 4
+  r &= r >> 4;                // 8
+  r &= m >> 8;                // 9
+  return (r & 0xffffu) != 0;
+}
+
+// FAST-9/16 segment test + cornerScore<16> of the pixel at p (an LDS tile with row stride ts).
+// The opposite-pair pre-tests of OpenCV only reject pixels that have no 9-run either, so the
+// test is the run check of both masks.
+__device__ __forceinline__ int fast_full(const uint8_t* p, int ts) {
+  const int v = p[0];
+  int x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x[k] = p[c_fast[k][1] * ts + c_fast[k][0]];
+  uint32_t dark = 0, bright = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    dark |= (uint32_t)(x[k] < v - kFastT) << k;
+    bright |= (uint32_t)(x[k] > v + kFastT) << k;
+  }
+  if (!has_run9(dark) && !has_run9(bright)) return 0;
+  int dd[25];
+#pragma unroll
+  for (int k = 0; k < 25; k++) dd[k] = v - x[k & 15];
+  return corner_score(dd, kFastT);
+}
+
+// FAST keypoints of a band of kFastBand ROI rows of a level: the band's pixels +-4 rows / columns
+// staged in LDS, FAST scores of the band +-1 (border pixels 0) into a second LDS tile, then
+// 3x3 non-max suppression of FAST_t, the pixel mask (runByPixelsMask) and the image border
+// (edgeThreshold 1): nms = the FAST score of a keypoint, else 0.
+__global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
+  extern __shared__ uint8_t ftile[];
   const Geom& g = a.g;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
-  if (i >= g.pix[kL]) return;
   int l = 0;
-  while (i >= g.pix[l + 1]) l++;
-  const int j = i - g.pix[l];
-  const int r = j / g.w[l], c = j % g.w[l];
+  while ((int)blockIdx.x >= g.fband[l + 1]) l++;
+  const int w = g.w[l], h = g.h[l];
+  const int r0 = ((int)blockIdx.x - g.fband[l]) * kFastBand;
+  const int nr = min(kFastBand, h - r0);
+  // image tile: rows r0-4 .. r0+nr+3, padded columns 16 .. (level columns -7 ..), dword rows
+  const int nd = (w + 12 + 3) >> 2, ts = 4 * nd;
+  constexpr int kC0 = kB - 16;                  // tile column of level column 0
+  uint8_t* img = ftile;
+  uint8_t* sct = ftile + (kFastBand + 8) * ts;  // scores: rows r0-1 .., columns -1 .. w
+  const int ss = w + 2;
+  uint16_t* lst = reinterpret_cast<uint16_t*>(ftile + (((kFastBand + 8) * ts + (kFastBand + 2) * ss + 1) & ~1));
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
-  int score = 0;
-  if (r >= 3 && r < g.h[l] - 3 && c >= 3 && c < g.w[l] - 3) {
-    const int v = pxc(base, g, l, r, c);
-    int x[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = pxc(base, g, l, r + c_fast[k][1], c + c_fast[k][0]);
-    auto tab = [&](int k) { const int dd = x[k] - v; return dd < -kFastT ? 1 : dd > kFastT ? 2 : 0; };
-    int d = tab(0) | tab(8);
-    if (d) {
-      d &= tab(2) | tab(10);
-      d &= tab(4) | tab(12);
-      d &= tab(6) | tab(14);
-    }
-    if (d) {
-      d &= tab(1) | tab(9);
-      d &= tab(3) | tab(11);
-      d &= tab(5) | tab(13);
-      d &= tab(7) | tab(15);
-    }
-    bool corner = false;
-    if (d & 1) {
-      const int vt = v - kFastT;
-      int count = 0;
-      for (int k = 0; k < 25; k++) {
-        if (x[k & 15] < vt) {
-          if (++count > 8) { corner = true; break; }
-        } else {
-          count = 0;
+  stage_rows<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), base + g.off[l] + (r0 - 4 + kB) * g.stride[l] + 16,
+                            g.stride[l], nr + 8, nd);
+  __syncthreads();
+  // Scores of rows r0-1 .. r0+nr (0 off the FAST area).  Per row: every pixel takes the cheap
+  // necessary test (an opposite pair on each axis has a pixel beyond the threshold on the same
+  // side), the survivors are compacted into an LDS list (double-buffered: one barrier per row),
+  // and the full test runs on the list with every lane busy.
+  for (int i = threadIdx.x; i < (nr + 2) * ss; i += blockDim.x) sct[i] = 0;
+  __shared__ int lcnt[kFastBand + 2];
+  if (threadIdx.x < kFastBand + 2) lcnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int rr = 0; rr < nr + 2; rr++) {
+    const int r = r0 - 1 + rr;
+    uint16_t* list = lst + (rr & 1) * w;
+    if (r >= 3 && r < h - 3) {
+      for (int c0 = 3; c0 < w - 3; c0 += blockDim.x) {
+        const int c = c0 + (int)threadIdx.x;
+        bool cand = false;
+        if (c < w - 3) {
+          const uint8_t* p = img + (rr + 3) * ts + c + kC0;
+          const int v = p[0];
+          auto tab = [&](int x) { const int dd = x - v; return dd < -kFastT ? 1 : dd > kFastT ? 2 : 0; };
+          cand = ((tab(p[3 * ts]) | tab(p[-3 * ts])) & (tab(p[3]) | tab(p[-3]))) != 0;
         }
+        const uint64_t m = __ballot(cand);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(&lcnt[rr], __popcll(m));
+        base = __shfl(base, 0);
+        if (cand) list[base + __popcll(m & lanemask_lt())] = (uint16_t)c;
       }
     }
-    if (!corner && (d & 2)) {
-      const int vt = v + kFastT;
-      int count = 0;
-      for (int k = 0; k < 25; k++) {
-        if (x[k & 15] > vt) {
-          if (++count > 8) { corner = true; break; }
-        } else {
-          count = 0;
-        }
-      }
-    }
-    if (corner) {
-      int dd[25];
-#pragma unroll
-      for (int k = 0; k < 25; k++) dd[k] = v - x[k & 15];
-      score = corner_score(dd, kFastT);
+    __syncthreads();
+    const int n = lcnt[rr];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int c = list[i];
+      sct[rr * ss + c + 1] = (uint8_t)fast_full(img + (rr + 3) * ts + c + kC0, ts);
     }
   }
-  a.score[(size_t)s * g.pix[kL] + i] = (uint8_t)score;
+  __syncthreads();
+  uint8_t* out = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
+  for (int rr = 0; rr < nr; rr++) {
+    const int r = r0 + rr;
+    for (int c = threadIdx.x; c < w; c += blockDim.x) {
+      const uint8_t* q = sct + (rr + 1) * ss + (c + 1);
+      const int v = q[0];
+      bool keep = false;
+      if (v && r >= 3 && r < h - 3) {
+        keep = v > q[1] && v > q[-1] && v > q[-ss - 1] && v > q[-ss] && v > q[-ss + 1] && v > q[ss - 1] &&
+               v > q[ss] && v > q[ss + 1];
+        if (keep && a.mpyr && pxc(a.mpyr, g, l, r, c) == 0) keep = false;
+        if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
+      }
+      out[r * w + c] = keep ? (uint8_t)v : 0;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ selection (1 WG per scan, level)
@@ -328,11 +429,6 @@ __device__ __forceinline__ int block_rank(SelShared& sh, bool flag, int* tot) {
   __syncthreads();
   *tot = all;
   return before + inwave;
-}
-
-__device__ __forceinline__ int score_at(const uint8_t* sc, const Geom& g, int l, int r, int c) {
-  if (r < 0 || r >= g.h[l] || c < 0 || c >= g.w[l]) return 0;
-  return sc[g.pix[l] + r * g.w[l] + c];
 }
 
 __device__ __forceinline__ uint32_t ord_key(float f) {  // larger float -> larger key
@@ -388,31 +484,6 @@ __device__ uint32_t nth_largest(SelShared& sh, const float* resp, int cnt, int n
   return sh.prefix;
 }
 
-// FAST keypoints of every level pixel: score if it beats its 8 neighbours (non-max suppression
-// of FAST_t), passes the pixel mask (runByPixelsMask) and the image border (edgeThreshold 1)
-__global__ __launch_bounds__(256) void k_orb_nms(Args a) {
-  const Geom& g = a.g;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
-  if (i >= g.pix[kL]) return;
-  int l = 0;
-  while (i >= g.pix[l + 1]) l++;
-  const int j = i - g.pix[l], w = g.w[l], h = g.h[l];
-  const int r = j / w, c = j % w;
-  const uint8_t* sc = a.score + (size_t)s * g.pix[kL];
-  const int v = sc[i];
-  bool keep = false;
-  if (v && r >= 3 && r < h - 3) {
-    keep = v > score_at(sc, g, l, r, c + 1) && v > score_at(sc, g, l, r, c - 1) &&
-           v > score_at(sc, g, l, r - 1, c - 1) && v > score_at(sc, g, l, r - 1, c) &&
-           v > score_at(sc, g, l, r - 1, c + 1) && v > score_at(sc, g, l, r + 1, c - 1) &&
-           v > score_at(sc, g, l, r + 1, c) && v > score_at(sc, g, l, r + 1, c + 1);
-    if (keep && a.mpyr && pxc(a.mpyr, g, l, r, c) == 0) keep = false;
-    if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
-  }
-  a.nms[(size_t)s * g.pix[kL] + i] = keep ? (uint8_t)v : 0;
-}
-
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -450,8 +521,8 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   const int l = blockIdx.x / S, s = a.smap ? a.smap[blockIdx.x % S] : blockIdx.x % S;
   const int w = g.w[l], h = g.h[l];
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
-  const uint8_t* sc = a.score + (size_t)s * g.pix[kL] + g.pix[l];
   const uint8_t* kf = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
+  const uint8_t* sc = kf;  // a keypoint's nms value is its FAST score
   int* cand = a.cand + (size_t)s * g.pix[kL] + g.pix[l];
   float* resp = a.cresp + (size_t)s * g.pix[kL] + g.pix[l];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -933,7 +1004,7 @@ struct OrbEngine {
   uint16_t *xc = nullptr, *yc = nullptr;
   int xs = 0, ys = 0;
   uint8_t* mpyr = nullptr;
-  uint8_t *pyr = nullptr, *blur = nullptr, *score = nullptr, *nms = nullptr, *desc = nullptr;
+  uint8_t *pyr = nullptr, *blur = nullptr, *nms = nullptr, *desc = nullptr;
   int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr;
   float *cresp = nullptr, *lkp = nullptr, *kp = nullptr;
   float4* p3d = nullptr;
@@ -955,7 +1026,7 @@ struct OrbEngine {
     a.t.xo = xo; a.t.xc = xc; a.t.yo = yo; a.t.yc = yc; a.t.lim = lim; a.t.xs = xs; a.t.ys = ys;
     a.S = max_scans;
     a.img = img; a.track = track;
-    a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.score = score; a.nms = nms; a.cand = cand; a.cresp = cresp;
+    a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.nms = nms; a.cand = cand; a.cresp = cresp;
     a.lkp = lkp; a.lcnt = lcnt; a.kp = kp; a.p3d = p3d; a.desc = desc; a.nkp = nkp; a.overflow = overflow;
     a.smap = nullptr;
     return a;
@@ -980,13 +1051,19 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
     g.w[l] = cv_round((float)W * inv);
     g.h[l] = cv_round((float)H * inv);
     if (g.w[l] < 1 || g.h[l] < 1) return ofail(c, LISLAM_ERR_ARG, "image %dx%d too small for 8 ORB levels", W, H);
-    g.stride[l] = g.w[l] + 2 * kB;
+    g.stride[l] = (g.w[l] + 2 * kB + 15) & ~15;  // 16-byte aligned rows (staged as dwords)
     g.off[l] = off;
     off += g.stride[l] * (g.h[l] + 2 * kB);
     g.pix[l + 1] = g.pix[l] + g.w[l] * g.h[l];
     g.pad[l + 1] = g.pad[l] + g.stride[l] * (g.h[l] + 2 * kB);
     g.lcap[l] = 2 * g.nper[l] + 64;
     g.lofs[l + 1] = g.lofs[l] + g.lcap[l];
+  }
+  g.fband[0] = 0;
+  g.bband[0] = 0;
+  for (int l = 0; l < kL; l++) {
+    g.fband[l + 1] = g.fband[l] + (g.h[l] + kFastBand - 1) / kFastBand;
+    g.bband[l + 1] = g.bband[l] + (g.h[l] + 2 * kB + kBlurBand - 1) / kBlurBand;
   }
   g.bytes = (off + 255) & ~255;
   g.cap = g.lofs[kL];
@@ -1064,7 +1141,6 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   const size_t S = max_scans;
   ORC(e->alloc(&e->pyr, S * g.bytes));
   ORC(e->alloc(&e->blur, S * g.bytes));
-  ORC(e->alloc(&e->score, S * g.pix[kL]));
   ORC(e->alloc(&e->nms, S * g.pix[kL]));
   ORC(e->alloc(&e->cand, S * g.pix[kL]));
   ORC(e->alloc(&e->cresp, S * g.pix[kL]));
@@ -1102,7 +1178,6 @@ Args args_slot(const OrbEngine* e, const uint8_t* img, const float4* track, int 
   a.track = track ? track + s * g.W * g.H : nullptr;
   a.pyr = e->pyr + s * g.bytes;
   a.blur = e->blur + s * g.bytes;
-  a.score = e->score + s * g.pix[kL];
   a.nms = e->nms + s * g.pix[kL];
   a.cand = e->cand + s * g.pix[kL];
   a.cresp = e->cresp + s * g.pix[kL];
@@ -1136,12 +1211,16 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   }
   {
     TimedScope t(c, kT_orb_fast);
-    hipLaunchKernelGGL(k_orb_fast, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_orb_nms, dim3(cdiv(g.pix[kL], 256), n), dim3(256), 0, st, a);
+    const size_t lds = (size_t)(kFastBand + 8) * 4 * ((g.w[0] + 15) >> 2) + (size_t)(kFastBand + 2) * (g.w[0] + 2) +
+                       1 + 2 * 2 * (size_t)g.w[0];  // image, scores, two candidate lists
+    hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
-  { TimedScope t(c, kT_orb_blur); hipLaunchKernelGGL(k_orb_blur, dim3(cdiv(g.pad[kL], 256), n), dim3(256), 0, st, a); }
+  {
+    TimedScope t(c, kT_orb_blur);
+    hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
+  }
   { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
@@ -1272,6 +1351,16 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     ob->has_mask = mask != nullptr;
     ob->e1 = new OrbEngine();
     ob->e2 = new OrbEngine();
+    OCHK(c, hipStreamCreateWithFlags(&ob->side, hipStreamNonBlocking));
+    OCHK(c, hipEventCreateWithFlags(&ob->done, hipEventDisableTiming));
+    // the engines' tables and mask pyramids are uploaded / built on the side stream, where the
+    // front end that reads them runs
+    struct StreamSwap {
+      lislam_ctx* c;
+      hipStream_t keep;
+      ~StreamSwap() { c->stream = keep; }
+    } swap{c, c->stream};
+    c->stream = ob->side;
     ORC(engine_init(ob->e1, c, b->H, b->W, b->max_scans, nfeatures, mask));
     ORC(engine_init(ob->e2, c, b->H, b->W, b->max_scans, 2 * nfeatures, mask));
     ORC(ob->pb.init(c, b->max_scans, std::max(ob->e1->g.cap, ob->e2->g.cap), false));
@@ -1282,8 +1371,6 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     OCHK(c, hipMalloc(&q, (size_t)b->max_scans * 8 * 4));
     ob->allocs.push_back(q);
     ob->outS = static_cast<int*>(q);
-    OCHK(c, hipStreamCreateWithFlags(&ob->side, hipStreamNonBlocking));
-    OCHK(c, hipEventCreateWithFlags(&ob->done, hipEventDisableTiming));
   }
   *out = ob;
   return LISLAM_OK;
@@ -1359,7 +1446,7 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
     for (int g2 = 0; g2 < 2; g2++)
       for (int k : dirty[g2]) ok1[k] = hs[(size_t)(k - 1) * 8] == 1;
   }
-  std::vector<int> redet, changed;
+  std::vector<int> redet, changed, one;  // `one`: host source of async copies, alive to the final sync
   for (int k = 1; k < n_scans; k++) {
     if (cur2[k]) redet.push_back(k);
     if (cur2[k] || pset[k]) changed.push_back(k);
@@ -1369,7 +1456,7 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
     for (int k : redet) { need.push_back(k - 1); need.push_back(k); q.push_back(k); t.push_back(k - 1); sl.push_back(k - 1); }
     ORC(detect2(need));
     ORC(run_pairs(c, ob->e2, ob->e2, q.data(), t.data(), (int)redet.size(), 0.2, ob->pb, 0, true, sl.data()));
-    std::vector<int> one(redet.size(), 1);
+    one.assign(redet.size(), 1);
     for (size_t i = 0; i < redet.size(); i++)
       OCHK(c, hipMemcpyAsync(ob->pb.stats + (redet[i] - 1) * 8 + 1, &one[i], 4, hipMemcpyHostToDevice, st));
   }

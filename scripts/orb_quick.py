@@ -4,6 +4,8 @@ import os; _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys
 import numpy as np
 import __graft_entry__ as g
 pkg = g.package()
+if os.environ.get('LISLAM_ALT_LIB'):
+    pkg.native.load(os.environ['LISLAM_ALT_LIB'])  # a developer variant of the library
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 scans = np.load('/tmp/lislam_scans.r0.npy')[:S] if len(sys.argv) > 2 else pkg.synth.make_sequence(S)
 ctx = pkg.Context()
