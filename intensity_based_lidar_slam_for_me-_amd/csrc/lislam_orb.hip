@@ -894,6 +894,31 @@ __device__ void pair_eval(LmSh& sh, const double* rec, int n) {
   __syncthreads();
 }
 
+// best[] rows of the launch's pairs to the "no match" sentinel (one launch for any slot list)
+__global__ __launch_bounds__(256) void k_orb_mfill(PairArgs p, int qcap) {
+  const int pr = p.pslot ? p.pslot[blockIdx.x] : blockIdx.x;
+  int* row = p.mscratch + (size_t)pr * p.bstride;
+  for (int j = blockIdx.y * 256 + threadIdx.x; j < qcap; j += gridDim.y * 256) row[j] = kNoMatch;
+}
+
+// Batch outputs: scan 0 is the first frame (stats -1, its keypoint count), scan k > 0 pair
+// (k-1, k) with its re-detection flag.
+__global__ __launch_bounds__(256) void k_orb_out(int* outS, double* outT, const int* stats, const double* T,
+                                                 const int* redet, const int* nkp0, int n_scans) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_scans) return;
+  int* o = outS + (size_t)k * 8;
+  double* t = outT + (size_t)k * 7;
+  if (k == 0) {
+    for (int e = 0; e < 8; e++) o[e] = e == 0 ? -1 : e == 2 ? nkp0[0] : 0;
+    for (int e = 0; e < 7; e++) t[e] = e == 3 ? 1.0 : 0.0;
+    return;
+  }
+  for (int e = 0; e < 8; e++) o[e] = stats[(size_t)(k - 1) * 8 + e];
+  if (redet[k - 1]) o[1] = 1;
+  for (int e = 0; e < 7; e++) t[e] = T[(size_t)(k - 1) * 7 + e];
+}
+
 __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
   __shared__ LmSh sh;
   const int pr = p.pslot ? p.pslot[blockIdx.x] : blockIdx.x;
@@ -1231,8 +1256,8 @@ struct PairBufs {
   lislam_ctx* ctx = nullptr;
   int maxp = 0, qcap = 0;
   std::vector<void*> allocs;
-  int *qscan = nullptr, *tscan = nullptr, *pslot = nullptr, *mscratch = nullptr, *mout = nullptr, *kind = nullptr,
-      *stats = nullptr;
+  int *args = nullptr;  // [3][maxp] staged per launch: query scans, train scans, slots
+  int *mscratch = nullptr, *mout = nullptr, *kind = nullptr, *stats = nullptr, *redet = nullptr;
   double *rec = nullptr, *T = nullptr;
   ~PairBufs() {
     for (void* p : allocs) (void)hipFree(p);
@@ -1248,9 +1273,8 @@ struct PairBufs {
   }
   int init(lislam_ctx* c, int maxp_, int qcap_, bool raw) {
     ctx = c; maxp = maxp_; qcap = qcap_;
-    ORC(alloc(&qscan, maxp));
-    ORC(alloc(&tscan, maxp));
-    ORC(alloc(&pslot, maxp));
+    ORC(alloc(&args, (size_t)3 * maxp));
+    ORC(alloc(&redet, maxp));
     ORC(alloc(&mscratch, (size_t)maxp * qcap));
     if (raw) ORC(alloc(&mout, (size_t)maxp * qcap * 3));
     ORC(alloc(&kind, (size_t)maxp * qcap));
@@ -1269,14 +1293,17 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   if (n <= 0) return LISLAM_OK;
   if (qe->g.cap > pb.qcap || (!slots && p0 + n > pb.maxp) || n > pb.maxp)
     return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
-  const int a0 = slots ? 0 : p0;  // argument arrays: where the scan / slot lists are staged
-  OCHK(c, hipMemcpyAsync(pb.qscan + a0, qs, n * 4, hipMemcpyHostToDevice, st));
-  OCHK(c, hipMemcpyAsync(pb.tscan + a0, ts, n * 4, hipMemcpyHostToDevice, st));
-  if (slots) OCHK(c, hipMemcpyAsync(pb.pslot, slots, n * 4, hipMemcpyHostToDevice, st));
+  // one upload of the launch's lists: query scans | train scans | slots (stream-ordered after
+  // the previous launch's kernels, which read the same staging area)
+  std::vector<int> host((size_t)3 * n);
+  std::copy(qs, qs + n, host.begin());
+  std::copy(ts, ts + n, host.begin() + n);
+  if (slots) std::copy(slots, slots + n, host.begin() + 2 * n);
+  OCHK(c, hipMemcpyAsync(pb.args, host.data(), (size_t)(slots ? 3 : 2) * n * 4, hipMemcpyHostToDevice, st));
   PairArgs p;
   p.npairs = n;
-  p.pslot = slots ? pb.pslot : nullptr;
-  p.qscan = pb.qscan + a0; p.tscan = pb.tscan + a0;
+  p.pslot = slots ? pb.args + 2 * n : nullptr;
+  p.qscan = pb.args; p.tscan = pb.args + n;
   p.qdesc = qe->desc; p.tdesc = te->desc;
   p.qp3d = qe->p3d; p.tp3d = te->p3d;
   p.qn = qe->nkp; p.tn = te->nkp;
@@ -1292,11 +1319,7 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   p.T = pb.T + b0 * 7;
   {
     TimedScope t(c, kT_orb_match);
-    if (slots) {
-      for (int i = 0; i < n; i++) OCHK(c, hipMemsetAsync(p.mscratch + (size_t)slots[i] * pb.qcap, 0x7f, (size_t)pb.qcap * 4, st));
-    } else {
-      OCHK(c, hipMemsetAsync(p.mscratch, 0x7f, (size_t)n * pb.qcap * 4, st));
-    }
+    hipLaunchKernelGGL(k_orb_mfill, dim3(n, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
     hipLaunchKernelGGL(k_orb_xdist, dim3(n, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
     hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p);
   }
@@ -1395,18 +1418,6 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
   std::vector<int> hs((size_t)std::max(np, 1) * 8);
   if (np > 0) OCHK(c, hipMemcpyAsync(hs.data(), ob->pb.stats, (size_t)np * 8 * 4, hipMemcpyDeviceToHost, st));
   OCHK(c, hipStreamSynchronize(st));
-  // outputs: scan 0 = first frame; scan k = pair (k-1, k)
-  {
-    std::vector<int> s0 = {-1, 0, 0, 0, 0, 0, 0, 0};
-    const double I[7] = {0, 0, 0, 1, 0, 0, 0};
-    OCHK(c, hipMemcpyAsync(ob->outS, s0.data(), 32, hipMemcpyHostToDevice, st));
-    OCHK(c, hipMemcpyAsync(ob->outT, I, 56, hipMemcpyHostToDevice, st));
-    OCHK(c, hipMemcpyAsync(ob->outS + 2, ob->e1->nkp, 4, hipMemcpyDeviceToDevice, st));
-    if (np > 0) {
-      OCHK(c, hipMemcpyAsync(ob->outS + 8, ob->pb.stats, (size_t)np * 32, hipMemcpyDeviceToDevice, st));
-      OCHK(c, hipMemcpyAsync(ob->outT + 7, ob->pb.T, (size_t)np * 56, hipMemcpyDeviceToDevice, st));
-    }
-  }
   // The sequential rule of detectfeatures: pair k re-detects both frames (2 * nfeatures, 20 %)
   // when its first attempt fails, and frame k then keeps the 2n set, against which pair k+1's
   // first attempt is made.  Resolved as a fixed point in batched rounds: cur2[k] follows from the
@@ -1440,30 +1451,26 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
       std::vector<int> q, t, sl;
       for (int k : d) { q.push_back(k); t.push_back(k - 1); sl.push_back(k - 1); pset[k] = g2; }
       ORC(run_pairs(c, ob->e1, g2 ? ob->e2 : ob->e1, q.data(), t.data(), (int)d.size(), 0.3, ob->pb, 0, true, sl.data()));
-      for (int k : d) OCHK(c, hipMemcpyAsync(&hs[(size_t)(k - 1) * 8], ob->pb.stats + (k - 1) * 8, 32, hipMemcpyDeviceToHost, st));
     }
+    OCHK(c, hipMemcpyAsync(hs.data(), ob->pb.stats, (size_t)np * 8 * 4, hipMemcpyDeviceToHost, st));
     OCHK(c, hipStreamSynchronize(st));
     for (int g2 = 0; g2 < 2; g2++)
       for (int k : dirty[g2]) ok1[k] = hs[(size_t)(k - 1) * 8] == 1;
   }
-  std::vector<int> redet, changed, one;  // `one`: host source of async copies, alive to the final sync
-  for (int k = 1; k < n_scans; k++) {
-    if (cur2[k]) redet.push_back(k);
-    if (cur2[k] || pset[k]) changed.push_back(k);
-  }
+  std::vector<int> redet, flag(std::max(np, 1), 0);
+  for (int k = 1; k < n_scans; k++)
+    if (cur2[k]) { redet.push_back(k); flag[k - 1] = 1; }
   if (!redet.empty()) {
     std::vector<int> need, q, t, sl;
     for (int k : redet) { need.push_back(k - 1); need.push_back(k); q.push_back(k); t.push_back(k - 1); sl.push_back(k - 1); }
     ORC(detect2(need));
     ORC(run_pairs(c, ob->e2, ob->e2, q.data(), t.data(), (int)redet.size(), 0.2, ob->pb, 0, true, sl.data()));
-    one.assign(redet.size(), 1);
-    for (size_t i = 0; i < redet.size(); i++)
-      OCHK(c, hipMemcpyAsync(ob->pb.stats + (redet[i] - 1) * 8 + 1, &one[i], 4, hipMemcpyHostToDevice, st));
   }
-  for (int k : changed) {
-    OCHK(c, hipMemcpyAsync(ob->outS + (size_t)k * 8, ob->pb.stats + (k - 1) * 8, 32, hipMemcpyDeviceToDevice, st));
-    OCHK(c, hipMemcpyAsync(ob->outT + (size_t)k * 7, ob->pb.T + (k - 1) * 7, 56, hipMemcpyDeviceToDevice, st));
-  }
+  // outputs: scan 0 = first frame; scan k = pair (k-1, k), whose final attempt sits in slot k-1
+  OCHK(c, hipMemcpyAsync(ob->pb.redet, flag.data(), (size_t)std::max(np, 1) * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_orb_out, dim3(cdiv(n_scans, 256)), dim3(256), 0, st, ob->outS, ob->outT, ob->pb.stats, ob->pb.T,
+                     ob->pb.redet, ob->e1->nkp, n_scans);
+  OCHK(c, hipGetLastError());
   OCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
 }
