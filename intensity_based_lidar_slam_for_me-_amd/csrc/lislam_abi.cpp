@@ -160,6 +160,10 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &f.stg_flat, (size_t)S * H * kCapFlatPerLine);
   rc |= dalloc(b, &f.stg_less_flat, SN);
   rc |= dalloc(b, &f.line_counts, (size_t)S * H * 4);
+  f.fr_R = (N + 1023) / 1024;
+  rc |= dalloc(b, &f.fr_hist, (size_t)S * f.fr_R * H);
+  rc |= dalloc(b, &f.fr_flip, (size_t)S * f.fr_R);
+  rc |= dalloc(b, &f.fr_ori, (size_t)S * 2);
   rc |= dalloc(b, &f.scr_picked, SN);
   rc |= dalloc(b, &f.scr_keys, 2 * SN);
   rc |= dalloc(b, &f.scr_list, SN);
@@ -316,7 +320,7 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
     return ms;
   };
   for (auto& v : b->ext_ev) {
-    for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += i == 3 ? 2 : 1; }  // k_target_index: 2 launches
+    for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += i == 3 ? 2 : i == 0 ? 3 : 1; }  // front: 3 launches, k_target_index: 2
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   for (auto& v : b->odo_ev) {

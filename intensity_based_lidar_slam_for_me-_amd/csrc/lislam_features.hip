@@ -1,16 +1,18 @@
 // lislam feature front end on gfx950: ImageHandler::cloud_handler + scanRegistration's
 // laserCloudHandler (a1..a7 of SURVEY.md §8(a)) for a batch of S organized scans resident in HBM.
 //
-//   k_scan_front   one 1024-thread workgroup per scan.  Streams the ring-ordered xyzI buffer
-//                  twice with 16-B coalesced loads:
-//                    pass 1: range/intensity images + cloud_track (image_handler.h_ouster:112-139),
-//                            close-point filter (scanRegistration.cpp:152-186), scan line
-//                            histogram (:285-331) and the index where halfPassed flips
-//                            (:336-353) as an LDS atomicMin — the only sequential state of the
-//                            loop is a monotone flag, so it reduces to "first index where".
-//                    pass 2: ori/relTime/intensity (:334-371) and a stable counting sort by
-//                            scanID (= the per-line push_back + concatenation, :373-394) using
-//                            64-lane ballot peer masks for in-wave ranks.
+//   k_front_count / k_front_scan / k_front_scatter ("k_scan_front" in the timers): one wave per
+//                  1024-point range streams the ring-ordered xyzI buffer with 16-B coalesced
+//                  loads, twice:
+//                    count:   range/intensity images + cloud_track (image_handler.h_ouster:112-139),
+//                             close-point filter (scanRegistration.cpp:152-186), per-range scan
+//                             line histogram (:285-331) and the first index where halfPassed flips
+//                             (:336-353) — the loop's only sequential state is a monotone flag, so
+//                             it reduces to "first index where";
+//                    scan:    per scan, line offsets, per-range write bases, the scan's flip index;
+//                    scatter: ori/relTime/intensity (:334-371) and the stable counting sort by
+//                             scanID (= the per-line push_back + concatenation, :373-394) using
+//                             64-lane ballot peer masks for in-wave ranks.
 //   k_scan_lines   one wave per (scan, line): curvature (:397-412), per-segment bitonic sort of
 //                  (curvature, index) keys in LDS (:445), the sharp / flat greedy walks with
 //                  ±5 neighbour suppression as ballot scans (:450-568), the less-flat collection
@@ -23,19 +25,11 @@
 
 namespace lislam {
 
-// ------------------------------------------------------------------------------- pass kernel
-constexpr int kFrontThreads = 1024;
-constexpr int kFrontWaves = kFrontThreads / 64;
-
-struct FrontShared {
-  int cnt[kMaxLines];
-  int base[kMaxLines];
-  int wcnt[kFrontWaves][kMaxLines];
-  int wpre[kFrontWaves][kMaxLines];
-  int first, last, flip;
-  float startOri, endOri;
-  int tmp;
-};
+// ------------------------------------------------------------------------------- front kernels
+// The scan is cut into ranges of kRange consecutive ring-order points, one wavefront per range
+// (4 per workgroup, S x ceil(R/4) workgroups: ~4.8k for a 300-scan batch, so every CU streams).
+constexpr int kRange = 1024;
+constexpr int kFrontWaves = 4;
 
 __device__ __forceinline__ bool keep_point(const P4& p, float thr2) {
   return !(p.x * p.x + p.y * p.y + p.z * p.z < thr2);
@@ -59,97 +53,159 @@ __device__ __forceinline__ float ori_passed(float ori, float endOri) {
   return ori;
 }
 
-__global__ __launch_bounds__(kFrontThreads) void k_scan_front(FeatureArgs a) {
-  __shared__ FrontShared sh;
-  const int s = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+// startOri / endOri of the scan from its first and last kept points (scanRegistration.cpp:247-262).
+// Every wave finds them itself (one or two cached 1 KiB reads in practice), so the count pass
+// needs no cross-wave step.
+__device__ __forceinline__ bool scan_oris(const P4* pts, int N, float thr2, float& so, float& eo) {
+  const int lane = lane_id();
+  int first = -1, last = -1;
+  for (int b = 0; b < N && first < 0; b += 64) {
+    const int i = b + lane;
+    const uint64_t m = __ballot(i < N && keep_point(ld4(pts + i), thr2));
+    if (m) first = b + (int)__builtin_ctzll(m);
+  }
+  if (first < 0) return false;
+  for (int b = N - 1; b >= 0 && last < 0; b -= 64) {
+    const int i = b - lane;
+    const uint64_t m = __ballot(i >= 0 && keep_point(ld4(pts + i), thr2));
+    if (m) last = b - (int)__builtin_ctzll(m);
+  }
+  const P4 p0 = ld4(pts + first), p1 = ld4(pts + last);
+  so = -atan2_f(p0.y, p0.x);
+  eo = (float)((double)(-atan2_f(p1.y, p1.x)) + 2 * kPi);
+  if ((double)(eo - so) > 3 * kPi)
+    eo = (float)((double)eo - 2 * kPi);
+  else if ((double)(eo - so) < kPi)
+    eo = (float)((double)eo + 2 * kPi);
+  return true;
+}
+
+// Lanes holding the same scan line as this lane (7 ballots over the bits of sid < 128).
+__device__ __forceinline__ uint64_t line_peers(int sid) {
+  uint64_t peers = __ballot(sid >= 0);
+  for (int bit = 0; bit < 7; bit++) {
+    const uint64_t m = __ballot((sid >> bit) & 1);
+    peers &= ((sid >> bit) & 1) ? m : ~m;
+  }
+  return peers;
+}
+
+// Pass 1 (one wave per range): range / intensity images + cloud_track (image_handler.h_ouster:
+// 112-139), the close-point filter (scanRegistration.cpp:152-186), the per-range scan-line
+// histogram (:285-331) and the first index of the range where halfPassed would flip (:336-353):
+// the loop's only sequential state is a monotone flag, so it reduces to "first index where".
+__global__ __launch_bounds__(64 * kFrontWaves) void k_front_count(FeatureArgs a) {
+  __shared__ int hist[kFrontWaves][kMaxLines];
+  const int RB = (a.fr_R + kFrontWaves - 1) / kFrontWaves;
+  const int s = blockIdx.x / RB, wave = threadIdx.x >> 6, lane = lane_id();
+  const int r = (blockIdx.x % RB) * kFrontWaves + wave;
+  if (r >= a.fr_R) return;
   const int N = a.N, H = a.H;
   const P4* pts = a.pts + (size_t)s * N;
-  const float thr = a.min_range;
-  const float thr2 = thr * thr;
-
-  if (tid == 0) { sh.first = N; sh.last = -1; sh.flip = N; }
-  for (int l = tid; l < H; l += kFrontThreads) sh.cnt[l] = 0;
-  __syncthreads();
-  // ---- first / last kept point -> startOri / endOri (scanRegistration.cpp:247-262)
-  for (int b = 0; b < N; b += kFrontThreads) {
-    const int i = b + tid;
-    if (i < N && keep_point(ld4(pts + i), thr2)) atomicMin(&sh.first, i);
-    __syncthreads();
-    const int f = sh.first;
-    __syncthreads();
-    if (f < N) break;
+  const float thr2 = a.min_range * a.min_range;
+  int* h = hist[wave];
+  for (int l = lane; l < H; l += 64) h[l] = 0;
+  float startOri = 0.f, endOri = 0.f;
+  const bool any = scan_oris(pts, N, thr2, startOri, endOri);
+  if (r == 0 && lane == 0) {
+    a.fr_ori[2 * s] = startOri;
+    a.fr_ori[2 * s + 1] = endOri;
   }
-  for (int b = N - 1; b >= 0; b -= kFrontThreads) {
-    const int i = b - tid;
-    if (i >= 0 && keep_point(ld4(pts + i), thr2)) atomicMax(&sh.last, i);
-    __syncthreads();
-    const int l = sh.last;
-    __syncthreads();
-    if (l >= 0) break;
-  }
-  if (tid == 0 && sh.first < N) {
-    const P4 p0 = ld4(pts + sh.first), p1 = ld4(pts + sh.last);
-    const float so = -atan2_f(p0.y, p0.x);
-    float eo = (float)((double)(-atan2_f(p1.y, p1.x)) + 2 * kPi);
-    if ((double)(eo - so) > 3 * kPi)
-      eo = (float)((double)eo - 2 * kPi);
-    else if ((double)(eo - so) < kPi)
-      eo = (float)((double)eo + 2 * kPi);
-    sh.startOri = so;
-    sh.endOri = eo;
-  }
-  __syncthreads();
-  const bool any = sh.first < N;
-  const float startOri = sh.startOri, endOri = sh.endOri;
-
-  // ---- pass 1: images, filter, line histogram, halfPassed flip index
   uint8_t* img_r = a.img_range ? a.img_range + (size_t)s * N : nullptr;
   uint8_t* img_i = a.img_int ? a.img_int + (size_t)s * N : nullptr;
   P4* track = a.track ? a.track + (size_t)s * N : nullptr;
-  for (int b = 0; b < N; b += kFrontThreads) {
-    const int i = b + tid;
-    if (i >= N) break;
-    const P4 p = ld4(pts + i);
-    const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
-    const float range = sqrtf(d2);
-    const float inten = fminf(p.i, 255.0f);
-    if (img_r) img_r[i] = (uint8_t)fminf(range * 20, 255.0f);
-    if (img_i) img_i[i] = (uint8_t)inten;
-    if (track) st4(track + i, (double)range >= 0.1 ? P4{p.x, p.y, p.z, inten} : P4{0.f, 0.f, 0.f, 0.f});
-    if (!(d2 < thr2) && any) {
-      const int sid = scan_id_of(elevation_deg(p), H);
-      if (sid >= 0) {
-        atomicAdd(&sh.cnt[sid], 1);
-        const float ori = ori_not_passed(-atan2_f(p.y, p.x), startOri);
-        if ((double)(ori - startOri) > kPi) atomicMin(&sh.flip, i);
+  int flip = N;
+  const int i0 = r * kRange, i1 = min(N, i0 + kRange);
+  for (int b = i0; b < i1; b += 64) {
+    const int i = b + lane;
+    int sid = -1;
+    if (i < i1) {
+      const P4 p = ld4(pts + i);
+      const float d2 = p.x * p.x + p.y * p.y + p.z * p.z;
+      const float range = sqrtf(d2);
+      const float inten = fminf(p.i, 255.0f);
+      if (img_r) img_r[i] = (uint8_t)fminf(range * 20, 255.0f);
+      if (img_i) img_i[i] = (uint8_t)inten;
+      if (track) st4(track + i, (double)range >= 0.1 ? P4{p.x, p.y, p.z, inten} : P4{0.f, 0.f, 0.f, 0.f});
+      if (!(d2 < thr2) && any) {
+        sid = scan_id_of(elevation_deg(p), H);
+        if (sid >= 0 && flip == N) {
+          const float ori = ori_not_passed(-atan2_f(p.y, p.x), startOri);
+          if ((double)(ori - startOri) > kPi) flip = i;
+        }
       }
     }
+    const uint64_t peers = line_peers(sid);
+    if (sid >= 0 && __popcll(peers & lanemask_lt()) == 0) h[sid] += __popcll(peers);  // one leader per line
+    __builtin_amdgcn_wave_barrier();
   }
+  flip = (int)wave_umin((uint32_t)flip);
+  int* dst = a.fr_hist + ((size_t)s * a.fr_R + r) * H;
+  for (int l = lane; l < H; l += 64) dst[l] = h[l];
+  if (lane == 0) a.fr_flip[(size_t)s * a.fr_R + r] = flip;
+}
+
+// Per scan: line totals -> line offsets (scanStartInd = off + 5, scanEndInd = off + len - 6,
+// :384-394), each range's per-line write base (in place of its histogram), and the scan's flip
+// index (minimum over the ranges).
+__global__ __launch_bounds__(kMaxLines) void k_front_scan(FeatureArgs a) {
+  __shared__ int tot[kMaxLines];
+  __shared__ uint32_t wflip[kMaxLines / 64];
+  const int s = blockIdx.x, l = threadIdx.x, H = a.H, R = a.fr_R;
+  int* hist = a.fr_hist + (size_t)s * R * H;
+  int t = 0;
+  if (l < H)
+    for (int r = 0; r < R; r++) t += hist[(size_t)r * H + l];
+  tot[l] = t;
+  uint32_t f = 0xffffffffu;
+  for (int r = l; r < R; r += kMaxLines) f = min(f, (uint32_t)a.fr_flip[(size_t)s * R + r]);
+  f = wave_umin(f);
+  if (lane_id() == 0) wflip[l >> 6] = f;
   __syncthreads();
-  // ---- line offsets (scanStartInd = off + 5, scanEndInd = off + len - 6)
-  if (tid == 0) {
-    int acc = 0;
-    for (int l = 0; l < H; l++) {
-      sh.base[l] = acc;
-      a.line_off[(size_t)s * (H + 1) + l] = acc;
-      acc += sh.cnt[l];
+  if (l < H) {
+    int off = 0;
+    for (int k = 0; k < l; k++) off += tot[k];
+    a.line_off[(size_t)s * (H + 1) + l] = off;
+    if (l == H - 1) {
+      a.line_off[(size_t)s * (H + 1) + H] = off + t;
+      a.n_cloud[s] = off + t;
     }
-    a.line_off[(size_t)s * (H + 1) + H] = acc;
-    a.n_cloud[s] = acc;
+    for (int r = 0; r < R; r++) {
+      const int c = hist[(size_t)r * H + l];
+      hist[(size_t)r * H + l] = off;
+      off += c;
+    }
   }
-  __syncthreads();
-  if (!any) return;
-  const int flip = sh.flip;
+  if (l == 0) a.fr_flip[(size_t)s * R] = (int)min(wflip[0], wflip[1]);  // range 0 slot = scan flip
+}
+
+// Pass 2 (one wave per range): ori / relTime / intensity = scanID + 0.1 relTime (:334-371) and the
+// stable scatter by scan line (= the per-line push_back + concatenation, :373-394): in-wave ranks
+// from ballot peer masks, the running per-line base of the range in LDS.
+__global__ __launch_bounds__(64 * kFrontWaves) void k_front_scatter(FeatureArgs a) {
+  __shared__ int base[kFrontWaves][kMaxLines];
+  const int RB = (a.fr_R + kFrontWaves - 1) / kFrontWaves;
+  const int s = blockIdx.x / RB, wave = threadIdx.x >> 6, lane = lane_id();
+  const int r = (blockIdx.x % RB) * kFrontWaves + wave;
+  if (r >= a.fr_R) return;
+  const int N = a.N, H = a.H;
+  if (a.n_cloud[s] == 0) return;
+  const P4* pts = a.pts + (size_t)s * N;
+  const float thr2 = a.min_range * a.min_range;
+  int* bs = base[wave];
+  const int* src = a.fr_hist + ((size_t)s * a.fr_R + r) * H;
+  for (int l = lane; l < H; l += 64) bs[l] = src[l];
+  const float startOri = a.fr_ori[2 * s], endOri = a.fr_ori[2 * s + 1];
+  const int flip = a.fr_flip[(size_t)s * a.fr_R];
   P4* cloud = a.cloud + (size_t)s * N;
-  // ---- pass 2: relTime / intensity + stable scatter by scanID
   const uint64_t lt = lanemask_lt();
-  for (int b = 0; b < N; b += kFrontThreads) {
-    const int i = b + tid;
+  __builtin_amdgcn_wave_barrier();
+  const int i0 = r * kRange, i1 = min(N, i0 + kRange);
+  for (int b = i0; b < i1; b += 64) {
+    const int i = b + lane;
     P4 p{0.f, 0.f, 0.f, 0.f};
     int sid = -1;
-    if (i < N) {
+    if (i < i1) {
       p = ld4(pts + i);
       if (keep_point(p, thr2)) sid = scan_id_of(elevation_deg(p), H);
     }
@@ -159,33 +215,14 @@ __global__ __launch_bounds__(kFrontThreads) void k_scan_front(FeatureArgs a) {
       const float relTime = (ori - startOri) / (endOri - startOri);
       p.i = (float)((double)sid + 0.1 * (double)relTime);
     }
-    // peer mask of lanes with the same scan line
-    const uint64_t valid = __ballot(sid >= 0);
-    uint64_t peers = valid;
-    for (int bit = 0; bit < 7; bit++) {
-      const uint64_t m = __ballot((sid >> bit) & 1);
-      peers &= ((sid >> bit) & 1) ? m : ~m;
-    }
-    for (int l = tid; l < kFrontWaves * H; l += kFrontThreads) sh.wcnt[l / H][l % H] = 0;
-    __syncthreads();
-    int rank = 0;
+    const uint64_t peers = line_peers(sid);
     if (sid >= 0) {
-      rank = __popcll(peers & lt);
-      if (rank == 0) sh.wcnt[wave][sid] = __popcll(peers);
+      const int rank = __popcll(peers & lt);
+      st4(cloud + bs[sid] + rank, p);
+      __builtin_amdgcn_wave_barrier();
+      if (rank == 0) bs[sid] += __popcll(peers);
     }
-    __syncthreads();
-    for (int e = tid; e < kFrontWaves * H; e += kFrontThreads) {
-      const int w = e / H, l = e % H;
-      int acc = 0;
-      for (int k = 0; k < w; k++) acc += sh.wcnt[k][l];
-      sh.wpre[w][l] = acc;
-    }
-    __syncthreads();
-    if (sid >= 0) st4(cloud + sh.base[sid] + sh.wpre[wave][sid] + rank, p);
-    __syncthreads();
-    for (int l = tid; l < H; l += kFrontThreads)
-      sh.base[l] += sh.wpre[kFrontWaves - 1][l] + sh.wcnt[kFrontWaves - 1][l];
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1006,9 +1043,12 @@ __global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEvent_t images_ready) {
   // ev (nullable): 4 events bracketing k_scan_front, k_scan_lines, k_scan_compact
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(k_scan_front, dim3(a.S), dim3(kFrontThreads), 0, st, a);
-  if (ev) (void)hipEventRecord(ev[1], st);
+  const int fb = a.S * ((a.fr_R + kFrontWaves - 1) / kFrontWaves);
+  hipLaunchKernelGGL(k_front_count, dim3(fb), dim3(64 * kFrontWaves), 0, st, a);
   if (images_ready) (void)hipEventRecord(images_ready, st);  // the a1 images are complete here
+  hipLaunchKernelGGL(k_front_scan, dim3(a.S), dim3(kMaxLines), 0, st, a);
+  hipLaunchKernelGGL(k_front_scatter, dim3(fb), dim3(64 * kFrontWaves), 0, st, a);
+  if (ev) (void)hipEventRecord(ev[1], st);
   if (a.W <= 512)
     hipLaunchKernelGGL(k_scan_lines<8>, dim3(a.S * a.H), dim3(64), 0, st, a);
   else if (a.W <= 1024)

@@ -35,6 +35,11 @@ struct FeatureArgs {
   P4* stg_flat;        // [S][H][24]
   P4* stg_less_flat;   // [S][N] (line regions at line_off)
   int* line_counts;    // [S][H][4]
+  // front pass scratch: ranges of 1024 ring-order points
+  int fr_R;            // ranges per scan = ceil(N / 1024)
+  int* fr_hist;        // [S][R][H] per-range line histogram, then per-range write bases
+  int* fr_flip;        // [S][R] first halfPassed flip index of each range; [s][0] = the scan's
+  float* fr_ori;       // [S][2] startOri, endOri
   // scratch for lines longer than the LDS fast path
   uint8_t* scr_picked;  // [S][N]
   uint64_t* scr_keys;   // [S][2N]
