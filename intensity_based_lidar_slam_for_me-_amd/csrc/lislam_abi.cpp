@@ -219,7 +219,12 @@ int lislam_batch_destroy(lislam_batch* b) {
   hipStreamSynchronize(b->ctx->stream);
   for (void* p : b->allocs) hipFree(p);
   for (auto& v : b->ext_ev) for (hipEvent_t e : v) hipEventDestroy(e);
-  for (auto& v : b->odo_ev) for (hipEvent_t e : v) hipEventDestroy(e);
+  for (auto& v : b->odo_ev) for (auto& t : v) { hipEventDestroy(t.b); hipEventDestroy(t.e); }
+  for (int g = 1; g < lislam_batch::kMaxGroups; g++) {
+    if (b->odo_stream[g]) hipStreamDestroy(b->odo_stream[g]);
+    if (b->odo_join[g]) hipEventDestroy(b->odo_join[g]);
+  }
+  if (b->odo_fork) hipEventDestroy(b->odo_fork);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
   if (b->ev_images) hipEventDestroy(b->ev_images);
@@ -290,12 +295,24 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
     o.init_state = b->d_init;
   }
-  std::vector<hipEvent_t>* ev = nullptr;
+  // chain groups: LISLAM_ODOM_GROUPS (default 2) streams, so one group's solves overlap another's
+  // association (a solve occupies one workgroup per chain, far from filling the device)
+  static const int groups_env = getenv("LISLAM_ODOM_GROUPS") ? atoi(getenv("LISLAM_ODOM_GROUPS")) : 2;
+  const int G = std::max(1, std::min(groups_env, (int)lislam_batch::kMaxGroups));
+  b->odo_stream[0] = c->stream;
+  for (int g = 1; g < G; g++) {
+    if (!b->odo_stream[g]) HIPCHK(c, hipStreamCreateWithFlags(&b->odo_stream[g], hipStreamNonBlocking));
+    if (!b->odo_join[g]) HIPCHK(c, hipEventCreateWithFlags(&b->odo_join[g], hipEventDisableTiming));
+  }
+  if (G > 1 && !b->odo_fork) HIPCHK(c, hipEventCreateWithFlags(&b->odo_fork, hipEventDisableTiming));
+  std::vector<lislam::OdoTimed>* ev = nullptr;
   if (b->timing) {
     b->odo_ev.emplace_back();
     ev = &b->odo_ev.back();
   }
-  launch_odometry(o, c->stream, ev, &lislam_batch::event_cb, b);
+  o.c0 = 0;
+  o.cn = o.n_chains;
+  launch_odometry(o, b->odo_stream, G, b->odo_fork, b->odo_join, ev, &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -324,14 +341,12 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   for (auto& v : b->odo_ev) {
-    // [start, after init, then after every assoc / lm launch]
-    if (v.size() >= 2) { acc[5] += el(v[0], v[1]); launches[5] += 1; }
-    for (size_t i = 1; i + 1 < v.size(); i++) {
-      const int k = (i % 2 == 1) ? 4 : 5;  // odd gaps: k_odom_assoc, even gaps: k_odom_lm
-      acc[k] += el(v[i], v[i + 1]);
-      launches[k] += 1;
+    for (auto& t : v) {  // every launch bracketed on its own stream
+      acc[t.kernel] += el(t.b, t.e);
+      launches[t.kernel] += 1;
+      b->pool.push_back(t.b);
+      b->pool.push_back(t.e);
     }
-    for (hipEvent_t e : v) b->pool.push_back(e);
   }
   const int ne = (int)b->ext_ev.size(), no = (int)b->odo_ev.size();
   for (int k = 0; k < LISLAM_NUM_KERNELS; k++) {

@@ -22,7 +22,13 @@ struct lislam_batch {
   bool timing = false;
   // per-call event sets recorded on the stream while timing is on; read back (and released)
   // by lislam_batch_kernel_times, so the timed region never blocks on the host.
-  std::vector<std::vector<hipEvent_t>> ext_ev, odo_ev;
+  std::vector<std::vector<hipEvent_t>> ext_ev;
+  std::vector<std::vector<lislam::OdoTimed>> odo_ev;
+  // chain groups of the odometry schedule: group 0 on the context stream, the others on their own
+  // streams (created on first use), forked / joined by events
+  static constexpr int kMaxGroups = 4;
+  hipStream_t odo_stream[kMaxGroups] = {};
+  hipEvent_t odo_fork = nullptr, odo_join[kMaxGroups] = {};
   std::vector<hipEvent_t> pool;
   int extracted = 0;
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits

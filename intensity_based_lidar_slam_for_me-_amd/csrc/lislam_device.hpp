@@ -122,6 +122,72 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { return ~wave_min_u64(~v); }
 
+// ---------------------------------------------------------------- register bitonic sort
+// Keys of one wave in registers: index i = base + 64 t + lane (slot t < kS, base = the wave's
+// offset in a workgroup-wide sort, a multiple of 64 kS).  One stage of the bitonic network
+// compare-exchanges i with i ^ j in direction ((i & k) == 0).
+template <int kS, int kJJ>  // partner i ^ (64 kJJ): slot t ^ kJJ of the same lane
+__device__ __forceinline__ void bx_slots(uint64_t (&key)[kS], int k, int base) {
+  if constexpr (kJJ < kS) {
+#pragma unroll
+    for (int t = 0; t < kS; t++) {
+      if (t & kJJ) continue;
+      const int u = t | kJJ;
+      const bool up = ((base | (t * 64)) & k) == 0;
+      const uint64_t x = key[t], y = key[u];
+      const bool sw = (x > y) == up;
+      key[t] = sw ? y : x;
+      key[u] = sw ? x : y;
+    }
+  }
+}
+template <int kJ>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+  if constexpr (kJ == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+  else if constexpr (kJ == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true);  // [2,3,0,1]
+  else if constexpr (kJ < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (kJ << 10) | 0x1f);  // xor mask
+  else return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ 32) << 2, (int)v);
+}
+template <int kS, int kJ>  // partner i ^ kJ: lane ^ kJ, same slot
+__device__ __forceinline__ void bx_lanes(uint64_t (&key)[kS], int k, int base) {
+  const int lane = lane_id();
+  const bool lower = (lane & kJ) == 0;
+#pragma unroll
+  for (int t = 0; t < kS; t++) {
+    const uint64_t x = key[t];
+    const uint64_t y = ((uint64_t)xor_lane32<kJ>((uint32_t)(x >> 32)) << 32) | xor_lane32<kJ>((uint32_t)x);
+    const bool up = ((base | (t * 64) | lane) & k) == 0;
+    key[t] = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
+    if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // four slots' exchanges in flight (registers)
+  }
+}
+// Every stage j < 64 kS of level k (the in-wave part of the network).
+template <int kS>
+__device__ __forceinline__ void reg_bitonic_level(uint64_t (&key)[kS], int k, int jmax, int base) {
+  for (int j = jmax; j > 0; j >>= 1) {
+    switch (j) {
+      case 1: bx_lanes<kS, 1>(key, k, base); break;
+      case 2: bx_lanes<kS, 2>(key, k, base); break;
+      case 4: bx_lanes<kS, 4>(key, k, base); break;
+      case 8: bx_lanes<kS, 8>(key, k, base); break;
+      case 16: bx_lanes<kS, 16>(key, k, base); break;
+      case 32: bx_lanes<kS, 32>(key, k, base); break;
+      case 64: bx_slots<kS, 1>(key, k, base); break;
+      case 128: bx_slots<kS, 2>(key, k, base); break;
+      case 256: bx_slots<kS, 4>(key, k, base); break;
+      case 512: bx_slots<kS, 8>(key, k, base); break;
+      default: bx_slots<kS, 16>(key, k, base); break;
+    }
+  }
+}
+// Ascending bitonic sort of the 64 kS keys of one wave (every slot: a runtime slot bound doubled
+// the registers the exchanges hold).
+template <int kS>
+__device__ __forceinline__ void reg_bitonic(uint64_t (&key)[kS]) {
+  constexpr int P = 64 * kS;
+  for (int k = 2; k <= P; k <<= 1) reg_bitonic_level<kS>(key, k, k >> 1, 0);
+}
+
 // ---------------------------------------------------------------- double 3-vectors / quats
 struct D3 {
   double x, y, z;

@@ -613,66 +613,6 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
 // link masks (uniform, for the suppression), the pick lists and a 64-point centroid window live
 // in LDS (about 2 KiB), so occupancy is set by registers, not by a line-sized LDS footprint.
 
-// Compare-exchange of one bitonic stage of the register layout i = 64 t + lane.
-template <int kS, int kJJ>  // partner i ^ (64 kJJ): slot t ^ kJJ of the same lane
-__device__ __forceinline__ void bx_slots(uint64_t (&key)[kS], int k) {
-  if constexpr (kJJ < kS) {
-#pragma unroll
-    for (int t = 0; t < kS; t++) {
-      if (t & kJJ) continue;
-      const int u = t | kJJ;
-      const bool up = ((t * 64) & k) == 0;
-      const uint64_t x = key[t], y = key[u];
-      const bool sw = (x > y) == up;
-      key[t] = sw ? y : x;
-      key[u] = sw ? x : y;
-    }
-  }
-}
-template <int kJ>
-__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
-  if constexpr (kJ == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
-  else if constexpr (kJ == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true);  // [2,3,0,1]
-  else if constexpr (kJ < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (kJ << 10) | 0x1f);  // xor mask
-  else return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ 32) << 2, (int)v);
-}
-template <int kS, int kJ>  // partner i ^ kJ: lane ^ kJ, same slot
-__device__ __forceinline__ void bx_lanes(uint64_t (&key)[kS], int k) {
-  const int lane = lane_id();
-  const bool lower = (lane & kJ) == 0;
-#pragma unroll
-  for (int t = 0; t < kS; t++) {
-    const uint64_t x = key[t];
-    const uint64_t y = ((uint64_t)xor_lane32<kJ>((uint32_t)(x >> 32)) << 32) | xor_lane32<kJ>((uint32_t)x);
-    const bool up = k < 64 ? (lane & k) == 0 : ((t * 64) & k) == 0;
-    key[t] = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
-    if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // four slots' exchanges in flight (registers)
-  }
-}
-// Ascending bitonic sort of the 64 kS keys (every slot: a runtime slot bound doubled the
-// registers the exchanges hold).
-template <int kS>
-__device__ __forceinline__ void reg_bitonic(uint64_t (&key)[kS]) {
-  constexpr int P = 64 * kS;
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      switch (j) {
-        case 1: bx_lanes<kS, 1>(key, k); break;
-        case 2: bx_lanes<kS, 2>(key, k); break;
-        case 4: bx_lanes<kS, 4>(key, k); break;
-        case 8: bx_lanes<kS, 8>(key, k); break;
-        case 16: bx_lanes<kS, 16>(key, k); break;
-        case 32: bx_lanes<kS, 32>(key, k); break;
-        case 64: bx_slots<kS, 1>(key, k); break;
-        case 128: bx_slots<kS, 2>(key, k); break;
-        case 256: bx_slots<kS, 4>(key, k); break;
-        case 512: bx_slots<kS, 8>(key, k); break;
-        default: bx_slots<kS, 16>(key, k); break;
-      }
-    }
-  }
-}
-
 // Same results as line_body (which documents the reference semantics); the differences are only
 // where the state lives.
 template <int kS>

@@ -87,6 +87,7 @@ struct OdomArgs {
   int cap_sharp, cap_less_sharp, cap_flat;
   int chain_len;
   int n_chains;
+  int c0, cn;      // the chains [c0, c0 + cn) one launch serves (a chain group)
   int max_iterations;  // ceres max_num_iterations (4, laserOdometry.cpp:707)
   const double* init_state;  // [n_chains][14] = para(7) + pose(7) at the chain start, or null
   double* state;             // [n_chains][16] = para(7), q_w(4), t_w(3)
@@ -113,9 +114,19 @@ struct FactorArgs {
 // cloud_track, which is all the ORB front end reads.
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/, hipEvent_t images_ready);
 void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st);
-// Issues the whole round/phase schedule; ev (nullable) receives the boundaries of every launch.
-void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>* ev,
-                     hipEvent_t (*get_event)(void*), void* ev_owner);
+// One timed launch of the odometry schedule: kernel id (4 k_odom_assoc, 5 k_odom_lm) and the events
+// recorded on its stream right before and after it.
+struct OdoTimed {
+  int kernel;
+  hipEvent_t b, e;
+};
+// Issues the whole round/phase schedule.  The chains are split into ngroups groups, group g on
+// streams[g] (streams[0] = the caller's stream, which the others fork from and join back into),
+// so one group's solves overlap another group's association.  fork / join: ngroups events.
+// ev (nullable) receives every launch's timing events (from get_event).
+void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups, hipEvent_t fork,
+                     const hipEvent_t* join, std::vector<OdoTimed>* ev, hipEvent_t (*get_event)(void*),
+                     void* ev_owner);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
 }  // namespace lislam

@@ -32,13 +32,16 @@ constexpr double kDistSq = 25.0;   // DISTANCE_SQ_THRESHOLD (laserOdometry.cpp:8
 constexpr double kNearby = 2.5;    // NEARBY_SCAN (:90)
 
 // ------------------------------------------------------------------ target index
-// Per feature cloud (less-sharp / less-flat of every scan), one 1024-thread workgroup:
+// Per feature cloud (less-sharp / less-flat of every scan), one workgroup of kW waves:
 //   1. chunk / super-chunk AABBs + scan-line label ranges in the cloud's own order;
-//   2. a z-order (Morton) permutation on a cubic grid over the cloud's AABB, sorted as
-//      (code, index) keys by a bitonic sort in LDS (global scratch beyond kSortCap keys), and the
-//      chunk / super-chunk AABBs of the permuted cloud, which are spatially compact.
-constexpr int kIdxThreads = 1024;
-constexpr int kSortCap = 16384;  // keys sorted in LDS (128 KiB)
+//   2. a z-order (Morton) permutation on a cubic grid over the cloud's AABB — (code, index) keys
+//      sorted by a workgroup bitonic network held in registers (16 keys per lane, index
+//      i = 1024 w + 64 t + lane): stages j < 64 in-lane DPP / swizzle exchanges, j < 1024 slot
+//      swaps, j >= 1024 through LDS in two halves; clouds beyond 1024 kW keys sort in global
+//      scratch — and the chunk / super-chunk AABBs of the permuted cloud, which are spatially
+//      compact.  The permutation only steers the search's pruning: every association result is
+//      independent of it (exact distances, ties by original index).
+constexpr int kKeysPerLane = 16;
 
 __device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
   v &= 0x3ffu;
@@ -56,7 +59,7 @@ __device__ __forceinline__ void stg4(float4* p, float4 v) {
 
 __device__ __forceinline__ void chunk_boxes(const float4* pts, int n, bool label_from_w, float4* chunk, float4* super) {
   const int nch = (n + kChunk - 1) / kChunk;
-  for (int c = threadIdx.x; c < nch; c += kIdxThreads) {
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
     float4 lo = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 1e9f), hi = make_float4(-3.4e38f, -3.4e38f, -3.4e38f, -1e9f);
     for (int j = c * kChunk; j < min(n, c * kChunk + kChunk); j++) {
       const float4 p = ldg(pts + j);
@@ -69,7 +72,7 @@ __device__ __forceinline__ void chunk_boxes(const float4* pts, int n, bool label
   }
   __syncthreads();
   const int nsu = (nch + kChunk - 1) / kChunk;
-  for (int c = threadIdx.x; c < nsu; c += kIdxThreads) {
+  for (int c = threadIdx.x; c < nsu; c += blockDim.x) {
     float4 lo = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 1e9f), hi = make_float4(-3.4e38f, -3.4e38f, -3.4e38f, -1e9f);
     for (int k = c * kChunk; k < min(nch, c * kChunk + kChunk); k++) {
       const float4 l = ldg(chunk + 2 * k), h = ldg(chunk + 2 * k + 1);
@@ -82,11 +85,13 @@ __device__ __forceinline__ void chunk_boxes(const float4* pts, int n, bool label
   __syncthreads();
 }
 
-template <typename KeyPtr>
-__device__ __forceinline__ void block_bitonic(KeyPtr keys, int P) {
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// Bitonic sort of P keys in global scratch (clouds larger than a workgroup's registers hold).
+__device__ __forceinline__ void global_bitonic(gu64* keys, int P) {
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += kIdxThreads) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
         const int ixj = i ^ j;
         if (ixj > i) {
           const uint64_t x = keys[i], y = keys[ixj];
@@ -98,12 +103,42 @@ __device__ __forceinline__ void block_bitonic(KeyPtr keys, int P) {
   }
 }
 
-typedef __attribute__((address_space(1))) uint64_t gu64;
+// Workgroup bitonic sort of the first P = 1024 nw keys (nw active waves, a power of two); the
+// other waves only join the barriers.  xch: kW * 8 * 64 keys of LDS.
+template <int kW>
+__device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kKeysPerLane], int P, uint64_t* xch) {
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const bool active = w * 1024 < P;
+  const int base = w * 1024;
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j >= 1024; j >>= 1) {  // partner wave w ^ (j / 1024), same slot and lane
+      const int pw = w ^ (j >> 10);
+      const bool up = (base & k) == 0, lower = (w & (j >> 10)) == 0;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        if (active)
+#pragma unroll
+          for (int t = 0; t < 8; t++) xch[(w * 8 + t) * 64 + lane] = key[h * 8 + t];
+        __syncthreads();
+        if (active)
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            const uint64_t x = key[h * 8 + t], y = xch[(pw * 8 + t) * 64 + lane];
+            key[h * 8 + t] = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
+          }
+        __syncthreads();
+      }
+    }
+    if (active) reg_bitonic_level<kKeysPerLane>(key, k, min(k >> 1, 512), base);
+  }
+}
 
-// which_map: blockIdx.x -> (scan, cloud) for the launch (0 less-sharp, 1 less-flat, 2 sharp, 3 flat)
-__global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2, int lds_keys) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t skeys[];
-  __shared__ float red[6][kIdxThreads / 64];
+// which: 0 less-sharp, 1 less-flat (targets), 2 sharp, 3 flat (queries: permutation only);
+// blockIdx.x -> (scan, w0 / w1 / w2 of the launch)
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+  __shared__ uint64_t xch[kW * 8 * 64];
+  __shared__ float red[6][kW];
   const int s = blockIdx.x / per_scan, wi = blockIdx.x % per_scan;
   const int which = wi == 0 ? w0 : wi == 1 ? w1 : w2;
   const bool query = which >= 2;
@@ -116,7 +151,7 @@ __global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a, int pe
   if (n == 0) return;
   // cloud AABB
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  for (int j = threadIdx.x; j < n; j += kIdxThreads) {
+  for (int j = threadIdx.x; j < n; j += 64 * kW) {
     const float4 p = ldg(pts + j);
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
@@ -132,41 +167,55 @@ __global__ __launch_bounds__(kIdxThreads) void k_target_index(OdomArgs a, int pe
   __syncthreads();
   for (int d = 0; d < 3; d++) {
     mn[d] = red[d][0]; mx[d] = red[3 + d][0];
-    for (int w = 1; w < kIdxThreads / 64; w++) { mn[d] = fminf(mn[d], red[d][w]); mx[d] = fmaxf(mx[d], red[3 + d][w]); }
+    for (int w = 1; w < kW; w++) { mn[d] = fminf(mn[d], red[d][w]); mx[d] = fmaxf(mx[d], red[3 + d][w]); }
   }
   const float ext = fmaxf(fmaxf(mx[0] - mn[0], mx[1] - mn[1]), fmaxf(mx[2] - mn[2], 1e-6f));
   const float inv = 1023.0f / ext;  // cubic cells
-  int P = 64;
+  auto key_of = [&](int j) -> uint64_t {
+    if (j >= n) return ~0ull;
+    const float4 p = ldg(pts + j);
+    const uint32_t qx = (uint32_t)fminf(fmaxf((p.x - mn[0]) * inv, 0.f), 1023.f);
+    const uint32_t qy = (uint32_t)fminf(fmaxf((p.y - mn[1]) * inv, 0.f), 1023.f);
+    const uint32_t qz = (uint32_t)fminf(fmaxf((p.z - mn[2]) * inv, 0.f), 1023.f);
+    const uint32_t code = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
+    return ((uint64_t)code << 32) | (uint32_t)j;
+  };
+  int P = 1024;
   while (P < n) P <<= 1;
-  const bool in_lds = P <= lds_keys;
+  uint64_t key[kKeysPerLane];
+  const bool in_regs = P <= 1024 * kW;
   gu64* gkeys = (gu64*)(ix.keys + (size_t)s * 2 * ix.cap);
-  for (int j = threadIdx.x; j < P; j += kIdxThreads) {
-    uint64_t key = ~0ull;
-    if (j < n) {
-      const float4 p = ldg(pts + j);
-      const uint32_t qx = (uint32_t)fminf(fmaxf((p.x - mn[0]) * inv, 0.f), 1023.f);
-      const uint32_t qy = (uint32_t)fminf(fmaxf((p.y - mn[1]) * inv, 0.f), 1023.f);
-      const uint32_t qz = (uint32_t)fminf(fmaxf((p.z - mn[2]) * inv, 0.f), 1023.f);
-      const uint32_t code = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
-      key = ((uint64_t)code << 32) | (uint32_t)j;
-    }
-    if (in_lds) skeys[j] = key;
-    else gkeys[j] = key;
+  if (in_regs) {
+#pragma unroll
+    for (int t = 0; t < kKeysPerLane; t++) key[t] = key_of(wave * 1024 + t * 64 + lane);
+    wg_bitonic<kW>(key, P, xch);
+  } else {
+    for (int j = threadIdx.x; j < P; j += 64 * kW) gkeys[j] = key_of(j);
+    __syncthreads();
+    global_bitonic(gkeys, P);
   }
-  __syncthreads();
-  if (in_lds) block_bitonic(skeys, P);
-  else block_bitonic(gkeys, P);
-  if (query) {  // association threads take their queries in this order (spatially coherent waves)
+  // sorted position i -> original index
+  auto emit = [&](auto&& f) {
+    if (in_regs) {
+#pragma unroll
+      for (int t = 0; t < kKeysPerLane; t++) {
+        const int i = wave * 1024 + t * 64 + lane;
+        if (i < n) f(i, (int)(uint32_t)key[t]);
+      }
+    } else {
+      for (int i = threadIdx.x; i < n; i += 64 * kW) f(i, (int)(uint32_t)gkeys[i]);
+    }
+  };
+  if (query) {  // association waves take their queries in this order (spatially coherent workgroups)
     int* perm = which == 2 ? a.qperm_sharp + (size_t)s * a.cap_sharp : a.qperm_flat + (size_t)s * a.cap_flat;
-    for (int j = threadIdx.x; j < n; j += kIdxThreads) perm[j] = (int)(uint32_t)(in_lds ? skeys[j] : gkeys[j]);
+    emit([&](int i, int o) { perm[i] = o; });
     return;
   }
   float4* sorted = ix.sorted + (size_t)s * ix.cap;
-  for (int j = threadIdx.x; j < n; j += kIdxThreads) {
-    const uint32_t o = (uint32_t)(in_lds ? skeys[j] : gkeys[j]);
+  emit([&](int i, int o) {
     const float4 p = ldg(pts + o);
-    stg4(sorted + j, make_float4(p.x, p.y, p.z, __int_as_float((int)o)));
-  }
+    stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+  });
   __syncthreads();
   chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
 }
@@ -206,7 +255,18 @@ constexpr int kAssocWaves = 4;  // queries per 256-thread workgroup
 
 #ifdef LISLAM_PHASE_PROF  // developer statistics of the searches (scripts/phase_prof.py)
 __device__ unsigned long long g_assoc_stats[16];
+#ifdef LISLAM_ASSOC_COUNT  // search statistics (global atomics: they distort the timing)
 #define ASTAT(i) do { if (lane_id() == 0) atomicAdd(&g_assoc_stats[i], 1ull); } while (0)
+#else
+#define ASTAT(i)
+#endif
+// per-wave (start, end, kind, target size) of one association launch (round g_wave_round)
+__device__ unsigned long long* g_wave_log;
+__device__ int g_wave_round;
+extern "C" int lislam_debug_wave_log(unsigned long long* dev_buf, int round) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_log), &dev_buf, sizeof(dev_buf)) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_round), &round, sizeof(round)) == hipSuccess ? 0 : -2;
+}
 extern "C" int lislam_debug_assoc_stats(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assoc_stats), sizeof(g_assoc_stats)) != hipSuccess) return -2;
   static const unsigned long long zero[16] = {0};
@@ -562,14 +622,14 @@ __device__ __forceinline__ bool pair_of(const OdomArgs& a, int c, int r, int* k)
   return *k <= k1;
 }
 
-// Grid: qblocks = ceil((cap_sharp + cap_flat) / 4) workgroups of 4 waves per chain.  Wave w of
+// Grid: qblocks = ceil((cap_sharp + cap_flat) / 4) workgroups of 4 waves per chain of the group.  Wave w of
 // pair k takes corner query w (w < n_sharp) or surf query w - n_sharp, in Morton order.  With
 // 8 or more chains, workgroup b serves chain 8 * ((b / 8) / qblocks) + b % 8: workgroups are
 // dealt round-robin over the 8 XCDs, so each XCD's L2 holds the target clouds of only its own
 // chains (placement is a speed matter only).
 __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int r, int qblocks) {
   int c, qb;
-  if (a.n_chains >= 8) {
+  if (a.cn >= 8) {
     const int b = blockIdx.x, x = b & 7, rr = b >> 3;
     c = 8 * (rr / qblocks) + x;
     qb = rr % qblocks;
@@ -577,13 +637,17 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
     c = blockIdx.x / qblocks;
     qb = blockIdx.x % qblocks;
   }
-  if (c >= a.n_chains) return;
+  if (c >= a.cn) return;
+  c += a.c0;
   int k;
   if (!pair_of(a, c, r, &k)) return;
   const int lane = lane_id();
   const int w = qb * kAssocWaves + (int)(threadIdx.x >> 6);
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   if (w >= ns + nf) return;  // whole waves leave; nothing below synchronizes the workgroup
+#ifdef LISLAM_PHASE_PROF
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const bool corner = w < ns;
   const int t = corner ? w : w - ns;
   const int q = corner ? a.qperm_sharp[(size_t)k * a.cap_sharp + t] : a.qperm_flat[(size_t)k * a.cap_flat + t];
@@ -630,6 +694,15 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   if (found && lane < 9) rec[lane] = v;
   // the LM kernel counts corner_correspondence / plane_correspondence (:562/:685) from the kinds
   if (lane == 0) a.blk_kind[(size_t)c * (a.cap_sharp + a.cap_flat) + slot] = found ? (corner ? 0 : 1) : -1;
+#ifdef LISLAM_PHASE_PROF
+  if (g_wave_log && r == g_wave_round && lane == 0) {
+    unsigned long long* o = g_wave_log + ((size_t)blockIdx.x * kAssocWaves + (threadIdx.x >> 6)) * 4;
+    o[0] = t_start;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+    o[2] = (unsigned long long)(corner ? 1 : 2) | ((unsigned long long)c << 8) | ((unsigned long long)q << 32);
+    o[3] = (unsigned long long)nL;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ phase 2: LM solve
@@ -696,7 +769,7 @@ __device__ __forceinline__ void evaluate(LmShared& sh, const double* blk, const 
 
 __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int outer) {
   __shared__ LmShared sh;
-  const int c = blockIdx.x;
+  const int c = a.c0 + blockIdx.x;
   int k;
   if (!pair_of(a, c, r, &k)) return;
   double* st = a.state + (size_t)c * 16;
@@ -799,41 +872,51 @@ void launch_factors(const FactorArgs& a, hipStream_t st) {
 }
 
 void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {  // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void*)k_target_index, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kSortCap * sizeof(uint64_t));
-    attr = true;
-  }
-  // less-flat clouds: 128 KiB of LDS keys; less-sharp + query clouds: 64 KiB (two workgroups per CU)
-  hipLaunchKernelGGL(k_target_index, dim3(n_scans), dim3(kIdxThreads), kSortCap * sizeof(uint64_t), st, a, 1, 1, 1, 1,
-                     kSortCap);
-  hipLaunchKernelGGL(k_target_index, dim3(3 * n_scans), dim3(kIdxThreads), (kSortCap / 2) * sizeof(uint64_t), st, a,
-                     3, 0, 2, 3, kSortCap / 2);
+  // less-flat clouds: 16 waves (16384 keys in registers, 64 KiB LDS exchange, two workgroups per
+  // CU); less-sharp + query clouds: 8 waves (8192 keys)
+  hipLaunchKernelGGL(k_target_index<16>, dim3(n_scans), dim3(1024), 0, st, a, 1, 1, 1, 1);
+  hipLaunchKernelGGL(k_target_index<8>, dim3(3 * n_scans), dim3(512), 0, st, a, 3, 0, 2, 3);
 }
 
-void launch_odometry(const OdomArgs& a, hipStream_t st, std::vector<hipEvent_t>* ev, hipEvent_t (*get_event)(void*),
+void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups, hipEvent_t fork,
+                     const hipEvent_t* join, std::vector<OdoTimed>* ev, hipEvent_t (*get_event)(void*),
                      void* owner) {
-  if (a.n_chains <= 0) return;
-  auto mark = [&]() {
-    if (ev) {
-      hipEvent_t e = get_event(owner);
-      (void)hipEventRecord(e, st);
-      ev->push_back(e);
-    }
+  if (a0.n_chains <= 0) return;
+  const hipStream_t st = streams[0];
+  hipLaunchKernelGGL(k_odom_init, dim3((a0.n_chains + 63) / 64), dim3(64), 0, st, a0);
+  const int G = max(1, min(ngroups, a0.n_chains));
+  if (G > 1) {
+    (void)hipEventRecord(fork, st);
+    for (int g = 1; g < G; g++) (void)hipStreamWaitEvent(streams[g], fork, 0);
+  }
+  const int qblocks = (a0.cap_sharp + a0.cap_flat + kAssocWaves - 1) / kAssocWaves;
+  const int rounds = min(a0.chain_len, a0.S - 1);
+  auto timed = [&](int kernel, hipStream_t s, auto&& launch) {
+    hipEvent_t b = nullptr, e = nullptr;
+    if (ev) { b = get_event(owner); (void)hipEventRecord(b, s); }
+    launch();
+    if (ev) { e = get_event(owner); (void)hipEventRecord(e, s); ev->push_back({kernel, b, e}); }
   };
-  mark();
-  hipLaunchKernelGGL(k_odom_init, dim3((a.n_chains + 63) / 64), dim3(64), 0, st, a);
-  const int qblocks = (a.cap_sharp + a.cap_flat + kAssocWaves - 1) / kAssocWaves;
-  const int rounds = min(a.chain_len, a.S - 1);
-  mark();
+  // round-major issue order: every group's round r is queued before any group's round r + 1
   for (int r = 0; r < rounds; r++) {
     for (int outer = 0; outer < 2; outer++) {
-      hipLaunchKernelGGL(k_odom_assoc, dim3(qblocks * (a.n_chains >= 8 ? (a.n_chains + 7) / 8 * 8 : a.n_chains)),
-                         dim3(64 * kAssocWaves), 0, st, a, r, qblocks);
-      mark();
-      hipLaunchKernelGGL(k_odom_lm, dim3(a.n_chains), dim3(kLmThreads), 0, st, a, r, outer);
-      mark();
+      for (int g = 0; g < G; g++) {
+        OdomArgs a = a0;
+        a.c0 = (int)((long)a0.n_chains * g / G);
+        a.cn = (int)((long)a0.n_chains * (g + 1) / G) - a.c0;
+        const hipStream_t s = streams[g];
+        const int cb = a.cn >= 8 ? (a.cn + 7) / 8 * 8 : a.cn;
+        timed(4, s, [&] {
+          hipLaunchKernelGGL(k_odom_assoc, dim3(qblocks * cb), dim3(64 * kAssocWaves), 0, s, a, r, qblocks);
+        });
+        timed(5, s, [&] { hipLaunchKernelGGL(k_odom_lm, dim3(a.cn), dim3(kLmThreads), 0, s, a, r, outer); });
+      }
+    }
+  }
+  if (G > 1) {
+    for (int g = 1; g < G; g++) {
+      (void)hipEventRecord(join[g], streams[g]);
+      (void)hipStreamWaitEvent(st, join[g], 0);
     }
   }
 }

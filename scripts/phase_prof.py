@@ -25,6 +25,47 @@ if sys.argv[1] == "build":
                     *srcs], check=True, cwd=g.CSRC)
     sys.exit(0)
 
+if sys.argv[1] == "waves":  # per-wave timeline of one association launch (round R, outer pass 1)
+    import numpy as np
+    import torch
+
+    pkg = g.package()
+    L = pkg.native.load(OUT)
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+    R = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    scans = pkg.synth.make_sequence(S)
+    with pkg.Context() as ctx:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, 10)
+        ctx.synchronize()
+        log = torch.zeros(4 * 4 * 2000 * 1000, dtype=torch.int64, device="cuda")
+        L.lislam_debug_wave_log(ctypes.c_void_p(log.data_ptr()), R)
+        b.odometry(S, 10)
+        ctx.synchronize()
+        L.lislam_debug_wave_log(ctypes.c_void_p(0), -1)
+        a = log.view(-1, 4).cpu().numpy()
+        a = a[a[:, 0] != 0]
+        t0 = a[:, 0].min()
+        st, en = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0  # 100 MHz -> us
+        d = en - st
+        kind = a[:, 2] & 0xff
+        print(f"waves {len(a)}  span {en.max():.1f} us  start: p50 {np.median(st):.1f} p99 {np.percentile(st, 99):.1f} "
+              f"max {st.max():.1f}")
+        for k, nm in ((1, "corner"), (2, "surf")):
+            dk = d[kind == k]
+            print(f"  {nm:6s} n={len(dk)} dur us: p50 {np.median(dk):.1f} p90 {np.percentile(dk, 90):.1f} "
+                  f"p99 {np.percentile(dk, 99):.1f} max {dk.max():.1f}  sum {dk.sum():.0f}")
+        top = np.argsort(-d)[:10]
+        for i in top:
+            print(f"    slow: kind {kind[i]} chain {(a[i, 2] >> 8) & 0xffffff} q {a[i, 2] >> 32} start {st[i]:.1f} "
+                  f"dur {d[i]:.1f} nL {a[i, 3]}")
+        hist, edges = np.histogram(en, bins=20)
+        print("  end-time histogram:", list(hist))
+        b.close()
+    sys.exit(0)
+
 pkg = g.package()
 L = pkg.native.load(OUT)
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 100
