@@ -72,6 +72,15 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Order this wave's earlier LDS writes before its later LDS reads (lanes exchanging data through
+// LDS inside one wave, no workgroup barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------- wave reductions (DPP)
 // Wave-wide unsigned minimum / maximum, returned uniform: DPP within each 16-lane row (quad xor 1,
 // xor 2, half-row mirror, row mirror; each folds into one v_min/max_u32_dpp), then row_bcast:15 /

@@ -11,7 +11,7 @@
 // octave; descriptors 32 B; cloud points float4.
 //
 // Kernels (the semantics are those of oracle/oracle_orb.cpp, which restates OpenCV 4.x):
-//   k_orb_level     per level (in order), 1 thread per padded pixel: level 0 copy, levels 1..7 by
+//   k_orb_level     per level (in order), 1 thread per 4 padded pixels: level 0 copy, levels 1..7 by
 //                   the bit-exact fixed-point INTER_LINEAR_EXACT resize of the previous level;
 //                   border pixels evaluate their reflect-101 source directly
 //   k_orb_blur      1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2 separable float
@@ -22,9 +22,10 @@
 //                   border
 //   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
 //                   thread), retainBest(2n) on the FAST score (256-bin histogram), Harris responses
-//                   (a wavefront per candidate), retainBest(n) on them (radix select of the n-th
-//                   largest), intensity-centroid angle (a wavefront per keypoint); detection order
-//                   is kept (OpenCV's set, canonical order)
+//                   (a wavefront per 4 candidates, all their loads in flight), retainBest(n) on
+//                   them (radix select of the n-th largest; bin searches by a wave suffix scan),
+//                   intensity-centroid angle (a wavefront per 4 keypoints); detection order is
+//                   kept (OpenCV's set, canonical order)
 //   k_orb_finish    1 WG per scan: levels concatenated, coordinates scaled to level 0,
 //                   cloud-track lookup + |x| < 0.01 filter (extractPointsAndFilterZeroValue)
 //   k_orb_desc      32 threads per keypoint: steered rBRIEF-256 bytes
@@ -147,38 +148,72 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* base, const Geom& g, con
   return (uint32_t)pxc(base, g, l - 1, row, t.xo[l * t.xs + g.w[l] - 1]) << 8;
 }
 
-// Level l of the pyramid (one thread per padded pixel, levels launched in order): a border pixel
-// takes the value of its reflect-101 image (mode 0) or 0 (mode 1, the mask pyramid); a ROI pixel
-// is level 0's image or the INTER_LINEAR_EXACT resize of level l-1 (mask: threshold 254 to 0).
+// Level l of the pyramid (one thread per kLevelPx consecutive padded pixels of a row — rows are
+// 16-byte aligned — levels launched in order): a border pixel takes the value of its reflect-101
+// image (mode 0) or 0 (mode 1, the mask pyramid); a ROI pixel is level 0's image or the
+// INTER_LINEAR_EXACT resize of level l-1 (mask: threshold 254 to 0).
+#ifndef LISLAM_LEVEL_PX
+#define LISLAM_LEVEL_PX 4
+#endif
+constexpr int kLevelPx = LISLAM_LEVEL_PX;
 __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
   const int w = g.w[l], h = g.h[l], pw = g.stride[l];
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= pw * (h + 2 * kB)) return;
+  const int i0 = (blockIdx.x * blockDim.x + threadIdx.x) * kLevelPx;
+  if (i0 >= pw * (h + 2 * kB)) return;
   uint8_t* base = mode ? const_cast<uint8_t*>(a.mpyr) : a.pyr + (size_t)s * g.bytes;
-  const int r = i / pw - kB, c = i % pw - kB;
-  const bool roi = r >= 0 && r < h && c >= 0 && c < w;
-  uint8_t v = 0;
-  if (roi || !mode) {
-    const int y = reflect101(r, h), x = reflect101(c, w);
-    if (l == 0) {
-      v = a.img[(size_t)s * g.W * g.H + y * g.W + x];
+  const int r = i0 / pw - kB, c0 = i0 % pw - kB;
+  const bool roi_r = r >= 0 && r < h;
+  const int y = reflect101(r, h);
+  const uint8_t* img = a.img + (size_t)s * g.W * g.H + (size_t)y * g.W;
+  // row terms of the vertical interpolation (levels >= 1)
+  int ya = 0, yb = 0;
+  uint32_t cy = 0;
+  bool yclamp = false;
+  if (l > 0) {
+    const int* lim = a.t.lim + l * 4;
+    yclamp = y < lim[2] || y >= lim[3];
+    if (yclamp) {
+      ya = y < lim[2] ? 0 : g.h[l - 1] - 1;
     } else {
-      const int* lim = a.t.lim + l * 4;
-      if (y < lim[2] || y >= lim[3]) {
-        const uint32_t hv = hval(base, g, a.t, l, y < lim[2] ? 0 : g.h[l - 1] - 1, x);
-        v = (uint8_t)min(255u, (hv + 128u) >> 8);
-      } else {
-        const int yo = a.t.yo[l * a.t.ys + y];
-        const uint32_t c1 = a.t.yc[l * a.t.ys + y];
-        const uint32_t rr = hval(base, g, a.t, l, yo, x) * (256u - c1) + hval(base, g, a.t, l, yo + 1, x) * c1;
-        v = (uint8_t)min(255u, (rr + 32768u) >> 16);
-      }
-      if (mode && v <= 254) v = 0;  // threshold(254, THRESH_TOZERO)
+      ya = a.t.yo[l * a.t.ys + y];
+      yb = ya + 1;
+      cy = a.t.yc[l * a.t.ys + y];
     }
   }
-  base[g.off[l] + i] = v;
+  uint32_t word[(kLevelPx + 3) / 4] = {};
+#pragma unroll
+  for (int k = 0; k < kLevelPx; k++) {
+    const int c = c0 + k;
+    const bool roi = roi_r && c >= 0 && c < w;
+    uint32_t v = 0;
+    if (roi || !mode) {
+      const int x = reflect101(c, w);
+      if (l == 0) {
+        v = img[x];
+      } else {
+        if (yclamp) {
+          v = min(255u, (hval(base, g, a.t, l, ya, x) + 128u) >> 8);
+        } else {
+          const uint32_t rr = hval(base, g, a.t, l, ya, x) * (256u - cy) + hval(base, g, a.t, l, yb, x) * cy;
+          v = min(255u, (rr + 32768u) >> 16);
+        }
+        if (mode && v <= 254) v = 0;  // threshold(254, THRESH_TOZERO)
+      }
+    }
+    word[k >> 2] |= v << (8 * (k & 3));
+  }
+  uint8_t* dst = base + g.off[l] + i0;
+  typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+  if constexpr (kLevelPx == 8)
+    *(__attribute__((address_space(1))) u2v*)dst = u2v{word[0], word[kLevelPx / 8]};
+  else if constexpr (kLevelPx == 4)
+    *(__attribute__((address_space(1))) uint32_t*)dst = word[0];
+  else if constexpr (kLevelPx == 2)
+    *(__attribute__((address_space(1))) uint16_t*)dst = (uint16_t)word[0];
+  else
+    *(__attribute__((address_space(1))) uint8_t*)dst = (uint8_t)word[0];
 }
 
 // Stage `rows` (<= kMaxRows) rows of nd dwords (source rows 4-byte aligned, sstride bytes apart)
@@ -207,8 +242,8 @@ __device__ __forceinline__ void stage_rows(uint32_t* dst, const uint8_t* src, in
 
 // GaussianBlur(level ROI, 7x7, 2, 2, BORDER_REFLECT_101): row sums then symmetric column sum.
 // One workgroup per band of kBlurBand padded rows of a level: the band's rows +-3 staged in LDS
-// (row-coalesced byte loads), then one thread per column keeps the band's row sums in registers;
-// border rows / columns are copies.
+// (row-coalesced dword loads), then one thread per 4 columns keeps the band's row sums in
+// registers (3 LDS dwords per staged row); border rows / columns are copies.
 __global__ __launch_bounds__(256) void k_orb_blur(Args a) {
   extern __shared__ uint8_t btile[];  // (kBlurBand + 6) x stride[l]
   const Geom& g = a.g;
@@ -225,21 +260,42 @@ __global__ __launch_bounds__(256) void k_orb_blur(Args a) {
   stage_rows<kBlurBand + 6>(reinterpret_cast<uint32_t*>(btile + (t0 - (p0 - 3)) * pw), src + (size_t)t0 * pw, pw,
                             t1 - t0, pw >> 2);
   __syncthreads();
-  for (int c = threadIdx.x; c < pw; c += blockDim.x) {
-    const int cr = c - kB;  // ROI column
-    const bool roi_c = cr >= 0 && cr < w;
-    float rs[kBlurBand + 6];
-    if (roi_c) {
+  // one thread per 4 columns: each staged row's 10 source bytes come from 3 LDS dwords
+  const uint32_t* t32 = reinterpret_cast<const uint32_t*>(btile);
+  const int pw4 = pw >> 2;
+  for (int c4 = 4 * (int)threadIdx.x; c4 < pw; c4 += 4 * (int)blockDim.x) {
+    bool roi_c[4];
+    bool any_roi = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int cr = c4 + j - kB;  // ROI column
+      roi_c[j] = cr >= 0 && cr < w;
+      any_roi |= roi_c[j];
+    }
+    float rs[kBlurBand + 6][4];
+    if (any_roi) {  // then c4 >= kB - 3, so the dword at c4 - 4 is inside the row
 #pragma unroll
       for (int k = 0; k < kBlurBand + 6; k++) {
         const int pr = p0 - 3 + k;
-        rs[k] = 0.f;
-        if (pr >= kB - 3 && pr < h + kB + 3 && k < nr + 6) {  // rows some ROI output of the band reads
-          const uint8_t* row = btile + k * pw + c - 3;
-          float v = g.gk[0] * (float)row[0];
 #pragma unroll
-          for (int t = 1; t < 7; t++) v += g.gk[t] * (float)row[t];
-          rs[k] = v;
+        for (int j = 0; j < 4; j++) rs[k][j] = 0.f;
+        if (pr >= kB - 3 && pr < h + kB + 3 && k < nr + 6) {  // rows some ROI output of the band reads
+          const uint32_t* rw = t32 + k * pw4 + (c4 >> 2) - 1;
+          const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
+          float b[12];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            b[e] = (float)((d0 >> (8 * e)) & 255u);
+            b[4 + e] = (float)((d1 >> (8 * e)) & 255u);
+            b[8 + e] = (float)((d2 >> (8 * e)) & 255u);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) {  // column c4 + j: bytes c4 + j - 3 .. c4 + j + 3 = b[j + 1 .. j + 7]
+            float v = g.gk[0] * b[j + 1];
+#pragma unroll
+            for (int t = 1; t < 7; t++) v += g.gk[t] * b[j + 1 + t];
+            rs[k][j] = v;
+          }
         }
       }
     }
@@ -247,14 +303,19 @@ __global__ __launch_bounds__(256) void k_orb_blur(Args a) {
     for (int k = 0; k < kBlurBand; k++) {
       if (k >= nr) break;
       const int pr = p0 + k, r = pr - kB;
-      uint8_t o = btile[(k + 3) * pw + c];
-      if (roi_c && r >= 0 && r < h) {
-        float v = g.gk[3] * rs[k + 3];
+      uint32_t o = t32[(k + 3) * pw4 + (c4 >> 2)];
+      if (r >= 0 && r < h) {
 #pragma unroll
-        for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[k + 3 + t] + rs[k + 3 - t]);
-        o = (uint8_t)min(255, max(0, (int)rintf(v)));
+        for (int j = 0; j < 4; j++) {
+          if (!roi_c[j]) continue;
+          float v = g.gk[3] * rs[k + 3][j];
+#pragma unroll
+          for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[k + 3 + t][j] + rs[k + 3 - t][j]);
+          const uint32_t ob = (uint32_t)min(255, max(0, (int)rintf(v)));
+          o = (o & ~(255u << (8 * j))) | (ob << (8 * j));
+        }
       }
-      dst[pr * pw + c] = o;
+      *(__attribute__((address_space(1))) uint32_t*)(dst + (size_t)pr * pw + c4) = o;
     }
   }
 }
@@ -457,31 +518,63 @@ __device__ float fast_atan2(float y, float x) {
   return a;
 }
 
+// Wave 0 of the block: the largest bin b of the 256-bin histogram whose suffix sum
+// S(b) = sum_{b' >= b} hist[b'] reaches want (the first bin of a walk from 255 down where the
+// running count reaches it), and rem = want - S(b + 1); b = -1 if the total is below want.
+// Lane l holds bins 4l .. 4l + 3; suffix sums by a wave scan.
+__device__ __forceinline__ void top_bin(const int* hist, int want, int* b_out, int* rem_out) {
+  const int lane = threadIdx.x & 63;
+  int h[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) h[u] = hist[4 * lane + u];
+  const int tl = h[0] + h[1] + h[2] + h[3];
+  int suf = tl;  // sum over lanes >= this lane
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_down(suf, o, 64);
+    if (lane + o < 64) suf += t;
+  }
+  int above = suf - tl;  // S(4 lane + 4)
+  int found = -1, rem = 0;
+#pragma unroll
+  for (int u = 3; u >= 0; u--) {
+    const int sb = above + h[u];
+    if (found < 0 && sb >= want) { found = 4 * lane + u; rem = want - above; }
+    above = sb;
+  }
+  const uint64_t m = __ballot(found >= 0);
+  if (!m) { *b_out = -1; *rem_out = want; return; }
+  const int L = 63 - __builtin_clzll(m);
+  *b_out = __shfl(found, L, 64);
+  *rem_out = __shfl(rem, L, 64);
+}
+
 // n-th largest key among cnt keys (radix select, 4 x 8 bits); all threads get it
 __device__ uint32_t nth_largest(SelShared& sh, const float* resp, int cnt, int n) {
-  if (threadIdx.x == 0) { sh.prefix = 0; sh.want = n; }
-  __syncthreads();
+  uint32_t prefix = 0;
+  int want = n;
   for (int pass = 3; pass >= 0; pass--) {
     for (int b = threadIdx.x; b < 256; b += blockDim.x) sh.hist[b] = 0;
     __syncthreads();
-    const uint32_t prefix = sh.prefix;
     const uint32_t hmask = pass == 3 ? 0u : (0xffffffffu << ((pass + 1) * 8));
     for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
       const uint32_t k = ord_key(resp[i]);
       if ((k & hmask) == prefix) atomicAdd(&sh.hist[(k >> (pass * 8)) & 255], 1);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int want = sh.want;
-      for (int b = 255; b >= 0; b--) {
-        if (sh.hist[b] >= want) { sh.prefix = prefix | ((uint32_t)b << (pass * 8)); break; }
-        want -= sh.hist[b];
+    if (threadIdx.x < 64) {
+      int b, rem;
+      top_bin(sh.hist, want, &b, &rem);
+      if (threadIdx.x == 0) {
+        sh.prefix = prefix | ((uint32_t)max(b, 0) << (pass * 8));
+        sh.want = rem;
       }
-      sh.want = want;
     }
     __syncthreads();
+    prefix = sh.prefix;
+    want = sh.want;
   }
-  return sh.prefix;
+  return prefix;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -512,8 +605,32 @@ __device__ __forceinline__ int block_excl(SelShared& sh, int v, int* tot) {
   return before + incl - v;
 }
 
+#ifdef LISLAM_PHASE_PROF
+__device__ unsigned long long g_sel_phase[8];
+extern "C" int lislam_debug_sel_phases(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_phase), sizeof(g_sel_phase)) != hipSuccess) return -2;
+  static const unsigned long long zero[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sel_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+#define SEL_PHASE(i)                                                          \
+  do {                                                                        \
+    __syncthreads();                                                          \
+    if (threadIdx.x == 0) {                                                   \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();      \
+      atomicAdd(&g_sel_phase[i], now_ - t_ph);                                \
+      t_ph = now_;                                                            \
+    }                                                                         \
+  } while (0)
+#else
+#define SEL_PHASE(i)
+#endif
+constexpr int kPatchDw = 2 * 279;  // LDS dwords per wave: 2 angle patches (31 x 9) >= 4 Harris patches (9 x 4)
 __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   __shared__ SelShared sh;
+  __shared__ uint32_t sh_patch[(kSelThreads / 64) * kPatchDw];
+#ifdef LISLAM_PHASE_PROF
+  unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
+#endif
   const Geom& g = a.g;
   // level-major blocks: consecutive blocks (dealt round-robin to the 8 XCDs) are different scans
   // of one level, so the heavy level-0 workgroups spread over every XCD
@@ -537,6 +654,7 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   for (int p = p0; p < p1; p++)
     if (kf[p]) cand[at++] = p;
   __syncthreads();
+  SEL_PHASE(0);
   // 2. retainBest(2 n_l) on the FAST score: keep every score >= the (2 n_l)-th largest
   const int n2 = 2 * g.nper[l];
   if (n > n2) {
@@ -544,13 +662,10 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&sh.hist[sc[cand[i]]], 1);
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int cum = 0, t = 0;
-      for (int b = 255; b >= 0; b--) {
-        cum += sh.hist[b];
-        if (n2 > 0 && cum >= n2) { t = b; break; }
-      }
-      sh.total = n2 > 0 ? t : 256;
+    if (threadIdx.x < 64) {
+      int b, rem;
+      top_bin(sh.hist, n2, &b, &rem);
+      if (threadIdx.x == 0) sh.total = n2 > 0 ? max(b, 0) : 256;
     }
     __syncthreads();
     const int thr = sh.total;
@@ -567,29 +682,61 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     n = m;
   }
   __syncthreads();
-  // 3. Harris responses: one wavefront per candidate, lane = one of the 7x7 block pixels (the
+  SEL_PHASE(1);
+  // 3. Harris responses: one wavefront per 4 candidates, lane = one of the 7x7 block pixels (the
   //    integer sums are order-free, so the float formula sees OpenCV's exact a, b, c)
-  for (int i = wv; i < n; i += nw) {
-    const int x0 = cand[i] % w, y0 = cand[i] / w;
-    int A = 0, B = 0, C = 0;
-    if (lane < 49) {
-      const int y = y0 - 3 + lane / 7, x = x0 - 3 + lane % 7;
-      const int Ix = (pxc(base, g, l, y, x + 1) - pxc(base, g, l, y, x - 1)) * 2 +
-                     (pxc(base, g, l, y - 1, x + 1) - pxc(base, g, l, y - 1, x - 1)) +
-                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y + 1, x - 1));
-      const int Iy = (pxc(base, g, l, y + 1, x) - pxc(base, g, l, y - 1, x)) * 2 +
-                     (pxc(base, g, l, y + 1, x - 1) - pxc(base, g, l, y - 1, x - 1)) +
-                     (pxc(base, g, l, y + 1, x + 1) - pxc(base, g, l, y - 1, x + 1));
-      A = Ix * Ix; B = Iy * Iy; C = Ix * Iy;
+  // The 9 x 16-byte patches (rows y0-4 .. y0+4 from the dword holding column x0-4) of 4
+  // candidates per wave iteration are staged in LDS by 144 dword loads, then each of 49 lanes
+  // reads its 8 neighbours per candidate from LDS.
+  constexpr int kPerWave = 4;
+  const int stride_l = g.stride[l];
+  const uint8_t* lvl = base + g.off[l];
+  for (int i0 = wv * kPerWave; i0 < n; i0 += nw * kPerWave) {
+    uint32_t* hp = sh_patch + wv * kPatchDw;
+#pragma unroll
+    for (int k = 0; k < (kPerWave * 36 + 63) / 64; k++) {
+      const int item = lane + 64 * k;
+      if (item < kPerWave * 36) {
+        const int u = item / 36, rr = (item % 36) >> 2, dw = item & 3;
+        const int ci = cand[min(i0 + u, n - 1)];
+        const int x0 = ci % w, y0 = ci / w;
+        hp[item] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y0 - 4 + rr + kB) * stride_l +
+                                                                           ((x0 - 4 + kB) & ~3) + 4 * dw);
+      }
     }
-    A = wave_sum(A); B = wave_sum(B); C = wave_sum(C);
+    wave_lds_sync();
+    const uint8_t* hb = reinterpret_cast<const uint8_t*>(hp);
+    int A[kPerWave], B[kPerWave], C[kPerWave];
+#pragma unroll
+    for (int u = 0; u < kPerWave; u++) {
+      A[u] = B[u] = C[u] = 0;
+      const int i = i0 + u;
+      if (i < n && lane < 49) {
+        const int x0 = cand[i] % w;
+        const uint8_t* P = hb + u * 144 + ((x0 - 4 + kB) & 3);  // P[r * 16 + c]: row y0-4+r, column x0-4+c
+        const int ar = lane / 7, bc = lane % 7;                // position (y0-3+ar, x0-3+bc) = patch (ar+1, bc+1)
+        auto at = [&](int r, int c) { return (int)P[r * 16 + c]; };
+        const int Ix = (at(ar + 1, bc + 2) - at(ar + 1, bc)) * 2 + (at(ar, bc + 2) - at(ar, bc)) +
+                       (at(ar + 2, bc + 2) - at(ar + 2, bc));
+        const int Iy = (at(ar + 2, bc + 1) - at(ar, bc + 1)) * 2 + (at(ar + 2, bc) - at(ar, bc)) +
+                       (at(ar + 2, bc + 2) - at(ar, bc + 2));
+        A[u] = Ix * Ix; B[u] = Iy * Iy; C[u] = Ix * Iy;
+      }
+    }
+    wave_lds_sync();  // the patch is rewritten by the next iteration
+#pragma unroll
+    for (int u = 0; u < kPerWave; u++) { A[u] = wave_sum(A[u]); B[u] = wave_sum(B[u]); C[u] = wave_sum(C[u]); }
     if (lane == 0) {
       const float scale = 1.f / ((1 << 2) * 7 * 255.f);
       const float sq = scale * scale * scale * scale;
-      resp[i] = ((float)A * B - (float)C * C - 0.04f * ((float)A + B) * ((float)A + B)) * sq;
+#pragma unroll
+      for (int u = 0; u < kPerWave; u++)
+        if (i0 + u < n)
+          resp[i0 + u] = ((float)A[u] * B[u] - (float)C[u] * C[u] - 0.04f * ((float)A[u] + B[u]) * ((float)A[u] + B[u])) * sq;
     }
   }
   __syncthreads();
+  SEL_PHASE(2);
   // 4. retainBest(n_l) on the Harris response
   const int n1 = g.nper[l];
   if (n > n1) {
@@ -609,40 +756,72 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     n = m;
   }
   __syncthreads();
+  SEL_PHASE(3);
   if (n > g.lcap[l]) {
     if (threadIdx.x == 0) atomicOr(a.overflow, 1);
     n = g.lcap[l];
   }
-  // 5. intensity-centroid angle: one wavefront per keypoint over the circular patch (integer
+  // 5. intensity-centroid angle: one wavefront per 4 keypoints over the circular patch (integer
   //    moments, order-free), fastAtan2 on lane 0; per-level staging
   float* out = a.lkp + ((size_t)s * g.cap + g.lofs[l]) * 6;
-  for (int i = wv; i < n; i += nw) {
-    const int x = cand[i] % w, y = cand[i] / w;
-    int m01 = 0, m10 = 0;
-    int v[kPatchIters];
+  // The 31 x 36-byte patches (rows y-15 .. y+15 from the dword holding column x-15) of 2
+  // keypoints per wave iteration are staged in LDS by 558 dword loads; lane t then reads the
+  // circle pixels t, t + 64, ... of each from LDS.
+  constexpr int kAngPerWave = 2;
+  for (int i0 = wv * kAngPerWave; i0 < n; i0 += nw * kAngPerWave) {
+    uint32_t* hp = sh_patch + wv * kPatchDw;
+    int xs[kAngPerWave], ys[kAngPerWave];
 #pragma unroll
-    for (int u = 0; u < kPatchIters; u++) {  // all loads in flight, then the integer moments
-      const int t = u * 64 + lane;
-      const short2 d = c_patch[t < kNPatch ? t : 0];
-      v[u] = t < kNPatch ? pxc(base, g, l, y + d.y, x + d.x) : 0;
+    for (int u = 0; u < kAngPerWave; u++) {
+      const int ci = cand[min(i0 + u, n - 1)];
+      xs[u] = ci % w; ys[u] = ci / w;
     }
 #pragma unroll
-    for (int u = 0; u < kPatchIters; u++) {
-      const int t = u * 64 + lane;
-      const short2 d = c_patch[t < kNPatch ? t : 0];
-      m10 += d.x * v[u];
-      m01 += d.y * v[u];
+    for (int k = 0; k < (kAngPerWave * 279 + 63) / 64; k++) {
+      const int item = lane + 64 * k;
+      if (item < kAngPerWave * 279) {
+        const int u = item / 279, rr = (item % 279) / 9, dw = (item % 279) % 9;
+        int x = xs[0], y = ys[0];
+#pragma unroll
+        for (int v = 1; v < kAngPerWave; v++)
+          if (u == v) { x = xs[v]; y = ys[v]; }
+        hp[item] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y - 15 + rr + kB) * stride_l +
+                                                                           ((x - 15 + kB) & ~3) + 4 * dw);
+      }
     }
-    m01 = wave_sum(m01);
-    m10 = wave_sum(m10);
+    wave_lds_sync();
+    const uint8_t* hb = reinterpret_cast<const uint8_t*>(hp);
+    int m01[kAngPerWave], m10[kAngPerWave];
+#pragma unroll
+    for (int u = 0; u < kAngPerWave; u++) {
+      const uint8_t* P = hb + u * 279 * 4 + ((xs[u] - 15 + kB) & 3);  // P[r * 36 + c]: row y-15+r, column x-15+c
+      m01[u] = m10[u] = 0;
+#pragma unroll
+      for (int k = 0; k < kPatchIters; k++) {
+        const int t = k * 64 + lane;
+        const short2 d = c_patch[t < kNPatch ? t : 0];
+        const int v = t < kNPatch ? (int)P[(d.y + 15) * 36 + d.x + 15] : 0;
+        m10[u] += d.x * v;
+        m01[u] += d.y * v;
+      }
+    }
+    wave_lds_sync();  // the patch is rewritten by the next iteration
+#pragma unroll
+    for (int u = 0; u < kAngPerWave; u++) { m01[u] = wave_sum(m01[u]); m10[u] = wave_sum(m10[u]); }
     if (lane == 0) {
-      float* o = out + (size_t)i * 6;
-      o[0] = (float)x; o[1] = (float)y; o[2] = 31 * g.scale[l];
-      o[3] = fast_atan2((float)m01, (float)m10);
-      o[4] = resp[i];
-      o[5] = (float)l;
+#pragma unroll
+      for (int u = 0; u < kAngPerWave; u++) {
+        const int i = i0 + u;
+        if (i >= n) break;
+        float* o = out + (size_t)i * 6;
+        o[0] = (float)xs[u]; o[1] = (float)ys[u]; o[2] = 31 * g.scale[l];
+        o[3] = fast_atan2((float)m01[u], (float)m10[u]);
+        o[4] = resp[i];
+        o[5] = (float)l;
+      }
     }
   }
+  SEL_PHASE(4);
   if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
 }
 
@@ -1185,7 +1364,8 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
     OCHK(c, hipMemcpyAsync(dmask, mask, (size_t)H * W, hipMemcpyDefault, st));
     Args a = e->args(dmask, nullptr);
     for (int l = 0; l < kL; l++)
-      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256), 1), dim3(256), 0, st, a, l, 1);
+      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256 * kLevelPx), 1), dim3(256), 0, st,
+                         a, l, 1);
     OCHK(c, hipGetLastError());
   }
   return LISLAM_OK;
@@ -1232,7 +1412,8 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   {
     TimedScope t(c, kT_orb_pyramid);
     for (int l = 0; l < kL; l++)
-      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256), n), dim3(256), 0, st, a, l, 0);
+      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256 * kLevelPx), n), dim3(256), 0, st,
+                         a, l, 0);
   }
   {
     TimedScope t(c, kT_orb_fast);

@@ -28,3 +28,16 @@ for k, (ms, n) in kt.items():
     if n: print(f'  {k:16s} {ms/3:9.3f} ms/batch {n/3:6.1f} launches', flush=True)
 st = np.stack([b.download(pkg.native.OUT_ORB_STATS, k) for k in range(S)])
 print('good', (st[:, 0] == 1).sum(), 'redetect', st[:, 1].sum(), 'kp mean', st[:, 2].mean(), 'good matches', st[1:, 4].mean())
+L = pkg.native.load()
+if hasattr(L, 'lislam_debug_sel_phases'):  # profiling build: k_orb_select phase split (WG-summed us)
+    import ctypes
+    buf = (ctypes.c_ulonglong * 8)()
+    L.lislam_debug_sel_phases(buf)
+    L.lislam_debug_sel_phases(buf)  # (cleared above; read what the next batch adds)
+    b.intensity_odometry(S, 1000, mask)
+    ctx.synchronize()
+    L.lislam_debug_sel_phases(buf)
+    names = ['compact', 'retain2n', 'harris', 'retainN', 'angles']
+    tot = sum(buf[i] for i in range(5))
+    for i, nm in enumerate(names):
+        print(f'  select {nm:9s} {buf[i] / 100.0:12.0f} WG-us  {100 * buf[i] / max(1, tot):5.1f}%')
