@@ -153,6 +153,12 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
 #define LISLAM_OUT_ORB_KEYPOINTS 16  /* float  [n][6] of the nfeatures detection */
 #define LISLAM_OUT_ORB_POINTS 17     /* float4 [n]   their cloud_track points */
 #define LISLAM_OUT_ORB_DESCRIPTORS 18 /* uint8 [n][32] */
+#define LISLAM_OUT_GROUND 19         /* float4 [n]   ground cloud x, y, z, 1 (lislam_batch_ground) */
+#define LISLAM_OUT_GROUND_PLANE 20   /* float  [4]   segmented plane A, B, C, D */
+#define LISLAM_OUT_GROUND_INFO 21    /* int32  [4]   status (1 ground, 0 plane rejected by the n.z >
+                                        cos 15 deg test, -1 < 3 candidates, -2 no model, -3 sampling
+                                        beyond the device map), RANSAC iterations, best inliers,
+                                        refit inliers */
 /* Copy one output of one scan to host memory; cap/n count elements of the listed type. */
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n);
 
@@ -189,6 +195,18 @@ int lislam_intensity_tracker_step(lislam_intensity_tracker* t, const uint8_t* im
 /* detectfeatures over scans [0, n_scans) of a batch (its a1 images, want_images = 1): scan k is
  * matched against scan k-1 exactly as the tracker would; outputs LISLAM_OUT_ORB_*. */
 int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask);
+
+/* ---- ground plane (ImageHandler::groundPlaneExtraction, src/image_handler.h_ouster:41-100):
+ * z-band screening [-2, -0.45], PCL SACSegmentation(SACMODEL_PLANE, SAC_RANSAC, 0.01, optimized
+ * coefficients) with PCL 1.10's single-thread sampling sequence, the n.z > cos(15 deg) test and
+ * the points within 0.03 m of the plane with z < 0 — the GroundPointOut cloud mapOptimization
+ * merges with the less-flat cloud (mapOptimization.cpp:136,148).  Outputs LISLAM_OUT_GROUND*. */
+int lislam_batch_ground(lislam_batch* b, int32_t n_scans);
+/* One organized cloud (the context's n_scans x width, any point layout): ground cloud out[cap][4]
+ * (x, y, z, 1), *n_out, plane[4] (A, B, C, D) and info[4] as LISLAM_OUT_GROUND_INFO (each
+ * nullable).  Replaces ImageHandler::groundPlaneExtraction's body. */
+int lislam_ground_extract(lislam_ctx* ctx, const void* points, const lislam_point_layout* layout, float* out,
+                          int32_t cap, int32_t* n_out, float* plane, int32_t* info);
 
 /* ---------------------------------------------------------------- scan-to-map (a19-a21) */
 /* A device-resident point map with the semantics of the vendored ikd-Tree
@@ -263,10 +281,11 @@ int lislam_laser_mapping(lislam_map* corner_map, lislam_map* surf_map, const flo
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
  * clears the record. */
-#define LISLAM_MAP_NUM_KERNELS 14 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+#define LISLAM_MAP_NUM_KERNELS 17 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
                                      gather + cell table), Add_Points downsample (claim + resolve),
                                      k_orb_pyramid, k_orb_fast, k_orb_select, k_orb_finish,
-                                     k_orb_blur, k_orb_desc, k_orb_match, k_orb_lm */
+                                     k_orb_blur, k_orb_desc, k_orb_match, k_orb_lm,
+                                     k_ground_screen, k_ground_ransac, k_ground_extract */
 int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
 int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 

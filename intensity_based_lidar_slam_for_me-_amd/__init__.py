@@ -5,6 +5,7 @@ name is not a Python identifier).  The compute path is the HIP library ``liblisl
 ``__graft_entry__.build()``; there is no CPU fallback.
 """
 from . import intensity, mapping, native, synth  # noqa: F401
-from .frontend import Batch, Context, Features, LaserOdometry, ScanRegistration, eval_factors  # noqa: F401
+from .frontend import Batch, Context, Features, ImageHandler, LaserOdometry, ScanRegistration, eval_factors  # noqa: F401
 
-__all__ = ["intensity", "mapping", "native", "synth", "Batch", "Context", "Features", "LaserOdometry", "ScanRegistration", "eval_factors"]
+__all__ = ["intensity", "mapping", "native", "synth", "Batch", "Context", "Features", "ImageHandler", "LaserOdometry",
+           "ScanRegistration", "eval_factors"]

@@ -227,6 +227,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (b->odo_fork) hipEventDestroy(b->odo_fork);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
+  if (b->ground) lislam_free_ground(b->ground);
   if (b->ev_images) hipEventDestroy(b->ev_images);
   delete b;
   return LISLAM_OK;
@@ -415,6 +416,13 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
       if (rc) return fail(c, rc, "ORB output %d unavailable (run lislam_batch_intensity_odometry first)", what);
       break;
     }
+    case LISLAM_OUT_GROUND:
+    case LISLAM_OUT_GROUND_PLANE:
+    case LISLAM_OUT_GROUND_INFO: {
+      const int rc = lislam_ground_batch_output(b, what, scan, &src, &cnt, &esz);
+      if (rc) return fail(c, rc, "ground output %d unavailable (run lislam_batch_ground first)", what);
+      break;
+    }
     default: return fail(c, LISLAM_ERR_ARG, "unknown output %d", what);
   }
   if (!src) return fail(c, LISLAM_ERR_STATE, "output %d not materialized (want_images=0?)", what);
@@ -453,6 +461,25 @@ int lislam_scan_registration(lislam_ctx* c, const void* points, const lislam_poi
   if (out->image_range && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_RANGE, 0, out->image_range, N, &n))) return rc;
   if (out->image_intensity && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_INTENSITY, 0, out->image_intensity, N, &n))) return rc;
   if (out->cloud_track && (rc = lislam_batch_download(b, LISLAM_OUT_CLOUD_TRACK, 0, out->cloud_track, N, &n))) return rc;
+  return LISLAM_OK;
+}
+
+int lislam_ground_extract(lislam_ctx* c, const void* points, const lislam_point_layout* layout, float* out,
+                          int32_t cap, int32_t* n_out, float* plane, int32_t* info) {
+  if (!c || !points) return LISLAM_ERR_ARG;
+  hipSetDevice(c->device);
+  int rc = ensure_single(c);
+  if (rc) return rc;
+  lislam_batch* b = c->single;
+  if ((rc = lislam_batch_upload(b, points, 1, layout))) return rc;
+  if ((rc = lislam_batch_ground(b, 1))) return rc;
+  int n = 0;
+  if (plane && (rc = lislam_batch_download(b, LISLAM_OUT_GROUND_PLANE, 0, plane, 4, &n))) return rc;
+  if (info && (rc = lislam_batch_download(b, LISLAM_OUT_GROUND_INFO, 0, info, 4, &n))) return rc;
+  if (out) {
+    if ((rc = lislam_batch_download(b, LISLAM_OUT_GROUND, 0, out, cap, &n))) return rc;
+    if (n_out) *n_out = n;
+  }
   return LISLAM_OK;
 }
 

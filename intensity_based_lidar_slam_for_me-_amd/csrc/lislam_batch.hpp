@@ -36,6 +36,7 @@ struct lislam_batch {
   // queued on the context stream after it.
   hipEvent_t ev_images = nullptr;
   void* orb = nullptr;  // ORB engine of lislam_batch_intensity_odometry (lislam_orb.hip)
+  void* ground = nullptr;  // ground-plane engine of lislam_batch_ground (lislam_ground.hip)
   hipEvent_t get_event() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e = nullptr;
@@ -53,6 +54,9 @@ struct lislam_odom {
 };
 
 
+// Frees lislam_batch::ground / returns the device source of a ground output (lislam_ground.hip).
+void lislam_free_ground(void* p);
+int lislam_ground_batch_output(lislam_batch* b, int what, int scan, const void** src, int* cnt, size_t* esz);
 // Frees lislam_batch::orb (lislam_orb.hip).
 void lislam_free_orb(void* p);
 // Device source of the ORB outputs (LISLAM_OUT_ORB_*) of one scan (lislam_orb.hip).

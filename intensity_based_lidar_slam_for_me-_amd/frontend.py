@@ -101,6 +101,30 @@ class ScanRegistration:
                         lf[: out.n_less_flat], ir.reshape(H, W), ii.reshape(H, W), tr.reshape(H, W, 4))
 
 
+class ImageHandler:
+    """ImageHandler's ground stage (src/image_handler.h_ouster:41-100) on the GPU."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def ground_plane_extraction(self, points: np.ndarray, layout: nat.PointLayout | None = None):
+        """groundPlaneExtraction of one organized cloud (the context's n_scans x width points):
+        (GroundPointOut (m, 4) x y z 1, plane (4,) A B C D, info (4,) = status, RANSAC iterations,
+        best inliers, refit inliers; status 1 = ground, 0 = plane rejected by the n.z > cos 15 deg
+        test, -1 / -2 / -3 = no model)."""
+        c = self.ctx
+        N = c.n_scans * c.width
+        pts = np.ascontiguousarray(points)
+        out = np.zeros((N, 4), np.float32)
+        plane = np.zeros(4, np.float32)
+        info = np.zeros(4, np.int32)
+        n = ctypes.c_int32()
+        rc = c.lib.lislam_ground_extract(c.h, nat.ptr(pts), ctypes.byref(layout or PACKED_XYZI), nat.ptr(out), N,
+                                         ctypes.byref(n), nat.ptr(plane), nat.ptr(info))
+        nat.check(rc, c.h, "lislam_ground_extract")
+        return out[: n.value].copy(), plane, info
+
+
 class LaserOdometry:
     """laserOdometry node in forced-geometric mode (every frame is optimized)."""
 
@@ -157,6 +181,15 @@ class Batch:
         nat.check(rc, self.ctx.h, "lislam_batch_intensity_odometry")
         self._mask_keep = m
 
+    def ground(self, n: int):
+        """groundPlaneExtraction of scans [0, n) of the batch (results: ground_result)."""
+        nat.check(self.ctx.lib.lislam_batch_ground(self.h, n), self.ctx.h, "lislam_batch_ground")
+
+    def ground_result(self, scan: int):
+        """(GroundPointOut (m, 4), plane (4,), info (4,)) of one scan after ground()."""
+        return (self.download(nat.OUT_GROUND, scan), self.download(nat.OUT_GROUND_PLANE, scan),
+                self.download(nat.OUT_GROUND_INFO, scan))
+
     def set_timing(self, on: bool):
         nat.check(self.ctx.lib.lislam_batch_set_timing(self.h, int(on)), self.ctx.h, "lislam_batch_set_timing")
 
@@ -178,7 +211,8 @@ class Batch:
            nat.OUT_FLAT: (np.float32, 4), nat.OUT_LESS_FLAT: (np.float32, 4), nat.OUT_PARA: (np.float64, 1),
            nat.OUT_POSE: (np.float64, 1), nat.OUT_STATS: (np.int32, 1), nat.OUT_ORB_T: (np.float64, 1),
            nat.OUT_ORB_STATS: (np.int32, 1), nat.OUT_ORB_KEYPOINTS: (np.float32, 6), nat.OUT_ORB_POINTS: (np.float32, 4),
-           nat.OUT_ORB_DESCRIPTORS: (np.uint8, 32)}
+           nat.OUT_ORB_DESCRIPTORS: (np.uint8, 32), nat.OUT_GROUND: (np.float32, 4),
+           nat.OUT_GROUND_PLANE: (np.float32, 1), nat.OUT_GROUND_INFO: (np.int32, 1)}
 
     def download(self, what: int, scan: int) -> np.ndarray:
         dt, w = self._DT[what]

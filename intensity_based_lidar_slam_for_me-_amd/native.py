@@ -21,6 +21,7 @@ OUT_CURVATURE, OUT_LABEL, OUT_LINE_OFFSETS = 4, 5, 6
 OUT_SHARP, OUT_LESS_SHARP, OUT_FLAT, OUT_LESS_FLAT = 7, 8, 9, 10
 OUT_PARA, OUT_POSE, OUT_STATS = 11, 12, 13
 OUT_ORB_T, OUT_ORB_STATS, OUT_ORB_KEYPOINTS, OUT_ORB_POINTS, OUT_ORB_DESCRIPTORS = 14, 15, 16, 17, 18
+OUT_GROUND, OUT_GROUND_PLANE, OUT_GROUND_INFO = 19, 20, 21
 
 KERNELS = ("k_scan_front", "k_scan_lines", "k_scan_compact", "k_target_index", "k_odom_assoc", "k_odom_lm")
 
@@ -36,11 +37,12 @@ EXPORTED_SYMBOLS = (
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_laser_mapping",
     "lislam_map_set_timing", "lislam_map_kernel_times",
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
-    "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry",
+    "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
 )
 
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
-               "k_orb_fast", "k_orb_select", "k_orb_finish", "k_orb_blur", "k_orb_desc", "k_orb_match", "k_orb_lm")
+               "k_orb_fast", "k_orb_select", "k_orb_finish", "k_orb_blur", "k_orb_desc", "k_orb_match", "k_orb_lm",
+               "k_ground_screen", "k_ground_ransac", "k_ground_extract")
 
 MATCH_LINE, MATCH_PLANE = 0, 1
 
@@ -144,6 +146,8 @@ def load(path: str = LIB_PATH):
     L.lislam_intensity_tracker_destroy.argtypes = [vp]
     L.lislam_intensity_tracker_step.argtypes = [vp, vp, vp, vp, vp]
     L.lislam_batch_intensity_odometry.argtypes = [vp, _i32, _i32, vp]
+    L.lislam_batch_ground.argtypes = [vp, _i32]
+    L.lislam_ground_extract.argtypes = [vp, vp, ctypes.POINTER(PointLayout), vp, _i32, _i32p, vp, vp]
     L.lislam_map_set_timing.argtypes = [vp, _i32]
     L.lislam_map_kernel_times.argtypes = [vp, _fp, _i32p]
     for name in EXPORTED_SYMBOLS:

@@ -60,8 +60,23 @@ def lib():
         L.oracle_orb_fast.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p, _i32p]
         L.oracle_intensity_odometry.argtypes = [ctypes.c_int, _u8p, _f32p, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 _i32p, _f64p]
+        L.oracle_ground_extract.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _i32p]
+        L.oracle_ground_extract.restype = ctypes.c_int
         _LIB = L
     return _LIB
+
+
+def ground_extract(points: np.ndarray):
+    """ImageHandler::groundPlaneExtraction (image_handler.h_ouster:41-100) of one cloud
+    ((n, 3|4) float32, or an organized (H, W, 4) scan).  Returns (ground (m, 4) x y z 1,
+    plane (4,) float32 A B C D, info (4,) int32 = status, iterations, best inliers, refit inliers)."""
+    P = np.ascontiguousarray(points, np.float32)
+    P = P.reshape(-1, P.shape[-1])
+    out = np.zeros((P.shape[0], 4), np.float32)
+    plane = np.zeros(4, np.float32)
+    info = np.zeros(4, np.int32)
+    m = lib().oracle_ground_extract(P, P.shape[0], P.shape[1], out, plane, info)
+    return out[:m].copy(), plane, info
 
 
 @dataclass
