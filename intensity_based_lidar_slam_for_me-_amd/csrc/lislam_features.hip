@@ -17,7 +17,8 @@
 //                  (curvature, index) keys in LDS (:445), the sharp / flat greedy walks with
 //                  ±5 neighbour suppression as ballot scans (:450-568), the less-flat collection
 //                  (:570-577) and a PCL-semantics VoxelGrid(0.2) of the line (:579-589).
-//   k_scan_compact one workgroup per scan: concatenates the per-line outputs in line order.
+//   k_scan_compact one wave per (scan, line): concatenates the per-line outputs in line order
+//                  (offsets = wave sums of the earlier lines' counts).
 #include <hip/hip_runtime.h>
 
 #include "lislam_device.hpp"
@@ -948,36 +949,43 @@ extern "C" int lislam_debug_phase_cycles(unsigned long long* out) {
 #endif
 
 // ------------------------------------------------------------------------------- compaction
-__global__ __launch_bounds__(256) void k_scan_compact(FeatureArgs a) {
-  const int s = blockIdx.x;
-  const int H = a.H, N = a.N;
-  __shared__ int pre[4][kMaxLines + 1];
+// One wave per (scan, line): the line's offsets in the four concatenated clouds are wave sums of
+// the earlier lines' counts, then the wave copies its line's staged features.
+__global__ __launch_bounds__(64) void k_scan_compact(FeatureArgs a) {
+  const int s = blockIdx.x / a.H, l = blockIdx.x % a.H;
+  const int H = a.H, N = a.N, lane = lane_id();
   const int* lc = a.line_counts + (size_t)s * H * 4;
-  if (threadIdx.x < 4) {
-    const int f = threadIdx.x;
-    int acc = 0;
-    for (int l = 0; l < H; l++) { pre[f][l] = acc; acc += lc[l * 4 + f]; }
-    pre[f][H] = acc;
-    a.n_feat[s * 4 + f] = acc;
-    if (f == 1 || f == 3) {  // line offsets of the clouds the odometry searches
-      int* lo = a.feat_loff + ((size_t)s * 2 + (f == 1 ? 0 : 1)) * (H + 1);
-      for (int l = 0; l <= H; l++) lo[l] = pre[f][l];
+  int pre[4], cnt[4];
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    uint32_t v = 0;
+    for (int k = lane; k < l; k += 64) v += (uint32_t)lc[k * 4 + f];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    pre[f] = (int)v;
+    cnt[f] = lc[l * 4 + f];
+  }
+  if (lane == 0) {
+    int* lo1 = a.feat_loff + ((size_t)s * 2 + 0) * (H + 1);
+    int* lo3 = a.feat_loff + ((size_t)s * 2 + 1) * (H + 1);
+    lo1[l] = pre[1];
+    lo3[l] = pre[3];
+    if (l == H - 1) {  // totals (sharp, less-sharp, flat, less-flat) and the closing offsets
+      lo1[H] = pre[1] + cnt[1];
+      lo3[H] = pre[3] + cnt[3];
+      for (int f = 0; f < 4; f++) a.n_feat[s * 4 + f] = pre[f] + cnt[f];
     }
   }
-  __syncthreads();
-  const int* lo = a.line_off + (size_t)s * (H + 1);
-  for (int l = 0; l < H; l++) {
-    const size_t stg = (size_t)s * H + l;
-    for (int k = threadIdx.x; k < lc[l * 4 + 0]; k += 256)
-      st4(a.sharp + (size_t)s * a.cap_sharp + pre[0][l] + k, ld4(a.stg_sharp + stg * kCapSharpPerLine + k));
-    for (int k = threadIdx.x; k < lc[l * 4 + 1]; k += 256)
-      st4(a.less_sharp + (size_t)s * a.cap_less_sharp + pre[1][l] + k,
-          ld4(a.stg_less_sharp + stg * kCapLessSharpPerLine + k));
-    for (int k = threadIdx.x; k < lc[l * 4 + 2]; k += 256)
-      st4(a.flat + (size_t)s * a.cap_flat + pre[2][l] + k, ld4(a.stg_flat + stg * kCapFlatPerLine + k));
-    for (int k = threadIdx.x; k < lc[l * 4 + 3]; k += 256)
-      st4(a.less_flat + (size_t)s * N + pre[3][l] + k, ld4(a.stg_less_flat + (size_t)s * N + lo[l] + k));
-  }
+  const size_t stg = (size_t)s * H + l;
+  for (int k = lane; k < cnt[0]; k += 64)
+    st4(a.sharp + (size_t)s * a.cap_sharp + pre[0] + k, ld4(a.stg_sharp + stg * kCapSharpPerLine + k));
+  for (int k = lane; k < cnt[1]; k += 64)
+    st4(a.less_sharp + (size_t)s * a.cap_less_sharp + pre[1] + k, ld4(a.stg_less_sharp + stg * kCapLessSharpPerLine + k));
+  for (int k = lane; k < cnt[2]; k += 64)
+    st4(a.flat + (size_t)s * a.cap_flat + pre[2] + k, ld4(a.stg_flat + stg * kCapFlatPerLine + k));
+  const int off = a.line_off[(size_t)s * (H + 1) + l];
+  for (int k = lane; k < cnt[3]; k += 64)
+    st4(a.less_flat + (size_t)s * N + pre[3] + k, ld4(a.stg_less_flat + (size_t)s * N + off + k));
 }
 
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEvent_t images_ready) {
@@ -996,7 +1004,7 @@ void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEv
   else
     hipLaunchKernelGGL(k_scan_lines<32>, dim3(a.S * a.H), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(k_scan_compact, dim3(a.S), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_scan_compact, dim3(a.S * a.H), dim3(64), 0, st, a);
   if (ev) (void)hipEventRecord(ev[3], st);
 }
 

@@ -767,8 +767,29 @@ __device__ __forceinline__ void evaluate(LmShared& sh, const double* blk, const 
   __syncthreads();
 }
 
+#ifdef LISLAM_PHASE_PROF
+__device__ unsigned long long g_lm_phase[8];
+extern "C" int lislam_debug_lm_phases(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_phase), sizeof(g_lm_phase)) != hipSuccess) return -2;
+  static const unsigned long long zero[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_lm_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+#define LM_PHASE(i)                                                     \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); \
+      atomicAdd(&g_lm_phase[i], now_ - t_ph);                           \
+      t_ph = now_;                                                      \
+    }                                                                   \
+  } while (0)
+#else
+#define LM_PHASE(i)
+#endif
 __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int outer) {
   __shared__ LmShared sh;
+#ifdef LISLAM_PHASE_PROF
+  unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
+#endif
   const int c = a.c0 + blockIdx.x;
   int k;
   if (!pair_of(a, c, r, &k)) return;
@@ -796,8 +817,10 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
     __syncthreads();
     go = sh.flag;
   }
+  LM_PHASE(0);
   while (go) {
     evaluate(sh, blk, kind, ns, a.cap_sharp, nf);  // cost + J^T J + J^T r at the candidate
+    LM_PHASE(1);
     if (threadIdx.x == 0) {
       const bool cont = lm_next(lm, sh.acc, a.max_iterations);
       sh.flag = cont;
@@ -805,6 +828,7 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
         for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
+    LM_PHASE(2);
     go = sh.flag;
   }
   if (threadIdx.x != 0) return;

@@ -25,6 +25,28 @@ if sys.argv[1] == "build":
                     *srcs], check=True, cwd=g.CSRC)
     sys.exit(0)
 
+if sys.argv[1] == "lm":  # k_odom_lm: first evaluation + start, later evaluations, step logic
+    pkg = g.package()
+    L = pkg.native.load(OUT)
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+    scans = pkg.synth.make_sequence(S)
+    buf = (ctypes.c_ulonglong * 8)()
+    with pkg.Context() as ctx:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, 10)
+        ctx.synchronize()
+        L.lislam_debug_lm_phases(buf)
+        b.odometry(S, 10)
+        ctx.synchronize()
+        L.lislam_debug_lm_phases(buf)
+        nwg = 2 * 10 * ((S - 1 + 9) // 10)
+        for i, nm in enumerate(["first eval + start", "evaluations", "steps (thread 0)"]):
+            print(f"{nm:20s} {buf[i] / 100.0 / nwg:9.1f} us per workgroup")
+        b.close()
+    sys.exit(0)
+
 if sys.argv[1] == "waves":  # per-wave timeline of one association launch (round R, outer pass 1)
     import numpy as np
     import torch
