@@ -618,7 +618,7 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
 // where the state lives.
 template <int kS>
 __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int line, LineLists& ll, uint64_t* lmask,
-                                              P4* stage) {
+                                              P4* stage, P4* ring) {
   const int lane = lane_id();
   const int N = a.N, H = a.H;
   const int* lo = a.line_off + (size_t)s * (H + 1);
@@ -631,20 +631,39 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   int8_t* glabel = a.label + (size_t)s * N;
   PHASE_BEGIN;
 
-  // curvature (scanRegistration.cpp:397-412) and neighbour links (suppress)
+  // curvature (scanRegistration.cpp:397-412) and neighbour links (suppress).  Every point of the
+  // line (and the 64 before / after it) is loaded once: slot t's neighbours come from an LDS ring
+  // of three 64-point slots (t - 1, t, t + 1), the next slot's load in flight meanwhile.
   float cr[kS];
   uint32_t linkb = 0;
+  auto ld_slot = [&](int t) -> P4 {  // cloud point off + 64 t + lane (zero outside the cloud)
+    const int i = off + 64 * t + lane;
+    return (i >= 0 && i < total) ? ld4(cloud + i) : P4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto ring_at = [&](int t) -> P4* { return ring + 64 * ((t + 3) % 3); };  // slot t >= -1
+  ring_at(-1)[lane] = ld_slot(-1);
+  ring_at(0)[lane] = ld_slot(0);
+  P4 nxt = ld_slot(1);
 #pragma unroll
   for (int t = 0; t < kS; t++) {
     cr[t] = 0.f;
     if (t >= nsl) continue;
+    ring_at(t + 1)[lane] = nxt;
+    if (t + 1 < nsl) nxt = ld_slot(t + 2);
+    wave_sync<true>();
     const int k = lane + 64 * t;
     if (k < len) {
       const int i = off + k;
+      // point k + d of the line: slot t + ((lane + d + 64) >> 6) - 1, lane (lane + d) & 63
+      auto nb = [&](int d) -> P4 {
+        const int j = lane + d + 64;
+        return ring_at(t + (j >> 6) - 1)[j & 63];
+      };
       float c = 0.f;
       if (i >= 5 && i < total - 5) {
         P4 q[11];
-        for (int d = 0; d < 11; d++) q[d] = ld4(cloud + i - 5 + d);
+#pragma unroll
+        for (int d = 0; d < 11; d++) q[d] = nb(d - 5);
         const float dX = q[0].x + q[1].x + q[2].x + q[3].x + q[4].x - 10 * q[5].x + q[6].x + q[7].x + q[8].x + q[9].x + q[10].x;
         const float dY = q[0].y + q[1].y + q[2].y + q[3].y + q[4].y - 10 * q[5].y + q[6].y + q[7].y + q[8].y + q[9].y + q[10].y;
         const float dZ = q[0].z + q[1].z + q[2].z + q[3].z + q[4].z - 10 * q[5].z + q[6].z + q[7].z + q[8].z + q[9].z + q[10].z;
@@ -653,12 +672,12 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       curv[i] = c;
       cr[t] = c;
       if (k + 1 < len) {
-        const P4 p0 = ld4(cloud + i), p1 = ld4(cloud + i + 1);
+        const P4 p0 = nb(0), p1 = nb(1);
         const float dx = p1.x - p0.x, dy = p1.y - p0.y, dz = p1.z - p0.z;
         if (!((double)(dx * dx + dy * dy + dz * dz) > 0.05)) linkb |= 1u << t;
       }
     }
-    __builtin_amdgcn_sched_barrier(0);  // one slot's 13 loads in flight at a time (registers)
+    wave_sync<true>();  // slot t - 1's ring entry is overwritten next
   }
   // lmask[1 + t]: link bits of points 64 t .. 64 t + 63; lmask[0] / lmask[kS + 1] stay zero
 #pragma unroll
@@ -930,12 +949,13 @@ template <int kS>
 __global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
   __shared__ LineLists ll;
   __shared__ P4 stage[64];
+  __shared__ P4 ring[3 * 64];
   __shared__ uint64_t lmask[kS + 2];
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
   if (len <= 64 * kS)
-    line_body_reg<kS>(a, s, line, ll, lmask, stage);
+    line_body_reg<kS>(a, s, line, ll, lmask, stage, ring);
   else
     line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, ll, stage);
 }
