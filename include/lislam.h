@@ -277,6 +277,26 @@ int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const doub
 int lislam_laser_mapping(lislam_map* corner_map, lislam_map* surf_map, const float* corner, int32_t n_corner,
                          const float* surf, int32_t n_surf, double* x, int32_t* stats);
 
+/* ---- laserMapping's cube map (laserMapping.cpp:70-99, 319-1002), device
+ * resident: 21 x 21 x 11 cubes of 50 m holding the corner / surf points in map frame. */
+typedef struct lislam_lmap lislam_lmap;
+/* line_res / plane_res: mapping_line_resolution / mapping_plane_resolution (spot.launch: 0.4 / 0.8). */
+int lislam_lmap_create(lislam_ctx* ctx, float line_res, float plane_res, lislam_lmap** out);
+int lislam_lmap_destroy(lislam_lmap* m);
+/* One laserMapping::process frame without publishing: corner_last / surf_last (stride 4, sensor
+ * frame, host or device), odom = q_wodom_curr, t_wodom_curr (7); state (in/out) = q_wmap_wodom,
+ * t_wmap_wodom (7); out_pose = q_w_curr, t_w_curr (7).  transformAssociateToMap, cube re-centring,
+ * the local map of the valid cubes, VoxelGrid of the current clouds, the optimization of
+ * lislam_laser_mapping when the map holds > 10 corner and > 50 surf points, transformUpdate,
+ * insertion and the VoxelGrid of every valid cube.  stats[8] (nullable) = corner / surf local-map
+ * sizes, corner / surf stack sizes, lislam_laser_mapping's stats (-1 when not optimized). */
+int lislam_lmap_step(lislam_lmap* m, const float* corner_last, int32_t nc, const float* surf_last, int32_t ns,
+                     const double* odom, double* state, double* out_pose, int32_t* stats);
+/* Points per cube (cube index order, 4851 each; either nullable) and a whole cloud (0 corner,
+ * 1 surf) as x, y, z, intensity in cube order (out nullable: *n only). */
+int lislam_lmap_counts(lislam_lmap* m, int32_t* corner_counts, int32_t* surf_counts);
+int lislam_lmap_points(lislam_lmap* m, int32_t which, float* out, int64_t cap, int64_t* n);
+
 /* HIP-event timing of the mapping kernels of a context (recorded on its stream, no host sync
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and

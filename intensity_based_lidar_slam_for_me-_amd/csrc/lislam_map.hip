@@ -1583,3 +1583,475 @@ int lislam_laser_mapping(lislam_map* mc, lislam_map* ms, const float* corner, in
 }
 
 }  // extern "C"
+
+// ===================================================================== laserMapping cube map
+// The A-LOAM local map of laserMapping::process (laserMapping.cpp:70-99,
+// 319-1002) kept on the device.  Semantics: oracle/oracle_map.cpp oracle_lmap_step.
+//   pool     per cloud (corner, surf): points float4 (x, y, z, intensity) sorted by cube index,
+//            with the cube index of each point and the CSR offsets of the 4851 cubes
+//   shift    re-centring moves cube (i, j, k) to (i + si, j + sj, k + sk) and clears the cubes
+//            that wrap around: a translation of every index — order-preserving — plus a drop
+//   local    the valid cubes (i, j, k loop order) concatenated into the maps the optimization
+//            searches (lislam_map_build + lislam_laser_mapping)
+//   update   the voxelized current clouds at the optimized pose join their cubes after the old
+//            points, and every valid cube is voxelized: one stable radix sort of
+//            (cube << 32 | voxel index) keys over old + new points — non-valid (and too-fine)
+//            cubes key by position, so each point is its own voxel and passes unchanged
+namespace lislam {
+namespace cubek {
+
+constexpr int kW = 21, kH = 21, kD = 11, kNC = kW * kH * kD;
+
+struct CubeSeg {  // per valid cube: VoxelGrid parameters of its points (old + new)
+  unsigned mn[3], mx[3];  // ord_f-encoded bounds
+  int min_b[3], mul1, mul2, overflow;
+};
+
+__device__ __forceinline__ int cube_of(double v, int cen) {
+  int c = int((v + 25.0) / 50.0) + cen;
+  if (v + 25.0 < 0) c--;
+  return c;
+}
+
+// re-centring: the kept flag and the translated cube index of every pool point
+__global__ void k_cm_shift(const int* cube, int n, int si, int sj, int sk, int* keep, int* ncube) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = cube[i];
+  const int ci = c % kW + si, cj = (c / kW) % kH + sj, ck = c / (kW * kH) + sk;
+  const bool ok = ci >= 0 && ci < kW && cj >= 0 && cj < kH && ck >= 0 && ck < kD;
+  keep[i] = ok;
+  ncube[i] = ok ? ci + kW * cj + kW * kH * ck : -1;
+}
+
+// CSR offsets of the cubes over a pool sorted by cube (off[kNC] = n)
+__global__ void k_cm_offsets(const int* cube, int n, int* off) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > kNC) return;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cube[mid] < c) lo = mid + 1; else hi = mid;
+  }
+  off[c] = lo;
+}
+
+// local map: workgroup v copies valid cube v (loop order) to its place in the concatenation
+__global__ __launch_bounds__(256) void k_cm_gather(const int* valid, int nvalid, const int* off, const float4* pts,
+                                                   float4* out, int* n_out) {
+  const int v = blockIdx.x;
+  int pre = 0;
+  for (int u = 0; u < v; u++) pre += off[valid[u] + 1] - off[valid[u]];
+  const int c = valid[v], b = off[c], cnt = off[c + 1] - b;
+  for (int k = threadIdx.x; k < cnt; k += blockDim.x) out[pre + k] = pts[b + k];
+  if (v == nvalid - 1 && threadIdx.x == 0) *n_out = pre + cnt;
+}
+
+// new points: pointAssociateToMap at the pose x (laserMapping.cpp:152-161) and their cube
+__global__ void k_cm_newpts(const float4* in, const int* n_in, const double* x, int cenW, int cenH, int cenD,
+                            float4* out, int* cube) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_in) return;
+  const float4 p = in[i];
+  const float4 w = mapk::to_world(x, p.x, p.y, p.z);
+  const int ci = cube_of(w.x, cenW), cj = cube_of(w.y, cenH), ck = cube_of(w.z, cenD);
+  const bool ok = ci >= 0 && ci < kW && cj >= 0 && cj < kH && ck >= 0 && ck < kD;
+  out[i] = make_float4(w.x, w.y, w.z, p.w);
+  cube[i] = ok ? ci + kW * cj + kW * kH * ck : -1;
+}
+
+// bounds and VoxelGrid parameters of valid cube v: its old pool points and its new points
+__global__ __launch_bounds__(256) void k_cm_bounds(const int* valid, const int* off, const float4* pts, const float4* newp,
+                                                   const int* ncube, const int* n_new, float inv, CubeSeg* seg) {
+  __shared__ unsigned smn[3][4], smx[3][4];
+  const int v = blockIdx.x, c = valid[v];
+  unsigned mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+  auto add = [&](float4 p) {
+    const unsigned q[3] = {mapk::ord_f(p.x), mapk::ord_f(p.y), mapk::ord_f(p.z)};
+    for (int k = 0; k < 3; k++) { mn[k] = min(mn[k], q[k]); mx[k] = max(mx[k], q[k]); }
+  };
+  for (int i = off[c] + threadIdx.x; i < off[c + 1]; i += blockDim.x) add(pts[i]);
+  for (int i = threadIdx.x; i < *n_new; i += blockDim.x)
+    if (ncube[i] == c) add(newp[i]);
+  for (int o = 32; o > 0; o >>= 1)
+    for (int k = 0; k < 3; k++) {
+      mn[k] = min(mn[k], (unsigned)__shfl_xor((int)mn[k], o));
+      mx[k] = max(mx[k], (unsigned)__shfl_xor((int)mx[k], o));
+    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 3; k++) { smn[k][w] = mn[k]; smx[k][w] = mx[k]; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  CubeSeg s;
+  float fmn[3], fmx[3];
+  for (int k = 0; k < 3; k++) {
+    unsigned a0 = smn[k][0], a1 = smx[k][0];
+    for (int j = 1; j < 4; j++) { a0 = min(a0, smn[k][j]); a1 = max(a1, smx[k][j]); }
+    s.mn[k] = a0; s.mx[k] = a1;
+    fmn[k] = mapk::unord_f(a0); fmx[k] = mapk::unord_f(a1);
+  }
+  // pcl::VoxelGrid::applyFilter (as k_vg_keys): 32-bit index space or the input unchanged
+  const int64_t dx = (int64_t)((fmx[0] - fmn[0]) * inv) + 1, dy = (int64_t)((fmx[1] - fmn[1]) * inv) + 1,
+                dz = (int64_t)((fmx[2] - fmn[2]) * inv) + 1;
+  s.overflow = dx * dy * dz > (int64_t)0x7fffffff;
+  int div_b[3];
+  for (int k = 0; k < 3; k++) {
+    s.min_b[k] = (int)floorf(fmn[k] * inv);
+    div_b[k] = (int)floorf(fmx[k] * inv) - s.min_b[k] + 1;
+  }
+  s.mul1 = div_b[0];
+  s.mul2 = div_b[0] * div_b[1];
+  seg[v] = s;
+}
+
+// keys over the concatenation [pool (n_pool), new points]: cube << 32 | voxel index in a
+// valid cube, | concatenation index otherwise; dropped new points sort last
+__global__ void k_cm_keys(const float4* pts, const int* cube, int n_pool, const float4* newp, const int* ncube,
+                          const int* n_new, const int* vrank, const CubeSeg* seg, float inv, uint64_t* keys, int* idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = n_pool + *n_new;
+  if (i >= m) return;
+  const bool old = i < n_pool;
+  const int c = old ? cube[i] : ncube[i - n_pool];
+  idx[i] = i;
+  if (c < 0) { keys[i] = ~0ull; return; }
+  const int v = vrank[c];
+  uint32_t low = (uint32_t)i;
+  if (v >= 0 && !seg[v].overflow) {
+    const float4 p = old ? pts[i] : newp[i - n_pool];
+    const CubeSeg& s = seg[v];
+    const int i0 = (int)(floorf(p.x * inv) - (float)s.min_b[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)s.min_b[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)s.min_b[2]);
+    low = (uint32_t)(i0 + i1 * s.mul1 + i2 * s.mul2);
+  }
+  keys[i] = ((uint64_t)(uint32_t)c << 32) | low;
+}
+
+__global__ void k_cm_runs(const uint64_t* skeys, const int* n_pool_new, int n_pool, int* flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pool + *n_pool_new) return;
+  flag[i] = skeys[i] != ~0ull && (i == 0 || skeys[i] != skeys[i - 1]) ? 1 : 0;
+}
+
+// centroids of the runs (sums in concatenation order), cube index from the key
+__global__ void k_cm_centroids(const float4* pts, int n_pool, const float4* newp, const int* n_new, const uint64_t* skeys,
+                               const int* sidx, const int* pos, const int* flag, float4* out, int* ocube, int* n_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = n_pool + *n_new;
+  if (i == 0) *n_out = m > 0 ? pos[m - 1] + flag[m - 1] : 0;
+  if (i >= m || !flag[i]) return;
+  auto at = [&](int j) { const int s = sidx[j]; return s < n_pool ? pts[s] : newp[s - n_pool]; };
+  float4 c = at(i);
+  int e = i + 1;
+  for (; e < m && skeys[e] == skeys[i]; e++) {
+    const float4 p = at(e);
+    c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
+  }
+  const float cnt = (float)(e - i);
+  c.x /= cnt; c.y /= cnt; c.z /= cnt; c.w /= cnt;
+  out[pos[i]] = c;
+  ocube[pos[i]] = (int)(skeys[i] >> 32);
+}
+
+__global__ void k_cm_vrank(int* vrank) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < kNC) vrank[c] = -1;
+}
+__global__ void k_cm_vrank_set(const int* valid, int nvalid, int* vrank) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < nvalid) vrank[valid[v]] = v;
+}
+
+}  // namespace cubek
+}  // namespace lislam
+
+namespace {
+// host restatements of the Eigen double quaternion operations (lislam_device.hpp term grouping)
+void h_qmul(const double* a, const double* b, double* r) {
+  r[0] = (a[3] * b[0] + a[1] * b[2]) + (-(a[2] * b[1] - a[0] * b[3]));
+  r[1] = (a[3] * b[1] + a[1] * b[3]) + (a[2] * b[0] - a[0] * b[2]);
+  r[2] = (a[3] * b[2] - a[1] * b[0]) + (a[2] * b[3] + a[0] * b[1]);
+  r[3] = (a[3] * b[3] - a[1] * b[1]) + (-(a[2] * b[2] + a[0] * b[0]));
+}
+void h_qrot(const double* q, const double* v, double* o) {
+  double u[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2], q[0] * v[1] - q[1] * v[0]};
+  for (int k = 0; k < 3; k++) u[k] = u[k] + u[k];
+  const double c[3] = {q[1] * u[2] - q[2] * u[1], q[2] * u[0] - q[0] * u[2], q[0] * u[1] - q[1] * u[0]};
+  for (int k = 0; k < 3; k++) o[k] = (v[k] + q[3] * u[k]) + c[k];
+}
+int h_cube_of(double v, int cen) {
+  int c = int((v + 25.0) / 50.0) + cen;
+  if (v + 25.0 < 0) c--;
+  return c;
+}
+}  // namespace
+
+struct lislam_lmap {
+  lislam_ctx* ctx = nullptr;
+  float res[2] = {0.4f, 0.8f};  // line (corner), plane (surf) resolutions
+  int cen[3] = {10, 10, 5};
+  int64_t n[2] = {0, 0};
+  DBuf pts[2], cube[2], off[2], tmp_pts, tmp_cube, keep, local[2], counts, valid, vrank, seg, newp, ncube, keys, keys2,
+      idx, idx2, flag, pos, sort_tmp, x, stack[2];
+  lislam_map* maps[2] = {nullptr, nullptr};
+  MapScratch sc;
+};
+
+namespace {
+
+using namespace lislam::cubek;
+
+// offsets of pool w after its points / cubes changed (n on the host)
+int cm_offsets(lislam_lmap* L, int w) {
+  lislam_ctx* c = L->ctx;
+  MCHK(c, L->off[w].reserve((kNC + 1) * sizeof(int)));
+  hipLaunchKernelGGL(k_cm_offsets, dim3(blocks(kNC + 1)), dim3(256), 0, stream_of(c), L->cube[w].as<int>(), (int)L->n[w],
+                     L->off[w].as<int>());
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// re-centring of pool w by (si, sj, sk)
+int cm_shift(lislam_lmap* L, int w, int si, int sj, int sk) {
+  lislam_ctx* c = L->ctx;
+  hipStream_t st = stream_of(c);
+  const int n = (int)L->n[w];
+  if (n == 0) return LISLAM_OK;
+  MCHK(c, L->keep.reserve((size_t)n * 4));
+  MCHK(c, L->tmp_cube.reserve((size_t)n * 4));
+  MCHK(c, L->tmp_pts.reserve((size_t)n * 16));
+  MCHK(c, L->counts.reserve(64));
+  hipLaunchKernelGGL(k_cm_shift, dim3(blocks(n)), dim3(256), 0, st, L->cube[w].as<int>(), n, si, sj, sk,
+                     L->keep.as<int>(), L->tmp_cube.as<int>());
+  size_t tb = 0, tb2 = 0;
+  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, L->pts[w].as<float4>(), L->keep.as<int>(), L->tmp_pts.as<float4>(),
+                                        L->counts.as<int>(), n, st));
+  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb2, L->tmp_cube.as<int>(), L->keep.as<int>(), L->cube[w].as<int>(),
+                                        L->counts.as<int>() + 1, n, st));
+  MCHK(c, L->sort_tmp.reserve(std::max(tb, tb2)));
+  MCHK(c, hipcub::DeviceSelect::Flagged(L->sort_tmp.p, tb, L->pts[w].as<float4>(), L->keep.as<int>(),
+                                        L->tmp_pts.as<float4>(), L->counts.as<int>(), n, st));
+  MCHK(c, hipcub::DeviceSelect::Flagged(L->sort_tmp.p, tb2, L->tmp_cube.as<int>(), L->keep.as<int>(),
+                                        L->cube[w].as<int>(), L->counts.as<int>() + 1, n, st));
+  int kept = 0;
+  MCHK(c, hipMemcpyAsync(&kept, L->counts.p, 4, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  MCHK(c, hipMemcpyAsync(L->pts[w].p, L->tmp_pts.p, (size_t)kept * 16, hipMemcpyDeviceToDevice, st));
+  L->n[w] = kept;
+  return cm_offsets(L, w);
+}
+
+// insertion of the (device, count on the device) stack of cloud w at the pose on the device, then
+// the VoxelGrid of every valid cube
+int cm_update(lislam_lmap* L, int w, const float4* stack, const int* n_stack, int n_stack_host, int nvalid) {
+  lislam_ctx* c = L->ctx;
+  hipStream_t st = stream_of(c);
+  const int np = (int)L->n[w], nn = n_stack_host, m = np + nn;
+  const float inv = 1.0f / L->res[w];
+  MCHK(c, L->newp.reserve((size_t)std::max(nn, 1) * 16));
+  MCHK(c, L->ncube.reserve((size_t)std::max(nn, 1) * 4));
+  if (nn > 0)
+    hipLaunchKernelGGL(k_cm_newpts, dim3(blocks(nn)), dim3(256), 0, st, stack, n_stack, L->x.as<double>(), L->cen[0],
+                       L->cen[1], L->cen[2], L->newp.as<float4>(), L->ncube.as<int>());
+  if (m == 0) return LISLAM_OK;
+  MCHK(c, L->seg.reserve((size_t)std::max(nvalid, 1) * sizeof(CubeSeg)));
+  if (nvalid > 0)
+    hipLaunchKernelGGL(k_cm_bounds, dim3(nvalid), dim3(256), 0, st, L->valid.as<int>(), L->off[w].as<int>(),
+                       L->pts[w].as<float4>(), L->newp.as<float4>(), L->ncube.as<int>(), n_stack, inv, L->seg.as<CubeSeg>());
+  MCHK(c, L->keys.reserve((size_t)m * 8));
+  MCHK(c, L->keys2.reserve((size_t)m * 8));
+  MCHK(c, L->idx.reserve((size_t)m * 4));
+  MCHK(c, L->idx2.reserve((size_t)m * 4));
+  MCHK(c, L->flag.reserve((size_t)m * 4));
+  MCHK(c, L->pos.reserve((size_t)m * 4));
+  hipLaunchKernelGGL(k_cm_keys, dim3(blocks(m)), dim3(256), 0, st, L->pts[w].as<float4>(), L->cube[w].as<int>(), np,
+                     L->newp.as<float4>(), L->ncube.as<int>(), n_stack, L->vrank.as<int>(), L->seg.as<CubeSeg>(), inv,
+                     L->keys.as<uint64_t>(), L->idx.as<int>());
+  MRC(sort_pairs_u64(c, L->sort_tmp, L->keys.as<uint64_t>(), L->keys2.as<uint64_t>(), L->idx.as<int>(),
+                     L->idx2.as<int>(), m));
+  hipLaunchKernelGGL(k_cm_runs, dim3(blocks(m)), dim3(256), 0, st, L->keys2.as<uint64_t>(), n_stack, np, L->flag.as<int>());
+  size_t tb = 0;
+  MCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, L->flag.as<int>(), L->pos.as<int>(), m, st));
+  MCHK(c, L->sort_tmp.reserve(tb));
+  MCHK(c, hipcub::DeviceScan::ExclusiveSum(L->sort_tmp.p, tb, L->flag.as<int>(), L->pos.as<int>(), m, st));
+  MCHK(c, L->tmp_pts.reserve((size_t)m * 16));
+  MCHK(c, L->tmp_cube.reserve((size_t)m * 4));
+  MCHK(c, L->counts.reserve(64));
+  hipLaunchKernelGGL(k_cm_centroids, dim3(blocks(m)), dim3(256), 0, st, L->pts[w].as<float4>(), np, L->newp.as<float4>(),
+                     n_stack, L->keys2.as<uint64_t>(), L->idx2.as<int>(), L->pos.as<int>(), L->flag.as<int>(),
+                     L->tmp_pts.as<float4>(), L->tmp_cube.as<int>(), L->counts.as<int>() + 2);
+  MCHK(c, hipGetLastError());
+  int nout = 0;
+  MCHK(c, hipMemcpyAsync(&nout, L->counts.as<int>() + 2, 4, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  MCHK(c, L->pts[w].reserve((size_t)std::max(nout, 1) * 16));
+  MCHK(c, L->cube[w].reserve((size_t)std::max(nout, 1) * 4));
+  MCHK(c, hipMemcpyAsync(L->pts[w].p, L->tmp_pts.p, (size_t)nout * 16, hipMemcpyDeviceToDevice, st));
+  MCHK(c, hipMemcpyAsync(L->cube[w].p, L->tmp_cube.p, (size_t)nout * 4, hipMemcpyDeviceToDevice, st));
+  L->n[w] = nout;
+  return cm_offsets(L, w);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lislam_lmap_create(lislam_ctx* c, float line_res, float plane_res, lislam_lmap** out) {
+  if (!c || !out || !(line_res > 0) || !(plane_res > 0)) return LISLAM_ERR_ARG;
+  *out = nullptr;
+  hipSetDevice(c->device);
+  lislam_lmap* L = new lislam_lmap();
+  L->ctx = c;
+  L->res[0] = line_res;
+  L->res[1] = plane_res;
+  const lislam_map_config mc{0.4f, 0.0f};
+  int rc = LISLAM_OK;
+  for (int w = 0; w < 2 && !rc; w++) {
+    rc = lislam_map_create(c, &mc, &L->maps[w]);
+    if (!rc && L->off[w].reserve((kNC + 1) * sizeof(int)) != hipSuccess) rc = LISLAM_ERR_DEVICE;
+    if (!rc && hipMemsetAsync(L->off[w].p, 0, (kNC + 1) * sizeof(int), c->stream) != hipSuccess) rc = LISLAM_ERR_DEVICE;
+  }
+  if (!rc && (L->vrank.reserve(kNC * sizeof(int)) != hipSuccess || L->valid.reserve(128 * sizeof(int)) != hipSuccess ||
+              L->x.reserve(64) != hipSuccess))
+    rc = LISLAM_ERR_DEVICE;
+  if (rc) {
+    for (auto* m : L->maps) lislam_map_destroy(m);
+    delete L;
+    return mfail(c, LISLAM_ERR_DEVICE, "lislam_lmap_create failed");
+  }
+  *out = L;
+  return LISLAM_OK;
+}
+
+int lislam_lmap_destroy(lislam_lmap* L) {
+  if (!L) return LISLAM_OK;
+  hipSetDevice(L->ctx->device);
+  (void)hipStreamSynchronize(L->ctx->stream);
+  for (auto* m : L->maps) lislam_map_destroy(m);
+  delete L;
+  return LISLAM_OK;
+}
+
+int lislam_lmap_counts(lislam_lmap* L, int32_t* corner_counts, int32_t* surf_counts) {
+  if (!L) return LISLAM_ERR_ARG;
+  lislam_ctx* c = L->ctx;
+  hipSetDevice(c->device);
+  int32_t* dst[2] = {corner_counts, surf_counts};
+  for (int w = 0; w < 2; w++) {
+    if (!dst[w]) continue;
+    std::vector<int> off(kNC + 1);
+    MCHK(c, hipMemcpyAsync(off.data(), L->off[w].p, off.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    MCHK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < kNC; k++) dst[w][k] = off[k + 1] - off[k];
+  }
+  return LISLAM_OK;
+}
+
+int lislam_lmap_points(lislam_lmap* L, int32_t which, float* out, int64_t cap, int64_t* n) {
+  if (!L || which < 0 || which > 1 || !n) return LISLAM_ERR_ARG;
+  lislam_ctx* c = L->ctx;
+  hipSetDevice(c->device);
+  *n = L->n[which];
+  if (!out) return LISLAM_OK;
+  if (L->n[which] > cap) return mfail(c, LISLAM_ERR_CAPACITY, "lislam_lmap_points: %lld points, cap %lld",
+                                      (long long)L->n[which], (long long)cap);
+  if (L->n[which]) MCHK(c, hipMemcpyAsync(out, L->pts[which].p, (size_t)L->n[which] * 16, hipMemcpyDefault, c->stream));
+  MCHK(c, hipStreamSynchronize(c->stream));
+  return LISLAM_OK;
+}
+
+int lislam_lmap_step(lislam_lmap* L, const float* corner_last, int32_t nc, const float* surf_last, int32_t ns,
+                     const double* odom, double* state, double* out_pose, int32_t* stats) {
+  if (!L || nc < 0 || ns < 0 || (nc && !corner_last) || (ns && !surf_last) || !odom || !state) return LISLAM_ERR_ARG;
+  lislam_ctx* c = L->ctx;
+  hipSetDevice(c->device);
+  hipStream_t st = stream_of(c);
+  const double* qo = odom;
+  const double* to = odom + 4;
+  double* qm = state;
+  double* tm = state + 4;
+  // transformAssociateToMap (laserMapping.cpp:138-142)
+  double x[7];
+  h_qmul(qm, qo, x);
+  {
+    double tr[3];
+    h_qrot(qm, to, tr);
+    for (int k = 0; k < 3; k++) x[4 + k] = tr[k] + tm[k];
+  }
+  // re-centring (:330-565): the total translation of the cube indices
+  int cc[3] = {h_cube_of(x[4], L->cen[0]), h_cube_of(x[5], L->cen[1]), h_cube_of(x[6], L->cen[2])};
+  const int dims[3] = {kW, kH, kD};
+  int sh[3] = {0, 0, 0};
+  for (int a = 0; a < 3; a++) {
+    while (cc[a] < 3) { cc[a]++; L->cen[a]++; sh[a]++; }
+    while (cc[a] >= dims[a] - 3) { cc[a]--; L->cen[a]--; sh[a]--; }
+  }
+  if (sh[0] || sh[1] || sh[2])
+    for (int w = 0; w < 2; w++) MRC(cm_shift(L, w, sh[0], sh[1], sh[2]));
+  // valid cubes in the reference's loop order (:566-588)
+  std::vector<int> valid;
+  for (int i = cc[0] - 2; i <= cc[0] + 2; i++)
+    for (int j = cc[1] - 2; j <= cc[1] + 2; j++)
+      for (int k = cc[2] - 1; k <= cc[2] + 1; k++)
+        if (i >= 0 && i < kW && j >= 0 && j < kH && k >= 0 && k < kD) valid.push_back(i + kW * j + kW * kH * k);
+  const int nvalid = (int)valid.size();
+  MCHK(c, hipMemcpyAsync(L->valid.p, valid.data(), (size_t)nvalid * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_cm_vrank, dim3(blocks(kNC)), dim3(256), 0, st, L->vrank.as<int>());
+  hipLaunchKernelGGL(k_cm_vrank_set, dim3(1), dim3(128), 0, st, L->valid.as<int>(), nvalid, L->vrank.as<int>());
+  // local maps (:590-602)
+  MCHK(c, L->counts.reserve(64));
+  int* dcnt = L->counts.as<int>() + 8;  // [8, 10) local map sizes, [10, 12) stack sizes
+  MCHK(c, hipMemsetAsync(dcnt, 0, 16, st));
+  for (int w = 0; w < 2; w++) {
+    MCHK(c, L->local[w].reserve((size_t)std::max<int64_t>(L->n[w], 1) * 16));
+    if (nvalid > 0 && L->n[w] > 0)
+      hipLaunchKernelGGL(k_cm_gather, dim3(nvalid), dim3(256), 0, st, L->valid.as<int>(), nvalid, L->off[w].as<int>(),
+                         L->pts[w].as<float4>(), L->local[w].as<float4>(), dcnt + w);
+  }
+  // the current clouds, voxelized (:608-616)
+  const float* last[2] = {corner_last, surf_last};
+  const int nlast[2] = {nc, ns};
+  for (int w = 0; w < 2; w++) {
+    DBuf& q = w == 0 ? L->sc.qc : L->sc.qs;
+    MRC(stage_points(c, L->sc, q, last[w], nlast[w], 4));
+    MCHK(c, L->stack[w].reserve((size_t)std::max(nlast[w], 1) * 16));
+    MRC(voxel_grid_device(c, L->sc, q.as<float4>(), nlast[w], L->res[w], L->stack[w].as<float4>(), dcnt + 2 + w));
+  }
+  int h4[4] = {0, 0, 0, 0};
+  MCHK(c, hipMemcpyAsync(h4, dcnt, 16, hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  const int ncm = h4[0], nsm = h4[1], ncs = h4[2], nss = h4[3];
+  if (stats) {
+    stats[0] = ncm; stats[1] = nsm; stats[2] = ncs; stats[3] = nss;
+    stats[4] = stats[5] = stats[6] = stats[7] = -1;
+  }
+  // the optimization (:620-857) when the map is large enough
+  if (ncm > 10 && nsm > 50) {
+    MRC(lislam_map_build(L->maps[0], L->local[0].as<float>(), ncm, 4));
+    MRC(lislam_map_build(L->maps[1], L->local[1].as<float>(), nsm, 4));
+    int s4[4];
+    MRC(lislam_laser_mapping(L->maps[0], L->maps[1], L->stack[0].as<float>(), ncs, L->stack[1].as<float>(), nss, x, s4));
+    if (stats) for (int k = 0; k < 4; k++) stats[4 + k] = s4[k];
+  }
+  // transformUpdate (:145-149) with Eigen's Quaternion::inverse (conjugate / squaredNorm)
+  {
+    const double n2 = (qo[0] * qo[0] + qo[2] * qo[2]) + (qo[1] * qo[1] + qo[3] * qo[3]);
+    const double qinv[4] = {-qo[0] / n2, -qo[1] / n2, -qo[2] / n2, qo[3] / n2};
+    double nq[4];
+    h_qmul(x, qinv, nq);
+    for (int k = 0; k < 4; k++) qm[k] = nq[k];
+    double r[3];
+    h_qrot(qm, to, r);
+    for (int k = 0; k < 3; k++) tm[k] = x[4 + k] - r[k];
+  }
+  // insertion at the optimized pose and the VoxelGrid of the valid cubes (:880-1002)
+  MCHK(c, hipMemcpyAsync(L->x.p, x, 56, hipMemcpyHostToDevice, st));
+  MRC(cm_update(L, 0, L->stack[0].as<float4>(), dcnt + 2, ncs, nvalid));
+  MRC(cm_update(L, 1, L->stack[1].as<float4>(), dcnt + 3, nss, nvalid));
+  if (out_pose) for (int e = 0; e < 7; e++) out_pose[e] = x[e];
+  return LISLAM_OK;
+}
+
+}  // extern "C"

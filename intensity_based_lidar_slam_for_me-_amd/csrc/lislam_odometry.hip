@@ -661,7 +661,13 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   for (int e = 0; e < 7; e++) x[e] = st[e];
   const P4 cur = corner ? ld4(a.sharp + (size_t)k * a.cap_sharp + q) : ld4(a.flat + (size_t)k * a.cap_flat + q);
   const P4 sel = transform_to_start(cur, x);
+#ifdef LISLAM_PHASE_PROF  // ablations for timing only (LISLAM_ASSOC_DEBUG): 1 skip the 1-NN, 2 skip the line searches
+  int closest = (a.dbg & 1) ? (nL > 0 ? (int)((unsigned)q * 2654435761u % (unsigned)nL) : -1)
+                            : nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel);
+  if (a.dbg & 2) closest = -1;
+#else
   const int closest = nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel);
+#endif
   const int slot = corner ? q : a.cap_sharp + q;
   double* rec = a.blk + ((size_t)c * (a.cap_sharp + a.cap_flat) + slot) * 9;
   bool found = false;

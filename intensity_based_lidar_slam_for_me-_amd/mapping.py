@@ -179,3 +179,54 @@ def kernel_times(ctx):
                                               n.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), ctx.h,
               "lislam_map_kernel_times")
     return {k: (float(a), int(b)) for k, a, b in zip(nat.MAP_KERNELS, ms, n)}
+
+
+class LaserMapping:
+    """laserMapping::process over its 21 x 21 x 11 cube map (laserMapping.cpp:319-1002), device
+    resident (lislam_lmap)."""
+
+    NC = 21 * 21 * 11
+
+    def __init__(self, ctx, line_res: float = 0.4, plane_res: float = 0.8):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        nat.check(ctx.lib.lislam_lmap_create(ctx.h, line_res, plane_res, ctypes.byref(h)), ctx.h, "lislam_lmap_create")
+        self.h = h
+        self.state = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)  # q_wmap_wodom, t_wmap_wodom
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lislam_lmap_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process(self, corner_last, surf_last, odom):
+        """One frame: (q_w_curr t_w_curr (7,), stats (8,) = corner / surf map sizes, stack sizes,
+        optimization stats or -1)."""
+        pc, nc, _, kc = _as_points(corner_last)
+        ps, ns, _, ks = _as_points(surf_last)
+        od = np.ascontiguousarray(odom, np.float64)
+        pose = np.zeros(7, np.float64)
+        stats = np.zeros(8, np.int32)
+        nat.check(self.ctx.lib.lislam_lmap_step(self.h, pc, nc, ps, ns, nat.ptr(od), nat.ptr(self.state), nat.ptr(pose),
+                                                nat.ptr(stats)), self.ctx.h, "lislam_lmap_step")
+        return pose, stats
+
+    def counts(self):
+        cc = np.zeros(self.NC, np.int32)
+        sc = np.zeros(self.NC, np.int32)
+        nat.check(self.ctx.lib.lislam_lmap_counts(self.h, nat.ptr(cc), nat.ptr(sc)), self.ctx.h, "lislam_lmap_counts")
+        return cc, sc
+
+    def points(self, which: int) -> np.ndarray:
+        n = ctypes.c_int64()
+        nat.check(self.ctx.lib.lislam_lmap_points(self.h, which, None, 0, ctypes.byref(n)), self.ctx.h, "lislam_lmap_points")
+        out = np.zeros((max(n.value, 1), 4), np.float32)
+        nat.check(self.ctx.lib.lislam_lmap_points(self.h, which, nat.ptr(out), n.value, ctypes.byref(n)), self.ctx.h,
+                  "lislam_lmap_points")
+        return out[: n.value]

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "lislam_map_set_timing", "lislam_map_kernel_times",
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
     "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
+    "lislam_lmap_create", "lislam_lmap_destroy", "lislam_lmap_step", "lislam_lmap_counts", "lislam_lmap_points",
 )
 
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
@@ -147,6 +148,11 @@ def load(path: str = LIB_PATH):
     L.lislam_intensity_tracker_step.argtypes = [vp, vp, vp, vp, vp]
     L.lislam_batch_intensity_odometry.argtypes = [vp, _i32, _i32, vp]
     L.lislam_batch_ground.argtypes = [vp, _i32]
+    L.lislam_lmap_create.argtypes = [vp, ctypes.c_float, ctypes.c_float, ctypes.POINTER(vp)]
+    L.lislam_lmap_destroy.argtypes = [vp]
+    L.lislam_lmap_step.argtypes = [vp, vp, _i32, vp, _i32, vp, vp, vp, vp]
+    L.lislam_lmap_counts.argtypes = [vp, vp, vp]
+    L.lislam_lmap_points.argtypes = [vp, _i32, vp, i64, i64p]
     L.lislam_ground_extract.argtypes = [vp, vp, ctypes.POINTER(PointLayout), vp, _i32, _i32p, vp, vp]
     L.lislam_map_set_timing.argtypes = [vp, _i32]
     L.lislam_map_kernel_times.argtypes = [vp, _fp, _i32p]

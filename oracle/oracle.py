@@ -61,9 +61,53 @@ def lib():
         L.oracle_intensity_odometry.argtypes = [ctypes.c_int, _u8p, _f32p, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 _i32p, _f64p]
         L.oracle_ground_extract.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _i32p]
+        L.oracle_lmap_create.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.oracle_lmap_create.restype = vp
+        L.oracle_lmap_destroy.argtypes = [vp]
+        L.oracle_lmap_counts.argtypes = [vp, _i32p, _i32p]
+        L.oracle_lmap_points.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_lmap_points.restype = ctypes.c_int
+        L.oracle_lmap_step.argtypes = [vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _f64p, _f64p, _i32p]
         L.oracle_ground_extract.restype = ctypes.c_int
         _LIB = L
     return _LIB
+
+
+class LaserMap:
+    """laserMapping's 21 x 21 x 11 cube map + one-frame process (oracle_lmap_*)."""
+
+    NC = 21 * 21 * 11
+
+    def __init__(self, line_res: float = 0.4, plane_res: float = 0.8):
+        self.h = lib().oracle_lmap_create(line_res, plane_res)
+        self.state = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)  # q_wmap_wodom, t_wmap_wodom
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_lmap_destroy(self.h)
+            self.h = None
+
+    def step(self, corner_last: np.ndarray, surf_last: np.ndarray, odom: np.ndarray):
+        """One laserMapping frame; returns (pose q_w_curr t_w_curr (7,), stats (8,))."""
+        c = np.ascontiguousarray(corner_last, np.float32).reshape(-1, 4)
+        s = np.ascontiguousarray(surf_last, np.float32).reshape(-1, 4)
+        pose = np.zeros(7, np.float64)
+        stats = np.zeros(8, np.int32)
+        lib().oracle_lmap_step(self.h, c, c.shape[0], s, s.shape[0], np.ascontiguousarray(odom, np.float64),
+                               self.state, pose, stats)
+        return pose, stats
+
+    def counts(self):
+        cc = np.zeros(self.NC, np.int32)
+        sc = np.zeros(self.NC, np.int32)
+        lib().oracle_lmap_counts(self.h, cc, sc)
+        return cc, sc
+
+    def points(self, which: int) -> np.ndarray:
+        n = lib().oracle_lmap_points(self.h, which, None)
+        out = np.zeros((max(n, 1), 4), np.float32)
+        lib().oracle_lmap_points(self.h, which, out.ctypes.data)
+        return out[:n]
 
 
 def ground_extract(points: np.ndarray):

@@ -649,3 +649,181 @@ void oracle_laser_mapping(void* hc, void* hs, const float* corner, int nc, const
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ laserMapping cube map
+// The A-LOAM local map of laserMapping::process: 21 x 21 x 11 cubes of
+// 50 m (laserMapping.cpp:70-99) holding the corner / surf points in map frame.  One frame
+// (:319-1002, without publishing; the duplicated surf insert :950-981 dropped, SURVEY.md §8(c)
+// repair 2): transformAssociateToMap (:138-142), re-centring shifts (:330-565), the local map of
+// the <= 5 x 5 x 3 valid cubes in i, j, k loop order (:566-602), VoxelGrid of the current corner /
+// surf clouds (:608-616), the optimization when the map holds > 10 corner and > 50 surf points
+// (:620-857, oracle_laser_mapping), transformUpdate (:145-149, Eigen's Quaternion::inverse),
+// insertion of the voxelized clouds at the optimized pose (:880-949) and a VoxelGrid of every
+// valid cube (:984-1002).
+namespace oracle {
+struct CubeMap {
+  static constexpr int W = 21, H = 21, D = 11, NC = W * H * D;
+  int cenW = 10, cenH = 10, cenD = 5;
+  float line_res = 0.4f, plane_res = 0.8f;
+  std::vector<std::vector<P4>> corner, surf;
+  CubeMap() : corner(NC), surf(NC) {}
+};
+}  // namespace oracle
+
+extern "C" {
+
+void* oracle_lmap_create(float line_res, float plane_res) {
+  auto* m = new oracle::CubeMap();
+  m->line_res = line_res;
+  m->plane_res = plane_res;
+  return m;
+}
+void oracle_lmap_destroy(void* h) { delete static_cast<oracle::CubeMap*>(h); }
+
+// cube counts (corner, surf) in cube index order
+void oracle_lmap_counts(void* h, int* cc, int* sc) {
+  auto* m = static_cast<oracle::CubeMap*>(h);
+  for (int i = 0; i < oracle::CubeMap::NC; i++) { cc[i] = (int)m->corner[i].size(); sc[i] = (int)m->surf[i].size(); }
+}
+// all points of one cloud (0 corner, 1 surf) in cube index order; returns the count
+int oracle_lmap_points(void* h, int which, float* out) {
+  auto* m = static_cast<oracle::CubeMap*>(h);
+  auto& arr = which ? m->surf : m->corner;
+  int n = 0;
+  for (auto& v : arr)
+    for (auto& p : v) {
+      if (out) { out[4 * n] = p.x; out[4 * n + 1] = p.y; out[4 * n + 2] = p.z; out[4 * n + 3] = p.i; }
+      n++;
+    }
+  return n;
+}
+
+// stats[8] = corner / surf local-map sizes, corner / surf stack sizes, optimization stats of
+// oracle_laser_mapping (-1 when the map is too small to optimize); out_pose = q_w_curr, t_w_curr.
+void oracle_lmap_step(void* h, const float* corner_last, int nc, const float* surf_last, int ns, const double* odom,
+                      double* state, double* out_pose, int* stats) {
+  using oracle::CubeMap;
+  using oracle::P4;
+  auto* m = static_cast<CubeMap*>(h);
+  const int W = CubeMap::W, H = CubeMap::H, D = CubeMap::D;
+  const double* qo = odom;
+  const double* to = odom + 4;
+  double* qm = state;
+  double* tm = state + 4;
+  // transformAssociateToMap
+  oracle::Q4<double> qw = oracle::qmul(oracle::Q4<double>{qm[0], qm[1], qm[2], qm[3]}, oracle::Q4<double>{qo[0], qo[1], qo[2], qo[3]});
+  double x[7] = {qw.x, qw.y, qw.z, qw.w, 0, 0, 0};
+  {
+    double tr[3];
+    oracle::qrot(qm, to, tr);
+    for (int k = 0; k < 3; k++) x[4 + k] = tr[k] + tm[k];
+  }
+  // re-centring (the pointer rotations of :340-565; the cube that wraps around is cleared)
+  auto cube_of = [](double v, int cen) {
+    int c = int((v + 25.0) / 50.0) + cen;
+    if (v + 25.0 < 0) c--;
+    return c;
+  };
+  int cI = cube_of(x[4], m->cenW), cJ = cube_of(x[5], m->cenH), cK = cube_of(x[6], m->cenD);
+  auto at = [&](int i, int j, int k) { return i + W * j + W * H * k; };
+  auto rot = [&](int a0, int step, int cnt) {  // a[a0 + step (cnt-1)] <- ... <- a[a0], a[a0] <- old last, cleared
+    for (auto* arr : {&m->corner, &m->surf}) {
+      std::vector<P4> last = std::move((*arr)[a0 + step * (cnt - 1)]);
+      for (int t = cnt - 1; t >= 1; t--) (*arr)[a0 + step * t] = std::move((*arr)[a0 + step * (t - 1)]);
+      last.clear();
+      (*arr)[a0] = std::move(last);
+    }
+  };
+  while (cI < 3) {
+    for (int j = 0; j < H; j++)
+      for (int k = 0; k < D; k++) rot(at(0, j, k), 1, W);
+    cI++; m->cenW++;
+  }
+  while (cI >= W - 3) {
+    for (int j = 0; j < H; j++)
+      for (int k = 0; k < D; k++) rot(at(W - 1, j, k), -1, W);
+    cI--; m->cenW--;
+  }
+  while (cJ < 3) {
+    for (int i = 0; i < W; i++)
+      for (int k = 0; k < D; k++) rot(at(i, 0, k), W, H);
+    cJ++; m->cenH++;
+  }
+  while (cJ >= H - 3) {
+    for (int i = 0; i < W; i++)
+      for (int k = 0; k < D; k++) rot(at(i, H - 1, k), -W, H);
+    cJ--; m->cenH--;
+  }
+  while (cK < 3) {
+    for (int i = 0; i < W; i++)
+      for (int j = 0; j < H; j++) rot(at(i, j, 0), W * H, D);
+    cK++; m->cenD++;
+  }
+  while (cK >= D - 3) {
+    for (int i = 0; i < W; i++)
+      for (int j = 0; j < H; j++) rot(at(i, j, D - 1), -W * H, D);
+    cK--; m->cenD--;
+  }
+  // valid cubes and the local map
+  std::vector<int> valid;
+  for (int i = cI - 2; i <= cI + 2; i++)
+    for (int j = cJ - 2; j <= cJ + 2; j++)
+      for (int k = cK - 1; k <= cK + 1; k++)
+        if (i >= 0 && i < W && j >= 0 && j < H && k >= 0 && k < D) valid.push_back(at(i, j, k));
+  std::vector<float> cmap, smap;
+  for (int v : valid) {
+    for (auto& p : m->corner[v]) cmap.insert(cmap.end(), {p.x, p.y, p.z, p.i});
+    for (auto& p : m->surf[v]) smap.insert(smap.end(), {p.x, p.y, p.z, p.i});
+  }
+  const int ncm = (int)cmap.size() / 4, nsm = (int)smap.size() / 4;
+  // current clouds, voxelized
+  std::vector<float> cst((size_t)std::max(nc, 1) * 4), sst((size_t)std::max(ns, 1) * 4);
+  int ncs = 0, nss = 0;
+  oracle_voxel_grid(corner_last, nc, m->line_res, 1, cst.data(), &ncs);
+  oracle_voxel_grid(surf_last, ns, m->plane_res, 1, sst.data(), &nss);
+  stats[0] = ncm; stats[1] = nsm; stats[2] = ncs; stats[3] = nss;
+  stats[4] = stats[5] = stats[6] = stats[7] = -1;
+  if (ncm > 10 && nsm > 50) {
+    oracle::IkdMap mc, ms;
+    mc.build(cmap.data(), ncm, 4);
+    ms.build(smap.data(), nsm, 4);
+    oracle_laser_mapping(&mc, &ms, cst.data(), ncs, sst.data(), nss, x, stats + 4);
+  }
+  // transformUpdate: q_wmap_wodom = q_w_curr * q_wodom_curr.inverse(); t_wmap_wodom = t_w_curr - q_wmap_wodom * t_wodom_curr
+  {
+    const double n2 = (qo[0] * qo[0] + qo[2] * qo[2]) + (qo[1] * qo[1] + qo[3] * qo[3]);  // Eigen SSE2 squaredNorm
+    const oracle::Q4<double> qinv{-qo[0] / n2, -qo[1] / n2, -qo[2] / n2, qo[3] / n2};
+    const oracle::Q4<double> nq = oracle::qmul(oracle::Q4<double>{x[0], x[1], x[2], x[3]}, qinv);
+    qm[0] = nq.x; qm[1] = nq.y; qm[2] = nq.z; qm[3] = nq.w;
+    double r[3];
+    oracle::qrot(qm, to, r);
+    for (int k = 0; k < 3; k++) tm[k] = x[4 + k] - r[k];
+  }
+  // insertion (pointAssociateToMap at the optimized pose)
+  auto insert = [&](const std::vector<float>& stack, int n, std::vector<std::vector<P4>>& arr) {
+    for (int i = 0; i < n; i++) {
+      float w[3];
+      oracle::to_world(x, &stack[(size_t)i * 4], w);
+      const int ci = cube_of(w[0], m->cenW), cj = cube_of(w[1], m->cenH), ck = cube_of(w[2], m->cenD);
+      if (ci >= 0 && ci < W && cj >= 0 && cj < H && ck >= 0 && ck < D) arr[at(ci, cj, ck)].push_back(P4{w[0], w[1], w[2], stack[(size_t)i * 4 + 3]});
+    }
+  };
+  insert(cst, ncs, m->corner);
+  insert(sst, nss, m->surf);
+  // VoxelGrid of the valid cubes
+  for (int v : valid) {
+    for (int t = 0; t < 2; t++) {
+      auto& cube = t == 0 ? m->corner[v] : m->surf[v];
+      const int n = (int)cube.size();
+      std::vector<P4> o((size_t)std::max(n, 1));
+      int no = 0;
+      oracle_voxel_grid(reinterpret_cast<const float*>(cube.data()), n, t == 0 ? m->line_res : m->plane_res, 1,
+                        reinterpret_cast<float*>(o.data()), &no);
+      o.resize(no);
+      cube = std::move(o);
+    }
+  }
+  for (int e = 0; e < 7; e++) out_pose[e] = x[e];
+}
+
+}  // extern "C"

@@ -4,6 +4,8 @@ sys.path.insert(0, ROOT)
 import numpy as np
 import __graft_entry__ as g
 pkg = g.package()
+if os.environ.get('LISLAM_ALT_LIB'):
+    pkg.native.load(os.environ['LISLAM_ALT_LIB'])  # a developer variant of the library
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 L = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 scans = pkg.synth.make_sequence(S)
