@@ -161,6 +161,13 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
                                         refit inliers */
 /* Copy one output of one scan to host memory; cap/n count elements of the listed type. */
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n);
+/* toROSMsg of a point-cloud output (laser cloud, the four feature clouds, cloud_track, ground,
+ * ORB points; scanRegistration.cpp:592-642): cap / n points written into dst in the given
+ * PointCloud2 layout (e.g. PCL PointXYZI: point_step 32, x 0, y 4, z 8, intensity 16), packed on
+ * the device; bytes outside the four fields are zero.  lislam_batch_upload parses any layout on
+ * the device the same way (fromROSMsg). */
+int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,
+                                int32_t cap, int32_t* n);
 
 /* ---------------------------------------------------------------- cost functors */
 /* Evaluate n residual blocks at (q[4] = x,y,z,w, t[3]) on the GPU.  kind[i]: 0 LidarEdgeFactor

@@ -50,19 +50,6 @@ int dalloc(lislam_batch* b, T** p, size_t count) {
 
 bool valid_lines(int n) { return n == 16 || n == 32 || n == 64 || n == 128; }
 
-// Pack host PointCloud2-style points into float4 (x, y, z, intensity).
-void pack_points(const void* src, size_t n, const lislam_point_layout* L, std::vector<float>& out) {
-  out.resize(n * 4);
-  const uint8_t* s = static_cast<const uint8_t*>(src);
-  for (size_t i = 0; i < n; i++) {
-    const uint8_t* p = s + i * L->point_step;
-    std::memcpy(&out[i * 4 + 0], p + L->off_x, 4);
-    std::memcpy(&out[i * 4 + 1], p + L->off_y, 4);
-    std::memcpy(&out[i * 4 + 2], p + L->off_z, 4);
-    std::memcpy(&out[i * 4 + 3], p + L->off_intensity, 4);
-  }
-}
-
 bool is_packed(const lislam_point_layout* L) {
   return !L || (L->point_step == 16 && L->off_x == 0 && L->off_y == 4 && L->off_z == 8 && L->off_intensity == 12);
 }
@@ -228,10 +215,24 @@ int lislam_batch_destroy(lislam_batch* b) {
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
   if (b->ground) lislam_free_ground(b->ground);
+  if (b->wire) hipFree(b->wire);
   if (b->ev_images) hipEventDestroy(b->ev_images);
   delete b;
   return LISLAM_OK;
 }
+
+// device staging buffer of at least `bytes` for PointCloud2 bytes
+static int rc_wire(lislam_batch* b, size_t bytes) {
+  if (b->wire_bytes >= bytes) return LISLAM_OK;
+  if (b->wire) hipFree(b->wire);
+  b->wire = nullptr;
+  b->wire_bytes = 0;
+  if (hipMalloc(&b->wire, bytes) != hipSuccess) return LISLAM_ERR_DEVICE;
+  b->wire_bytes = bytes;
+  return LISLAM_OK;
+}
+
+static int batch_output_source(lislam_batch* b, int what, int scan, const void** src, int* cnt);
 
 int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
@@ -241,14 +242,50 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
   if (is_packed(layout)) {
     HIPCHK(c, hipMemcpyAsync((void*)b->fa.pts, points, n * 16, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-  } else {
+  } else {  // the message bytes go to the device scan by scan, the fields are parsed there
     if (layout->point_step < 4 || std::max({layout->off_x, layout->off_y, layout->off_z, layout->off_intensity}) + 4 > layout->point_step)
       return fail(c, LISLAM_ERR_ARG, "bad point layout");
-    std::vector<float> tmp;
-    pack_points(points, n, layout, tmp);
-    HIPCHK(c, hipMemcpyAsync((void*)b->fa.pts, tmp.data(), n * 16, hipMemcpyHostToDevice, c->stream));
+    const size_t scan_bytes = (size_t)b->N * layout->point_step;
+    if ((rc_wire(b, scan_bytes)) != LISLAM_OK) return fail(c, LISLAM_ERR_DEVICE, "staging allocation failed");
+    const lislam::WireLayout L{layout->point_step, layout->off_x, layout->off_y, layout->off_z, layout->off_intensity};
+    for (int s = 0; s < n_scans; s++) {
+      HIPCHK(c, hipMemcpyAsync(b->wire, static_cast<const uint8_t*>(points) + s * scan_bytes, scan_bytes, hipMemcpyDefault,
+                               c->stream));
+      lislam::launch_unpack_layout(static_cast<const uint8_t*>(b->wire), b->N, L,
+                                   const_cast<lislam::P4*>(b->fa.pts) + (size_t)s * b->N, c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return LISLAM_OK;
+}
+
+int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,
+                                int32_t cap, int32_t* n) {
+  if (!b || !dst || !layout || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  if (layout->point_step < 4 || std::max({layout->off_x, layout->off_y, layout->off_z, layout->off_intensity}) + 4 > layout->point_step)
+    return fail(c, LISLAM_ERR_ARG, "bad point layout");
+  const bool cloud4 = what == LISLAM_OUT_LASER_CLOUD || what == LISLAM_OUT_SHARP || what == LISLAM_OUT_LESS_SHARP ||
+                      what == LISLAM_OUT_FLAT || what == LISLAM_OUT_LESS_FLAT || what == LISLAM_OUT_CLOUD_TRACK ||
+                      what == LISLAM_OUT_GROUND || what == LISLAM_OUT_ORB_POINTS;
+  if (!cloud4) return fail(c, LISLAM_ERR_ARG, "output %d is not a point cloud", what);
+  hipSetDevice(c->device);
+  // the device source of the cloud: lislam_batch_download with a null copy (cap 0) gives the count
+  int cnt = 0;
+  const void* src = nullptr;
+  int rc = batch_output_source(b, what, scan, &src, &cnt);
+  if (rc) return rc;
+  if (n) *n = cnt;
+  if (cnt > cap) return fail(c, LISLAM_ERR_CAPACITY, "cloud %d needs %d points, cap %d", what, cnt, cap);
+  if (cnt == 0) return LISLAM_OK;
+  const size_t bytes = (size_t)cnt * layout->point_step;
+  if (rc_wire(b, bytes) != LISLAM_OK) return fail(c, LISLAM_ERR_DEVICE, "staging allocation failed");
+  const lislam::WireLayout L{layout->point_step, layout->off_x, layout->off_y, layout->off_z, layout->off_intensity};
+  lislam::launch_pack_layout(static_cast<const lislam::P4*>(src), cnt, L, static_cast<uint8_t*>(b->wire), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(dst, b->wire, bytes, hipMemcpyDefault, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return LISLAM_OK;
 }
 
@@ -361,8 +398,10 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
   return LISLAM_OK;
 }
 
-int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n) {
-  if (!b || !dst || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+}  // extern "C"
+
+// Device source, element count and element size of one output of one scan (synchronizes).
+static int output_source(lislam_batch* b, int what, int scan, const void** src_out, int* cnt_out, size_t* esz_out) {
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -426,6 +465,27 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
     default: return fail(c, LISLAM_ERR_ARG, "unknown output %d", what);
   }
   if (!src) return fail(c, LISLAM_ERR_STATE, "output %d not materialized (want_images=0?)", what);
+  *src_out = src;
+  *cnt_out = cnt;
+  *esz_out = esz;
+  return LISLAM_OK;
+}
+
+static int batch_output_source(lislam_batch* b, int what, int scan, const void** src, int* cnt) {
+  size_t esz = 0;
+  return output_source(b, what, scan, src, cnt, &esz);
+}
+
+extern "C" {
+
+int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n) {
+  if (!b || !dst || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  int cnt = 0;
+  const void* src = nullptr;
+  size_t esz = 0;
+  const int rc = output_source(b, what, scan, &src, &cnt, &esz);
+  if (rc) return rc;
   if (n) *n = cnt;
   if (cnt > cap) return fail(c, LISLAM_ERR_CAPACITY, "output %d needs %d elements, cap %d", what, cnt, cap);
   if (cnt > 0) HIPCHK(c, hipMemcpy(dst, src, (size_t)cnt * esz, hipMemcpyDeviceToHost));

@@ -36,7 +36,9 @@ struct lislam_batch {
   // queued on the context stream after it.
   hipEvent_t ev_images = nullptr;
   void* orb = nullptr;  // ORB engine of lislam_batch_intensity_odometry (lislam_orb.hip)
-  void* ground = nullptr;  // ground-plane engine of lislam_batch_ground (lislam_ground.hip)
+  void* ground = nullptr;
+  void* wire = nullptr;        // device staging of PointCloud2 bytes (lislam_batch_upload / download_cloud)
+  size_t wire_bytes = 0;  // ground-plane engine of lislam_batch_ground (lislam_ground.hip)
   hipEvent_t get_event() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e = nullptr;

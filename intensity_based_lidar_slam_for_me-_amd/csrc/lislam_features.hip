@@ -1008,6 +1008,43 @@ __global__ __launch_bounds__(64) void k_scan_compact(FeatureArgs a) {
     st4(a.less_flat + (size_t)s * N + pre[3] + k, ld4(a.stg_less_flat + (size_t)s * N + off + k));
 }
 
+// ------------------------------------------------------------------------------- wire format
+// sensor_msgs/PointCloud2 points <-> float4 (x, y, z, intensity): fromROSMsg's field-offset
+// parsing (image_handler.h_ouster:105-106, scanRegistration.cpp:234-235) and toROSMsg of the
+// feature clouds (scanRegistration.cpp:592-642) as device kernels, one thread per point.
+__device__ __forceinline__ float ld_f32_bytes(const uint8_t* p) {
+  uint32_t u = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+  return __uint_as_float(u);
+}
+__device__ __forceinline__ void st_f32_bytes(uint8_t* p, float v) {
+  const uint32_t u = __float_as_uint(v);
+  p[0] = (uint8_t)u; p[1] = (uint8_t)(u >> 8); p[2] = (uint8_t)(u >> 16); p[3] = (uint8_t)(u >> 24);
+}
+__global__ void k_unpack_layout(const uint8_t* raw, int n, WireLayout L, P4* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = raw + (size_t)i * L.step;
+  st4(out + i, P4{ld_f32_bytes(p + L.ox), ld_f32_bytes(p + L.oy), ld_f32_bytes(p + L.oz), ld_f32_bytes(p + L.oi)});
+}
+// every byte of a point is written: the four fields, zeros elsewhere
+__global__ void k_pack_layout(const P4* in, int n, WireLayout L, uint8_t* raw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const P4 v = ld4(in + i);
+  uint8_t* p = raw + (size_t)i * L.step;
+  for (uint32_t k = 0; k < L.step; k++) p[k] = 0;
+  st_f32_bytes(p + L.ox, v.x);
+  st_f32_bytes(p + L.oy, v.y);
+  st_f32_bytes(p + L.oz, v.z);
+  st_f32_bytes(p + L.oi, v.i);
+}
+void launch_unpack_layout(const uint8_t* raw, int n, const WireLayout& L, P4* out, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_unpack_layout, dim3((n + 255) / 256), dim3(256), 0, st, raw, n, L, out);
+}
+void launch_pack_layout(const P4* in, int n, const WireLayout& L, uint8_t* raw, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_pack_layout, dim3((n + 255) / 256), dim3(256), 0, st, in, n, L, raw);
+}
+
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev, hipEvent_t images_ready) {
   // ev (nullable): 4 events bracketing k_scan_front, k_scan_lines, k_scan_compact
   if (ev) (void)hipEventRecord(ev[0], st);

@@ -110,6 +110,13 @@ struct FactorArgs {
   double* jac;         // [n][3][6] or null
 };
 
+// PointCloud2 point layout (point_step and the byte offsets of x, y, z, intensity).
+struct WireLayout {
+  uint32_t step, ox, oy, oz, oi;
+};
+void launch_unpack_layout(const uint8_t* raw, int n, const WireLayout& L, P4* out, hipStream_t st);
+void launch_pack_layout(const P4* in, int n, const WireLayout& L, uint8_t* raw, hipStream_t st);
+
 // images_ready (nullable): recorded once k_scan_front has written the range / intensity images and
 // cloud_track, which is all the ORB front end reads.
 void launch_features(const FeatureArgs& a, hipStream_t st, hipEvent_t* ev /*4 or null*/, hipEvent_t images_ready);

@@ -19,6 +19,7 @@ CAP_SHARP_PER_LINE, CAP_LESS_SHARP_PER_LINE, CAP_FLAT_PER_LINE = 12, 120, 24
 
 PACKED_XYZI = nat.PointLayout(16, 0, 4, 8, 12)
 OUSTER_LAYOUT = nat.PointLayout(48, 0, 4, 8, 16)  # os_cloud_node/points: x y z pad intensity ...
+PCL_XYZI_LAYOUT = nat.PointLayout(32, 0, 4, 8, 16)  # pcl::PointXYZI as toROSMsg writes it
 
 
 class Context:
@@ -223,6 +224,18 @@ class Batch:
         rc = self.ctx.lib.lislam_batch_download(self.h, what, scan, nat.ptr(buf), cap, ctypes.byref(n))
         nat.check(rc, self.ctx.h, "lislam_batch_download")
         return buf[: n.value].copy()
+
+    def download_cloud(self, what: int, scan: int, layout: nat.PointLayout | None = None) -> bytes:
+        """toROSMsg of a point-cloud output: the PointCloud2 data bytes in `layout` (PCL PointXYZI
+        by default), packed on the device."""
+        lay = layout or PCL_XYZI_LAYOUT
+        cap = max(self.ctx.n_scans * self.ctx.width, 16)
+        buf = np.zeros(cap * lay.point_step, np.uint8)
+        n = ctypes.c_int32()
+        rc = self.ctx.lib.lislam_batch_download_cloud(self.h, what, scan, nat.ptr(buf), ctypes.byref(lay), cap,
+                                                      ctypes.byref(n))
+        nat.check(rc, self.ctx.h, "lislam_batch_download_cloud")
+        return buf[: n.value * lay.point_step].tobytes()
 
     def features(self, scan: int) -> Features:
         return Features(self.download(nat.OUT_LASER_CLOUD, scan), self.download(nat.OUT_SHARP, scan),

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "lislam_ctx_create", "lislam_ctx_destroy", "lislam_last_error", "lislam_synchronize",
     "lislam_set_stream", "lislam_get_stream", "lislam_scan_registration", "lislam_odom_create",
     "lislam_odom_destroy", "lislam_odom_step", "lislam_batch_create", "lislam_batch_destroy",
-    "lislam_batch_upload", "lislam_batch_input_device_ptr", "lislam_batch_extract",
+    "lislam_batch_upload", "lislam_batch_download_cloud", "lislam_batch_input_device_ptr", "lislam_batch_extract",
     "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
     "lislam_batch_download", "lislam_eval_factors",
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
@@ -126,6 +126,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_set_timing.argtypes = [vp, _i32]
     L.lislam_batch_kernel_times.argtypes = [vp, _fp, _i32p, _i32p]
     L.lislam_batch_download.argtypes = [vp, _i32, _i32, vp, _i32, _i32p]
+    L.lislam_batch_download_cloud.argtypes = [vp, _i32, _i32, vp, ctypes.POINTER(PointLayout), _i32, _i32p]
     L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
     i64, i64p = ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)
     L.lislam_map_create.argtypes = [vp, ctypes.POINTER(MapConfig), ctypes.POINTER(vp)]
