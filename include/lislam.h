@@ -304,15 +304,55 @@ int lislam_lmap_step(lislam_lmap* m, const float* corner_last, int32_t nc, const
 int lislam_lmap_counts(lislam_lmap* m, int32_t* corner_counts, int32_t* surf_counts);
 int lislam_lmap_points(lislam_lmap* m, int32_t which, float* out, int64_t cap, int64_t* n);
 
+/* ---- loop closure and odometry fusion */
+/* loop_closure_parameters (config/spot.yaml:26-33) + the ICP settings of
+ * intensity_feature_tracker.cpp:219-232. */
+typedef struct {
+  int32_t use_crop;                   /* USE_CROP (spot.yaml: false) */
+  float crop_size;                    /* CROP_SIZE: CropBox [-c, c]^3 (spot.yaml: 200) */
+  int32_t use_downsample;             /* USE_DOWNSAMPLE (true) */
+  float voxel_size;                   /* VOXEL_SIZE = vf_scan_res (0.25) */
+  float max_correspondence_distance;  /* setMaxCorrespondenceDistance (100) */
+  int32_t max_iterations;             /* setMaximumIterations (100) */
+  double transformation_epsilon;      /* setTransformationEpsilon (1e-6) */
+  double euclidean_fitness_epsilon;   /* setEuclideanFitnessEpsilon (1e-6) */
+  double fitness_threshold;           /* FITNESS_SCORE = icp_fitness_score (0.5) */
+} lislam_icp_config;
+/* The USE_ICP block of feature_tracker::loopClosureThread (intensity_feature_tracker.cpp:217-366)
+ * with tranformCurrentScanToMap (:167-172) and getSubmapOfhistory (:174-193): cur = the new
+ * keyframe's cloud_track (n_cur x, y, z, intensity), T_cur = getTransformMatrix(keyframeId)
+ * (row-major 4x4); hist = the history keyframes' clouds concatenated (hist_counts[n_hist]) with
+ * their poses T_hist[n_hist][16].  removeNaN, CropBox, VoxelGrid, pcl::IterativeClosestPoint and
+ * getFitnessScore on the device.  Outputs (each nullable): T_icp[16] = getFinalTransformation,
+ * T_cur2map[16] = T_icp * T_cur (the loop factor's pose_from, :316-321), fitness, info[8] =
+ * accepted (1 converged and fitness <= threshold, 0 not, -1 empty submap, -2 <= 10 points after
+ * filtering), converged, convergence state (0 none, 1 iterations, 2 transform, 3 absolute MSE,
+ * 4 relative MSE, 5 < 3 correspondences), iterations, source points, target points, last
+ * correspondences, 0.  Point arrays may be host or device memory. */
+int lislam_loop_icp(lislam_ctx* ctx, const lislam_icp_config* cfg, const float* cur, int32_t n_cur, const double* T_cur,
+                    const float* hist, const int32_t* hist_counts, int32_t n_hist, const double* T_hist, double* T_icp,
+                    double* T_cur2map, double* fitness, int32_t* info);
+/* odomHandler's callback (src/odom_handler_node.cpp:44-132) over n synchronized pairs in order:
+ * aloam[n][7] = /laser_odom_to_init_aloam, intensity[n][7] = /laser_odom_to_init_intensity
+ * (q x,y,z,w, t), skip[n] = 1 when the intensity message's child_frame_id is "/odom_skip";
+ * fused[n][7] = the published /laser_odom_to_init.  The fuser keeps the previous poses and
+ * odom_cur on the device between calls.  Pointers may be host or device memory. */
+typedef struct lislam_odom_fuser lislam_odom_fuser;
+int lislam_odom_fuser_create(lislam_ctx* ctx, lislam_odom_fuser** out);
+int lislam_odom_fuser_destroy(lislam_odom_fuser* f);
+int lislam_odom_fuse(lislam_odom_fuser* f, const double* aloam, const double* intensity, const int32_t* skip, int32_t n,
+                     double* fused);
+
 /* HIP-event timing of the mapping kernels of a context (recorded on its stream, no host sync
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
  * clears the record. */
-#define LISLAM_MAP_NUM_KERNELS 17 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+#define LISLAM_MAP_NUM_KERNELS 20 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
                                      gather + cell table), Add_Points downsample (claim + resolve),
                                      k_orb_pyramid, k_orb_fast, k_orb_select, k_orb_finish,
                                      k_orb_blur, k_orb_desc, k_orb_match, k_orb_lm,
-                                     k_ground_screen, k_ground_ransac, k_ground_extract */
+                                     k_ground_screen, k_ground_ransac, k_ground_extract,
+                                     k_lc_step, k_lc_apply, k_fuse */
 int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
 int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 

@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -968,10 +969,13 @@ uint32_t pow2_at_least(uint64_t v) {
 
 }  // namespace
 
+struct LoopState;  // lislam_loop_icp's target map and buffers (end of file)
+
 // Scratch shared by the stateless entry points of a context (voxel grid, solve, association).
 struct MapScratch {
   DBuf sort_tmp, keys32a, keys32b, idxa, idxb, flag, pos, vin, vout, bounds, counters;
   DBuf lm, partial, rec, kind, x, nb, d2, found, q, vox, qc, qs;
+  LoopState* loop = nullptr;
 };
 
 struct lislam_map {
@@ -1260,7 +1264,6 @@ bool valid_stride(int s) { return s >= 3; }
 
 }  // namespace
 
-void lislam_free_map_scratch(void* p) { delete static_cast<MapScratch*>(p); }
 
 extern "C" {
 
@@ -2051,6 +2054,628 @@ int lislam_lmap_step(lislam_lmap* L, const float* corner_last, int32_t nc, const
   MRC(cm_update(L, 0, L->stack[0].as<float4>(), dcnt + 2, ncs, nvalid));
   MRC(cm_update(L, 1, L->stack[1].as<float4>(), dcnt + 3, nss, nvalid));
   if (out_pose) for (int e = 0; e < 7; e++) out_pose[e] = x[e];
+  return LISLAM_OK;
+}
+
+}  // extern "C"
+
+// ================================================================== loop-closure ICP
+// feature_tracker::loopClosureThread's USE_ICP block (src/intensity_feature_tracker.cpp:217-366)
+// with tranformCurrentScanToMap (:167-172) and getSubmapOfhistory (:174-193), device resident:
+//   k_lc_tf_d      transformPointCloud with the Matrix4d keyframe poses (double, stored as float)
+//   k_lc_flags     removeNaNFromPointCloud + CropBox, compacted with hipCUB Select::Flagged
+//   VoxelGrid      voxel_grid_device (PCL VoxelGrid semantics, as a21)
+//   target map     the hash-grid k-NN map of a19-a21 (exact 1-NN, ties by target index)
+//   per iteration  k_knn (1-NN of every source point) -> k_lc_step (one 1024-thread workgroup:
+//                  correspondence MSE, means, demeaned cross-covariance in a fixed strided +
+//                  halving-tree double order, Horn's quaternion eigenproblem by cyclic Jacobi,
+//                  final = T * final, DefaultConvergenceCriteria) -> k_lc_apply (source *= T).
+//   The host launches the iterations in chunks and reads one flag per chunk; once converged the
+//   k-NN query count on the device drops to 0 and every later launch of the chunk exits at once.
+//   getFitnessScore: the original source under `final`, 1-NN, mean squared distance.
+// The restatement (oracle/oracle_map.cpp oracle_loop_icp) performs the same floating-point
+// operations in the same order: results are bit-identical.
+namespace lislam {
+namespace loopk {
+
+using mapk::MapView;
+
+constexpr int kRed = 1024;
+
+struct Mat34d {
+  double m[12];
+};
+
+struct IcpParams {
+  int max_iter;
+  double rot_thr, trans_thr, mse_abs, mse_rel;
+};
+
+struct IcpDev {
+  float T[16];  // transformation_ of the last iteration
+  float F[16];  // final_transformation_
+  double prev_mse, fitness;
+  int iter, state, done, run, nq, ncorr;
+};
+
+__global__ void k_lc_tf_d(const float4* in, int n, Mat34d T, float4* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  const double x = p.x, y = p.y, z = p.z;
+  const double* m = T.m;
+  out[i] = make_float4((float)(((m[0] * x + m[1] * y) + m[2] * z) + m[3]), (float)(((m[4] * x + m[5] * y) + m[6] * z) + m[7]),
+                       (float)(((m[8] * x + m[9] * y) + m[10] * z) + m[11]), p.w);
+}
+
+__global__ void k_lc_flags(const float4* in, int n, int use_crop, float lo, float hi, uint8_t* flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  bool keep = isfinite(p.x) && isfinite(p.y) && isfinite(p.z);
+  if (keep && use_crop) keep = !(p.x < lo || p.y < lo || p.z < lo || p.x > hi || p.y > hi || p.z > hi);
+  flag[i] = keep ? 1 : 0;
+}
+
+// target points for the k-NN map: w = index (the map's tie-break id)
+__global__ void k_lc_ids(const float4* in, int n, float4* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = in[i];
+  out[i] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+}
+
+__device__ void jacobi4(double A[4][4], double V[4][4]) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) V[i][j] = i == j ? 1.0 : 0.0;
+  double tot = 0;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) tot += A[i][j] * A[i][j];
+  for (int sweep = 0; sweep < 32; sweep++) {
+    double off = 0;
+    for (int p = 0; p < 4; p++)
+      for (int q = p + 1; q < 4; q++) off += A[p][q] * A[p][q];
+    if (!(off > 1e-36 * tot)) break;
+    for (int p = 0; p < 4; p++)
+      for (int q = p + 1; q < 4; q++) {
+        const double apq = A[p][q];
+        if (apq == 0.0) continue;
+        const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+        double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+        if (theta < 0) t = -t;
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 4; k++) {
+          const double akp = A[k][p], akq = A[k][q];
+          A[k][p] = c * akp - s * akq;
+          A[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 4; k++) {
+          const double apk = A[p][k], aqk = A[q][k];
+          A[p][k] = c * apk - s * aqk;
+          A[q][k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < 4; k++) {
+          const double vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = c * vkp - s * vkq;
+          V[k][q] = s * vkp + c * vkq;
+        }
+      }
+  }
+}
+
+// umeyama(src, tgt, false) through Horn's 4x4 quaternion matrix of S[a][b] = mean s'_a t'_b
+__device__ void horn_rt(const double S[3][3], const double ms[3], const double mt[3], double R[3][3], double t[3]) {
+  const double Sxx = S[0][0], Sxy = S[0][1], Sxz = S[0][2], Syx = S[1][0], Syy = S[1][1], Syz = S[1][2], Szx = S[2][0],
+               Szy = S[2][1], Szz = S[2][2];
+  double N[4][4] = {{(Sxx + Syy) + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx},
+                    {Syz - Szy, (Sxx - Syy) - Szz, Sxy + Syx, Szx + Sxz},
+                    {Szx - Sxz, Sxy + Syx, (Syy - Sxx) - Szz, Syz + Szy},
+                    {Sxy - Syx, Szx + Sxz, Syz + Szy, (Szz - Sxx) - Syy}};
+  double V[4][4];
+  jacobi4(N, V);
+  int k = 0;
+  for (int j = 1; j < 4; j++)
+    if (N[j][j] > N[k][k]) k = j;
+  double w = V[0][k], x = V[1][k], y = V[2][k], z = V[3][k];
+  const double nn = sqrt(((w * w + x * x) + y * y) + z * z);
+  w /= nn; x /= nn; y /= nn; z /= nn;
+  const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x, tyy = ty * y,
+               tyz = tz * y, tzz = tz * z;
+  R[0][0] = 1 - (tyy + tzz); R[0][1] = txy - twz; R[0][2] = txz + twy;
+  R[1][0] = txy + twz; R[1][1] = 1 - (txx + tzz); R[1][2] = tyz - twx;
+  R[2][0] = txz - twy; R[2][1] = tyz + twx; R[2][2] = 1 - (txx + tyy);
+  for (int a = 0; a < 3; a++) t[a] = mt[a] - ((R[a][0] * ms[0] + R[a][1] * ms[1]) + R[a][2] * ms[2]);
+}
+
+// in-place halving tree over red[V][kRed] (every thread of the 1024-thread block calls it)
+template <int V>
+__device__ __forceinline__ void tree_sum(double (*red)[kRed]) {
+  const int t = threadIdx.x;
+  for (int s = kRed / 2; s > 0; s >>= 1) {
+    if (t < s)
+#pragma unroll
+      for (int k = 0; k < V; k++) red[k][t] += red[k][t + s];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kRed) void k_lc_step(IcpDev* st, const float4* src, const float4* nb, const float* d2,
+                                                  const int* found, int n, IcpParams P) {
+  __shared__ double red[9][kRed];
+  const int t = threadIdx.x;
+  if (st->done) {
+    if (t == 0) st->run = 0;
+    return;
+  }
+  {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = t; i < n; i += kRed) {
+      if (found[i] <= 0) continue;
+      const float4 s = src[i], q = nb[i];
+      a[0] += 1.0; a[1] += (double)d2[i];
+      a[2] += (double)s.x; a[3] += (double)s.y; a[4] += (double)s.z;
+      a[5] += (double)q.x; a[6] += (double)q.y; a[7] += (double)q.z;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) red[k][t] = a[k];
+  }
+  __syncthreads();
+  tree_sum<8>(red);
+  const double cnt = red[0][0], sd2 = red[1][0];
+  if (cnt < 3.0) {
+    if (t == 0) {
+      st->ncorr = (int)cnt;
+      st->state = 5;
+      st->done = 1;
+      st->run = 0;
+      st->nq = 0;
+    }
+    return;
+  }
+  const double ms[3] = {red[2][0] / cnt, red[3][0] / cnt, red[4][0] / cnt};
+  const double mt[3] = {red[5][0] / cnt, red[6][0] / cnt, red[7][0] / cnt};
+  __syncthreads();  // everyone has read the pass-1 sums
+  {
+    double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = t; i < n; i += kRed) {
+      if (found[i] <= 0) continue;
+      const float4 s = src[i], q = nb[i];
+      const double u[3] = {s.x - ms[0], s.y - ms[1], s.z - ms[2]};
+      const double v[3] = {q.x - mt[0], q.y - mt[1], q.z - mt[2]};
+#pragma unroll
+      for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) a[3 * r + c] += u[r] * v[c];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) red[k][t] = a[k];
+  }
+  __syncthreads();
+  tree_sum<9>(red);
+  if (t != 0) return;
+  double S[3][3], R[3][3], tr[3];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) S[r][c] = red[3 * r + c][0] / cnt;
+  horn_rt(S, ms, mt, R, tr);
+  float T[16] = {(float)R[0][0], (float)R[0][1], (float)R[0][2], (float)tr[0], (float)R[1][0], (float)R[1][1],
+                 (float)R[1][2], (float)tr[1], (float)R[2][0], (float)R[2][1], (float)R[2][2], (float)tr[2],
+                 0.f, 0.f, 0.f, 1.f};
+  float F[16], G[16];
+  for (int k = 0; k < 16; k++) F[k] = st->F[k];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++)
+      G[4 * r + c] = ((T[4 * r] * F[c] + T[4 * r + 1] * F[4 + c]) + T[4 * r + 2] * F[8 + c]) + T[4 * r + 3] * F[12 + c];
+  for (int k = 0; k < 16; k++) { st->T[k] = T[k]; st->F[k] = G[k]; }
+  const int it = st->iter + 1;
+  st->iter = it;
+  st->ncorr = (int)cnt;
+  st->run = 1;
+  int state = 0;
+  const double mse = sd2 / cnt, prev = st->prev_mse;
+  const double cos_angle = 0.5 * ((((double)T[0] + (double)T[5]) + (double)T[10]) - 1.0);
+  const double tsq = ((double)T[3] * (double)T[3] + (double)T[7] * (double)T[7]) + (double)T[11] * (double)T[11];
+  if (it >= P.max_iter) state = 1;
+  else if (cos_angle >= P.rot_thr && tsq <= P.trans_thr) state = 2;
+  else if (fabs(mse - prev) < P.mse_abs) state = 3;
+  else if (fabs(mse - prev) / prev < P.mse_rel) state = 4;
+  st->prev_mse = mse;
+  if (state) {
+    st->state = state;
+    st->done = 1;
+    st->nq = 0;
+  }
+}
+
+// source *= T of this iteration (skipped when k_lc_step did not run)
+__global__ void k_lc_apply(const IcpDev* st, float4* src, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !st->run) return;
+  const float* T = st->T;
+  const float4 p = src[i];
+  src[i] = make_float4(((T[0] * p.x + T[1] * p.y) + T[2] * p.z) + T[3], ((T[4] * p.x + T[5] * p.y) + T[6] * p.z) + T[7],
+                       ((T[8] * p.x + T[9] * p.y) + T[10] * p.z) + T[11], p.w);
+}
+
+// getFitnessScore's transformPointCloud(*input_, final_transformation_)
+__global__ void k_lc_final_tf(const IcpDev* st, const float4* src, int n, float4* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* T = st->F;
+  const float4 p = src[i];
+  out[i] = make_float4(((T[0] * p.x + T[1] * p.y) + T[2] * p.z) + T[3], ((T[4] * p.x + T[5] * p.y) + T[6] * p.z) + T[7],
+                       ((T[8] * p.x + T[9] * p.y) + T[10] * p.z) + T[11], p.w);
+}
+
+__global__ __launch_bounds__(kRed) void k_lc_fitness(IcpDev* st, const float* d2, const int* found, int n) {
+  __shared__ double red[2][kRed];
+  const int t = threadIdx.x;
+  double a0 = 0, a1 = 0;
+  for (int i = t; i < n; i += kRed) {
+    if (found[i] <= 0) continue;
+    a0 += 1.0;
+    a1 += (double)d2[i];
+  }
+  red[0][t] = a0;
+  red[1][t] = a1;
+  __syncthreads();
+  tree_sum<2>(red);
+  if (t == 0) st->fitness = red[0][0] > 0 ? red[1][0] / red[0][0] : DBL_MAX;
+}
+
+}  // namespace loopk
+}  // namespace lislam
+
+using namespace lislam::loopk;
+
+struct LoopState {
+  lislam_map map;
+  DBuf raw, tf, flag, sel, cnt, src, src0, tgt, nb, d2, found, st, tmp, ftf;
+  IcpDev* host = nullptr;  // pinned
+  LoopState() { (void)hipHostMalloc((void**)&host, sizeof(IcpDev)); }
+  ~LoopState() { if (host) (void)hipHostFree(host); }
+};
+
+void lislam_free_map_scratch(void* p) {
+  auto* s = static_cast<MapScratch*>(p);
+  delete s->loop;
+  delete s;
+}
+
+namespace {
+
+// transform n staged points (device raw) by T (row-major 4x4 double) into tf[off..]
+void lc_transform(lislam_ctx* c, const float4* raw, int n, const double* T, float4* out) {
+  if (n <= 0) return;
+  Mat34d m;
+  for (int k = 0; k < 12; k++) m.m[k] = T[k];
+  hipLaunchKernelGGL(k_lc_tf_d, dim3(blocks(n)), dim3(256), 0, stream_of(c), raw, n, m, out);
+}
+
+// removeNaN + CropBox + VoxelGrid of the n device points in ls.tf (in place through ls.sel) ->
+// dst; returns the count (host)
+int lc_prepare(lislam_ctx* c, LoopState& ls, int n, const lislam_icp_config* cfg, DBuf& dst, int* n_out) {
+  hipStream_t st = stream_of(c);
+  MapScratch& sc = ctx_scratch(c);
+  *n_out = 0;
+  MCHK(c, dst.reserve((size_t)std::max(n, 1) * sizeof(float4)));
+  if (n == 0) return LISLAM_OK;
+  MCHK(c, ls.flag.reserve((size_t)n));
+  MCHK(c, ls.sel.reserve((size_t)n * sizeof(float4)));
+  MCHK(c, ls.cnt.reserve(16));
+  hipLaunchKernelGGL(k_lc_flags, dim3(blocks(n)), dim3(256), 0, st, ls.tf.as<float4>(), n, cfg->use_crop ? 1 : 0,
+                     -cfg->crop_size, cfg->crop_size, ls.flag.as<uint8_t>());
+  size_t tb = 0;
+  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, ls.tf.as<float4>(), ls.flag.as<uint8_t>(), ls.sel.as<float4>(),
+                                        ls.cnt.as<int>(), n, st));
+  MCHK(c, ls.tmp.reserve(tb));
+  MCHK(c, hipcub::DeviceSelect::Flagged(ls.tmp.p, tb, ls.tf.as<float4>(), ls.flag.as<uint8_t>(), ls.sel.as<float4>(),
+                                        ls.cnt.as<int>(), n, st));
+  int m = 0;
+  MCHK(c, hipMemcpyAsync(&m, ls.cnt.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  if (!cfg->use_downsample || m == 0) {
+    if (m) MCHK(c, hipMemcpyAsync(dst.p, ls.sel.p, (size_t)m * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    *n_out = m;
+    return LISLAM_OK;
+  }
+  MRC(voxel_grid_device(c, sc, ls.sel.as<float4>(), m, cfg->voxel_size, dst.as<float4>(), ls.cnt.as<int>() + 1));
+  MCHK(c, hipMemcpyAsync(n_out, ls.cnt.as<int>() + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  return LISLAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lislam_loop_icp(lislam_ctx* c, const lislam_icp_config* cfg, const float* cur, int32_t n_cur, const double* T_cur,
+                    const float* hist, const int32_t* hist_counts, int32_t n_hist, const double* T_hist, double* T_icp,
+                    double* T_cur2map, double* fitness, int32_t* info) {
+  if (!c || !cfg || n_cur < 0 || (n_cur > 0 && !cur) || !T_cur || n_hist < 0 || (n_hist > 0 && (!hist_counts || !T_hist)))
+    return LISLAM_ERR_ARG;
+  if (cfg->use_downsample && !(cfg->voxel_size > 0)) return mfail(c, LISLAM_ERR_ARG, "lislam_loop_icp: voxel_size <= 0");
+  int64_t n_h = 0;
+  for (int h = 0; h < n_hist; h++) {
+    if (hist_counts[h] < 0) return LISLAM_ERR_ARG;
+    n_h += hist_counts[h];
+  }
+  if (n_h > 0 && !hist) return LISLAM_ERR_ARG;
+  if (n_h > 0x3fffffff || n_cur > 0x3fffffff) return mfail(c, LISLAM_ERR_CAPACITY, "lislam_loop_icp: clouds too large");
+  hipSetDevice(c->device);
+  hipStream_t st = stream_of(c);
+  MapScratch& sc = ctx_scratch(c);
+  if (!sc.loop) {
+    sc.loop = new LoopState();
+    sc.loop->map.ctx = c;
+  }
+  LoopState& ls = *sc.loop;
+  if (!ls.host) return mfail(c, LISLAM_ERR_DEVICE, "lislam_loop_icp: pinned allocation failed");
+  int32_t inf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double Ti[16], Tc[16], fit = DBL_MAX;
+  for (int k = 0; k < 16; k++) { Ti[k] = (k % 5 == 0) ? 1.0 : 0.0; Tc[k] = T_cur[k]; }
+  auto finish = [&]() {
+    if (T_icp) std::memcpy(T_icp, Ti, sizeof(Ti));
+    if (T_cur2map) std::memcpy(T_cur2map, Tc, sizeof(Tc));
+    if (fitness) *fitness = fit;
+    if (info) std::memcpy(info, inf, sizeof(inf));
+    return LISLAM_OK;
+  };
+  // stage + transform: the current keyframe, then the history keyframes in order
+  const int64_t ntot = std::max<int64_t>(n_cur, n_h);
+  MCHK(c, ls.raw.reserve((size_t)std::max<int64_t>(ntot, 1) * sizeof(float4)));
+  MCHK(c, ls.tf.reserve((size_t)std::max<int64_t>(ntot, 1) * sizeof(float4)));
+  if (n_h == 0) {
+    inf[0] = -1;
+    return finish();
+  }
+  int ns = 0, nt = 0;
+  if (n_cur) MCHK(c, hipMemcpyAsync(ls.raw.p, cur, (size_t)n_cur * 16, hipMemcpyDefault, st));
+  lc_transform(c, ls.raw.as<float4>(), n_cur, T_cur, ls.tf.as<float4>());
+  MRC(lc_prepare(c, ls, n_cur, cfg, ls.src0, &ns));
+  MCHK(c, hipMemcpyAsync(ls.raw.p, hist, (size_t)n_h * 16, hipMemcpyDefault, st));
+  for (int h = 0, off = 0; h < n_hist; off += hist_counts[h], h++)
+    lc_transform(c, ls.raw.as<float4>() + off, hist_counts[h], T_hist + 16 * h, ls.tf.as<float4>() + off);
+  MRC(lc_prepare(c, ls, (int)n_h, cfg, ls.tgt, &nt));
+  inf[4] = ns;
+  inf[5] = nt;
+  if (ns <= 10 || nt <= 10) {
+    inf[0] = -2;
+    return finish();
+  }
+  // target map (ids = target index)
+  lislam_map& m = ls.map;
+  m.cell = std::max(1.0f, cfg->use_downsample ? 2.0f * cfg->voxel_size : 1.0f);
+  m.ds = m.cell;
+  MCHK(c, m.tmp.reserve((size_t)nt * sizeof(float4)));
+  hipLaunchKernelGGL(k_lc_ids, dim3(blocks(nt)), dim3(256), 0, st, ls.tgt.as<float4>(), nt, m.tmp.as<float4>());
+  MRC(rebuild(&m, nt));
+  // ICP state
+  MCHK(c, ls.src.reserve((size_t)ns * sizeof(float4)));
+  MCHK(c, ls.ftf.reserve((size_t)ns * sizeof(float4)));
+  MCHK(c, ls.nb.reserve((size_t)ns * sizeof(float4)));
+  MCHK(c, ls.d2.reserve((size_t)ns * 4));
+  MCHK(c, ls.found.reserve((size_t)ns * 4));
+  MCHK(c, ls.st.reserve(sizeof(IcpDev)));
+  MCHK(c, hipMemcpyAsync(ls.src.p, ls.src0.p, (size_t)ns * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  IcpDev* h = ls.host;
+  std::memset(h, 0, sizeof(IcpDev));
+  for (int k = 0; k < 16; k++) h->T[k] = h->F[k] = (k % 5 == 0) ? 1.f : 0.f;
+  h->prev_mse = DBL_MAX;
+  h->nq = ns;
+  IcpDev* d = ls.st.as<IcpDev>();
+  MCHK(c, hipMemcpyAsync(d, h, sizeof(IcpDev), hipMemcpyHostToDevice, st));
+  IcpParams P;
+  P.max_iter = cfg->max_iterations;
+  P.rot_thr = 1.0 - cfg->transformation_epsilon;
+  P.trans_thr = cfg->transformation_epsilon;
+  P.mse_abs = 1e-12;
+  P.mse_rel = cfg->euclidean_fitness_epsilon;
+  const float md2 = cfg->max_correspondence_distance * cfg->max_correspondence_distance;
+  const int cap = std::max(cfg->max_iterations, 1);
+  constexpr int kChunk = 6;
+  for (int it0 = 0; it0 < cap; it0 += kChunk) {
+    for (int j = 0; j < kChunk && it0 + j < cap; j++) {
+      MRC(knn_device(&m, ls.src.as<float>(), 4, &d->nq, ns, nullptr, 1, md2, ls.nb.as<float4>(), ls.d2.as<float>(),
+                     ls.found.as<int>()));
+      {
+        TimedScope ts(c, kT_icp_step);
+        hipLaunchKernelGGL(k_lc_step, dim3(1), dim3(kRed), 0, st, d, ls.src.as<float4>(), ls.nb.as<float4>(),
+                           ls.d2.as<float>(), ls.found.as<int>(), ns, P);
+      }
+      TimedScope ts(c, kT_icp_apply);
+      hipLaunchKernelGGL(k_lc_apply, dim3(blocks(ns)), dim3(256), 0, st, d, ls.src.as<float4>(), ns);
+    }
+    MCHK(c, hipMemcpyAsync(h, d, sizeof(IcpDev), hipMemcpyDeviceToHost, st));
+    MCHK(c, hipStreamSynchronize(st));
+    if (h->done) break;
+  }
+  if (!h->done) return mfail(c, LISLAM_ERR_STATE, "lislam_loop_icp: iteration loop did not terminate");
+  // fitness
+  hipLaunchKernelGGL(k_lc_final_tf, dim3(blocks(ns)), dim3(256), 0, st, d, ls.src0.as<float4>(), ns, ls.ftf.as<float4>());
+  MRC(knn_device(&m, ls.ftf.as<float>(), 4, nullptr, ns, nullptr, 1, mapk::kInf, ls.nb.as<float4>(), ls.d2.as<float>(),
+                 ls.found.as<int>()));
+  hipLaunchKernelGGL(k_lc_fitness, dim3(1), dim3(kRed), 0, st, d, ls.d2.as<float>(), ls.found.as<int>(), ns);
+  MCHK(c, hipGetLastError());
+  MCHK(c, hipMemcpyAsync(h, d, sizeof(IcpDev), hipMemcpyDeviceToHost, st));
+  MCHK(c, hipStreamSynchronize(st));
+  fit = h->fitness;
+  inf[1] = (h->state >= 1 && h->state <= 4) ? 1 : 0;
+  inf[2] = h->state;
+  inf[3] = h->iter;
+  inf[6] = h->ncorr;
+  inf[0] = (inf[1] && fit <= cfg->fitness_threshold) ? 1 : 0;
+  for (int k = 0; k < 16; k++) Ti[k] = h->F[k];
+  for (int r = 0; r < 4; r++)
+    for (int col = 0; col < 4; col++)
+      Tc[4 * r + col] = ((Ti[4 * r] * T_cur[col] + Ti[4 * r + 1] * T_cur[4 + col]) + Ti[4 * r + 2] * T_cur[8 + col]) +
+                        Ti[4 * r + 3] * T_cur[12 + col];
+  return finish();
+}
+
+}  // extern "C"
+
+// ================================================================== odometry fusion
+// odomHandler's callback (src/odom_handler_node.cpp:44-132): per synchronized pair both poses
+// become 4x4 (Quaterniond::toRotationMatrix, :65-67, :83-85); the first pair sets prev and
+// odom_cur = intensity (:88-95); afterwards odom_cur *= prev.inverse() * cur of the A-LOAM pose
+// when the intensity tracker skipped the frame ("/odom_skip", intensity_feature_tracker.cpp:
+// 722-730, 861-866), else of the intensity pose (:98-107); prev = cur; published as
+// Quaterniond(rot_cur), t_cur (:113-128).  A sequential chain of ~250 flops per pair: one lane
+// walks the n pairs of a call, the state stays on the device between calls.  Rigid inverse
+// [R^T, -R^T t]; 4x4 products sum k = 0..3 left to right (oracle/oracle_fuse.cpp, same order).
+namespace lislam {
+namespace fusek {
+
+__device__ void to_mat(const double* p, double* M) {
+  const double x = p[0], y = p[1], z = p[2], w = p[3];
+  const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x, tyy = ty * y,
+               tyz = tz * y, tzz = tz * z;
+  const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+                       txz - twy, tyz + twx, 1 - (txx + tyy)};
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) M[4 * r + c] = R[3 * r + c];
+    M[4 * r + 3] = p[4 + r];
+  }
+  M[12] = M[13] = M[14] = 0;
+  M[15] = 1;
+}
+
+__device__ void inv_rigid(const double* M, double* I) {
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) I[4 * r + c] = M[4 * c + r];
+    I[4 * r + 3] = -((M[r] * M[3] + M[4 + r] * M[7]) + M[8 + r] * M[11]);
+  }
+  I[12] = I[13] = I[14] = 0;
+  I[15] = 1;
+}
+
+__device__ void mul(const double* A, const double* B, double* C) {
+  double T[16];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++)
+      T[4 * r + c] = ((A[4 * r] * B[c] + A[4 * r + 1] * B[4 + c]) + A[4 * r + 2] * B[8 + c]) + A[4 * r + 3] * B[12 + c];
+  for (int k = 0; k < 16; k++) C[k] = T[k];
+}
+
+// Quaterniond(Matrix3d) (Eigen: trace branch / largest diagonal) + translation
+__device__ void to_pose(const double* M, double* out) {
+  double q[4];
+  double t = (M[0] + M[5]) + M[10];
+  if (t > 0) {
+    t = sqrt(t + 1.0);
+    q[3] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (M[9] - M[6]) * t;
+    q[1] = (M[2] - M[8]) * t;
+    q[2] = (M[4] - M[1]) * t;
+  } else {
+    int i = 0;
+    if (M[5] > M[0]) i = 1;
+    if (M[10] > M[5 * i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = sqrt(((M[5 * i] - M[5 * j]) - M[5 * k]) + 1.0);
+    q[i] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (M[4 * k + j] - M[4 * j + k]) * t;
+    q[j] = (M[4 * j + i] + M[4 * i + j]) * t;
+    q[k] = (M[4 * k + i] + M[4 * i + k]) * t;
+  }
+  for (int e = 0; e < 4; e++) out[e] = q[e];
+  out[4] = M[3];
+  out[5] = M[7];
+  out[6] = M[11];
+}
+
+// state[49] = prev A-LOAM, prev intensity, odom_cur (4x4 each), initialised flag
+__global__ void k_fuse(double* state, const double* aloam, const double* intensity, const int* skip, int n, double* fused) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double pa[16], pi[16], cur[16];
+  for (int k = 0; k < 16; k++) { pa[k] = state[k]; pi[k] = state[16 + k]; cur[k] = state[32 + k]; }
+  bool init = state[48] != 0;
+  for (int f = 0; f < n; f++) {
+    double A[16], I[16];
+    to_mat(aloam + 7 * f, A);
+    to_mat(intensity + 7 * f, I);
+    if (!init) {
+      for (int k = 0; k < 16; k++) { pa[k] = A[k]; pi[k] = I[k]; cur[k] = I[k]; }
+      init = true;
+    } else {
+      double inv[16], d[16];
+      if (skip[f]) {
+        inv_rigid(pa, inv);
+        mul(inv, A, d);
+      } else {
+        inv_rigid(pi, inv);
+        mul(inv, I, d);
+      }
+      mul(cur, d, cur);
+      for (int k = 0; k < 16; k++) { pa[k] = A[k]; pi[k] = I[k]; }
+    }
+    to_pose(cur, fused + 7 * f);
+  }
+  for (int k = 0; k < 16; k++) { state[k] = pa[k]; state[16 + k] = pi[k]; state[32 + k] = cur[k]; }
+  state[48] = init ? 1.0 : 0.0;
+}
+
+}  // namespace fusek
+}  // namespace lislam
+
+struct lislam_odom_fuser {
+  lislam_ctx* ctx = nullptr;
+  DBuf state, io;
+};
+
+extern "C" {
+
+int lislam_odom_fuser_create(lislam_ctx* c, lislam_odom_fuser** out) {
+  if (!c || !out) return LISLAM_ERR_ARG;
+  *out = nullptr;
+  hipSetDevice(c->device);
+  auto* f = new lislam_odom_fuser();
+  f->ctx = c;
+  if (f->state.reserve(49 * 8) != hipSuccess || hipMemsetAsync(f->state.p, 0, 49 * 8, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    delete f;
+    return mfail(c, LISLAM_ERR_DEVICE, "lislam_odom_fuser_create: allocation failed");
+  }
+  *out = f;
+  return LISLAM_OK;
+}
+
+int lislam_odom_fuser_destroy(lislam_odom_fuser* f) {
+  if (!f) return LISLAM_OK;
+  hipSetDevice(f->ctx->device);
+  (void)hipStreamSynchronize(f->ctx->stream);
+  delete f;
+  return LISLAM_OK;
+}
+
+int lislam_odom_fuse(lislam_odom_fuser* f, const double* aloam, const double* intensity, const int32_t* skip, int32_t n,
+                     double* fused) {
+  if (!f || n < 0 || (n > 0 && (!aloam || !intensity || !skip || !fused))) return LISLAM_ERR_ARG;
+  if (n == 0) return LISLAM_OK;
+  lislam_ctx* c = f->ctx;
+  hipSetDevice(c->device);
+  hipStream_t st = c->stream;
+  const size_t pb = (size_t)n * 7 * 8;
+  MCHK(c, f->io.reserve(3 * pb + (size_t)n * 4));
+  char* base = f->io.as<char>();
+  double* da = reinterpret_cast<double*>(base);
+  double* di = reinterpret_cast<double*>(base + pb);
+  double* dout = reinterpret_cast<double*>(base + 2 * pb);
+  int* ds = reinterpret_cast<int*>(base + 3 * pb);
+  MCHK(c, hipMemcpyAsync(da, aloam, pb, hipMemcpyDefault, st));
+  MCHK(c, hipMemcpyAsync(di, intensity, pb, hipMemcpyDefault, st));
+  MCHK(c, hipMemcpyAsync(ds, skip, (size_t)n * 4, hipMemcpyDefault, st));
+  {
+    TimedScope ts(c, kT_fuse);
+    hipLaunchKernelGGL(lislam::fusek::k_fuse, dim3(1), dim3(64), 0, st, f->state.as<double>(), da, di, ds, n, dout);
+  }
+  MCHK(c, hipGetLastError());
+  MCHK(c, hipMemcpyAsync(fused, dout, pb, hipMemcpyDefault, st));
+  MCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
 }
 

@@ -39,11 +39,12 @@ EXPORTED_SYMBOLS = (
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
     "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
     "lislam_lmap_create", "lislam_lmap_destroy", "lislam_lmap_step", "lislam_lmap_counts", "lislam_lmap_points",
+    "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
 )
 
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
                "k_orb_fast", "k_orb_select", "k_orb_finish", "k_orb_blur", "k_orb_desc", "k_orb_match", "k_orb_lm",
-               "k_ground_screen", "k_ground_ransac", "k_ground_extract")
+               "k_ground_screen", "k_ground_ransac", "k_ground_extract", "k_lc_step", "k_lc_apply", "k_fuse")
 
 MATCH_LINE, MATCH_PLANE = 0, 1
 
@@ -75,6 +76,22 @@ class ScanOut(ctypes.Structure):
 
 class MapConfig(ctypes.Structure):
     _fields_ = [("downsample_size", ctypes.c_float), ("cell_size", ctypes.c_float)]
+
+
+class IcpConfig(ctypes.Structure):
+    """lislam_icp_config: loop_closure_parameters (config/spot.yaml:26-33) + the ICP settings of
+    intensity_feature_tracker.cpp:219-232; defaults = spot.yaml."""
+
+    _fields_ = [("use_crop", _i32), ("crop_size", ctypes.c_float), ("use_downsample", _i32),
+                ("voxel_size", ctypes.c_float), ("max_correspondence_distance", ctypes.c_float),
+                ("max_iterations", _i32), ("transformation_epsilon", ctypes.c_double),
+                ("euclidean_fitness_epsilon", ctypes.c_double), ("fitness_threshold", ctypes.c_double)]
+
+    def __init__(self, use_crop=False, crop_size=200.0, use_downsample=True, voxel_size=0.25,
+                 max_correspondence_distance=100.0, max_iterations=100, transformation_epsilon=1e-6,
+                 euclidean_fitness_epsilon=1e-6, fitness_threshold=0.5):
+        super().__init__(int(use_crop), crop_size, int(use_downsample), voxel_size, max_correspondence_distance,
+                         max_iterations, transformation_epsilon, euclidean_fitness_epsilon, fitness_threshold)
 
 
 class Frame(ctypes.Structure):
@@ -155,6 +172,10 @@ def load(path: str = LIB_PATH):
     L.lislam_lmap_counts.argtypes = [vp, vp, vp]
     L.lislam_lmap_points.argtypes = [vp, _i32, vp, i64, i64p]
     L.lislam_ground_extract.argtypes = [vp, vp, ctypes.POINTER(PointLayout), vp, _i32, _i32p, vp, vp]
+    L.lislam_loop_icp.argtypes = [vp, ctypes.POINTER(IcpConfig), vp, _i32, vp, vp, vp, _i32, vp, vp, vp, vp, vp]
+    L.lislam_odom_fuser_create.argtypes = [vp, ctypes.POINTER(vp)]
+    L.lislam_odom_fuser_destroy.argtypes = [vp]
+    L.lislam_odom_fuse.argtypes = [vp, vp, vp, vp, _i32, vp]
     L.lislam_map_set_timing.argtypes = [vp, _i32]
     L.lislam_map_kernel_times.argtypes = [vp, _fp, _i32p]
     for name in EXPORTED_SYMBOLS:

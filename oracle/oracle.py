@@ -69,6 +69,9 @@ def lib():
         L.oracle_lmap_points.restype = ctypes.c_int
         L.oracle_lmap_step.argtypes = [vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _f64p, _f64p, _i32p]
         L.oracle_ground_extract.restype = ctypes.c_int
+        L.oracle_loop_icp.argtypes = [_f32p, _i32p, _f64p, _f32p, ctypes.c_int, _f64p, _f32p, _i32p, ctypes.c_int,
+                                      _f64p, _f64p, _f64p, _f64p, _i32p]
+        L.oracle_odom_fuse.argtypes = [_f64p, _f64p, _f64p, _i32p, ctypes.c_int, _f64p]
         _LIB = L
     return _LIB
 
@@ -108,6 +111,70 @@ class LaserMap:
         out = np.zeros((max(n, 1), 4), np.float32)
         lib().oracle_lmap_points(self.h, which, out.ctypes.data)
         return out[:n]
+
+
+@dataclass
+class IcpConfig:
+    """loop_closure_parameters of config/spot.yaml:26-33 and the ICP settings of
+    intensity_feature_tracker.cpp:219-232 (defaults = spot.yaml)."""
+
+    use_crop: bool = False
+    crop_size: float = 200.0
+    use_downsample: bool = True
+    voxel_size: float = 0.25
+    max_correspondence_distance: float = 100.0
+    max_iterations: int = 100
+    transformation_epsilon: float = 1e-6
+    euclidean_fitness_epsilon: float = 1e-6
+    fitness_threshold: float = 0.5
+
+    def arrays(self):
+        f = np.array([self.crop_size, self.voxel_size, self.max_correspondence_distance, 0], np.float32)
+        i = np.array([int(self.use_crop), int(self.use_downsample), self.max_iterations, 0], np.int32)
+        d = np.array([self.transformation_epsilon, self.euclidean_fitness_epsilon, self.fitness_threshold], np.float64)
+        return f, i, d
+
+
+def _cloud4(c) -> np.ndarray:
+    c = np.ascontiguousarray(c, np.float32)
+    return c.reshape(-1, 4)
+
+
+def loop_icp(cur, T_cur, hist, T_hist, cfg: IcpConfig | None = None):
+    """The USE_ICP loop-closure block (intensity_feature_tracker.cpp:217-366) on one keyframe pair:
+    cur = the keyframe's cloud_track (n, 4), T_cur its 4x4 pose; hist = list of history keyframe
+    clouds with their 4x4 poses.  Returns (T_icp (4, 4), T_cur2map (4, 4), fitness, info (8,))."""
+    cfg = cfg or IcpConfig()
+    f, i, d = cfg.arrays()
+    c = _cloud4(cur)
+    hs = [_cloud4(h) for h in hist]
+    counts = np.array([h.shape[0] for h in hs], np.int32)
+    H = np.concatenate(hs) if hs else np.zeros((1, 4), np.float32)
+    if H.shape[0] == 0:
+        H = np.zeros((1, 4), np.float32)
+    Th = np.ascontiguousarray(np.array(T_hist, np.float64).reshape(-1, 16)) if len(hs) else np.zeros((1, 16))
+    T_icp = np.zeros(16)
+    T_c2m = np.zeros(16)
+    fit = np.zeros(1)
+    info = np.zeros(8, np.int32)
+    lib().oracle_loop_icp(f, i, d, c, c.shape[0], np.ascontiguousarray(T_cur, np.float64).reshape(16), H, counts,
+                          len(hs), Th, T_icp, T_c2m, fit, info)
+    return T_icp.reshape(4, 4), T_c2m.reshape(4, 4), float(fit[0]), info
+
+
+class OdomFuser:
+    """odomHandler's callback (odom_handler_node.cpp:44-132) over a stream of synchronized pairs."""
+
+    def __init__(self):
+        self.state = np.zeros(49, np.float64)
+
+    def step(self, aloam, intensity, skip):
+        a = np.ascontiguousarray(aloam, np.float64).reshape(-1, 7)
+        b = np.ascontiguousarray(intensity, np.float64).reshape(-1, 7)
+        s = np.ascontiguousarray(np.asarray(skip).reshape(-1), np.int32)
+        out = np.zeros_like(a)
+        lib().oracle_odom_fuse(self.state, a, b, s, a.shape[0], out)
+        return out
 
 
 def ground_extract(points: np.ndarray):

@@ -827,3 +827,281 @@ void oracle_lmap_step(void* h, const float* corner_last, int nc, const float* su
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ loop-closure ICP
+// feature_tracker::loopClosureThread's USE_ICP block (src/intensity_feature_tracker.cpp:217-366)
+// with its helpers tranformCurrentScanToMap (:167-172) and getSubmapOfhistory (:174-193):
+//   current = keyframe cloud_track transformed by T_cur (pcl::transformPointCloud with a Matrix4d:
+//   per point ((T00 x + T01 y) + T02 z) + T03 in double, stored as float; intensity copied),
+//   submap = the history keyframes' clouds transformed by their poses, concatenated in order;
+//   removeNaNFromPointCloud (non-finite x, y or z dropped), CropBox [-crop, crop]^3 inclusive
+//   (USE_CROP), VoxelGrid(vf_scan_res) (USE_DOWNSAMPLE), and when both clouds hold > 10 points
+//   pcl::IterativeClosestPoint (PCL 1.10, absent here: restated from its published algorithm):
+//     setMaxCorrespondenceDistance(100), setMaximumIterations(100), setTransformationEpsilon(1e-6),
+//     setEuclideanFitnessEpsilon(1e-6), RANSAC iterations 0 (:219-223).
+//   Each iteration: CorrespondenceEstimation (1-NN of every source point in the target, squared
+//   float distance <= max^2; ties by target index), < 3 correspondences -> NO_CORRESPONDENCES;
+//   TransformationEstimationSVD (umeyama without scaling) — the rotation maximising
+//   trace(R^T Sigma) is taken from Horn's 4x4 quaternion eigenproblem in double (cyclic Jacobi):
+//   the same minimiser as Eigen's JacobiSVD route, parity against PCL's float SVD unpinned; the
+//   float transformation_ is applied to the source (((m00 x + m01 y) + m02 z) + m03 in float),
+//   final = transformation_ * final (float 4x4, k = 0..3 left to right); then
+//   DefaultConvergenceCriteria (max iterations -> ITERATIONS, translation^2 <= eps and
+//   cos(angle) >= 1 - eps -> TRANSFORM, |dMSE| < 1e-12 -> ABS_MSE, |dMSE| / MSE_prev < fitness eps
+//   -> REL_MSE; max_iterations_similar_transforms 0).  getFitnessScore: the original source under
+//   `final`, mean 1-NN squared distance.  accepted = converged && fitness <= icp_fitness_score
+//   (:314); T_cur2map_gt = double(final) * T_cur (:316-321).
+// Sums over points (MSE, means, cross-covariance, fitness) use one fixed order shared with the
+// device: 1024 strided partial sums in double, then a halving tree.
+namespace oracle {
+
+constexpr int kIcpRed = 1024;
+
+template <int V, class F>
+static void icp_sum(int n, F f, double out[V]) {
+  std::vector<double> acc((size_t)kIcpRed * V, 0.0);
+  for (int t = 0; t < kIcpRed; t++)
+    for (int i = t; i < n; i += kIcpRed) {
+      double v[V];
+      if (f(i, v))
+        for (int k = 0; k < V; k++) acc[(size_t)t * V + k] += v[k];
+    }
+  for (int s = kIcpRed / 2; s > 0; s >>= 1)
+    for (int t = 0; t < s; t++)
+      for (int k = 0; k < V; k++) acc[(size_t)t * V + k] += acc[(size_t)(t + s) * V + k];
+  for (int k = 0; k < V; k++) out[k] = acc[k];
+}
+
+// cyclic Jacobi of a symmetric 4x4 (A is destroyed; V = eigenvectors in columns)
+static void jacobi4(double A[4][4], double V[4][4]) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) V[i][j] = i == j ? 1.0 : 0.0;
+  double tot = 0;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) tot += A[i][j] * A[i][j];
+  for (int sweep = 0; sweep < 32; sweep++) {
+    double off = 0;
+    for (int p = 0; p < 4; p++)
+      for (int q = p + 1; q < 4; q++) off += A[p][q] * A[p][q];
+    if (!(off > 1e-36 * tot)) break;
+    for (int p = 0; p < 4; p++)
+      for (int q = p + 1; q < 4; q++) {
+        const double apq = A[p][q];
+        if (apq == 0.0) continue;
+        const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+        double t = 1.0 / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        if (theta < 0) t = -t;
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 4; k++) {
+          const double akp = A[k][p], akq = A[k][q];
+          A[k][p] = c * akp - s * akq;
+          A[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 4; k++) {
+          const double apk = A[p][k], aqk = A[q][k];
+          A[p][k] = c * apk - s * aqk;
+          A[q][k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < 4; k++) {
+          const double vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = c * vkp - s * vkq;
+          V[k][q] = s * vkp + c * vkq;
+        }
+      }
+  }
+}
+
+// umeyama(src, tgt, false) from the demeaned cross-covariance S[a][b] = mean (s_a - ms_a)(t_b - mt_b)
+static void horn_rt(const double S[3][3], const double ms[3], const double mt[3], double R[3][3], double t[3]) {
+  const double Sxx = S[0][0], Sxy = S[0][1], Sxz = S[0][2], Syx = S[1][0], Syy = S[1][1], Syz = S[1][2], Szx = S[2][0],
+               Szy = S[2][1], Szz = S[2][2];
+  double N[4][4] = {{(Sxx + Syy) + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx},
+                    {Syz - Szy, (Sxx - Syy) - Szz, Sxy + Syx, Szx + Sxz},
+                    {Szx - Sxz, Sxy + Syx, (Syy - Sxx) - Szz, Syz + Szy},
+                    {Sxy - Syx, Szx + Sxz, Syz + Szy, (Szz - Sxx) - Syy}};
+  double V[4][4];
+  jacobi4(N, V);
+  int k = 0;
+  for (int j = 1; j < 4; j++)
+    if (N[j][j] > N[k][k]) k = j;
+  double w = V[0][k], x = V[1][k], y = V[2][k], z = V[3][k];
+  const double nn = std::sqrt(((w * w + x * x) + y * y) + z * z);
+  w /= nn; x /= nn; y /= nn; z /= nn;
+  const double tx = 2 * x, ty = 2 * y, tz = 2 * z;  // Eigen's toRotationMatrix
+  const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x, tyy = ty * y,
+               tyz = tz * y, tzz = tz * z;
+  R[0][0] = 1 - (tyy + tzz); R[0][1] = txy - twz; R[0][2] = txz + twy;
+  R[1][0] = txy + twz; R[1][1] = 1 - (txx + tzz); R[1][2] = tyz - twx;
+  R[2][0] = txz - twy; R[2][1] = tyz + twx; R[2][2] = 1 - (txx + tyy);
+  for (int a = 0; a < 3; a++) t[a] = mt[a] - ((R[a][0] * ms[0] + R[a][1] * ms[1]) + R[a][2] * ms[2]);
+}
+
+static inline P4 tf_f(const float* T, const P4& p) {
+  return P4{((T[0] * p.x + T[1] * p.y) + T[2] * p.z) + T[3], ((T[4] * p.x + T[5] * p.y) + T[6] * p.z) + T[7],
+            ((T[8] * p.x + T[9] * p.y) + T[10] * p.z) + T[11], p.i};
+}
+static inline P4 tf_d(const double* T, const P4& p) {
+  const double x = p.x, y = p.y, z = p.z;
+  return P4{(float)(((T[0] * x + T[1] * y) + T[2] * z) + T[3]), (float)(((T[4] * x + T[5] * y) + T[6] * z) + T[7]),
+            (float)(((T[8] * x + T[9] * y) + T[10] * z) + T[11]), p.i};
+}
+
+struct IcpCfg {
+  int use_crop;
+  float crop_size;
+  int use_downsample;
+  float voxel_size;
+  float max_corr_dist;
+  int max_iterations;
+  double trans_eps, fitness_eps, fitness_threshold;
+};
+
+static void icp_prepare(const IcpCfg& cfg, std::vector<P4>& c) {
+  std::vector<P4> o;
+  o.reserve(c.size());
+  const float lo = -cfg.crop_size, hi = cfg.crop_size;
+  for (const P4& p : c) {
+    if (!std::isfinite(p.x) || !std::isfinite(p.y) || !std::isfinite(p.z)) continue;
+    if (cfg.use_crop && (p.x < lo || p.y < lo || p.z < lo || p.x > hi || p.y > hi || p.z > hi)) continue;
+    o.push_back(p);
+  }
+  if (cfg.use_downsample && !o.empty()) {
+    std::vector<P4> v(o.size());
+    int nv = 0;
+    oracle_voxel_grid(reinterpret_cast<const float*>(o.data()), (int)o.size(), cfg.voxel_size, 1,
+                      reinterpret_cast<float*>(v.data()), &nv);
+    v.resize(nv);
+    o.swap(v);
+  }
+  c.swap(o);
+}
+
+}  // namespace oracle
+
+extern "C" {
+
+// cfg_f[4] = crop_size, voxel_size, max_corr_dist, (unused); cfg_i[4] = use_crop, use_downsample,
+// max_iterations, (unused); cfg_d[3] = transformation eps, euclidean fitness eps, icp_fitness_score.
+// cur: n_cur points (x, y, z, i); hist: the history clouds concatenated, hist_counts[n_hist];
+// T_cur[16], T_hist[n_hist][16] row-major.  Outputs T_icp[16] (the float final transformation),
+// T_cur2map[16], fitness[1], info[8] = accepted (1 / 0; -1 submap empty, -2 <= 10 points),
+// converged, convergence state (0 not converged, 1 iterations, 2 transform, 3 abs MSE,
+// 4 rel MSE, 5 no correspondences), iterations, source points, target points, last
+// correspondences, 0.
+void oracle_loop_icp(const float* cfg_f, const int* cfg_i, const double* cfg_d, const float* cur, int n_cur,
+                     const double* T_cur, const float* hist, const int* hist_counts, int n_hist, const double* T_hist,
+                     double* T_icp, double* T_cur2map, double* fitness, int* info) {
+  using namespace oracle;
+  IcpCfg cfg{cfg_i[0], cfg_f[0], cfg_i[1], cfg_f[1], cfg_f[2], cfg_i[2], cfg_d[0], cfg_d[1], cfg_d[2]};
+  for (int k = 0; k < 8; k++) info[k] = 0;
+  for (int k = 0; k < 16; k++) { T_icp[k] = (k % 5 == 0) ? 1.0 : 0.0; T_cur2map[k] = T_cur[k]; }
+  *fitness = DBL_MAX;
+  std::vector<P4> src, tgt;
+  const P4* cp = reinterpret_cast<const P4*>(cur);
+  for (int i = 0; i < n_cur; i++) src.push_back(tf_d(T_cur, cp[i]));
+  const P4* hp = reinterpret_cast<const P4*>(hist);
+  for (int h = 0, off = 0; h < n_hist; off += hist_counts[h], h++)
+    for (int i = 0; i < hist_counts[h]; i++) tgt.push_back(tf_d(T_hist + 16 * h, hp[off + i]));
+  if (tgt.empty()) { info[0] = -1; return; }
+  icp_prepare(cfg, src);
+  icp_prepare(cfg, tgt);
+  const int ns = (int)src.size(), nt = (int)tgt.size();
+  info[4] = ns;
+  info[5] = nt;
+  if (ns <= 10 || nt <= 10) { info[0] = -2; return; }
+  KnnTree tree;
+  {
+    std::vector<MapPoint> mp(nt);
+    for (int i = 0; i < nt; i++) mp[i] = MapPoint{tgt[i].x, tgt[i].y, tgt[i].z, i};
+    tree.build(mp);
+  }
+  std::vector<int> nn(ns);
+  std::vector<float> nd(ns);
+  auto nearest = [&](const std::vector<P4>& q, float maxd2) {
+    std::vector<KnnTree::Best> best;
+    for (int i = 0; i < ns; i++) {
+      best.clear();
+      const float qq[3] = {q[i].x, q[i].y, q[i].z};
+      tree.search(0, qq, 1, maxd2, best);
+      nn[i] = best.empty() ? -1 : best[0].id;
+      nd[i] = best.empty() ? 0.f : best[0].d;
+    }
+  };
+  const float md2 = cfg.max_corr_dist * cfg.max_corr_dist;
+  float F[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  std::vector<P4> cur_src = src;
+  double prev_mse = DBL_MAX;
+  int it = 0, state = 0;
+  const double rot_thr = 1.0 - cfg.trans_eps, trans_thr = cfg.trans_eps, mse_abs = 1e-12, mse_rel = cfg.fitness_eps;
+  while (true) {
+    nearest(cur_src, md2);
+    double s1[8];
+    icp_sum<8>(ns, [&](int i, double* v) {
+      if (nn[i] < 0) return false;
+      const P4& t = tgt[nn[i]];
+      v[0] = 1; v[1] = nd[i];
+      v[2] = cur_src[i].x; v[3] = cur_src[i].y; v[4] = cur_src[i].z;
+      v[5] = t.x; v[6] = t.y; v[7] = t.z;
+      return true;
+    }, s1);
+    const int cnt = (int)s1[0];
+    info[6] = cnt;
+    if (cnt < 3) { state = 5; break; }
+    const double ms[3] = {s1[2] / s1[0], s1[3] / s1[0], s1[4] / s1[0]}, mt[3] = {s1[5] / s1[0], s1[6] / s1[0], s1[7] / s1[0]};
+    double s2[9];
+    icp_sum<9>(ns, [&](int i, double* v) {
+      if (nn[i] < 0) return false;
+      const P4& t = tgt[nn[i]];
+      const double a[3] = {cur_src[i].x - ms[0], cur_src[i].y - ms[1], cur_src[i].z - ms[2]};
+      const double b[3] = {t.x - mt[0], t.y - mt[1], t.z - mt[2]};
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) v[3 * r + c] = a[r] * b[c];
+      return true;
+    }, s2);
+    double S[3][3], R[3][3], tr[3];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) S[r][c] = s2[3 * r + c] / s1[0];
+    horn_rt(S, ms, mt, R, tr);
+    float T[16] = {(float)R[0][0], (float)R[0][1], (float)R[0][2], (float)tr[0], (float)R[1][0], (float)R[1][1],
+                   (float)R[1][2], (float)tr[1], (float)R[2][0], (float)R[2][1], (float)R[2][2], (float)tr[2],
+                   0.f, 0.f, 0.f, 1.f};
+    for (int i = 0; i < ns; i++) cur_src[i] = tf_f(T, cur_src[i]);
+    float G[16];
+    for (int r = 0; r < 4; r++)
+      for (int c = 0; c < 4; c++)
+        G[4 * r + c] = ((T[4 * r] * F[c] + T[4 * r + 1] * F[4 + c]) + T[4 * r + 2] * F[8 + c]) + T[4 * r + 3] * F[12 + c];
+    std::memcpy(F, G, sizeof(F));
+    ++it;
+    // DefaultConvergenceCriteria::hasConverged
+    if (it >= cfg.max_iterations) { state = 1; break; }
+    const double cos_angle = 0.5 * ((((double)T[0] + (double)T[5]) + (double)T[10]) - 1.0);
+    const double tsq = ((double)T[3] * (double)T[3] + (double)T[7] * (double)T[7]) + (double)T[11] * (double)T[11];
+    if (cos_angle >= rot_thr && tsq <= trans_thr) { state = 2; break; }
+    const double mse = s1[1] / s1[0];
+    if (std::fabs(mse - prev_mse) < mse_abs) { state = 3; break; }
+    if (std::fabs(mse - prev_mse) / prev_mse < mse_rel) { state = 4; break; }
+    prev_mse = mse;
+  }
+  info[1] = (state >= 1 && state <= 4) ? 1 : 0;
+  info[2] = state;
+  info[3] = it;
+  for (int k = 0; k < 16; k++) T_icp[k] = F[k];
+  // getFitnessScore: the original source under final
+  std::vector<P4> fsrc(ns);
+  for (int i = 0; i < ns; i++) fsrc[i] = tf_f(F, src[i]);
+  nearest(fsrc, INFINITY);
+  double s3[2];
+  icp_sum<2>(ns, [&](int i, double* v) {
+    if (nn[i] < 0) return false;
+    v[0] = 1; v[1] = nd[i];
+    return true;
+  }, s3);
+  *fitness = s3[0] > 0 ? s3[1] / s3[0] : DBL_MAX;
+  info[0] = (info[1] && *fitness <= cfg.fitness_threshold) ? 1 : 0;
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++)
+      T_cur2map[4 * r + c] = ((T_icp[4 * r] * T_cur[c] + T_icp[4 * r + 1] * T_cur[4 + c]) + T_icp[4 * r + 2] * T_cur[8 + c]) +
+                             T_icp[4 * r + 3] * T_cur[12 + c];
+}
+
+}  // extern "C"

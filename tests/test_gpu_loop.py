@@ -1,0 +1,90 @@
+"""GPU parity of the loop-closure ICP (lislam_loop_icp, intensity_feature_tracker.cpp:217-366)
+and of the odometry fusion (lislam_odom_fuse, odom_handler_node.cpp:44-132) through the C ABI
+against the CPU oracle.
+
+The device performs the oracle's floating-point operations in the same order (fixed-order double
+reductions, the same Jacobi sweeps, float transforms): the final transformation, fitness score,
+convergence state, iteration and point counts must be bit-identical; poses within 1e-4 would be
+the contract's bar, the test holds them to equality."""
+import numpy as np
+import pytest
+
+from loop_cases import corridor_loop, drift, random_room
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(n_scans=64, width=1024)
+    yield c
+    c.close()
+
+
+def _same(got, ref):
+    Ti, Tc2m, fit, info = got
+    rTi, rTc2m, rfit, rinfo = ref
+    assert list(info) == list(rinfo)
+    assert np.array_equal(Ti, rTi)
+    assert np.array_equal(Tc2m, rTc2m)
+    assert fit == rfit
+
+
+@pytest.mark.parametrize("d", [(0.3, -0.2, 0.05, 2.0, 0.5), (1.0, 0.4, 0.0, -5.0, 0.0)])
+def test_loop_icp_corridor_bit_exact(pkg, oracle, synth, ctx, d):
+    cur, Tc, hs, Th, T_true = corridor_loop(synth, d=d)
+    ref = oracle.loop_icp(cur, Tc, hs, Th)
+    got = pkg.loop.loop_closure_icp(ctx, cur, Tc, hs, Th)
+    _same(got, ref)
+    assert got[3][1] == 1 and got[3][3] > 1
+
+
+def test_loop_icp_configs(pkg, oracle, synth, ctx):
+    cur, Tc, hs, Th, _ = corridor_loop(synth, k=20, hist=(19,), n_scans=64)
+    for kw in (dict(use_crop=True, crop_size=6.0), dict(voxel_size=0.4, fitness_threshold=0.01),
+               dict(max_iterations=3), dict(max_correspondence_distance=0.3)):
+        ref = oracle.loop_icp(cur, Tc, hs, Th, oracle.IcpConfig(**kw))
+        got = pkg.loop.loop_closure_icp(ctx, cur, Tc, hs, Th, pkg.loop.IcpConfig(**kw))
+        _same(got, ref)
+
+
+def test_loop_icp_no_downsample_room(pkg, oracle, ctx):
+    rng = np.random.default_rng(3)
+    room = random_room(rng)
+    D = drift(0.15, -0.1, 0.03, 3.0, 1.0)
+    cur = room.copy()
+    X = cur[:, :3].astype(np.float64) @ np.linalg.inv(D)[:3, :3].T + np.linalg.inv(D)[:3, 3]
+    cur[:, :3] = X.astype(np.float32)
+    ref = oracle.loop_icp(cur, np.eye(4), [room], [np.eye(4)], oracle.IcpConfig(use_downsample=False))
+    got = pkg.loop.loop_closure_icp(ctx, cur, np.eye(4), [room], [np.eye(4)], pkg.loop.IcpConfig(use_downsample=False))
+    _same(got, ref)
+    assert got[3][0] == 1 and np.max(np.abs(got[0] - D)) < 1e-3
+
+
+def test_loop_icp_edge_cases(pkg, oracle, synth, ctx):
+    cur = synth.make_scan(5).reshape(-1, 4)
+    _same(pkg.loop.loop_closure_icp(ctx, cur, np.eye(4), [], []), oracle.loop_icp(cur, np.eye(4), [], []))
+    tiny = np.zeros((5, 4), np.float32)
+    _same(pkg.loop.loop_closure_icp(ctx, tiny, np.eye(4), [cur], [np.eye(4)]),
+          oracle.loop_icp(tiny, np.eye(4), [cur], [np.eye(4)]))
+    nan = cur.copy()
+    nan[::7, 1] = np.nan
+    _same(pkg.loop.loop_closure_icp(ctx, nan, np.eye(4), [cur, cur[::2]], [np.eye(4), np.eye(4)]),
+          oracle.loop_icp(nan, np.eye(4), [cur, cur[::2]], [np.eye(4), np.eye(4)]))
+
+
+def test_odom_fusion_bit_exact(pkg, oracle, ctx):
+    rng = np.random.default_rng(11)
+    n = 64
+    q = rng.normal(size=(2, n, 4))
+    q /= np.linalg.norm(q, axis=2, keepdims=True)
+    a = np.concatenate([q[0], rng.normal(scale=5, size=(n, 3))], 1)
+    b = np.concatenate([q[1], rng.normal(scale=5, size=(n, 3))], 1)
+    skip = (rng.random(n) < 0.3).astype(np.int32)
+    ref = oracle.OdomFuser().step(a, b, skip)
+    h = pkg.loop.OdomHandler(ctx)
+    got = np.concatenate([h.fuse(a[:20], b[:20], skip[:20]),
+                          np.stack([h.callback(a[k], b[k], "/odom_skip" if skip[k] else "/laser_odom") for k in range(20, 30)]),
+                          h.fuse(a[30:], b[30:], skip[30:])])
+    h.close()
+    assert np.array_equal(got, ref)
