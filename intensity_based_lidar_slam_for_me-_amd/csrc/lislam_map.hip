@@ -41,7 +41,7 @@ namespace mapk {
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kG = 64;          // lanes per query in k_knn (one wavefront)
-constexpr int kMaxShell = 24;   // beyond this the search scans the whole map (unbounded max_dist only)
+constexpr int kMaxShell = 24;   // beyond this the search scans the whole map (exact either way)
 constexpr float kInf = __builtin_huge_valf();
 
 __host__ __device__ __forceinline__ uint64_t pack_cell(int ix, int iy, int iz) {
@@ -70,7 +70,19 @@ struct MapView {
   uint32_t hmask;
   float cell, inv_cell;
   int n;
+  int scan_shell;  // after this shell a query scans the whole map: the shells' cell probes would cost more
 };
+
+// first shell s whose cells walked so far (27 + sum_{j=2..s} 24 j^2 + 2) reach n / 4 point loads
+inline int scan_shell_for(int64_t n) {
+  int64_t cum = 27;
+  int s = 1;
+  while (s < kMaxShell && cum * 4 < n) {
+    s++;
+    cum += 24 * (int64_t)s * s + 2;
+  }
+  return std::max(s, 2);
+}
 
 __device__ __forceinline__ int2 cell_lookup(const MapView& m, uint64_t key) {
   uint32_t h = mix64(key) & m.hmask;
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
     const double gap = fmin(block_gap(q.x, cx, s, m.cell), fmin(block_gap(q.y, cy, s, m.cell), block_gap(q.z, cz, s, m.cell)));
     if (gap >= maxd * (1.0 + 1e-6)) break;                                  // every point within max_dist seen
     if (kth != kInf && (double)kth < gap * gap * (1.0 - 1e-6)) break;  // none closer outside
-    if (s >= kMaxShell) {                                                   // far from the map: scan it all
+    if (s >= m.scan_shell) {                                                // far from the map: scan it all
       kb_clear(b);
       for (int p = lane; p < m.n; p += 64) {
         const float4 v = m.pts[p];
@@ -750,13 +762,33 @@ __global__ void k_vg_centroids(const float4* in, const uint32_t* skeys, const in
   }
   if (i == 0) *n_out = n > 0 ? pos[n - 1] + flag[n - 1] : 0;
   if (i >= n || !flag[i]) return;
+  // the run's points are summed one after another in sorted (input) order; the loads of 16
+  // points are issued ahead of their adds so a long run (e.g. the dropout points of a scan)
+  // costs one memory latency per 16 points
+  const uint32_t key = skeys[i];
   float4 c = in[sidx[i]];
   int e = i + 1;
-  for (; e < n && skeys[e] == skeys[i]; e++) {
-    const float4 p = in[sidx[e]];
-    c.x += p.x; c.y += p.y; c.z += p.z; c.w += p.w;
+  constexpr int U = 16;
+  int cntn = 1;
+  bool more = true;
+  while (more) {
+    int ix[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) ix[u] = (e + u < n && skeys[e + u] == key) ? sidx[e + u] : -1;
+    float4 p[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) p[u] = ix[u] >= 0 ? in[ix[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (ix[u] >= 0) {
+        c.x += p[u].x; c.y += p[u].y; c.z += p[u].z; c.w += p[u].w;
+        cntn++;
+      }
+    }
+    more = ix[U - 1] >= 0;
+    e += U;
   }
-  const float cnt = (float)(e - i);
+  const float cnt = (float)cntn;
   c.x /= cnt; c.y /= cnt; c.z /= cnt; c.w /= cnt;
   out[pos[i]] = c;
 }
@@ -995,6 +1027,7 @@ struct lislam_map {
     v.cell = cell;
     v.inv_cell = 1.0f / cell;
     v.n = (int)n;
+    v.scan_shell = mapk::scan_shell_for(n);
     return v;
   }
 };
