@@ -122,6 +122,12 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans);
 /* a12..a18 for scans [0, n_scans): ceil((n_scans-1)/chain_len) independent chains, chain c is a
  * fresh laserOdometry node over scans [c*chain_len, min((c+1)*chain_len, n_scans-1)]. */
 int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len);
+/* The reference's default gating (laserOdometry.cpp:403-417): pair (k-1, k) is associated and
+ * optimized only when use_aloam[k] != 0 — the sharp cloud's frame_id is "skip_intensity", i.e.
+ * the intensity tracker skipped scan k (scanRegistration.cpp:603-609; LISLAM_OUT_ORB_STATS[0] ==
+ * 0).  Otherwise para keeps the previous estimate and the pose accumulates it (:716-717).
+ * use_aloam[n_scans]: host or device memory.  lislam_batch_odometry = every use_aloam set. */
+int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_len, const int32_t* use_aloam);
 /* Enable per-kernel HIP-event timing: every following extract / odometry call records events on
  * the stream (no host synchronization). */
 int lislam_batch_set_timing(lislam_batch* b, int32_t enable);

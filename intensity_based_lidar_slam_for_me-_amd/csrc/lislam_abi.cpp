@@ -192,6 +192,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.pose, (size_t)S * 7);
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
+  rc |= dalloc(b, &b->d_gate, (size_t)S);
   if (rc != LISLAM_OK) {
     lislam_batch_destroy(b);
     return LISLAM_ERR_DEVICE;
@@ -321,9 +322,15 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   return LISLAM_OK;
 }
 
-static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const double* init_host) {
+static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const double* init_host,
+                        const int32_t* use_aloam = nullptr) {
   lislam_ctx* c = b->ctx;
   OdomArgs o = b->oa;
+  o.gate = nullptr;
+  if (use_aloam) {
+    HIPCHK(c, hipMemcpyAsync(b->d_gate, use_aloam, sizeof(int) * n_scans, hipMemcpyDefault, c->stream));
+    o.gate = b->d_gate;
+  }
   o.S = n_scans;
   o.chain_len = chain_len;
   o.n_chains = n_scans > 1 ? (n_scans - 1 + chain_len - 1) / chain_len : 0;
@@ -360,6 +367,13 @@ int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len) {
   if (b->extracted < n_scans) return fail(b->ctx, LISLAM_ERR_STATE, "extract %d scans before odometry", n_scans);
   hipSetDevice(b->ctx->device);
   return run_odometry(b, n_scans, chain_len, nullptr);
+}
+
+int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_len, const int32_t* use_aloam) {
+  if (!b || n_scans < 1 || n_scans > b->max_scans || chain_len < 1 || !use_aloam) return LISLAM_ERR_ARG;
+  if (b->extracted < n_scans) return fail(b->ctx, LISLAM_ERR_STATE, "extract %d scans before odometry", n_scans);
+  hipSetDevice(b->ctx->device);
+  return run_odometry(b, n_scans, chain_len, nullptr, use_aloam);
 }
 
 int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls) {

@@ -19,6 +19,7 @@ struct lislam_batch {
   FeatureArgs fa{};
   OdomArgs oa{};
   double* d_init = nullptr;
+  int* d_gate = nullptr;  // [max_scans] use_aloam of lislam_batch_odometry_gated
   bool timing = false;
   // per-call event sets recorded on the stream while timing is on; read back (and released)
   // by lislam_batch_kernel_times, so the timed region never blocks on the host.

@@ -98,6 +98,7 @@ struct OdomArgs {
   double* pose;    // [S][7] q_w_curr, t_w_curr in the chain's frame
   int* stats;      // [S][8] corners/planes for outer 0/1, LM iterations 0/1, terminations 0/1
   int dbg;         // ablation switch for profiling (0 in production): 1 skip 1-NN, 2 skip line search
+  const int* gate;  // [S] use_aloam per scan (laserOdometry.cpp:403-417), or null = every scan
 };
 
 // Batched evaluation of the cost functors (lislam_eval_factors).

@@ -641,6 +641,7 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   c += a.c0;
   int k;
   if (!pair_of(a, c, r, &k)) return;
+  if (a.gate && !a.gate[k]) return;  // not optimized: no association (laserOdometry.cpp:417)
   const int lane = lane_id();
   const int w = qb * kAssocWaves + (int)(threadIdx.x >> 6);
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
@@ -803,7 +804,13 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const double* blk = a.blk + (size_t)c * (a.cap_sharp + a.cap_flat) * 9;
   const int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
-  count_kinds(sh, kind, ns, a.cap_sharp, nf);
+  const bool gated_off = a.gate && !a.gate[k];  // use_aloam false: no solve, the pose still accumulates
+  if (gated_off) {
+    if (threadIdx.x == 0) sh.nc = sh.np = 0;
+    __syncthreads();
+  } else {
+    count_kinds(sh, kind, ns, a.cap_sharp, nf);
+  }
   const int nc = sh.nc, np = sh.np;
   // The solver state lives in LDS and is in registers only inside thread 0's step, so it does not
   // stack on the evaluation's registers (which spilled to scratch when it was held across).

@@ -171,8 +171,23 @@ class Batch:
     def extract(self, n: int):
         nat.check(self.ctx.lib.lislam_batch_extract(self.h, n), self.ctx.h, "lislam_batch_extract")
 
-    def odometry(self, n: int, chain_len: int):
-        nat.check(self.ctx.lib.lislam_batch_odometry(self.h, n, chain_len), self.ctx.h, "lislam_batch_odometry")
+    def odometry(self, n: int, chain_len: int, use_aloam=None):
+        """a12-a18 over scans [0, n) in chains of chain_len pairs.  use_aloam (n,) switches to the
+        reference's default gating (laserOdometry.cpp:403-417): scan k is optimized only where
+        use_aloam[k] != 0 (see skip_flags)."""
+        if use_aloam is None:
+            nat.check(self.ctx.lib.lislam_batch_odometry(self.h, n, chain_len), self.ctx.h, "lislam_batch_odometry")
+            return
+        u = np.ascontiguousarray(np.asarray(use_aloam).reshape(-1), np.int32)
+        if u.shape[0] < n:
+            raise ValueError("use_aloam needs one flag per scan")
+        nat.check(self.ctx.lib.lislam_batch_odometry_gated(self.h, n, chain_len, nat.ptr(u)), self.ctx.h,
+                  "lislam_batch_odometry_gated")
+
+    def skip_flags(self, n: int) -> np.ndarray:
+        """use_aloam per scan from the ORB front end's results (intensity_odometry first): 1 where
+        detectfeatures skipped the frame (the "skip_intensity" frame_id, scanRegistration.cpp:603-609)."""
+        return np.array([int(self.download(nat.OUT_ORB_STATS, k)[0] == 0) for k in range(n)], np.int32)
 
     def intensity_odometry(self, n: int, nfeatures: int = 1000, mask=None):
         """feature_tracker::detectfeatures over scans [0, n) of the batch (ORB path a8-a11)."""

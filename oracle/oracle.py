@@ -37,6 +37,8 @@ def lib():
         L.oracle_voxel_grid.argtypes = [_f32p, ctypes.c_int, ctypes.c_float, ctypes.c_int, _f32p, _i32p]
         L.oracle_odometry_chain.argtypes = [
             ctypes.c_int, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f64p, _f64p, _i32p]
+        L.oracle_odometry_chain_gated.argtypes = [
+            ctypes.c_int, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _f32p, _i32p, _i32p, _f64p, _f64p, _i32p]
         L.oracle_nn1.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, _i32p, _f32p]
         L.oracle_eval_factor.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, _f64p, _f64p]
         vp = ctypes.c_void_p
@@ -250,8 +252,10 @@ def _pack(arrs):
     return np.ascontiguousarray(cat, np.float32).reshape(-1), off
 
 
-def odometry_chain(feats: list[ScanFeatures]):
-    """Fresh laserOdometry node over ``feats``; returns (world poses (n,7), para (n,7), stats (n,6))."""
+def odometry_chain(feats: list[ScanFeatures], use_aloam=None):
+    """Fresh laserOdometry node over ``feats``; returns (world poses (n,7), para (n,7), stats (n,6)).
+    use_aloam (n,) (None: every frame): frame k is optimized only where use_aloam[k] != 0
+    (laserOdometry.cpp:403-417), the pose accumulates the previous estimate otherwise."""
     n = len(feats)
     s, so = _pack([f.sharp for f in feats])
     ls, lso = _pack([f.less_sharp for f in feats])
@@ -260,8 +264,13 @@ def odometry_chain(feats: list[ScanFeatures]):
     pose = np.zeros((n, 7), np.float64)
     rel = np.zeros((n, 7), np.float64)
     st = np.zeros((n, 6), np.int32)
-    lib().oracle_odometry_chain(n, s, so, ls, lso, fl, flo, lf, lfo, pose.reshape(-1), rel.reshape(-1),
-                                st.reshape(-1))
+    if use_aloam is None:
+        lib().oracle_odometry_chain(n, s, so, ls, lso, fl, flo, lf, lfo, pose.reshape(-1), rel.reshape(-1),
+                                    st.reshape(-1))
+    else:
+        u = np.ascontiguousarray(np.asarray(use_aloam).reshape(-1), np.int32)
+        lib().oracle_odometry_chain_gated(n, s, so, ls, lso, fl, flo, lf, lfo, u, pose.reshape(-1), rel.reshape(-1),
+                                          st.reshape(-1))
     return pose, rel, st
 
 

@@ -212,10 +212,27 @@ extern "C" {
 // out_pose[7n] = world pose (qx,qy,qz,qw,tx,ty,tz) after each frame (laserOdometry.cpp:716-744);
 // out_rel[7n] = para_q/para_t after each frame; out_stats[6n] = corner/plane counts and LM
 // iterations for the two outer passes.  Returns 0.
+// use_aloam (nullable = every frame, the forced geometric mode): frame f > 0 is optimized only
+// when use_aloam[f] != 0 (laserOdometry.cpp:403-417: the sharp cloud's frame_id ==
+// "skip_intensity"); otherwise para keeps the previous estimate and the pose still accumulates
+// (:716-717).
+int oracle_odometry_chain_gated(int n, const float* sharp, const int* sharp_off, const float* less_sharp,
+                                const int* less_sharp_off, const float* flat, const int* flat_off,
+                                const float* less_flat, const int* less_flat_off, const int* use_aloam,
+                                double* out_pose, double* out_rel, int* out_stats);
+
 int oracle_odometry_chain(int n, const float* sharp, const int* sharp_off, const float* less_sharp,
                           const int* less_sharp_off, const float* flat, const int* flat_off,
                           const float* less_flat, const int* less_flat_off, double* out_pose,
                           double* out_rel, int* out_stats) {
+  return oracle_odometry_chain_gated(n, sharp, sharp_off, less_sharp, less_sharp_off, flat, flat_off, less_flat,
+                                     less_flat_off, nullptr, out_pose, out_rel, out_stats);
+}
+
+int oracle_odometry_chain_gated(int n, const float* sharp, const int* sharp_off, const float* less_sharp,
+                                const int* less_sharp_off, const float* flat, const int* flat_off,
+                                const float* less_flat, const int* less_flat_off, const int* use_aloam,
+                                double* out_pose, double* out_rel, int* out_stats) {
   double para[7] = {0, 0, 0, 1, 0, 0, 0};
   Q4<double> qw{0, 0, 0, 1};
   double tw[3] = {0, 0, 0};
@@ -234,7 +251,7 @@ int oracle_odometry_chain(int n, const float* sharp, const int* sharp_off, const
              LF + less_flat_off[f], less_flat_off[f + 1] - less_flat_off[f]};
     OdomStats st{{0, 0}, {0, 0}, {0, 0}};
     if (f > 0) {
-      associate_and_solve(fr, cornerLast, nCL, kdC, surfLast, nSL, kdS, para, st);
+      if (!use_aloam || use_aloam[f]) associate_and_solve(fr, cornerLast, nCL, kdC, surfLast, nSL, kdS, para, st);
       // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr
       V3<double> tr = rotate(qw, V3<double>{para[4], para[5], para[6]});
       tw[0] = tw[0] + tr.x; tw[1] = tw[1] + tr.y; tw[2] = tw[2] + tr.z;

@@ -157,6 +157,37 @@ def test_odometry_chains(pkg, oracle, synth, contexts, chain_len):
     b.close()
 
 
+@pytest.mark.parametrize("chain_len", [3, 7])
+def test_odometry_gated_reference_default(pkg, oracle, synth, contexts, chain_len):
+    """The reference's default gating (laserOdometry.cpp:403-417): only "skip_intensity" scans are
+    optimized, the others carry the previous estimate into the pose."""
+    S = 8
+    ctx = contexts(64, 1024)
+    scans = synth.make_sequence(S, start=50)
+    use = np.array([0, 1, 0, 0, 1, 1, 0, 1], np.int32)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.odometry(S, chain_len, use_aloam=use)
+    feats = [oracle.scan_registration(s) for s in scans]
+    for c0 in range(0, S - 1, chain_len):
+        chain = feats[c0:c0 + chain_len + 1]
+        pose, rel, st = oracle.odometry_chain(chain, use_aloam=use[c0:c0 + chain_len + 1])
+        for j in range(1, len(chain)):
+            k = c0 + j
+            assert np.max(np.abs(b.download(pkg.native.OUT_PARA, k) - rel[j])) < POSE_TOL, k
+            assert np.max(np.abs(b.download(pkg.native.OUT_POSE, k) - pose[j])) < POSE_TOL, k
+            assert np.array_equal(b.download(pkg.native.OUT_STATS, k)[:4], st[j][:4]), k
+    # the gate the ORB front end produces for this stream (detectfeatures' skipped frames)
+    b.intensity_odometry(S, 1000, pkg.intensity.set_mask())
+    flags = b.skip_flags(S)
+    b.odometry(S, S - 1, use_aloam=flags)
+    pose, rel, _ = oracle.odometry_chain(feats, use_aloam=flags)
+    for k in range(1, S):
+        assert np.max(np.abs(b.download(pkg.native.OUT_POSE, k) - pose[k])) < POSE_TOL
+    b.close()
+
+
 def test_odometry_node_stream_api(pkg, oracle, synth, contexts):
     """lislam_odom_step frame by frame == a single oracle chain over the whole stream."""
     ctx = contexts(64, 1024)

@@ -190,3 +190,19 @@ def test_full_size_digests(oracle, synth):
             a = getattr(f, name)
             assert a.shape[0] == v["n"], name
             assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == v["sha256"], name
+
+
+def test_odometry_gating_semantics(oracle, synth):
+    """laserOdometry.cpp:403-417 / :716-717: without use_aloam the estimate is carried, not
+    re-solved; all flags set == the forced geometric chain."""
+    feats = [oracle.scan_registration(synth.make_scan(k, 16, 256)) for k in range(30, 35)]
+    pose, rel, st = oracle.odometry_chain(feats)
+    pose1, rel1, st1 = oracle.odometry_chain(feats, use_aloam=np.ones(5, np.int32))
+    assert np.array_equal(pose, pose1) and np.array_equal(rel, rel1) and np.array_equal(st, st1)
+    use = np.array([0, 1, 0, 1, 0], np.int32)
+    pose2, rel2, st2 = oracle.odometry_chain(feats, use_aloam=use)
+    assert np.array_equal(rel2[1], rel[1])           # frame 1 optimized exactly as forced
+    assert np.array_equal(rel2[2], rel2[1])          # frame 2 carries frame 1's estimate
+    assert not st2[2].any() and st2[1][:2].sum() > 0
+    none = oracle.odometry_chain(feats, use_aloam=np.zeros(5, np.int32))
+    assert np.allclose(none[0][:, :3], 0) and np.allclose(none[0][:, 3], 1)
