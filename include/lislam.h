@@ -165,7 +165,8 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
                                         cos 15 deg test, -1 < 3 candidates, -2 no model, -3 sampling
                                         beyond the device map), RANSAC iterations, best inliers,
                                         refit inliers */
-/* Copy one output of one scan to host memory; cap/n count elements of the listed type. */
+/* Copy one output of one scan to host memory; cap/n count elements of the listed type.  dst null:
+ * only *n is set (the element count). */
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n);
 /* toROSMsg of a point-cloud output (laser cloud, the four feature clouds, cloud_track, ground,
  * ORB points; scanRegistration.cpp:592-642): cap / n points written into dst in the given

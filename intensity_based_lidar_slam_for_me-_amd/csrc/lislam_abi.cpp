@@ -493,7 +493,7 @@ static int batch_output_source(lislam_batch* b, int what, int scan, const void**
 extern "C" {
 
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n) {
-  if (!b || !dst || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  if (!b || (!dst && !n) || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
   lislam_ctx* c = b->ctx;
   int cnt = 0;
   const void* src = nullptr;
@@ -501,6 +501,7 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
   const int rc = output_source(b, what, scan, &src, &cnt, &esz);
   if (rc) return rc;
   if (n) *n = cnt;
+  if (!dst) return LISLAM_OK;  // count only
   if (cnt > cap) return fail(c, LISLAM_ERR_CAPACITY, "output %d needs %d elements, cap %d", what, cnt, cap);
   if (cnt > 0) HIPCHK(c, hipMemcpy(dst, src, (size_t)cnt * esz, hipMemcpyDeviceToHost));
   return LISLAM_OK;

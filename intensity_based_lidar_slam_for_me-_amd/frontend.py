@@ -240,6 +240,13 @@ class Batch:
         nat.check(rc, self.ctx.h, "lislam_batch_download")
         return buf[: n.value].copy()
 
+    def count(self, what: int, scan: int) -> int:
+        """Element count of one output (lislam_batch_download with no destination)."""
+        n = ctypes.c_int32()
+        nat.check(self.ctx.lib.lislam_batch_download(self.h, what, scan, None, 0, ctypes.byref(n)), self.ctx.h,
+                  "lislam_batch_download")
+        return n.value
+
     def download_cloud(self, what: int, scan: int, layout: nat.PointLayout | None = None) -> bytes:
         """toROSMsg of a point-cloud output: the PointCloud2 data bytes in `layout` (PCL PointXYZI
         by default), packed on the device."""

@@ -38,6 +38,7 @@ def assert_features_equal(pkg, b, k, ref, images=True):
         a, r = getattr(g, name), getattr(ref, name)
         assert a.shape == r.shape, (k, name, a.shape, r.shape)
         assert np.array_equal(a, r), (k, name)
+    assert b.count(n.OUT_LESS_FLAT, k) == ref.less_flat.shape[0]  # count-only download
     assert np.array_equal(b.download(n.OUT_CURVATURE, k), ref.curvature)
     assert np.array_equal(b.download(n.OUT_LABEL, k), ref.label)
     lo = b.download(n.OUT_LINE_OFFSETS, k)
