@@ -393,6 +393,25 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
   if (!(dk_d(ub) < 25.f)) return -1;  // every point is at least 25 away
   const int u0 = dk_key(ub);
   ASTAT(0);
+  // The next four super-chunks by bound in the first window (< 25): lane group g fetches the 16
+  // chunk bounds of the g-th one in the same round trip as u0's points, so the common case needs
+  // no separate super-chunk round.  Visiting extra bounds never changes the result.
+  int spec = -1;           // this lane group's speculative super-chunk
+  bool spec_lane = false;  // this lane's super-chunk (window 0) was fetched speculatively
+  {
+    dkey v = (lane < nsu && lane != u0) ? dk(lb0, lane) : kIdent;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const dkey m = wave_min(v);
+      const int sg = dk_d(m) < 25.f ? dk_key(m) : -1;
+      if ((lane >> 4) == g) spec = sg;
+      if (sg >= 0 && lane == sg) { v = kIdent; spec_lane = true; }
+    }
+  }
+  int c[2] = {spec >= 0 ? spec * kChunk + (lane & 15) : -1, -1};
+  bool cpend[2] = {c[0] >= 0 && c[0] < nch, false};
+  float4 slo = make_float4(0.f, 0.f, 0.f, 0.f), shi = slo;
+  if (cpend[0]) { slo = ldg(chm + 2 * c[0]); shi = ldg(chm + 2 * c[0] + 1); }
   dkey best = dk(25.f, kNone);
   {  // the nearest super-chunk, all 256 points in one round trip
     dkey v = kIdent;
@@ -407,11 +426,30 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
     }
     best = dmin(best, wave_min(v));
   }
+  // evaluate the pending chunks (cc, clb, cp) eight per round trip while their bound can beat best
+  auto chunk_rounds = [&](int (&cc)[2], float (&clb)[2], bool (&cp)[2]) {
+    for (;;) {
+      const float bd2 = dk_d(best);
+      const uint64_t m0 = __ballot(cp[0] && !(clb[0] > bd2));
+      const uint64_t m1 = __ballot(cp[1] && !(clb[1] > bd2));
+      if (!m0 && !m1) break;
+      ASTAT(2);
+      const Picked pk = pick(m0, cc[0], m1, cc[1]);
+      if (pk.took0) cp[0] = false;
+      if (pk.took1) cp[1] = false;
+      nn_eval(sorted, n, pk.v, q, best);
+    }
+  };
+  if (__ballot(cpend[0])) {
+    ASTAT(3);
+    float clb[2] = {cpend[0] ? box_lb(slo, shi, q) : 3.4e38f, 3.4e38f};
+    chunk_rounds(c, clb, cpend);
+  }
   for (int ub = 0; ub < nsu; ub += 64) {
     const int u = ub + lane;
     float slb = ub == 0 ? lb0 : 3.4e38f;
     if (ub > 0 && u < nsu) slb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
-    bool spend = u < nsu && u != u0;
+    bool spend = u < nsu && u != u0 && !(ub == 0 && spec_lane);
     for (;;) {
       const float bd = dk_d(best);
       const uint64_t um = __ballot(spend && !(slb > bd));
@@ -420,9 +458,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
       const Picked su = pick(um, u, 0ull, 0);
       if (su.took0) spend = false;
       // the 16 chunk bounds of each of those super-chunks: lane group g, slots 0 / 1
-      int c[2];
       float clb[2];
-      bool cpend[2];
       float4 lo[2], hi[2];
 #pragma unroll
       for (int t = 0; t < 2; t++) {
@@ -433,17 +469,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
       }
 #pragma unroll
       for (int t = 0; t < 2; t++) clb[t] = cpend[t] ? box_lb(lo[t], hi[t], q) : 3.4e38f;
-      for (;;) {
-        const float bd2 = dk_d(best);
-        const uint64_t m0 = __ballot(cpend[0] && !(clb[0] > bd2));
-        const uint64_t m1 = __ballot(cpend[1] && !(clb[1] > bd2));
-        if (!m0 && !m1) break;
-        ASTAT(2);
-        const Picked pk = pick(m0, c[0], m1, c[1]);
-        if (pk.took0) cpend[0] = false;
-        if (pk.took1) cpend[1] = false;
-        nn_eval(sorted, n, pk.v, q, best);
-      }
+      chunk_rounds(c, clb, cpend);
     }
   }
   const int bi = dk_key(best);
