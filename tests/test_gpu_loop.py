@@ -88,3 +88,26 @@ def test_odom_fusion_bit_exact(pkg, oracle, ctx):
                           h.fuse(a[30:], b[30:], skip[30:])])
     h.close()
     assert np.array_equal(got, ref)
+
+
+def test_loop_icp_device_resident_inputs(pkg, oracle, synth, ctx):
+    """Clouds already in HBM (torch tensors, as the bench passes them) give the host-input result."""
+    import ctypes
+
+    import torch
+
+    cur, Tc, hs, Th, _ = corridor_loop(synth, k=60, hist=(58, 59))
+    ref = pkg.loop.loop_closure_icp(ctx, cur, Tc, hs, Th)
+    dc = torch.from_numpy(cur).cuda()
+    dh = torch.from_numpy(np.concatenate(hs)).cuda()
+    counts = np.array([h.shape[0] for h in hs], np.int32)
+    T = np.ascontiguousarray(Tc.reshape(16))
+    TH = np.ascontiguousarray(np.stack(Th).reshape(-1, 16))
+    out = [np.zeros(16), np.zeros(16), np.zeros(1), np.zeros(8, np.int32)]
+    cfg = pkg.loop.IcpConfig()
+    torch.cuda.synchronize()
+    rc = ctx.lib.lislam_loop_icp(ctx.h, ctypes.byref(cfg), ctypes.c_void_p(dc.data_ptr()), dc.shape[0], T.ctypes.data,
+                                 ctypes.c_void_p(dh.data_ptr()), counts.ctypes.data, len(counts), TH.ctypes.data,
+                                 *(o.ctypes.data for o in out))
+    assert rc == 0
+    assert np.array_equal(out[0].reshape(4, 4), ref[0]) and out[2][0] == ref[2] and list(out[3]) == list(ref[3])
