@@ -30,6 +30,16 @@
  *   lislam_mapopt_step        <- mapOptimization::mapOptimizationCallback ground-map stage
  *                                                                      src/mapOptimization.cpp:99-479
  *   lislam_laser_mapping      <- laserMapping::process optimization    src/laserMapping.cpp:620-850
+ *   lislam_lmap_*             <- laserMapping::process with its cube map src/laserMapping.cpp:319-1002
+ *   lislam_batch_intensity_odometry / lislam_intensity_tracker_*
+ *                             <- feature_tracker::detectfeatures       src/intensity_feature_tracker.cpp:597-738
+ *   lislam_ground_extract / lislam_batch_ground
+ *                             <- ImageHandler::groundPlaneExtraction   src/image_handler.h_ouster:41-100
+ *   lislam_batch_upload / lislam_batch_download_cloud
+ *                             <- pcl::fromROSMsg / toROSMsg            src/image_handler.h_ouster:105-106,
+ *                                                                      src/scanRegistration.cpp:592-642
+ *   lislam_loop_icp           <- loopClosureThread's USE_ICP block     src/intensity_feature_tracker.cpp:217-366
+ *   lislam_odom_fuse          <- odomHandler callback                 src/odom_handler_node.cpp:44-132
  */
 #ifndef LISLAM_H_
 #define LISLAM_H_
@@ -109,6 +119,11 @@ int lislam_odom_destroy(lislam_odom* od);
  * of each pass, termination of each pass (0 max-iterations, 1 convergence, 2 failure). */
 int lislam_odom_step(lislam_odom* od, const lislam_frame* frame, double* para_out, double* pose_out,
                      int32_t* stats_out);
+/* The reference's default gating (laserOdometry.cpp:403-417): the frame is associated and
+ * optimized only when use_aloam != 0 (its sharp cloud's frame_id == "skip_intensity"); otherwise
+ * para_q/para_t carry over and the pose accumulates them (:716-717). */
+int lislam_odom_step_gated(lislam_odom* od, const lislam_frame* frame, int32_t use_aloam, double* para_out,
+                           double* pose_out, int32_t* stats_out);
 
 /* ---------------------------------------------------------------- batch (device resident) */
 int lislam_batch_create(lislam_ctx* ctx, int32_t max_scans, lislam_batch** out);

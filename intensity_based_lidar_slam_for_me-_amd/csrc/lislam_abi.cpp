@@ -628,7 +628,8 @@ static int put_frame(lislam_batch* b, int slot, const lislam_frame* fr) {
   return rc ? LISLAM_ERR_DEVICE : LISLAM_OK;
 }
 
-int lislam_odom_step(lislam_odom* od, const lislam_frame* fr, double* para_out, double* pose_out, int32_t* stats_out) {
+static int odom_step(lislam_odom* od, const lislam_frame* fr, int use_aloam, double* para_out, double* pose_out,
+                     int32_t* stats_out) {
   if (!od || !fr) return LISLAM_ERR_ARG;
   lislam_ctx* c = od->ctx;
   hipSetDevice(c->device);
@@ -641,7 +642,8 @@ int lislam_odom_step(lislam_odom* od, const lislam_frame* fr, double* para_out, 
   } else {
     if ((rc = put_frame(b, 1, fr))) return rc;
     b->extracted = 2;
-    if ((rc = run_odometry(b, 2, 1, od->state))) return rc;
+    od->gate[1] = use_aloam != 0;
+    if ((rc = run_odometry(b, 2, 1, od->state, use_aloam < 0 ? nullptr : od->gate))) return rc;
     int n;
     if ((rc = lislam_batch_download(b, LISLAM_OUT_PARA, 1, od->state, 7, &n))) return rc;
     if ((rc = lislam_batch_download(b, LISLAM_OUT_POSE, 1, od->state + 7, 7, &n))) return rc;
@@ -654,6 +656,15 @@ int lislam_odom_step(lislam_odom* od, const lislam_frame* fr, double* para_out, 
   if (pose_out) std::memcpy(pose_out, od->state + 7, 7 * sizeof(double));
   if (stats_out) std::memcpy(stats_out, st, sizeof(st));
   return LISLAM_OK;
+}
+
+int lislam_odom_step(lislam_odom* od, const lislam_frame* fr, double* para_out, double* pose_out, int32_t* stats_out) {
+  return odom_step(od, fr, -1, para_out, pose_out, stats_out);
+}
+
+int lislam_odom_step_gated(lislam_odom* od, const lislam_frame* fr, int32_t use_aloam, double* para_out,
+                           double* pose_out, int32_t* stats_out) {
+  return odom_step(od, fr, use_aloam ? 1 : 0, para_out, pose_out, stats_out);
 }
 
 // ------------------------------------------------------------------------------ functors

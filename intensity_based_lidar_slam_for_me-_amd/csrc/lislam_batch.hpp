@@ -54,6 +54,7 @@ struct lislam_odom {
   bool have_last = false;
   double state[14] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0};
   int frames = 0;
+  int32_t gate[2] = {1, 1};  // use_aloam of the two scans of a gated step (kept alive for the async copy)
 };
 
 

@@ -127,7 +127,9 @@ class ImageHandler:
 
 
 class LaserOdometry:
-    """laserOdometry node in forced-geometric mode (every frame is optimized)."""
+    """laserOdometry node.  step(f) is the forced geometric mode (every frame is optimized);
+    step(f, skip_flag=...) follows the reference's default gating (laserOdometry.cpp:403-417): the
+    frame is optimized only when the sharp cloud's frame_id is "skip_intensity"."""
 
     def __init__(self, ctx: Context):
         self.ctx = ctx
@@ -135,14 +137,20 @@ class LaserOdometry:
         nat.check(ctx.lib.lislam_odom_create(ctx.h, ctypes.byref(h)), ctx.h, "lislam_odom_create")
         self.h = h
 
-    def step(self, f: Features):
+    SKIP_INTENSITY = "skip_intensity"
+
+    def step(self, f: Features, skip_flag: str | None = None):
         arrs = [np.ascontiguousarray(a, np.float32) for a in (f.sharp, f.less_sharp, f.flat, f.less_flat)]
         fr = nat.Frame(_fp(arrs[0]), arrs[0].shape[0], _fp(arrs[1]), arrs[1].shape[0], _fp(arrs[2]), arrs[2].shape[0],
                        _fp(arrs[3]), arrs[3].shape[0])
         para = np.zeros(7)
         pose = np.zeros(7)
         st = np.zeros(8, np.int32)
-        rc = self.ctx.lib.lislam_odom_step(self.h, ctypes.byref(fr), nat.ptr(para), nat.ptr(pose), nat.ptr(st))
+        if skip_flag is None:
+            rc = self.ctx.lib.lislam_odom_step(self.h, ctypes.byref(fr), nat.ptr(para), nat.ptr(pose), nat.ptr(st))
+        else:
+            rc = self.ctx.lib.lislam_odom_step_gated(self.h, ctypes.byref(fr), int(skip_flag == self.SKIP_INTENSITY),
+                                                     nat.ptr(para), nat.ptr(pose), nat.ptr(st))
         nat.check(rc, self.ctx.h, "lislam_odom_step")
         return para, pose, st
 

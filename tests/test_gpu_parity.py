@@ -204,6 +204,23 @@ def test_odometry_node_stream_api(pkg, oracle, synth, contexts):
     node.close()
 
 
+def test_odometry_node_gated_stream(pkg, oracle, synth, contexts):
+    """lislam_odom_step_gated frame by frame (the sharp cloud's frame_id decides) == the oracle's
+    gated chain."""
+    ctx = contexts(64, 1024)
+    scans = synth.make_sequence(6, start=70)
+    feats = [oracle.scan_registration(s) for s in scans]
+    use = np.array([0, 1, 0, 1, 1, 0], np.int32)
+    pose, rel, st = oracle.odometry_chain(feats, use_aloam=use)
+    node = pkg.LaserOdometry(ctx)
+    for k, f in enumerate(feats):
+        para, pw, gst = node.step(f, skip_flag="skip_intensity" if use[k] else "os_sensor")
+        assert np.max(np.abs(para - rel[k])) < POSE_TOL, k
+        assert np.max(np.abs(pw - pose[k])) < POSE_TOL, k
+        assert np.array_equal(gst[:4], st[k][:4]), k
+    node.close()
+
+
 def test_scan_registration_single_api(pkg, oracle, synth, contexts):
     ctx = contexts(64, 1024)
     scan = synth.make_scan(77)
