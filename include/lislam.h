@@ -300,6 +300,11 @@ int lislam_voxel_grid(lislam_ctx* ctx, const float* pts, int32_t n, float leaf, 
  * out_pose = q_w_curr, t_w_curr; summary[3] = planes, iterations, termination (-1: built). */
 int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const double* odom, double* state,
                        double* out_pose, int32_t* summary);
+/* The same stage fed from a batch without a host round trip: GroundPointOut of `scan`
+ * (lislam_batch_ground) followed by its less-flat cloud, concatenated on the device
+ * (mapOptimization.cpp:136-150).  The map's context must be the batch's. */
+int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
+                        double* out_pose, int32_t* summary);
 /* laserMapping::process optimization (laserMapping.cpp:620-850) against a corner map and a surf
  * map: the downsampled current corner / surf clouds (stride 4), pose x (in/out), two outer
  * passes of association + Ceres(4 it).  stats[4] = corner / surf blocks of each pass. */

@@ -234,6 +234,7 @@ static int rc_wire(lislam_batch* b, size_t bytes) {
 }
 
 static int batch_output_source(lislam_batch* b, int what, int scan, const void** src, int* cnt);
+static int output_source(lislam_batch* b, int what, int scan, const void** src_out, int* cnt_out, size_t* esz_out);
 
 int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
@@ -259,6 +260,29 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   return LISLAM_OK;
+}
+
+// mapOptimizationCallback's input assembly (mapOptimization.cpp:136-150): GroundPointOut of the
+// scan (lislam_batch_ground) followed by its less-flat cloud (the plane cloud), concatenated on the
+// device (the 4th field is not read by the ground-map stage), then lislam_mapopt_step.
+int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
+                        double* out_pose, int32_t* summary) {
+  if (!b || !m || !odom || !state || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  const void *g = nullptr, *lf = nullptr;
+  int ng = 0, nlf = 0;
+  size_t eg = 0, elf = 0;
+  int rc = output_source(b, LISLAM_OUT_GROUND, scan, &g, &ng, &eg);
+  if (rc) return rc;
+  if ((rc = output_source(b, LISLAM_OUT_LESS_FLAT, scan, &lf, &nlf, &elf))) return rc;
+  const size_t bytes = (size_t)(ng + nlf) * 16;
+  if ((rc = rc_wire(b, std::max<size_t>(bytes, 16)))) return fail(c, rc, "lislam_batch_mapopt: staging allocation");
+  uint8_t* dst = static_cast<uint8_t*>(b->wire);
+  if (ng) HIPCHK(c, hipMemcpyAsync(dst, g, (size_t)ng * 16, hipMemcpyDeviceToDevice, c->stream));
+  if (nlf) HIPCHK(c, hipMemcpyAsync(dst + (size_t)ng * 16, lf, (size_t)nlf * 16, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return lislam_mapopt_step(m, reinterpret_cast<const float*>(dst), ng + nlf, odom, state, out_pose, summary);
 }
 
 int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,

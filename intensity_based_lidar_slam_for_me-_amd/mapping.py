@@ -152,6 +152,17 @@ class MapOptimization:
                                              nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_mapopt_step")
         return pose, summ
 
+    def callback_batch(self, batch, scan: int, odom):
+        """The same frame fed from a batch on the device: GroundPointOut of `scan` (batch.ground
+        first) + its less-flat cloud, as mapOptimizationCallback assembles them (:136-150)."""
+        od = np.ascontiguousarray(odom, np.float64)
+        pose = np.zeros(7)
+        summ = np.zeros(3, np.int32)
+        ctx = self.map.ctx
+        nat.check(ctx.lib.lislam_batch_mapopt(batch.h, self.map.h, scan, nat.ptr(od), nat.ptr(self.state),
+                                              nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_batch_mapopt")
+        return pose, summ
+
 
 def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):
     """laserMapping optimization: (x (7,), stats (corner / surf blocks of the two passes)).

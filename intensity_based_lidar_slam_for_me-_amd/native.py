@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
     "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
     "lislam_lmap_create", "lislam_lmap_destroy", "lislam_lmap_step", "lislam_lmap_counts", "lislam_lmap_points",
-    "lislam_batch_odometry_gated", "lislam_odom_step_gated", "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
+    "lislam_batch_odometry_gated", "lislam_odom_step_gated", "lislam_batch_mapopt", "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
 )
 
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
@@ -174,6 +174,7 @@ def load(path: str = LIB_PATH):
     L.lislam_ground_extract.argtypes = [vp, vp, ctypes.POINTER(PointLayout), vp, _i32, _i32p, vp, vp]
     L.lislam_batch_odometry_gated.argtypes = [vp, _i32, _i32, vp]
     L.lislam_odom_step_gated.argtypes = [vp, vp, _i32, vp, vp, vp]
+    L.lislam_batch_mapopt.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
     L.lislam_loop_icp.argtypes = [vp, ctypes.POINTER(IcpConfig), vp, _i32, vp, vp, vp, _i32, vp, vp, vp, vp, vp]
     L.lislam_odom_fuser_create.argtypes = [vp, ctypes.POINTER(vp)]
     L.lislam_odom_fuser_destroy.argtypes = [vp]

@@ -254,3 +254,31 @@ def test_laser_mapping(pkg, oracle, ctx, synth):
     assert np.linalg.norm(xg[4:] - truth[4:]) < np.linalg.norm(x0[4:] - truth[4:])
     gs.close()
     gc.close()
+
+
+def test_mapopt_fed_from_batch(pkg, oracle, ctx, synth):
+    """mapOptimizationCallback's input assembled on the device (lislam_batch_mapopt): the scan's
+    GroundPointOut followed by its less-flat cloud (mapOptimization.cpp:136-150), against the
+    oracle's ground extraction + scan registration concatenated on the host."""
+    S = 4
+    scans = synth.make_sequence(S, start=12)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.ground(S)
+    go = pkg.mapping.MapOptimization(ctx, 0.4, 0.2)
+    om = oracle.IkdMap(0.4)
+    ostate = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    for k in range(S):
+        g_ref, _, _ = oracle.ground_extract(scans[k])
+        lf = oracle.scan_registration(scans[k]).less_flat
+        merged = np.concatenate([g_ref, lf]).astype(np.float32)
+        q, t = synth.ground_truth_pose(12 + k).as_qt()
+        odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=30 + k)
+        pg, sg = go.callback_batch(b, k, odom)
+        po, ostate, so = oracle.mapopt_step(om, merged, odom, ostate)
+        assert np.max(np.abs(pg - po)) < POSE_TOL, (k, pg, po)
+        assert list(sg) == list(so), (k, sg, so)
+        assert go.map.size() == om.size(), k
+    go.map.close()
+    b.close()
