@@ -181,8 +181,8 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
     rc |= dalloc(b, &ti->sorted, (size_t)S * ti->cap);
     rc |= dalloc(b, &ti->keys, (size_t)S * 2 * ti->cap);
   }
-  rc |= dalloc(b, &o.qperm_sharp, (size_t)S * b->cap_sharp);
-  rc |= dalloc(b, &o.qperm_flat, (size_t)S * b->cap_flat);
+  rc |= dalloc(b, &o.qpts_sharp, (size_t)S * b->cap_sharp);
+  rc |= dalloc(b, &o.qpts_flat, (size_t)S * b->cap_flat);
   rc |= dalloc(b, &o.state, (size_t)S * 16);
   o.cap_sharp = b->cap_sharp; o.cap_less_sharp = b->cap_less_sharp; o.cap_flat = b->cap_flat;
   o.max_iterations = c->cfg.max_iterations;
@@ -635,8 +635,8 @@ static int put_frame(lislam_batch* b, int slot, const lislam_frame* fr) {
   o.less_flat = f.less_flat + (size_t)slot * b->N;
   o.sharp = f.sharp + (size_t)slot * b->cap_sharp;
   o.flat = f.flat + (size_t)slot * b->cap_flat;
-  o.qperm_sharp += (size_t)slot * b->cap_sharp;
-  o.qperm_flat += (size_t)slot * b->cap_flat;
+  o.qpts_sharp += (size_t)slot * b->cap_sharp;
+  o.qpts_flat += (size_t)slot * b->cap_flat;
   o.n_feat = f.n_feat + slot * 4;
   for (TargetIndex* ti : {&o.idx_ls, &o.idx_lf}) {
     ti->chunk += (size_t)slot * ti->nchunk * 2;

@@ -82,8 +82,8 @@ struct OdomArgs {
   const int* n_feat;
   const int* feat_loff;  // [S][2][H+1] line offsets of less_sharp / less_flat
   TargetIndex idx_ls, idx_lf;
-  int* qperm_sharp;  // [S][cap_sharp] sharp queries in Morton order (association thread -> query)
-  int* qperm_flat;   // [S][cap_flat]
+  float4* qpts_sharp;  // [S][cap_sharp] sharp queries in Morton order: x, y, z, query index bits
+  float4* qpts_flat;   // [S][cap_flat]    (association wave -> its query in one load)
   int cap_sharp, cap_less_sharp, cap_flat;
   int chain_len;
   int n_chains;

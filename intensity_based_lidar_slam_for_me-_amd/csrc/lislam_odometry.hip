@@ -207,8 +207,11 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     }
   };
   if (query) {  // association waves take their queries in this order (spatially coherent workgroups)
-    int* perm = which == 2 ? a.qperm_sharp + (size_t)s * a.cap_sharp : a.qperm_flat + (size_t)s * a.cap_flat;
-    emit([&](int i, int o) { perm[i] = o; });
+    float4* qp = which == 2 ? a.qpts_sharp + (size_t)s * a.cap_sharp : a.qpts_flat + (size_t)s * a.cap_flat;
+    emit([&](int i, int o) {
+      const float4 p = ldg(pts + o);
+      stg4(qp + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+    });
     return;
   }
   float4* sorted = ix.sorted + (size_t)s * ix.cap;
@@ -677,7 +680,9 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
 #endif
   const bool corner = w < ns;
   const int t = corner ? w : w - ns;
-  const int q = corner ? a.qperm_sharp[(size_t)k * a.cap_sharp + t] : a.qperm_flat[(size_t)k * a.cap_flat + t];
+  const P4 qp = ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
+                           : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t);
+  const int q = __float_as_int(qp.i);
   const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
   const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
   const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
@@ -686,7 +691,7 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   double x[7];
   const double* st = a.state + (size_t)c * 16;
   for (int e = 0; e < 7; e++) x[e] = st[e];
-  const P4 cur = corner ? ld4(a.sharp + (size_t)k * a.cap_sharp + q) : ld4(a.flat + (size_t)k * a.cap_flat + q);
+  const P4 cur{qp.x, qp.y, qp.z, 0.f};  // the query point (its intensity is not read)
   const P4 sel = transform_to_start(cur, x);
 #ifdef LISLAM_PHASE_PROF  // ablations for timing only (LISLAM_ASSOC_DEBUG): 1 skip the 1-NN, 2 skip the line searches
   int closest = (a.dbg & 1) ? (nL > 0 ? (int)((unsigned)q * 2654435761u % (unsigned)nL) : -1)
