@@ -401,7 +401,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
   // no separate super-chunk round.  Visiting extra bounds never changes the result.
   int spec = -1;           // this lane group's speculative super-chunk
   bool spec_lane = false;  // this lane's super-chunk (window 0) was fetched speculatively
-  {
+  {  // (ranking by bound beat taking u0's Morton neighbours u0 -+1, -+2 in an A/B: 4.15 vs 4.18 ms)
     dkey v = (lane < nsu && lane != u0) ? dk(lb0, lane) : kIdent;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
