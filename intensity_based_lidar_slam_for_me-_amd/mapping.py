@@ -152,6 +152,23 @@ class MapOptimization:
                                              nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_mapopt_step")
         return pose, summ
 
+    def laser_odometry_handler(self, odom) -> np.ndarray:
+        """laserOdometryHandler (mapOptimization.cpp:19-49): the high-frequency pose
+        q_w_curr = q_wmap_wodom * q_wodom_curr, t_w_curr = q_wmap_wodom * t_wodom_curr + t_wmap_wodom
+        from the latest map correction (13 flops of ROS glue, computed on the host)."""
+        qm, tm = self.state[:4], self.state[4:]
+        qo, to = np.asarray(odom[:4], np.float64), np.asarray(odom[4:7], np.float64)
+
+        def qmul(a, b):
+            ax, ay, az, aw = a
+            bx, by, bz, bw = b
+            return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                             aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz])
+
+        qw = qmul(qm, qo)
+        tq = qmul(qmul(qm, np.array([to[0], to[1], to[2], 0.0])), qm * np.array([-1, -1, -1, 1.0]))[:3]
+        return np.concatenate([qw, tq + tm])
+
     def callback_batch(self, batch, scan: int, odom):
         """The same frame fed from a batch on the device: GroundPointOut of `scan` (batch.ground
         first) + its less-flat cloud, as mapOptimizationCallback assembles them (:136-150)."""

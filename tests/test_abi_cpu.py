@@ -65,3 +65,17 @@ def _load_missing(pkg, path):
         pkg.native.load(path)
     finally:
         pkg.native._LIB = saved
+
+
+def test_mapopt_high_frequency_pose(pkg):
+    """MapOptimization.laser_odometry_handler (mapOptimization.cpp:19-49): host glue, no GPU."""
+    from scipy.spatial.transform import Rotation as R
+
+    m = pkg.mapping.MapOptimization.__new__(pkg.mapping.MapOptimization)
+    q = np.array([0.1, 0.2, 0.3, 0.9])
+    q /= np.linalg.norm(q)
+    m.state = np.concatenate([q, [1.0, 2.0, 3.0]])
+    od = np.array([0, 0, np.sin(0.2), np.cos(0.2), 4.0, 5.0, 6.0])
+    p = m.laser_odometry_handler(od)
+    assert np.allclose(p[4:], R.from_quat(q).apply(od[4:]) + [1, 2, 3])
+    assert np.allclose(R.from_quat(p[:4]).as_matrix(), (R.from_quat(q) * R.from_quat(od[:4])).as_matrix())
