@@ -965,6 +965,100 @@ __global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
   if (ib < nt && bjb >= 0) atomicMin(&best[bjb], (bdb << 16) | ib);
 }
 
+// The same result on the matrix cores: Hamming(q, t) = |q| + |t| - 2 <q, t> with the 256
+// descriptor bits as 0/1 int8 vectors and <q, t> from v_mfma_i32_16x16x64_i8 (four k-steps of 64
+// bits; A and B fragments use one and the same lane -> k map, so the dot product does not depend
+// on the hardware's k order).  A workgroup = 16 waves x 16 trains; each 256-query tile is expanded
+// to 0/1 bytes in LDS once and read by the 16 waves.  By the C/D layout lane l owns train column
+// l & 15 and query rows 4 (l >> 4) .. +3 of every 16-query tile, so its running first minimum
+// follows query order; the four lanes of a column merge by (distance, query) at the end.
+constexpr int kXmWaves = 16;                // waves per workgroup
+constexpr int kXmTrains = 16 * kXmWaves;    // trains per workgroup (16 per wave)
+constexpr int kXmQTile = 256;   // queries expanded per LDS tile
+constexpr int kXmRow = 272;     // LDS bytes per expanded query (256 + 16: rows start on distinct banks)
+using i32x4 = __attribute__((ext_vector_type(4))) int;
+
+__device__ __forceinline__ uint32_t spread4(uint32_t n) { return (n * 0x00204081u) & 0x01010101u; }
+__device__ __forceinline__ i32x4 expand16(uint32_t b) {  // 16 bits -> 16 bytes of 0 / 1
+  i32x4 v;
+  v.x = (int)spread4(b & 15u);
+  v.y = (int)spread4((b >> 4) & 15u);
+  v.z = (int)spread4((b >> 8) & 15u);
+  v.w = (int)spread4((b >> 12) & 15u);
+  return v;
+}
+
+__global__ __launch_bounds__(64 * kXmWaves) void k_orb_xdist_mfma(PairArgs p) {
+  __shared__ i32x4 qx[kXmQTile * kXmRow / 16];
+  __shared__ int qpop[kXmQTile];
+  const int pi = blockIdx.x;
+  const int pr = p.pslot ? p.pslot[pi] : pi;
+  const int qs = p.qscan[pi], ts = p.tscan[pi];
+  const int nq = p.qn[qs], nt = p.tn[ts];
+  const int t0 = blockIdx.y * kXmTrains;
+  if (t0 >= nt) return;
+  const uint32_t* Q = reinterpret_cast<const uint32_t*>(p.qdesc + (size_t)qs * p.qcap * 32);
+  const uint32_t* T = reinterpret_cast<const uint32_t*>(p.tdesc + (size_t)ts * p.tcap * 32);
+  int* best = p.mscratch + (size_t)pr * p.bstride;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 4, col = lane & 15;
+  const int ti = t0 + wv * 16 + col;  // this lane's train
+  // B fragments: bits 64 s + 16 h .. +15 of train ti for k-step s
+  i32x4 bfr[4];
+  int tpop = 0;
+  {
+    uint32_t td[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) td[e] = ti < nt ? T[(size_t)ti * 8 + e] : 0u;
+#pragma unroll
+    for (int e = 0; e < 8; e++) tpop += __popc(td[e]);
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint32_t w = td[2 * s + (h >> 1)];
+      bfr[s] = expand16((h & 1) ? (w >> 16) : (w & 0xffffu));
+    }
+  }
+  int bd = 0x7fffffff, bj = -1;
+  for (int q0 = 0; q0 < nq; q0 += kXmQTile) {
+    const int tn = min(kXmQTile, nq - q0);
+    __syncthreads();  // the previous tile is no longer read
+    for (int it = threadIdx.x; it < kXmQTile * 16; it += 64 * kXmWaves) {
+      const int q = it >> 4, c = it & 15;
+      const uint32_t w = q < tn ? Q[(size_t)(q0 + q) * 8 + (c >> 1)] : 0u;
+      qx[(q * kXmRow + c * 16) / 16] = expand16((c & 1) ? (w >> 16) : (w & 0xffffu));
+    }
+    if (threadIdx.x < kXmQTile) {
+      const int q = threadIdx.x;
+      int pc = 0;
+      if (q < tn)
+#pragma unroll
+        for (int e = 0; e < 8; e++) pc += __popc(Q[(size_t)(q0 + q) * 8 + e]);
+      qpop[q] = pc;
+    }
+    __syncthreads();
+    for (int r0 = 0; r0 < tn; r0 += 16) {
+      i32x4 acc = {0, 0, 0, 0};
+      const int rowb = ((r0 + col) * kXmRow + h * 16) / 16;
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(qx[rowb + s * 4], bfr[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int reg = 0; reg < 4; reg++) {
+        const int j = r0 + 4 * h + reg;
+        if (j < tn) {
+          const int d = qpop[j] + tpop - 2 * acc[reg];
+          if (d < bd) { bd = d; bj = q0 + j; }
+        }
+      }
+    }
+  }
+  // merge the four lanes of each column: first minimum in query order
+#pragma unroll
+  for (int o = 16; o <= 32; o <<= 1) {
+    const int od = __shfl_xor(bd, o), oj = __shfl_xor(bj, o);
+    if (od < bd || (od == bd && oj >= 0 && (bj < 0 || oj < bj))) { bd = od; bj = oj; }
+  }
+  if (h == 0 && ti < nt && bj >= 0) atomicMin(&best[bj], (bd << 16) | ti);
+}
+
 // Selection part: std::sort by distance (stable, query order), the first ceil(frac M), the
 // good-frame test and the front_end_residual records.
 __global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
@@ -1501,7 +1595,11 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   {
     TimedScope t(c, kT_orb_match);
     hipLaunchKernelGGL(k_orb_mfill, dim3(n, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
-    hipLaunchKernelGGL(k_orb_xdist, dim3(n, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
+    static const bool valu = getenv("LISLAM_XDIST_VALU") != nullptr;  // developer A/B switch
+    if (valu)
+      hipLaunchKernelGGL(k_orb_xdist, dim3(n, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
+    else
+      hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(n, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
     hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p);
   }
   if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(n), dim3(kLmThreads), 0, st, p, 20); }
