@@ -643,16 +643,29 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   int* cand = a.cand + (size_t)s * g.pix[kL] + g.pix[l];
   float* resp = a.cresp + (size_t)s * g.pix[kL] + g.pix[l];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // 1. FAST keypoints in row-major order: each thread compacts one contiguous pixel segment
+  // 1. FAST keypoints in row-major order: each thread compacts one contiguous pixel segment,
+  //    read as the aligned dwords that cover it (bit 7 of each byte of nz = a nonzero score)
   const int npx = w * h, seg = (npx + blockDim.x - 1) / blockDim.x;
   const int p0 = min(npx, (int)threadIdx.x * seg), p1 = min(npx, p0 + seg);
+  const uintptr_t b0 = (uintptr_t)kf + p0, b1 = (uintptr_t)kf + p1;
+  auto nz_of = [&](uintptr_t a) {
+    const uint32_t v = *(const __attribute__((address_space(1))) uint32_t*)(a);
+    uint32_t nz = (((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v) & 0x80808080u;
+    if (b0 > a) nz &= 0xffffffffu << (8 * (int)(b0 - a));        // bytes before the segment
+    if (b1 - a < 4) nz &= 0xffffffffu >> (8 * (4 - (int)(b1 - a)));  // bytes after it
+    return nz;
+  };
   int mine = 0;
-#pragma unroll 8
-  for (int p = p0; p < p1; p++) mine += kf[p] != 0;
+  for (uintptr_t a = b0 & ~(uintptr_t)3; a < b1; a += 4) mine += __popc(nz_of(a));
   int n;
   int at = block_excl(sh, mine, &n);
-  for (int p = p0; p < p1; p++)
-    if (kf[p]) cand[at++] = p;
+  for (uintptr_t a = b0 & ~(uintptr_t)3; a < b1; a += 4) {
+    uint32_t nz = nz_of(a);
+    while (nz) {
+      cand[at++] = (int)((intptr_t)a - (intptr_t)kf) + (__builtin_ctz(nz) >> 3);
+      nz &= nz - 1;
+    }
+  }
   __syncthreads();
   SEL_PHASE(0);
   // 2. retainBest(2 n_l) on the FAST score: keep every score >= the (2 n_l)-th largest
@@ -1439,7 +1452,7 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   const size_t S = max_scans;
   ORC(e->alloc(&e->pyr, S * g.bytes));
   ORC(e->alloc(&e->blur, S * g.bytes));
-  ORC(e->alloc(&e->nms, S * g.pix[kL]));
+  ORC(e->alloc(&e->nms, S * g.pix[kL] + 16));  // + 16: k_orb_select reads whole aligned dwords
   ORC(e->alloc(&e->cand, S * g.pix[kL]));
   ORC(e->alloc(&e->cresp, S * g.pix[kL]));
   ORC(e->alloc(&e->lkp, S * g.cap * 6));
