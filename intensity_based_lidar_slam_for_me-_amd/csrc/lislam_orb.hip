@@ -577,10 +577,19 @@ __device__ uint32_t nth_largest(SelShared& sh, const float* resp, int cnt, int n
   return prefix;
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// every lane of each 16-lane row gets the row's sum (DPP: pairs, quads, half rows, rows)
+__device__ __forceinline__ int row_sum16(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+  v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false);  // row_mirror
   return v;
+}
+// the wave's sum (uniform): row sums + the four rows read as scalars
+__device__ __forceinline__ int wave_sum(int v) {
+  v = row_sum16(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
 }
 
 // block-wide exclusive prefix of an int per thread; *tot = the sum
