@@ -705,11 +705,11 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   }
   __syncthreads();
   SEL_PHASE(1);
-  // 3. Harris responses: one wavefront per 4 candidates, lane = one of the 7x7 block pixels (the
-  //    integer sums are order-free, so the float formula sees OpenCV's exact a, b, c)
+  // 3. Harris responses: one wavefront per 4 candidates, 16 lanes per candidate over the 7x7 block
+  //    pixels (the integer sums are order-free, so the float formula sees OpenCV's exact a, b, c)
   // The 9 x 16-byte patches (rows y0-4 .. y0+4 from the dword holding column x0-4) of 4
-  // candidates per wave iteration are staged in LDS by 144 dword loads, then each of 49 lanes
-  // reads its 8 neighbours per candidate from LDS.
+  // candidates per wave iteration are staged in LDS by 144 dword loads, then each 16-lane row
+  // reads the neighbourhoods of its candidate's 49 block pixels from LDS.
   constexpr int kPerWave = 4;
   const int stride_l = g.stride[l];
   const uint8_t* lvl = base + g.off[l];
@@ -727,34 +727,34 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
       }
     }
     wave_lds_sync();
+    // lane row u = lane >> 4 takes candidate i0 + u; its 16 lanes cover the 49 block pixels
+    // (pixel t, t + 16, t + 32, t + 48) and the integer sums close with one row sum each
     const uint8_t* hb = reinterpret_cast<const uint8_t*>(hp);
-    int A[kPerWave], B[kPerWave], C[kPerWave];
+    const int u = lane >> 4, t16 = lane & 15, i = i0 + u;
+    int A = 0, B = 0, C = 0;
+    if (i < n) {
+      const int x0 = cand[i] % w;
+      const uint8_t* P = hb + u * 144 + ((x0 - 4 + kB) & 3);  // P[r * 16 + c]: row y0-4+r, column x0-4+c
+      auto at = [&](int r, int c) { return (int)P[r * 16 + c]; };
 #pragma unroll
-    for (int u = 0; u < kPerWave; u++) {
-      A[u] = B[u] = C[u] = 0;
-      const int i = i0 + u;
-      if (i < n && lane < 49) {
-        const int x0 = cand[i] % w;
-        const uint8_t* P = hb + u * 144 + ((x0 - 4 + kB) & 3);  // P[r * 16 + c]: row y0-4+r, column x0-4+c
-        const int ar = lane / 7, bc = lane % 7;                // position (y0-3+ar, x0-3+bc) = patch (ar+1, bc+1)
-        auto at = [&](int r, int c) { return (int)P[r * 16 + c]; };
-        const int Ix = (at(ar + 1, bc + 2) - at(ar + 1, bc)) * 2 + (at(ar, bc + 2) - at(ar, bc)) +
-                       (at(ar + 2, bc + 2) - at(ar + 2, bc));
-        const int Iy = (at(ar + 2, bc + 1) - at(ar, bc + 1)) * 2 + (at(ar + 2, bc) - at(ar, bc)) +
-                       (at(ar + 2, bc + 2) - at(ar, bc + 2));
-        A[u] = Ix * Ix; B[u] = Iy * Iy; C[u] = Ix * Iy;
+      for (int k = 0; k < 4; k++) {
+        const int px = t16 + 16 * k;
+        if (px < 49) {
+          const int ar = px / 7, bc = px % 7;  // position (y0-3+ar, x0-3+bc) = patch (ar+1, bc+1)
+          const int Ix = (at(ar + 1, bc + 2) - at(ar + 1, bc)) * 2 + (at(ar, bc + 2) - at(ar, bc)) +
+                         (at(ar + 2, bc + 2) - at(ar + 2, bc));
+          const int Iy = (at(ar + 2, bc + 1) - at(ar, bc + 1)) * 2 + (at(ar + 2, bc) - at(ar, bc)) +
+                         (at(ar + 2, bc + 2) - at(ar, bc + 2));
+          A += Ix * Ix; B += Iy * Iy; C += Ix * Iy;
+        }
       }
     }
     wave_lds_sync();  // the patch is rewritten by the next iteration
-#pragma unroll
-    for (int u = 0; u < kPerWave; u++) { A[u] = wave_sum(A[u]); B[u] = wave_sum(B[u]); C[u] = wave_sum(C[u]); }
-    if (lane == 0) {
+    A = row_sum16(A); B = row_sum16(B); C = row_sum16(C);
+    if (t16 == 0 && i < n) {
       const float scale = 1.f / ((1 << 2) * 7 * 255.f);
       const float sq = scale * scale * scale * scale;
-#pragma unroll
-      for (int u = 0; u < kPerWave; u++)
-        if (i0 + u < n)
-          resp[i0 + u] = ((float)A[u] * B[u] - (float)C[u] * C[u] - 0.04f * ((float)A[u] + B[u]) * ((float)A[u] + B[u])) * sq;
+      resp[i] = ((float)A * B - (float)C * C - 0.04f * ((float)A + B) * ((float)A + B)) * sq;
     }
   }
   __syncthreads();
