@@ -790,6 +790,16 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   // keypoints per wave iteration are staged in LDS by 558 dword loads; lane t then reads the
   // circle pixels t, t + 64, ... of each from LDS.
   constexpr int kAngPerWave = 2;
+  // this lane's circle pixels t = 64 k + lane, once per workgroup: LDS offset | (du + 16) << 16 |
+  // (dv + 16) << 24 (du = dv = 0 past the end)
+  uint32_t cpx[kPatchIters];
+#pragma unroll
+  for (int k = 0; k < kPatchIters; k++) {
+    const int t = k * 64 + lane;
+    const short2 d = c_patch[t < kNPatch ? t : 0];
+    cpx[k] = t < kNPatch ? (uint32_t)((d.y + 15) * 36 + d.x + 15) | (uint32_t)(d.x + 16) << 16 | (uint32_t)(d.y + 16) << 24
+                         : (16u << 16) | (16u << 24);
+  }
   for (int i0 = wv * kAngPerWave; i0 < n; i0 += nw * kAngPerWave) {
     uint32_t* hp = sh_patch + wv * kPatchDw;
     int xs[kAngPerWave], ys[kAngPerWave];
@@ -820,11 +830,9 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
       m01[u] = m10[u] = 0;
 #pragma unroll
       for (int k = 0; k < kPatchIters; k++) {
-        const int t = k * 64 + lane;
-        const short2 d = c_patch[t < kNPatch ? t : 0];
-        const int v = t < kNPatch ? (int)P[(d.y + 15) * 36 + d.x + 15] : 0;
-        m10[u] += d.x * v;
-        m01[u] += d.y * v;
+        const int v = (int)P[cpx[k] & 0xffffu];
+        m10[u] += ((int)((cpx[k] >> 16) & 0xffu) - 16) * v;
+        m01[u] += ((int)(cpx[k] >> 24) - 16) * v;
       }
     }
     wave_lds_sync();  // the patch is rewritten by the next iteration
