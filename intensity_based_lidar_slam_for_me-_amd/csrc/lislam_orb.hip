@@ -800,16 +800,19 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
     cpx[k] = t < kNPatch ? (uint32_t)((d.y + 15) * 36 + d.x + 15) | (uint32_t)(d.x + 16) << 16 | (uint32_t)(d.y + 16) << 24
                          : (16u << 16) | (16u << 24);
   }
-  for (int i0 = wv * kAngPerWave; i0 < n; i0 += nw * kAngPerWave) {
-    uint32_t* hp = sh_patch + wv * kPatchDw;
-    int xs[kAngPerWave], ys[kAngPerWave];
+  // software pipelined: the next iteration's patch dwords are loaded into registers while this
+  // iteration's moments are summed from LDS
+  constexpr int kStg = (kAngPerWave * 279 + 63) / 64;
+  uint32_t rbuf[kStg];
+  int xs[kAngPerWave], ys[kAngPerWave];
+  auto fetch = [&](int i0f) {
 #pragma unroll
     for (int u = 0; u < kAngPerWave; u++) {
-      const int ci = cand[min(i0 + u, n - 1)];
+      const int ci = cand[min(i0f + u, n - 1)];
       xs[u] = ci % w; ys[u] = ci / w;
     }
 #pragma unroll
-    for (int k = 0; k < (kAngPerWave * 279 + 63) / 64; k++) {
+    for (int k = 0; k < kStg; k++) {
       const int item = lane + 64 * k;
       if (item < kAngPerWave * 279) {
         const int u = item / 279, rr = (item % 279) / 9, dw = (item % 279) % 9;
@@ -817,16 +820,29 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
 #pragma unroll
         for (int v = 1; v < kAngPerWave; v++)
           if (u == v) { x = xs[v]; y = ys[v]; }
-        hp[item] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y - 15 + rr + kB) * stride_l +
-                                                                           ((x - 15 + kB) & ~3) + 4 * dw);
+        rbuf[k] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y - 15 + rr + kB) * stride_l +
+                                                                          ((x - 15 + kB) & ~3) + 4 * dw);
       }
     }
+  };
+  if (wv * kAngPerWave < n) fetch(wv * kAngPerWave);
+  for (int i0 = wv * kAngPerWave; i0 < n; i0 += nw * kAngPerWave) {
+    uint32_t* hp = sh_patch + wv * kPatchDw;
+#pragma unroll
+    for (int k = 0; k < kStg; k++) {
+      const int item = lane + 64 * k;
+      if (item < kAngPerWave * 279) hp[item] = rbuf[k];
+    }
+    int cx[kAngPerWave], cy[kAngPerWave];
+#pragma unroll
+    for (int u = 0; u < kAngPerWave; u++) { cx[u] = xs[u]; cy[u] = ys[u]; }
+    if (i0 + nw * kAngPerWave < n) fetch(i0 + nw * kAngPerWave);
     wave_lds_sync();
     const uint8_t* hb = reinterpret_cast<const uint8_t*>(hp);
     int m01[kAngPerWave], m10[kAngPerWave];
 #pragma unroll
     for (int u = 0; u < kAngPerWave; u++) {
-      const uint8_t* P = hb + u * 279 * 4 + ((xs[u] - 15 + kB) & 3);  // P[r * 36 + c]: row y-15+r, column x-15+c
+      const uint8_t* P = hb + u * 279 * 4 + ((cx[u] - 15 + kB) & 3);  // P[r * 36 + c]: row y-15+r, column x-15+c
       m01[u] = m10[u] = 0;
 #pragma unroll
       for (int k = 0; k < kPatchIters; k++) {
@@ -844,7 +860,7 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
         const int i = i0 + u;
         if (i >= n) break;
         float* o = out + (size_t)i * 6;
-        o[0] = (float)xs[u]; o[1] = (float)ys[u]; o[2] = 31 * g.scale[l];
+        o[0] = (float)cx[u]; o[1] = (float)cy[u]; o[2] = 31 * g.scale[l];
         o[3] = fast_atan2((float)m01[u], (float)m10[u]);
         o[4] = resp[i];
         o[5] = (float)l;
