@@ -198,6 +198,17 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
  * parameterization Jacobians jac[3n x 6] (d/d delta-theta, d/d t), both optional. */
 int lislam_eval_factors(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,
                         const double* t, double* residuals, double* jac);
+/* ceres::AutoDiffCostFunction<F, R, 4, 3>::Evaluate of the reference functors on the GPU: the
+ * Jacobians w.r.t. the raw parameter blocks, jac_q[n][3][4] (q x, y, z, w) and jac_t[n][3][3],
+ * as Ceres' Jet differentiation gives them (lidarFeaturePointsFunction.hpp:29,49-54,157,183-190,
+ * 208,228-234,252,282-288).  kind[i]: 0 LidarEdgeFactor (pts: curr, a, b), 1 LidarPlaneFactor
+ * (curr, j, l, m), 2 LidarPlaneNormFactor (curr, n, d), 3 front_end_residual /
+ * FeatureMatchingResidual (curr / src, dst; :21-99), 4 LidarGroundPlaneNormFactor (curr, n, d;
+ * q block only, jac_t rows zero; :101-141).  Residual rows past the block's size are zero.  All
+ * pointers may be host or device memory; outputs are optional.  include/lislam_factors.h wraps
+ * this behind the reference's functor structs and their Create(). */
+int lislam_eval_factors_raw(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,
+                            const double* t, double* residuals, double* jac_q, double* jac_t);
 
 /* ---------------------------------------------------------------- ORB intensity front end (a8-a11) */
 /* cv::ORB::create(nfeatures, 1.2f, 8, 1) detect (with the feature_tracker MASK, H x W u8, 0 =

@@ -720,4 +720,39 @@ int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const dou
   return LISLAM_OK;
 }
 
+int lislam_eval_factors_raw(lislam_ctx* c, int32_t n, const int32_t* kind, const double* pts, const double* q,
+                            const double* t, double* residuals, double* jac_q, double* jac_t) {
+  if (!c || n < 0 || (n > 0 && (!kind || !pts)) || !q || !t) return LISLAM_ERR_ARG;
+  for (int32_t i = 0; i < n; i++)
+    if (kind[i] < 0 || kind[i] > 4) return fail(c, LISLAM_ERR_ARG, "lislam_eval_factors_raw: block %d has kind %d", i, kind[i]);
+  if (n == 0) return LISLAM_OK;
+  hipSetDevice(c->device);
+  int* dk = nullptr;
+  double *dp = nullptr, *dx = nullptr, *dr = nullptr, *djq = nullptr, *djt = nullptr;
+  const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
+  auto cleanup = [&]() { hipFree(dk); hipFree(dp); hipFree(dx); hipFree(dr); hipFree(djq); hipFree(djt); };
+  if (hipMalloc(&dk, n * sizeof(int)) != hipSuccess || hipMalloc(&dp, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&dx, 7 * sizeof(double)) != hipSuccess || hipMalloc(&dr, (size_t)n * 3 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&djq, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&djt, (size_t)n * 9 * sizeof(double)) != hipSuccess) {
+    cleanup();
+    return fail(c, LISLAM_ERR_DEVICE, "hipMalloc failed in lislam_eval_factors_raw");
+  }
+  hipError_t e = hipMemcpyAsync(dk, kind, n * sizeof(int), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dp, pts, (size_t)n * 12 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dx, x, sizeof(x), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    RawFactorArgs a{n, dk, dp, dx, dr, djq, djt};
+    launch_factors_raw(a, c->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && residuals) e = hipMemcpyAsync(residuals, dr, (size_t)n * 3 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess && jac_q) e = hipMemcpyAsync(jac_q, djq, (size_t)n * 12 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess && jac_t) e = hipMemcpyAsync(jac_t, djt, (size_t)n * 9 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  cleanup();
+  if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors_raw: %s", hipGetErrorString(e));
+  return LISLAM_OK;
+}
+
 }  // extern "C"

@@ -137,4 +137,18 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
                      void* ev_owner);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
+// AutoDiffCostFunction<F, R, 4, 3>::Evaluate of the functors of lidarFeaturePointsFunction.hpp:
+// Jacobians w.r.t. the raw parameter blocks q[4] (x, y, z, w) and t[3], as ceres::Jet computes them.
+struct RawFactorArgs {
+  int n;
+  const int* kind;     // 0 edge, 1 plane, 2 plane-norm, 3 front_end_residual / FeatureMatchingResidual,
+                       // 4 LidarGroundPlaneNormFactor (q block only)
+  const double* pts;   // [n][12]
+  const double* x;     // q(4), t(3)
+  double* res;         // [n][3] or null
+  double* jq;          // [n][3][4] or null
+  double* jt;          // [n][3][3] or null
+};
+void launch_factors_raw(const RawFactorArgs& a, hipStream_t st);
+
 }  // namespace lislam

@@ -935,6 +935,70 @@ __global__ __launch_bounds__(256) void k_eval_factors(FactorArgs a) {
       for (int cc = 0; cc < 6; cc++) a.jac[((size_t)i * 3 + k) * 6 + cc] = J[k][cc];
 }
 
+// d(q * c)/dq of Eigen's _transformVector p = c + w uv + u x uv, uv = 2 (u x c), u = (x, y, z):
+// columns x, y, z, w of the raw quaternion block (the polynomial ceres::Jet differentiates).
+__device__ __forceinline__ void drot_dq(const DQ& q, const D3& c, double (*P)[4]) {
+  const D3 u{q.x, q.y, q.z};
+  const D3 uv = 2.0 * cross(u, c);
+  const D3 e[3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  for (int i = 0; i < 3; i++) {
+    const D3 duv = 2.0 * cross(e[i], c);
+    const D3 d = q.w * duv + cross(e[i], uv) + cross(u, duv);
+    P[0][i] = d.x; P[1][i] = d.y; P[2][i] = d.z;
+  }
+  P[0][3] = uv.x; P[1][3] = uv.y; P[2][3] = uv.z;
+}
+
+// One thread per residual block.  r(lp) with lp = q * c (+ t): J_q = dr/dlp . dlp/dq, J_t = dr/dlp.
+// The functors' identity.slerp(s = 1, q) is +-q (lidarFeaturePointsFunction.hpp:165,262), which
+// rotates exactly like q and has the same raw derivative (the sign squares out).
+__global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const DQ q{a.x[0], a.x[1], a.x[2], a.x[3]};
+  const D3 t{a.x[4], a.x[5], a.x[6]};
+  const double* p = a.pts + (size_t)i * 12;
+  const D3 c{p[0], p[1], p[2]};
+  const int kd = a.kind[i];
+  double r[3] = {0, 0, 0}, G[3][3] = {{0}};  // G = dr/dlp (rows = residuals)
+  int R = 1;
+  if (kd == 0) {
+    double J[3][6];
+    edge_factor(q, t, c, D3{p[3], p[4], p[5]}, D3{p[6], p[7], p[8]}, r, J);
+    for (int k = 0; k < 3; k++) for (int cc = 0; cc < 3; cc++) G[k][cc] = J[k][3 + cc];
+    R = 3;
+  } else if (kd == 1) {
+    const D3 n = plane_normal(D3{p[3], p[4], p[5]}, D3{p[6], p[7], p[8]}, D3{p[9], p[10], p[11]});
+    double J[6];
+    plane_factor(q, t, c, D3{p[3], p[4], p[5]}, n, r, J);
+    G[0][0] = n.x; G[0][1] = n.y; G[0][2] = n.z;
+  } else if (kd == 2 || kd == 4) {
+    const D3 n{p[3], p[4], p[5]};
+    const D3 pr = qrot(q, c);
+    r[0] = dot(n, kd == 2 ? pr + t : pr) + p[6];
+    G[0][0] = n.x; G[0][1] = n.y; G[0][2] = n.z;
+  } else {
+    double J[3][6];
+    p2p_factor(q, t, c, D3{p[3], p[4], p[5]}, r, J);
+    for (int k = 0; k < 3; k++) G[k][k] = 1.0;
+    R = 3;
+  }
+  double P[3][4];
+  drot_dq(q, c, P);
+  for (int k = 0; k < 3; k++) {
+    if (a.res) a.res[(size_t)i * 3 + k] = k < R ? r[k] : 0.0;
+    if (a.jq)
+      for (int cc = 0; cc < 4; cc++)
+        a.jq[((size_t)i * 3 + k) * 4 + cc] = k < R ? G[k][0] * P[0][cc] + G[k][1] * P[1][cc] + G[k][2] * P[2][cc] : 0.0;
+    if (a.jt)
+      for (int cc = 0; cc < 3; cc++) a.jt[((size_t)i * 3 + k) * 3 + cc] = (k < R && kd != 4) ? G[k][cc] : 0.0;
+  }
+}
+
+void launch_factors_raw(const RawFactorArgs& a, hipStream_t st) {
+  if (a.n > 0) hipLaunchKernelGGL(k_eval_factors_raw, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+}
+
 void launch_factors(const FactorArgs& a, hipStream_t st) {
   if (a.n > 0) hipLaunchKernelGGL(k_eval_factors, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
 }

@@ -1,0 +1,176 @@
+// A ROS-free C++ consumer of the drop-in boundary (include/lislam.h + include/lislam_factors.h):
+// residual blocks are built through the reference functors' Create() (lidarFeaturePointsFunction.hpp
+// signatures), evaluated on the GPU through their CostFunction::Evaluate and through one batched
+// lislam::EvaluateBlocks launch, and compared with the oracle's Ceres-Jet autodiff restatement
+// (oracle/oracle_solver.hpp, test infrastructure) and with the header functors' own operator()<double>.
+// Run by tests/test_gpu_factors_cpp.py; prints "factors ok" and exits 0 on success.
+#include <cmath>
+#include <cstdio>
+#include <memory>
+#include <random>
+#include <vector>
+
+#include "lislam.h"
+#include "lislam_factors.h"
+#include "oracle_solver.hpp"
+
+static int g_fail = 0;
+static void check(bool ok, const char* what, int i, double a, double b) {
+  if (!ok) {
+    if (g_fail < 20) std::fprintf(stderr, "MISMATCH %s block %d: %.17g vs %.17g\n", what, i, a, b);
+    g_fail++;
+  }
+}
+static bool close(double a, double b, double rtol, double atol) { return std::fabs(a - b) <= atol + rtol * std::fabs(b); }
+
+int main() {
+  lislam_config cfg{64, 1024, 0.3f, 4, 0};
+  lislam_ctx* ctx = nullptr;
+  if (lislam_ctx_create(&cfg, 0, &ctx) != LISLAM_OK) {
+    std::fprintf(stderr, "lislam_ctx_create failed\n");
+    return 2;
+  }
+  lislam::SetFactorContext(ctx);
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(-5.0, 5.0), A(-0.3, 0.3);
+  auto v3 = [&]() { return lislam::Vector3d(U(rng), U(rng), U(rng)); };
+  const int n_per = 40;
+  std::vector<std::unique_ptr<lislam::CostFunction>> owned;
+  std::vector<const lislam::CostFunction*> blocks;
+  struct Ref {
+    int kind;
+    double rec[12];
+  };
+  std::vector<Ref> refs;
+  // parameters: a unit quaternion (x, y, z, w) near identity and a translation
+  double q[4] = {A(rng), A(rng), A(rng), 0.0}, t[3] = {U(rng), U(rng), U(rng)};
+  q[3] = std::sqrt(1.0 - q[0] * q[0] - q[1] * q[1] - q[2] * q[2]);
+  for (int kind = 0; kind < 5; kind++) {
+    for (int i = 0; i < n_per; i++) {
+      Ref r{kind, {0}};
+      lislam::Vector3d c = v3(), a = v3(), b = v3(), m = v3();
+      lislam::Vector3d nrm = v3();
+      nrm.normalize();
+      const double d = U(rng);
+      lislam::CostFunction* f = nullptr;
+      double host_r[3] = {0, 0, 0};
+      int R = 1;
+      switch (kind) {
+        case 0: {
+          f = LidarEdgeFactor::Create(c, a, b, 1.0);
+          LidarEdgeFactor(c, a, b, 1.0)(q, t, host_r);
+          R = 3;
+          for (int k = 0; k < 3; k++) { r.rec[k] = c.v[k]; r.rec[3 + k] = a.v[k]; r.rec[6 + k] = b.v[k]; }
+          break;
+        }
+        case 1: {
+          f = LidarPlaneFactor::Create(c, a, b, m, 1.0);
+          LidarPlaneFactor(c, a, b, m, 1.0)(q, t, host_r);
+          for (int k = 0; k < 3; k++) { r.rec[k] = c.v[k]; r.rec[3 + k] = a.v[k]; r.rec[6 + k] = b.v[k]; r.rec[9 + k] = m.v[k]; }
+          break;
+        }
+        case 2: {
+          f = LidarPlaneNormFactor::Create(c, nrm, d);
+          LidarPlaneNormFactor(c, nrm, d)(q, t, host_r);
+          for (int k = 0; k < 3; k++) { r.rec[k] = c.v[k]; r.rec[3 + k] = nrm.v[k]; }
+          r.rec[6] = d;
+          break;
+        }
+        case 3: {
+          f = (i & 1) ? FeatureMatchingResidual::Create(c, a) : front_end_residual::Create(c, a);
+          if (i & 1) FeatureMatchingResidual(c, a)(q, t, host_r);
+          else front_end_residual(c, a)(q, t, host_r);
+          R = 3;
+          for (int k = 0; k < 3; k++) { r.rec[k] = c.v[k]; r.rec[3 + k] = a.v[k]; }
+          break;
+        }
+        default: {
+          f = LidarGroundPlaneNormFactor::Create(c, nrm, d);
+          LidarGroundPlaneNormFactor(c, nrm, d)(q, host_r);
+          for (int k = 0; k < 3; k++) { r.rec[k] = c.v[k]; r.rec[3 + k] = nrm.v[k]; }
+          r.rec[6] = d;
+        }
+      }
+      if (!f || f->num_residuals() != R) {
+        std::fprintf(stderr, "Create failed for kind %d\n", kind);
+        return 3;
+      }
+      const int idx = (int)refs.size();
+      // the block's own Evaluate (one GPU launch)
+      double res[3], jq[12], jt[9];
+      const double* params[2] = {q, t};
+      double* jacs[2] = {jq, jt};
+      if (!f->Evaluate(params, res, jacs)) {
+        std::fprintf(stderr, "Evaluate failed: %s\n", lislam_last_error(ctx));
+        return 4;
+      }
+      // oracle: Ceres-Jet autodiff of the restated functor (7 columns: q x y z w, t)
+      double orr[3] = {0, 0, 0}, oJ[21] = {0};
+      const double tz[3] = {0, 0, 0};
+      switch (kind) {
+        case 0: {
+          oracle::EdgeFactor F{{c.v[0], c.v[1], c.v[2]}, {a.v[0], a.v[1], a.v[2]}, {b.v[0], b.v[1], b.v[2]}, 1.0};
+          oracle::autodiff_eval(F, q, t, orr, oJ);
+          break;
+        }
+        case 1: {
+          oracle::PlaneFactor F(c.v, a.v, b.v, m.v, 1.0);
+          oracle::autodiff_eval(F, q, t, orr, oJ);
+          break;
+        }
+        case 3: {
+          oracle::P2PFactor F{{c.v[0], c.v[1], c.v[2]}, {a.v[0], a.v[1], a.v[2]}};
+          oracle::autodiff_eval(F, q, t, orr, oJ);
+          break;
+        }
+        default: {  // plane-norm; the ground factor is the same expression without t
+          oracle::PlaneNormFactor F{{c.v[0], c.v[1], c.v[2]}, {nrm.v[0], nrm.v[1], nrm.v[2]}, d};
+          oracle::autodiff_eval(F, q, kind == 4 ? tz : t, orr, oJ);
+        }
+      }
+      for (int k = 0; k < R; k++) {
+        check(close(res[k], orr[k], 1e-12, 1e-12), "residual vs oracle", idx, res[k], orr[k]);
+        check(close(res[k], host_r[k], 1e-12, 1e-12), "residual vs header operator()", idx, res[k], host_r[k]);
+        for (int cc = 0; cc < 4; cc++)
+          check(close(jq[k * 4 + cc], oJ[k * 7 + cc], 1e-9, 1e-10), "d r / d q vs oracle autodiff", idx, jq[k * 4 + cc],
+                oJ[k * 7 + cc]);
+        if (kind != 4)
+          for (int cc = 0; cc < 3; cc++)
+            check(close(jt[k * 3 + cc], oJ[k * 7 + 4 + cc], 1e-9, 1e-10), "d r / d t vs oracle autodiff", idx,
+                  jt[k * 3 + cc], oJ[k * 7 + 4 + cc]);
+      }
+      refs.push_back(r);
+      blocks.push_back(f);
+      owned.emplace_back(f);
+    }
+  }
+  // every block in one launch == the per-block evaluations above (same device code)
+  const size_t n = blocks.size();
+  std::vector<double> R3(n * 3), JQ(n * 12), JT(n * 9);
+  if (lislam::EvaluateBlocks(blocks, q, t, R3.data(), JQ.data(), JT.data()) != LISLAM_OK) {
+    std::fprintf(stderr, "EvaluateBlocks failed: %s\n", lislam_last_error(ctx));
+    return 5;
+  }
+  for (size_t i = 0; i < n; i++) {
+    double res[3], jq[12], jt[9];
+    const double* params[2] = {q, t};
+    double* jacs[2] = {jq, jt};
+    blocks[i]->Evaluate(params, res, jacs);
+    for (int k = 0; k < blocks[i]->num_residuals(); k++) {
+      check(R3[i * 3 + k] == res[k], "batched residual", (int)i, R3[i * 3 + k], res[k]);
+      for (int cc = 0; cc < 4; cc++) check(JQ[i * 12 + k * 4 + cc] == jq[k * 4 + cc], "batched J_q", (int)i, 0, 0);
+    }
+  }
+  // s != 1 is refused (DISTORTION 0 only)
+  if (LidarEdgeFactor::Create(v3(), v3(), v3(), 0.5) != nullptr) {
+    std::fprintf(stderr, "Create with s != 1 should return nullptr\n");
+    return 6;
+  }
+  lislam_ctx_destroy(ctx);
+  if (g_fail) {
+    std::fprintf(stderr, "%d mismatches\n", g_fail);
+    return 1;
+  }
+  std::printf("factors ok: %zu blocks (5 kinds x %d)\n", n, n_per);
+  return 0;
+}

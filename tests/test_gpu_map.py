@@ -282,3 +282,38 @@ def test_mapopt_fed_from_batch(pkg, oracle, ctx, synth):
         assert go.map.size() == om.size(), k
     go.map.close()
     b.close()
+
+
+def test_laser_mapping_config5_full_map(pkg, oracle, ctx, synth):
+    """Config 5 at its full size (bench.py --workload map): 20k surf queries of one 64x1024 scan
+    against a 5M-point corridor map, pose perturbed 5 cm / 0.5 deg, 2 outer passes of exact 5-NN
+    + plane fits + LidarPlaneNormFactor + Ceres(4) (laserMapping.cpp:620-850).  The 5-NN of a
+    2000-query sample is bit-exact; pose within 1e-4 and block counts equal."""
+    M = synth.make_corridor_map(5_000_000, spacing=0.05)
+    k = 50
+    scan = synth.make_scan(k).reshape(-1, 4)
+    scan = scan[np.abs(scan[:, :3]).sum(1) > 0]
+    rng = np.random.default_rng(7)
+    Q = _f32(scan[rng.choice(len(scan), 20000, replace=False)])
+    vi = np.floor(Q[:, :3] / 0.4).astype(np.int64)  # VoxelGrid output order (laserMapping.cpp:613-615)
+    Q = Q[np.lexsort((vi[:, 0], vi[:, 1], vi[:, 2]))]
+    q, t = synth.ground_truth_pose(k).as_qt()
+    x0 = synth.perturb_pose(q, t, 0.05, 0.5, seed=3)
+    g = pkg.mapping.IkdMap(ctx, 0.4, 0.3)  # the bench's hash-grid cell
+    g.build(M)
+    o = oracle.IkdMap(0.4)
+    o.build(M)
+    assert g.size() == o.size() == len(M)
+    # the sample's queries in the map frame at the initial guess
+    from scipy.spatial.transform import Rotation
+
+    S = Q[:2000, :3].astype(np.float64)
+    Sw = _f32(Rotation.from_quat(x0[:4]).apply(S) + x0[4:7])
+    _knn_equal(g.nearest_search(Sw, 5), o.knn(Sw, 5), 5)
+    empty = np.zeros((0, 4), np.float32)
+    xg, stg = pkg.mapping.laser_mapping(g, g, empty, Q, x0)
+    xo, sto = oracle.laser_mapping(o, o, empty, Q, x0)
+    assert np.max(np.abs(xg - xo)) < POSE_TOL, (xg, xo)
+    assert list(stg) == list(sto), (stg, sto)
+    assert sto[1] > 19000  # almost every query found a plane
+    g.close()
