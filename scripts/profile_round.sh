@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python bench.py --scan-cache /tmp/lislam_scans > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $ROOT/bench.py --steps 3 --warmup 1 --cpu-budget 0 --scan-cache /tmp/lislam_scans > $OUT/trace_bench.json 2> $OUT/trace.err || exit 2
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 $ROOT/bench.py --steps 1 --warmup 0 --cpu-budget 0 --scan-cache /tmp/lislam_scans > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit 3
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 $ROOT/bench.py --steps 1 --warmup 0 --cpu-budget 0 --scan-cache /tmp/lislam_scans > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit 4
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $ROOT/bench.py --steps 3 --warmup 1 --cpu-budget 0 --sustain-s 0 --scan-cache /tmp/lislam_scans > $OUT/trace_bench.json 2> $OUT/trace.err || exit 2
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 $ROOT/bench.py --steps 1 --warmup 0 --cpu-budget 0 --sustain-s 0 --scan-cache /tmp/lislam_scans > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit 3
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 $ROOT/bench.py --steps 1 --warmup 0 --cpu-budget 0 --sustain-s 0 --scan-cache /tmp/lislam_scans > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit 4
 echo done > $OUT/DONE
