@@ -191,6 +191,16 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
 int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,
                                 int32_t cap, int32_t* n);
 
+/* Order of equal keys in the scan-line VoxelGrid(0.2) of the less-flat cloud (a7,
+ * scanRegistration.cpp:583-586): PCL 1.10's VoxelGrid sorts (voxel, point) pairs with std::sort
+ * by voxel alone, so a voxel's points are summed in the order libstdc++'s introsort leaves them.
+ * LISLAM_TIES_REFERENCE (the default) replays that order exactly (bit-exact centroids);
+ * LISLAM_TIES_INDEX sums them in input order (faster; centroids differ by float rounding, poses by
+ * up to 1e-4 on the bench data, tests/test_oracle.py).  Applies to later extractions of ctx. */
+#define LISLAM_TIES_REFERENCE 0
+#define LISLAM_TIES_INDEX 1
+int lislam_set_tie_order(lislam_ctx* ctx, int32_t order);
+
 /* ---------------------------------------------------------------- cost functors */
 /* Evaluate n residual blocks at (q[4] = x,y,z,w, t[3]) on the GPU.  kind[i]: 0 LidarEdgeFactor
  * (pts: curr, a, b), 1 LidarPlaneFactor (curr, j, l, m), 2 LidarPlaneNormFactor (curr, n, d);

@@ -332,6 +332,7 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   hipSetDevice(c->device);
   FeatureArgs f = b->fa;
   f.S = n_scans;
+  f.voxel_ties = c->voxel_ties;
   hipEvent_t* ev = nullptr;
   if (b->timing) {
     b->ext_ev.emplace_back();
@@ -717,6 +718,12 @@ int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const dou
   if (e == hipSuccess && jac) e = hipMemcpy(jac, dj, (size_t)n * 18 * sizeof(double), hipMemcpyDeviceToHost);
   cleanup();
   if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors: %s", hipGetErrorString(e));
+  return LISLAM_OK;
+}
+
+int lislam_set_tie_order(lislam_ctx* c, int32_t order) {
+  if (!c || (order != LISLAM_TIES_REFERENCE && order != LISLAM_TIES_INDEX)) return LISLAM_ERR_ARG;
+  c->voxel_ties = order;
   return LISLAM_OK;
 }
 

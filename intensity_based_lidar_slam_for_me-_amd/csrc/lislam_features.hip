@@ -21,6 +21,7 @@
 //                  (offsets = wave sums of the earlier lines' counts).
 #include <hip/hip_runtime.h>
 
+#include "../../include/lislam.h"
 #include "lislam_device.hpp"
 #include "lislam_internal.hpp"
 
@@ -307,6 +308,351 @@ __device__ __forceinline__ void bitonic_sort(KeyPtr keys, int P) {
 
 __device__ __forceinline__ uint64_t first_lane(uint64_t m) { return (uint64_t)__builtin_ctzll(m); }
 
+// ------------------------------------------------------------------ libstdc++ std::sort tie order
+// PCL VoxelGrid sorts (voxel, point) pairs with std::sort comparing the voxel only
+// (scanRegistration.cpp:583-586 -> pcl::VoxelGrid::applyFilter), so the order of a voxel's points
+// — the order its centroid is summed in — is whatever libstdc++'s introsort leaves.  These
+// functions reproduce that order on one wave (checked against std::sort itself by
+// tests/cpp/introsort_emu.cpp, which restates the same formulation on the host):
+//   std::__introsort_loop: ranges of more than 16 elements are split by
+//     __unguarded_partition_pivot (median of first + 1, mid, last - 1 moved to first, then the
+//     two-pointer walk); below depth 2 floor(log2 n) a range is heap-sorted instead;
+//   the walk is computed with prefix counts: the m-th element >= pivot from the left, L[m], swaps
+//     with the m-th element <= pivot from the right, R[m], while L[m] < R[m]; the cut is
+//     min(L[m*], R[m* - 1]) for the first m* where that fails;
+//   std::__final_insertion_sort never reorders equal keys, so the final order is a stable sort
+//     by key of the array the loop leaves (the caller's bitonic sort of (key, position)).
+// a: the elements (LDS or global), ordered by kof(element) (an unsigned key; the element's other
+// bits are its payload); lidx / ridx: scratch of at least n / 2 + 1 entries each.  Ranges of the
+// partition stack live one per lane.
+template <bool kLds, typename ElemPtr, typename KeyOf, typename IdxPtr>
+__device__ __forceinline__ int introsort_partition(ElemPtr a, KeyOf kof, int f, int l, IdxPtr lidx, IdxPtr ridx) {
+  const int lane = lane_id();
+  const int mid = f + (l - f) / 2;
+  // std::__move_median_to_first(f, f + 1, mid, l - 1)
+  const auto ea = a[f + 1], eb = a[mid], ec = a[l - 1], e0 = a[f];
+  const auto ka = kof(ea), kb = kof(eb), kc = kof(ec);
+  int pick;
+  if (ka < kb) pick = kb < kc ? mid : (ka < kc ? l - 1 : f + 1);
+  else pick = ka < kc ? f + 1 : (kb < kc ? l - 1 : mid);
+  const auto ep = pick == f + 1 ? ea : pick == mid ? eb : ec;
+  const auto p = kof(ep);
+  wave_sync<kLds>();  // every lane has read before lane 0 swaps
+  if (lane == 0) { a[f] = ep; a[pick] = e0; }
+  wave_sync<kLds>();
+  const int lo = f + 1, hi = l - 1;
+  const int cap = ((hi - lo + 1) >> 1) + 1;  // L[m] < R[m] pairs use 2m distinct positions
+  int total_le = 0;
+  for (int b = lo; b <= hi; b += 64) {
+    const int i = b + lane;
+    total_le += __popcll(__ballot(i <= hi && !(p < kof(a[i]))));
+  }
+  int ge_before = 0, le_seen = 0, mstar = 0, next_ge = -1;
+  const uint64_t lt = lanemask_lt();
+  for (int b = lo; b <= hi; b += 64) {
+    const int i = b + lane;
+    const bool valid = i <= hi;
+    const auto k = valid ? kof(a[i]) : p;
+    const bool ge = valid && !(k < p), le = valid && !(p < k);
+    const uint64_t mge = __ballot(ge), mle = __ballot(le);
+    const int rank = ge_before + __popcll(mge & lt);                        // L rank of i
+    const int after = total_le - (le_seen + __popcll(mle & lt) + (int)le);  // <= elements after i = R rank
+    const bool cond = ge && after >= rank + 1;                               // L[rank] < R[rank]
+    const uint64_t mc = __ballot(cond);
+    if (cond) lidx[rank] = i;
+    if (le && after < cap) ridx[after] = i;
+    if (next_ge < 0) {
+      const uint64_t nc = mge & ~mc;  // the first >= element left unmatched is L[m*]
+      if (nc) next_ge = b + (int)first_lane(nc);
+    }
+    mstar += __popcll(mc);
+    ge_before += __popcll(mge);
+    le_seen += __popcll(mle);
+  }
+  wave_sync<kLds>();
+  for (int r = lane; r < mstar; r += 64) {
+    const int x = lidx[r], y = ridx[r];
+    const auto ex = a[x], ey = a[y];
+    a[x] = ey;
+    a[y] = ex;
+  }
+  int cut = mstar > 0 ? (int)ridx[mstar - 1] : l;
+  if (next_ge >= 0 && next_ge < cut) cut = next_ge;
+  wave_sync<kLds>();
+  return cut;
+}
+
+// std::__heap_select + std::__sort_heap of [first, first + len) (the introsort depth fallback);
+// serial on lane 0.
+template <typename ElemPtr, typename KeyOf>
+__device__ __forceinline__ void heap_sort_serial(ElemPtr a, KeyOf kof, int first, int len) {
+  auto adjust = [&](int hole, int n, auto v) {  // std::__adjust_heap + std::__push_heap
+    const int top = hole;
+    int child = hole;
+    while (child < (n - 1) / 2) {
+      child = 2 * (child + 1);
+      if (kof(a[first + child]) < kof(a[first + child - 1])) child--;
+      a[first + hole] = a[first + child];
+      hole = child;
+    }
+    if ((n & 1) == 0 && child == (n - 2) / 2) {
+      child = 2 * (child + 1);
+      a[first + hole] = a[first + child - 1];
+      hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && kof(a[first + parent]) < kof(v)) {
+      a[first + hole] = a[first + parent];
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    a[first + hole] = v;
+  };
+  if (len >= 2)
+    for (int parent = (len - 2) / 2;; parent--) {
+      adjust(parent, len, a[first + parent]);
+      if (parent == 0) break;
+    }
+  for (int last = len; last > 1;) {
+    --last;
+    const auto v = a[first + last];
+    a[first + last] = a[first];
+    adjust(0, last, v);
+  }
+}
+
+template <bool kLds, typename ElemPtr, typename KeyOf, typename IdxPtr>
+__device__ __forceinline__ void introsort_order(ElemPtr a, KeyOf kof, int n, IdxPtr lidx, IdxPtr ridx) {
+  if (n <= 16) return;
+  const int lane = lane_id();
+  int sf = 0, sl = 0, sd = 0, sp = 0;  // lane sp holds stack entry sp
+  int f = 0, l = n, d = 2 * (31 - __builtin_clz((unsigned)n));
+  for (;;) {
+    while (l - f > 16) {
+      if (d == 0) {
+        if (lane == 0) heap_sort_serial(a, kof, f, l - f);
+        wave_sync<kLds>();
+        break;
+      }
+      d--;
+      const int cut = introsort_partition<kLds>(a, kof, f, l, lidx, ridx);
+      if (lane == sp) { sf = cut; sl = l; sd = d; }
+      sp++;
+      l = cut;
+    }
+    if (sp == 0) break;
+    sp--;
+    f = __builtin_amdgcn_readlane(sf, sp);
+    l = __builtin_amdgcn_readlane(sl, sp);
+    d = __builtin_amdgcn_readlane(sd, sp);
+  }
+}
+
+// ---- the same order with the line in LDS (the register path): ranges of up to 64 elements run
+// their whole subtree in registers (one element per lane; the partition's swaps are lane
+// permutes), larger ranges read their elements once into registers per partition.
+
+// std::__unguarded_partition_pivot of lanes [f, l) of e (one element per lane).
+template <typename KeyOf>
+__device__ __forceinline__ int partition_reg(uint32_t& e, KeyOf kof, int f, int l) {
+  const int lane = lane_id();
+  const int mid = f + (l - f) / 2;
+  const uint32_t ea = (uint32_t)__builtin_amdgcn_readlane((int)e, f + 1);
+  const uint32_t eb = (uint32_t)__builtin_amdgcn_readlane((int)e, mid);
+  const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)e, l - 1);
+  const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)e, f);
+  const uint32_t ka = kof(ea), kb = kof(eb), kc = kof(ec);
+  int pick;
+  if (ka < kb) pick = kb < kc ? mid : (ka < kc ? l - 1 : f + 1);
+  else pick = ka < kc ? f + 1 : (kb < kc ? l - 1 : mid);
+  const uint32_t ep = pick == f + 1 ? ea : pick == mid ? eb : ec;
+  if (lane == f) e = ep;
+  else if (lane == pick) e = e0;
+  const uint32_t p = kof(ep), k = kof(e);
+  const bool in = lane > f && lane < l;
+  const bool ge = in && !(k < p), le = in && !(p < k);
+  const uint64_t mge = __ballot(ge), mle = __ballot(le), lt = lanemask_lt();
+  const int rank = __popcll(mge & lt);
+  const int after = __popcll(mle) - __popcll(mle & lt) - (int)le;
+  const bool cond = ge && after >= rank + 1;
+  const uint64_t mc = __ballot(cond);
+  const int mstar = __popcll(mc);
+  const bool isR = le && after < mstar;  // L[m] < R[m]: the swapped L and R lanes are disjoint
+  // slot m <- the lane of R[m] / of L[m] (lanes outside the swap push to slot 63, never read)
+  const int toR = __builtin_amdgcn_ds_permute((isR ? after : 63) << 2, lane);
+  const int toL = __builtin_amdgcn_ds_permute((cond ? rank : 63) << 2, lane);
+  const int slot = cond ? rank : (isR ? after : 0);
+  const int pR = __builtin_amdgcn_ds_bpermute(slot << 2, toR), pL = __builtin_amdgcn_ds_bpermute(slot << 2, toL);
+  const int partner = cond ? pR : (isR ? pL : lane);
+  e = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)e);
+  int cut = l;
+  if (mstar > 0) cut = (int)first_lane(__ballot(le && after == mstar - 1));
+  const uint64_t nc = mge & ~mc;  // L[m*]
+  if (nc) cut = min(cut, (int)first_lane(nc));
+  return cut;
+}
+
+// std::__heap_select + std::__sort_heap of lanes [f, l) of e (uniform serial steps).
+template <typename KeyOf>
+__device__ __forceinline__ void heap_sort_reg(uint32_t& e, KeyOf kof, int f, int l) {
+  auto get = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)e, f + i); };
+  const int lane = lane_id();
+  auto set = [&](int i, uint32_t v) { e = lane == f + i ? v : e; };
+  auto adjust = [&](int hole, int n, uint32_t v) {
+    const int top = hole;
+    int child = hole;
+    while (child < (n - 1) / 2) {
+      child = 2 * (child + 1);
+      if (kof(get(child)) < kof(get(child - 1))) child--;
+      set(hole, get(child));
+      hole = child;
+    }
+    if ((n & 1) == 0 && child == (n - 2) / 2) {
+      child = 2 * (child + 1);
+      set(hole, get(child - 1));
+      hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && kof(get(parent)) < kof(v)) {
+      set(hole, get(parent));
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    set(hole, v);
+  };
+  const int len = l - f;
+  for (int parent = (len - 2) / 2;; parent--) {
+    adjust(parent, len, get(parent));
+    if (parent == 0) break;
+  }
+  for (int last = len; last > 1;) {
+    --last;
+    const uint32_t v = get(last);
+    set(last, get(0));
+    adjust(0, last, v);
+  }
+}
+
+// The introsort subtree of a[F, F + n), n <= 64, with depth limit D, in registers.
+template <typename KeyOf>
+__device__ __forceinline__ void introsort_small(uint32_t* a, KeyOf kof, int F, int n, int D) {
+  const int lane = lane_id();
+  uint32_t e = lane < n ? a[F + lane] : 0u;
+  int sf = 0, sl = 0, sd = 0, sp = 0;
+  int f = 0, l = n, d = D;
+  for (;;) {
+    while (l - f > 16) {
+      if (d == 0) {
+        heap_sort_reg(e, kof, f, l);
+        break;
+      }
+      d--;
+      const int cut = partition_reg(e, kof, f, l);
+      if (lane == sp) { sf = cut; sl = l; sd = d; }
+      sp++;
+      l = cut;
+    }
+    if (sp == 0) break;
+    sp--;
+    f = __builtin_amdgcn_readlane(sf, sp);
+    l = __builtin_amdgcn_readlane(sl, sp);
+    d = __builtin_amdgcn_readlane(sd, sp);
+  }
+  if (lane < n) a[F + lane] = e;
+}
+
+// A partition of a range of more than 64 elements of the LDS array (two counting passes over the
+// range, then the swaps).
+template <int kC, typename KeyOf>
+__device__ __forceinline__ int partition_lds(uint32_t* a, KeyOf kof, int f, int l, uint16_t* lidx, uint16_t* ridx) {
+  const int lane = lane_id();
+  const int mid = f + (l - f) / 2;
+  const uint32_t ea = a[f + 1], eb = a[mid], ec = a[l - 1], e0 = a[f];
+  const uint32_t ka = kof(ea), kb = kof(eb), kc = kof(ec);
+  int pick;
+  if (ka < kb) pick = kb < kc ? mid : (ka < kc ? l - 1 : f + 1);
+  else pick = ka < kc ? f + 1 : (kb < kc ? l - 1 : mid);
+  const uint32_t ep = pick == f + 1 ? ea : pick == mid ? eb : ec;
+  const uint32_t p = kof(ep);
+  const int lo = f + 1, hi = l - 1;
+  // the median swap (a[f] <-> a[pick]) as the reads below see it; the swap itself is written
+  // after the counting passes
+  auto key_at = [&](int i) { return i == pick ? kof(e0) : kof(a[i]); };
+  int total_le = 0;
+  for (int b = lo; b <= hi; b += 64) {
+    const int i = b + lane;
+    total_le += __popcll(__ballot(i <= hi && !(p < key_at(i))));
+  }
+  const int cap = ((hi - lo + 1) >> 1) + 1;
+  int ge_before = 0, le_seen = 0, mstar = 0, next_ge = -1;
+  const uint64_t lt = lanemask_lt();
+  for (int b = lo; b <= hi; b += 64) {
+    const int i = b + lane;
+    const bool valid = i <= hi;
+    const uint32_t k = valid ? key_at(i) : p;
+    const bool ge = valid && !(k < p), le = valid && !(p < k);
+    const uint64_t mge = __ballot(ge), mle = __ballot(le);
+    const int rank = ge_before + __popcll(mge & lt);
+    const int after = total_le - (le_seen + __popcll(mle & lt) + (int)le);
+    const bool cond = ge && after >= rank + 1;
+    const uint64_t mc = __ballot(cond);
+    if (cond) lidx[rank] = (uint16_t)i;
+    if (le && after < cap) ridx[after] = (uint16_t)i;
+    if (next_ge < 0) {
+      const uint64_t nc = mge & ~mc;
+      if (nc) next_ge = b + (int)first_lane(nc);
+    }
+    mstar += __popcll(mc);
+    ge_before += __popcll(mge);
+    le_seen += __popcll(mle);
+  }
+  if (lane == 0) { a[f] = ep; a[pick] = e0; }
+  wave_sync<true>();
+  for (int r = lane; r < mstar; r += 64) {
+    const int x = lidx[r], y = ridx[r];
+    const uint32_t ex = a[x], ey = a[y];
+    a[x] = ey;
+    a[y] = ex;
+  }
+  int cut = mstar > 0 ? (int)ridx[mstar - 1] : l;
+  if (next_ge >= 0 && next_ge < cut) cut = next_ge;
+  wave_sync<true>();
+  return cut;
+}
+
+// introsort_order for an LDS array of at most 64 kC elements (the register path's line).
+template <int kC, typename KeyOf>
+__device__ __forceinline__ void introsort_order_lds(uint32_t* a, KeyOf kof, int n, uint16_t* lidx, uint16_t* ridx) {
+  if (n <= 16) return;
+  const int lane = lane_id();
+  int sf = 0, sl = 0, sd = 0, sp = 0;
+  int f = 0, l = n, d = 2 * (31 - __builtin_clz((unsigned)n));
+  for (;;) {
+    while (l - f > 16) {
+      if (l - f <= 64) {
+        introsort_small(a, kof, f, l - f, d);
+        wave_sync<true>();
+        break;
+      }
+      if (d == 0) {
+        if (lane == 0) heap_sort_serial(a, kof, f, l - f);
+        wave_sync<true>();
+        break;
+      }
+      d--;
+      const int cut = partition_lds<kC>(a, kof, f, l, lidx, ridx);
+      if (lane == sp) { sf = cut; sl = l; sd = d; }
+      sp++;
+      l = cut;
+    }
+    if (sp == 0) break;
+    sp--;
+    f = __builtin_amdgcn_readlane(sf, sp);
+    l = __builtin_amdgcn_readlane(sl, sp);
+    d = __builtin_amdgcn_readlane(sd, sp);
+  }
+}
+
 
 struct LineCounts {
   int sharp, less_sharp, flat, less_flat;
@@ -337,7 +683,9 @@ struct LineLists {
   int flat[kCapFlatPerLine];
 };
 
-// One scan line: curvature, the six-segment sharp/flat selection and the line's VoxelGrid.
+// One scan line: curvature, the six-segment sharp/flat selection and the line's VoxelGrid.  The
+// kernel runs it on global scratch (kLds = false) for lines longer than the register path holds;
+// the VoxelGrid's key buffer layout assumes that scratch (16 B per line point).
 //
 // The reference sorts each segment by curvature (std::sort, scanRegistration.cpp:440-448; the
 // canonical tie order is the point index) and walks it from the largest (sharp, :450-506) and
@@ -508,18 +856,34 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
       const int mul1 = divb[0], mul2 = divb[0] * divb[1];
       int P = 64;
       while (P < nlist) P <<= 1;
-      // the key buffer of the fast path holds kLineCap keys; the list never exceeds the line
-      for (int k = lane; k < P; k += 64) {
-        uint64_t key = ~0ull;
-        if (k < nlist) {
+      // std::sort's order of equal voxels (introsort_order) on the list: the key buffer's 16 B per
+      // line point hold the (voxel, line position) elements (second half) and the two index
+      // scratches (first half) until the final keys overwrite them.
+      {
+        uint8_t* region = reinterpret_cast<uint8_t*>(keys);
+        uint64_t* el = reinterpret_cast<uint64_t*>(region + 8 * (size_t)len);  // (voxel, line position)
+        uint32_t* lidx = reinterpret_cast<uint32_t*>(region);
+        uint32_t* ridx = reinterpret_cast<uint32_t*>(region + 4 * (size_t)len);
+        for (int k = lane; k < nlist; k += 64) {
           const P4 p = ld4(cloud + off + list[k]);
           const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
           const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
           const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
-          const uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
-          key = ((uint64_t)idx << 32) | (uint32_t)k;
+          el[k] = ((uint64_t)(uint32_t)(i0 + i1 * mul1 + i2 * mul2) << 32) | (uint32_t)list[k];
         }
-        keys[k] = key;
+        wave_sync<kLds>();
+        if (a.voxel_ties == LISLAM_TIES_REFERENCE)
+          introsort_order<kLds>(el, [](uint64_t e) { return (uint32_t)(e >> 32); }, nlist, lidx, ridx);
+        // keys (voxel, position after the introsort loop) and the list in that order.  Key k
+        // occupies bytes 8 k .. 8 k + 7 < 8 len, below the elements; the padding keys beyond the
+        // list may cover the elements, so they are written afterwards.
+        for (int k = lane; k < nlist; k += 64) {
+          const uint64_t e = el[k];
+          keys[k] = (e & 0xffffffff00000000ull) | (uint32_t)k;
+          list[k] = (int)(uint32_t)e;
+        }
+        wave_sync<kLds>();
+        for (int k = nlist + lane; k < P; k += 64) keys[k] = ~0ull;
       }
       wave_sync<kLds>();
       PHASE(6);
@@ -618,7 +982,7 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
 // where the state lives.
 template <int kS>
 __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int line, LineLists& ll, uint64_t* lmask,
-                                              P4* stage, P4* ring) {
+                                              P4* stage, P4* ring, uint32_t* vel, uint16_t* vidx) {
   const int lane = lane_id();
   const int N = a.N, H = a.H;
   const int* lo = a.line_off + (size_t)s * (H + 1);
@@ -854,6 +1218,70 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
           key[t] = ((uint64_t)idx << 32) | (uint32_t)k;
         }
       }
+      // std::sort's order of equal voxels (introsort_order): the list in LDS, in list order, as
+      // 32-bit elements (sort key, line position), reordered as the introsort loop leaves it; the
+      // keys then become (voxel, position after the loop, line position) for the stable sort
+      // below.  Voxel indices below 2^21 pack with the 11-bit line position directly; otherwise a
+      // first sort of (voxel, list position) numbers the voxels densely for the element.
+      if (a.voxel_ties == LISLAM_TIES_REFERENCE) {
+        uint32_t vmax = 0u;
+#pragma unroll
+        for (int t = 0; t < kS; t++)
+          if ((lfl >> t) & 1u) vmax = max(vmax, (uint32_t)(key[t] >> 32));
+        for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o));
+        const bool packed = vmax < (1u << 21);
+        int base = 0;
+#pragma unroll
+        for (int t = 0; t < kS; t++) {  // list positions: ballot prefix over the line
+          if (t >= nsl) continue;
+          const bool f = (lfl >> t) & 1u;
+          const uint64_t m = __ballot(f);
+          const int j = base + __popcll(m & lanemask_lt());
+          if (f && packed) vel[j] = ((uint32_t)(key[t] >> 32) << 11) | (uint32_t)(lane + 64 * t);
+          if (f && !packed)
+            key[t] = (key[t] & 0xffffffff00000000ull) | ((uint32_t)j << 16) | (uint32_t)(lane + 64 * t);
+          base += __popcll(m);
+        }
+        PHASE(6);
+        if (packed) {
+          wave_sync<true>();
+          introsort_order_lds<kS>(vel, [](uint32_t e) { return e >> 11; }, nlist, vidx, vidx + 32 * kS + 1);
+#pragma unroll
+          for (int t = 0; t < kS; t++) {
+            const int j = lane + 64 * t;
+            const uint32_t e = j < nlist ? vel[j] : 0u;
+            key[t] = j < nlist ? ((uint64_t)(e >> 11) << 32) | ((uint32_t)j << 16) | (e & 0x7ffu) : ~0ull;
+          }
+        } else {
+          reg_bitonic<kS>(key);
+          uint32_t prev_hi = 0xffffffffu;
+          int nvox = 0;
+#pragma unroll
+          for (int t = 0; t < kS; t++) {  // dense voxel numbers in sorted order
+            if (64 * t >= nlist) continue;
+            const bool valid = lane + 64 * t < nlist;
+            const uint32_t v = (uint32_t)(key[t] >> 32);
+            const uint32_t up1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, (int)v);
+            const uint32_t vprev = lane == 0 ? prev_hi : up1;
+            prev_hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+            const bool start = valid && v != vprev;
+            const uint64_t m = __ballot(start);
+            const int num = nvox + __popcll(m & lanemask_lt()) + (int)start - 1;
+            if (valid) vel[(key[t] >> 16) & 0xffffu] = ((uint32_t)num << 16) | (uint32_t)(key[t] & 0xffffu);
+            nvox += __popcll(m);
+          }
+          wave_sync<true>();
+          introsort_order_lds<kS>(vel, [](uint32_t e) { return e >> 16; }, nlist, vidx, vidx + 32 * kS + 1);
+#pragma unroll
+          for (int t = 0; t < kS; t++) {
+            const int j = lane + 64 * t;
+            const uint32_t e = j < nlist ? vel[j] : 0u;
+            key[t] = j < nlist ? ((uint64_t)(e >> 16) << 32) | ((uint32_t)j << 16) | (e & 0xffffu) : ~0ull;
+          }
+        }
+        PHASE(11);
+        wave_sync<true>();
+      }
       PHASE(6);
       reg_bitonic<kS>(key);
       PHASE(7);
@@ -875,7 +1303,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         const uint32_t up1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 63) & 63) << 2, (int)v);  // lane - 1
         const uint32_t vprev = lane == 0 ? prev_hi : up1;
         prev_hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-        if (valid) stage[lane] = ld4(cloud + off + (int)(uint32_t)key[t]);
+        if (valid) stage[lane] = ld4(cloud + off + (int)((uint32_t)key[t] & 0xffffu));
         const bool start = valid && (k == 0 || v != vprev);
         const uint64_t m = __ballot(start);
         wave_sync<true>();
@@ -951,11 +1379,18 @@ __global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
   __shared__ P4 stage[64];
   __shared__ P4 ring[3 * 64];
   __shared__ uint64_t lmask[kS + 2];
+  // the VoxelGrid's std::sort order (introsort_order): the list elements, and the partition's
+  // index scratch, which fits the curvature ring (dead by then) up to 16 slots
+  __shared__ uint32_t vel[64 * kS];
+  constexpr int kIdx = 2 * (32 * kS + 1);
+  constexpr bool kIdxInRing = kIdx * 2 <= (int)sizeof(P4) * 3 * 64;
+  __shared__ uint16_t vidx_own[kIdxInRing ? 1 : kIdx];
+  uint16_t* vidx = kIdxInRing ? reinterpret_cast<uint16_t*>(ring) : vidx_own;
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
   if (len <= 64 * kS)
-    line_body_reg<kS>(a, s, line, ll, lmask, stage, ring);
+    line_body_reg<kS>(a, s, line, ll, lmask, stage, ring, vel, vidx);
   else
     line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, ll, stage);
 }

@@ -53,6 +53,7 @@ struct FeatureArgs {
   int* n_feat;     // [S][4] = sharp, less_sharp, flat, less_flat
   int* feat_loff;  // [S][2][H+1] per-line offsets of less_sharp / less_flat
   int cap_sharp, cap_less_sharp, cap_flat;
+  int voxel_ties;  // a7 VoxelGrid order of equal voxels: LISLAM_TIES_REFERENCE (std::sort) / _INDEX
 };
 
 // Spatial index of a feature cloud: chunks of kChunk consecutive points (in the cloud's own,

@@ -44,6 +44,13 @@ class Context:
     def synchronize(self):
         nat.check(self.lib.lislam_synchronize(self.h), self.h, "lislam_synchronize")
 
+    TIES_REFERENCE, TIES_INDEX = 0, 1
+
+    def set_tie_order(self, order: int):
+        """Order of equal voxels in the a7 VoxelGrid (lislam_set_tie_order): TIES_REFERENCE
+        (default, PCL 1.10's std::sort order, bit-exact) or TIES_INDEX (input order, faster)."""
+        nat.check(self.lib.lislam_set_tie_order(self.h, int(order)), self.h, "lislam_set_tie_order")
+
     def __enter__(self):
         return self
 

@@ -209,7 +209,17 @@ class ScanFeatures:
     less_flat: np.ndarray
 
 
-def scan_registration(scan: np.ndarray, min_range: float = 0.3, canonical: bool = True) -> ScanFeatures:
+TIES_REFERENCE, TIES_CANONICAL = 0, 3  # oracle_scanreg.cpp: bit 0 segment sort, bit 1 VoxelGrid by index
+TIES_GPU = 1  # index order in the segment sorts, std::sort's order in the VoxelGrid (the HIP path)
+
+
+def scan_registration(scan: np.ndarray, min_range: float = 0.3, canonical: bool | None = None,
+                      ties: int | None = None) -> ScanFeatures:
+    """scanRegistration a1-a7 of one organized scan.  Tie order of equal sort keys: `ties`
+    (TIES_*), or canonical=True (index order throughout) / False (the reference's std::sort
+    throughout); the default is the HIP path's TIES_GPU."""
+    if ties is None:
+        ties = TIES_GPU if canonical is None else (TIES_CANONICAL if canonical else TIES_REFERENCE)
     scan = np.ascontiguousarray(scan, dtype=np.float32)
     H, W = scan.shape[:2]
     N = H * W
@@ -228,7 +238,7 @@ def scan_registration(scan: np.ndarray, min_range: float = 0.3, canonical: bool 
     fl = np.zeros((24 * H, 4), np.float32)
     lf = np.zeros((N, 4), np.float32)
     n = [np.zeros(1, np.int32) for _ in range(4)]
-    L.oracle_scan_registration(scan.reshape(-1), H, W, H, min_range, int(canonical), img_r, img_i,
+    L.oracle_scan_registration(scan.reshape(-1), H, W, H, min_range, int(ties), img_r, img_i,
                                track.reshape(-1), cloud.reshape(-1), ncl, ss, se, curv, lab,
                                sh.reshape(-1), n[0], ls.reshape(-1), n[1], fl.reshape(-1), n[2],
                                lf.reshape(-1), n[3])

@@ -11,10 +11,13 @@
 // with the repair interpretation of SURVEY.md §8(c)-1: the segment loop closes after :577,
 // so the VoxelGrid runs once per scan line (A-LOAM structure).
 //
-// canonical == 0 : ties in std::sort are resolved exactly as libstdc++'s introsort does
-//                  (std::sort with the reference's comparators, as the reference build would).
-// canonical == 1 : ties resolved by ascending point index (the order the HIP path uses).
-// The two differ only when two curvatures (or two voxel indices) compare equal.
+// ties (bit mask) selects how equal sort keys are ordered:
+//   bit 0 clear / set: the segment curvature sort (:445) as libstdc++'s std::sort leaves ties
+//                      (the reference build) / by ascending point index;
+//   bit 1 clear / set: the VoxelGrid's (voxel, point) sort (PCL std::sort by voxel) likewise.
+// 0 is the reference throughout; the HIP path uses 1 (index order in the segment sorts, whose ties
+// decide nothing on the benchmark data, tests/test_oracle.py; std::sort's order in the VoxelGrid,
+// whose ties are structural).  The orders differ only when two keys compare equal.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -132,7 +135,7 @@ struct ScanRegOut {
 };
 
 // scanRegistration.cpp:189-589 for one organized scan (points in ring-major order).
-static void scan_registration(const P4* raw, int npts, int n_scans, float min_range, bool canonical,
+static void scan_registration(const P4* raw, int npts, int n_scans, float min_range, int ties,
                               ScanRegOut& o) {
   // a2: removeClosedPointCloud(laserCloudIn, laserCloudIn, MINIMUM_RANGE) — thres is a float.
   const float thres = min_range;
@@ -231,7 +234,7 @@ static void scan_registration(const P4* raw, int npts, int n_scans, float min_ra
     for (int j = 0; j < 6; j++) {
       int sp = s + (e - s) * j / 6;
       int ep = s + (e - s) * (j + 1) / 6 - 1;
-      if (canonical)
+      if (ties & 1)
         std::stable_sort(sortInd.begin() + sp, sortInd.begin() + ep + 1,
                          [&](int a, int b) { return curv[a] < curv[b]; });
       else
@@ -271,7 +274,7 @@ static void scan_registration(const P4* raw, int npts, int n_scans, float min_ra
       for (int k = sp; k <= ep; k++)
         if (label[k] <= 0) lessFlatScan.push_back(cloud[k]);
     }
-    voxel_grid(lessFlatScan, 0.2f, canonical, o.less_flat);
+    voxel_grid(lessFlatScan, 0.2f, (ties & 2) != 0, o.less_flat);
   }
 }
 
@@ -285,7 +288,7 @@ extern "C" {
 // per-point arrays, 12*n_scans / 120*n_scans / 24*n_scans for sharp / less_sharp / flat and
 // H*W for less_flat.  Any output pointer may be NULL.  Returns 0.
 int oracle_scan_registration(const float* xyzi, int H, int W, int n_scans, float min_range,
-                             int canonical, uint8_t* img_range, uint8_t* img_int, float* cloud_track,
+                             int ties, uint8_t* img_range, uint8_t* img_int, float* cloud_track,
                              float* laser_cloud, int* n_cloud, int* scan_start, int* scan_end,
                              float* curvature, int8_t* label, float* sharp, int* n_sharp,
                              float* less_sharp, int* n_less_sharp, float* flat, int* n_flat,
@@ -293,7 +296,7 @@ int oracle_scan_registration(const float* xyzi, int H, int W, int n_scans, float
   const P4* raw = reinterpret_cast<const P4*>(xyzi);
   cloud_handler(raw, H, W, img_range, img_int, reinterpret_cast<P4*>(cloud_track));
   ScanRegOut o;
-  scan_registration(raw, H * W, n_scans, min_range, canonical != 0, o);
+  scan_registration(raw, H * W, n_scans, min_range, ties, o);
   auto put = [](const std::vector<P4>& v, float* dst, int* n) {
     if (n) *n = (int)v.size();
     if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(P4));

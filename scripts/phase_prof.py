@@ -14,9 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as g  # noqa: E402
 
-OUT = os.path.join(ROOT, "scripts", "_prof", "liblislam_prof.so")
+OUT = os.environ.get("LISLAM_PROF_LIB", os.path.join(ROOT, "scripts", "_prof", "liblislam_prof.so"))
 PHASES = ["curv+links", "seg sort", "sharp walk", "flat walk", "lessflat list", "label/feature writes",
-          "voxel keys", "voxel sort", "voxel centroids"]
+          "voxel keys", "voxel sort", "voxel centroids", "voxel numbering sort", "voxel numbering",
+          "voxel introsort order"]
 
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(OUT), exist_ok=True)

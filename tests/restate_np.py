@@ -110,8 +110,119 @@ def curvature(cloud):
     return c
 
 
-def voxel_grid(pts, leaf=0.2):
-    """PCL VoxelGrid with ties in voxel index resolved by input order (pure Python sums)."""
+def libstdcxx_sort(keys):
+    """The permutation libstdc++'s std::sort applies to `keys` (pure Python, serial): the
+    two-pointer introsort loop (median of first + 1 / mid / last - 1 moved to first,
+    __unguarded_partition), heap sort below depth 2 floor(log2 n), then the final insertion sort
+    (16-element head, unguarded tail).  An independent restatement of what the oracle gets from
+    calling std::sort and the HIP kernels compute with prefix counts."""
+    a = list(range(len(keys)))
+    k = keys
+
+    def lt(x, y):
+        return k[x] < k[y]
+
+    def adjust_heap(first, hole, n, v):
+        top = hole
+        child = hole
+        while child < (n - 1) // 2:
+            child = 2 * (child + 1)
+            if lt(a[first + child], a[first + child - 1]):
+                child -= 1
+            a[first + hole] = a[first + child]
+            hole = child
+        if n % 2 == 0 and child == (n - 2) // 2:
+            child = 2 * (child + 1)
+            a[first + hole] = a[first + child - 1]
+            hole = child - 1
+        parent = (hole - 1) // 2
+        while hole > top and lt(a[first + parent], v):
+            a[first + hole] = a[first + parent]
+            hole = parent
+            parent = (hole - 1) // 2
+        a[first + hole] = v
+
+    def heap_sort(first, last):
+        n = last - first
+        if n >= 2:
+            parent = (n - 2) // 2
+            while True:
+                adjust_heap(first, parent, n, a[first + parent])
+                if parent == 0:
+                    break
+                parent -= 1
+        while last - first > 1:
+            last -= 1
+            v = a[last]
+            a[last] = a[first]
+            adjust_heap(first, 0, last - first, v)
+
+    def partition_pivot(first, last):
+        mid = first + (last - first) // 2
+        x, y, z = first + 1, mid, last - 1
+        if lt(a[x], a[y]):
+            m = y if lt(a[y], a[z]) else (z if lt(a[x], a[z]) else x)
+        elif lt(a[x], a[z]):
+            m = x
+        elif lt(a[y], a[z]):
+            m = z
+        else:
+            m = y
+        a[first], a[m] = a[m], a[first]
+        lo, hi, piv = first + 1, last, a[first]
+        while True:
+            while lt(a[lo], piv):
+                lo += 1
+            hi -= 1
+            while lt(piv, a[hi]):
+                hi -= 1
+            if not lo < hi:
+                return lo
+            a[lo], a[hi] = a[hi], a[lo]
+            lo += 1
+
+    def loop(first, last, depth):
+        while last - first > 16:
+            if depth == 0:
+                heap_sort(first, last)
+                return
+            depth -= 1
+            cut = partition_pivot(first, last)
+            loop(cut, last, depth)
+            last = cut
+
+    def linear_insert(i):
+        v = a[i]
+        j = i - 1
+        while lt(v, a[j]):
+            a[j + 1] = a[j]
+            j -= 1
+        a[j + 1] = v
+
+    def insertion_sort(first, last):
+        for i in range(first + 1, last):
+            if lt(a[i], a[first]):
+                v = a[i]
+                a[first + 1:i + 1] = a[first:i]
+                a[first] = v
+            else:
+                linear_insert(i)
+
+    n = len(a)
+    if n:
+        loop(0, n, 2 * (n.bit_length() - 1))
+        if n > 16:
+            insertion_sort(0, 16)
+            for i in range(16, n):
+                linear_insert(i)
+        else:
+            insertion_sort(0, n)
+    return a
+
+
+def voxel_grid(pts, leaf=0.2, std_sort=True):
+    """PCL VoxelGrid (pure Python sums): the (voxel, point) pairs sorted by voxel as std::sort
+    leaves them (std_sort, the reference and the HIP path) or with ties in input order."""
     if len(pts) == 0:
         return np.zeros((0, 4), f32)
     pts = np.asarray(pts, f32)
@@ -122,7 +233,7 @@ def voxel_grid(pts, leaf=0.2):
     div = maxb - minb + 1
     ijk = (np.floor(pts[:, :3] * inv) - minb.astype(f32)).astype(np.int64)
     idx = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
-    order = np.argsort(idx, kind="stable")
+    order = libstdcxx_sort([int(v) for v in idx]) if std_sort else np.argsort(idx, kind="stable")
     out = []
     a = 0
     while a < len(order):
@@ -138,7 +249,8 @@ def voxel_grid(pts, leaf=0.2):
 
 
 def select_features(cloud, off, curv, n_scans):
-    """a6/a7 as pure-Python loops (canonical (curvature, index) order)."""
+    """a6/a7 as pure-Python loops: segment walks in (curvature, index) order, the VoxelGrid in
+    std::sort's order (the oracle's TIES_GPU)."""
     N = cloud.shape[0]
     picked = np.zeros(N, np.int8)
     label = np.zeros(N, np.int8)

@@ -293,3 +293,70 @@ def test_pointcloud2_wire_format_in_out(pkg, oracle, synth, contexts):
             assert np.array_equal(f[:, [0, 1, 2, 4]], ref)
             assert not msg[:, 12:16].any() and not msg[:, 20:].any()
     b.close()
+
+
+@pytest.mark.parametrize("quantum", [0.05, 0.1, 0.2])
+def test_voxel_grid_std_sort_order_heavy_ties(pkg, oracle, synth, contexts, quantum):
+    """The a7 VoxelGrid replays the order libstdc++'s std::sort leaves equal voxels in
+    (PCL VoxelGrid, scanRegistration.cpp:583-586): coordinates snapped to `quantum` put many
+    points of a line into each 0.2 m voxel, so the centroids' summation order (introsort
+    partitions, heap-sort fallback, final insertion sort) decides their float bits.  64 x 1024
+    (register path) plus a doubled-line scan (global-scratch path), bit-exact against the oracle
+    in the reference's VoxelGrid order; the index order (canonical) differs."""
+    ctx = contexts(64, 1024)
+    scans = synth.make_sequence(3, start=70).copy()
+    xyz = scans[..., :3]
+    nz = np.abs(xyz).sum(-1) > 0
+    xyz[nz] = np.round(xyz[nz] / quantum) * quantum
+    b = pkg.Batch(ctx, 3)
+    b.upload(scans)
+    b.extract(3)
+    differs = False
+    for k in range(3):
+        ref = oracle.scan_registration(scans[k])
+        assert_features_equal(pkg, b, k, ref)
+        can = oracle.scan_registration(scans[k], canonical=True).less_flat
+        differs |= can.shape != ref.less_flat.shape or not np.array_equal(can, ref.less_flat)
+    assert differs  # the tie order matters on these inputs
+    b.close()
+    # far points: voxel indices of 2^21 and more (the kernel's dense-numbering path)
+    far = synth.make_sequence(2, start=80).copy()
+    far[..., :3] *= np.float32(25.0)
+    b = pkg.Batch(ctx, 2)
+    b.upload(far)
+    b.extract(2)
+    for k in range(2):
+        assert_features_equal(pkg, b, k, oracle.scan_registration(far[k]))
+    b.close()
+    ctx2 = contexts(16, 1024)
+    s = synth.make_scan(9, 16, 1024).copy()
+    s[8:] = s[:8]
+    nz = np.abs(s[..., :3]).sum(-1) > 0
+    s[..., :3][nz] = np.round(s[..., :3][nz] / quantum) * quantum
+    b = pkg.Batch(ctx2, 1)
+    b.upload(s[None])
+    b.extract(1)
+    assert_features_equal(pkg, b, 0, oracle.scan_registration(s))
+    b.close()
+
+
+def test_tie_order_index_mode(pkg, oracle, synth, contexts):
+    """lislam_set_tie_order(LISLAM_TIES_INDEX): the VoxelGrid sums a voxel's points in input order,
+    bit-exact against the oracle's index-order mode (canonical); the reference order is the
+    default and comes back when set again."""
+    ctx = contexts(64, 1024)
+    scans = synth.make_sequence(2, start=90)
+    try:
+        ctx.set_tie_order(ctx.TIES_INDEX)
+        b = pkg.Batch(ctx, 2)
+        b.upload(scans)
+        b.extract(2)
+        for k in range(2):
+            assert_features_equal(pkg, b, k, oracle.scan_registration(scans[k], canonical=True))
+        ctx.set_tie_order(ctx.TIES_REFERENCE)
+        b.extract(2)
+        for k in range(2):
+            assert_features_equal(pkg, b, k, oracle.scan_registration(scans[k]))
+        b.close()
+    finally:
+        ctx.set_tie_order(ctx.TIES_REFERENCE)

@@ -91,11 +91,32 @@ def test_voxel_grid_vs_python(oracle):
     rng = np.random.default_rng(5)
     pts = rng.uniform(-2, 2, size=(500, 4)).astype(np.float32)
     got = oracle.voxel_grid(pts, 0.2, canonical=True)
-    ref = R.voxel_grid(pts, 0.2)
+    ref = R.voxel_grid(pts, 0.2, std_sort=False)
     assert np.array_equal(got, ref)
-    # non-canonical (PCL std::sort) differs at most in float rounding of centroids
+    # PCL's std::sort order: the oracle's std::sort call == the pure-Python libstdc++ introsort
+    # restatement, bit for bit; it differs from index order only in the centroids' float rounding
     nc = oracle.voxel_grid(pts, 0.2, canonical=False)
+    assert np.array_equal(nc, R.voxel_grid(pts, 0.2, std_sort=True))
     assert nc.shape == ref.shape and np.allclose(nc, ref, atol=1e-6)
+    for n, seed in ((17, 1), (64, 2), (333, 3), (2000, 4)):  # heavy ties: a few voxels
+        p = np.random.default_rng(seed).uniform(-0.3, 0.3, size=(n, 4)).astype(np.float32)
+        assert np.array_equal(oracle.voxel_grid(p, 0.2, canonical=False), R.voxel_grid(p, 0.2, std_sort=True)), n
+
+
+def test_introsort_order_formulation_vs_std_sort():
+    """The prefix-count formulation of std::sort's tie order that the HIP kernels use
+    (lislam_features.hip introsort_order), restated on the host in tests/cpp/introsort_emu.cpp,
+    against std::sort itself on 1360 arrays with heavy ties (and heap-sort fallback inputs)."""
+    import subprocess
+    import tempfile
+
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "introsort_emu.cpp")
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "introsort_emu")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, src], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("introsort ok")
 
 
 def test_nn1_vs_scipy(oracle):
