@@ -656,7 +656,8 @@ __device__ __forceinline__ bool pair_of(const OdomArgs& a, int c, int r, int* k)
 // 8 or more chains, workgroup b serves chain 8 * ((b / 8) / qblocks) + b % 8: workgroups are
 // dealt round-robin over the 8 XCDs, so each XCD's L2 holds the target clouds of only its own
 // chains (placement is a speed matter only).
-__global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int r, int qblocks) {
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_odom_assoc(OdomArgs a, int r, int qblocks) {
   int c, qb;
   if (a.cn >= 8) {
     const int b = blockIdx.x, x = b & 7, rr = b >> 3;
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   if (!pair_of(a, c, r, &k)) return;
   if (a.gate && !a.gate[k]) return;  // not optimized: no association (laserOdometry.cpp:417)
   const int lane = lane_id();
-  const int w = qb * kAssocWaves + (int)(threadIdx.x >> 6);
+  const int w = qb * kW + (int)(threadIdx.x >> 6);
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   if (w >= ns + nf) return;  // whole waves leave; nothing below synchronizes the workgroup
 #ifdef LISLAM_PHASE_PROF
@@ -734,13 +735,266 @@ __global__ __launch_bounds__(64 * kAssocWaves) void k_odom_assoc(OdomArgs a, int
   if (lane == 0) a.blk_kind[(size_t)c * (a.cap_sharp + a.cap_flat) + slot] = found ? (corner ? 0 : 1) : -1;
 #ifdef LISLAM_PHASE_PROF
   if (g_wave_log && r == g_wave_round && lane == 0) {
-    unsigned long long* o = g_wave_log + ((size_t)blockIdx.x * kAssocWaves + (threadIdx.x >> 6)) * 4;
+    unsigned long long* o = g_wave_log + ((size_t)blockIdx.x * kW + (threadIdx.x >> 6)) * 4;
     o[0] = t_start;
     o[1] = __builtin_amdgcn_s_memrealtime();
     o[2] = (unsigned long long)(corner ? 1 : 2) | ((unsigned long long)c << 8) | ((unsigned long long)q << 32);
     o[3] = (unsigned long long)nL;
   }
 #endif
+}
+
+// ------------------------------------------------------------------ 16-lane association
+// The same exact searches as k_odom_assoc with one query per 16-lane row, four queries per wave:
+// a round trip looks at one 16-point chunk per query (lane r = lane & 15 takes point r of it),
+// and the lexicographic minima are row reductions by DPP inside the row.  The four rows advance
+// in lockstep; a row with nothing left to do contributes the identity, so every lane is active at
+// every reduction.  Results are the same by construction: 1-NN = lexicographic min (distance,
+// original index) over the points with d < 25, chunks skipped only when their float bound is
+// above the row's best distance; line searches = the first strict improvement along the
+// reference's walk (distance, walk rank), over chunks up to the one where the walk breaks.
+template <int kCtrl>
+__device__ __forceinline__ dkey dpp_dkey(dkey v) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), kCtrl, 0xf, 0xf, true);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, kCtrl, 0xf, 0xf, true);
+  return ((dkey)hi << 32) | lo;
+}
+// minimum over the 16 lanes of the row (quad xor 1, xor 2, half-row mirror, row mirror)
+__device__ __forceinline__ dkey row_min(dkey v) {
+  v = dmin(v, dpp_dkey<0xB1>(v));
+  v = dmin(v, dpp_dkey<0x4E>(v));
+  v = dmin(v, dpp_dkey<0x141>(v));
+  v = dmin(v, dpp_dkey<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t row_bits(uint64_t m) { return (uint32_t)(m >> (lane_id() & 48)) & 0xffffu; }
+
+// Best-first over the 16 chunks of super-chunk u (u < 0: the row takes no part), the two
+// smallest pending bounds per round trip (evaluating a chunk too many never changes a minimum).
+__device__ __forceinline__ void nn16_super(const P4* sorted, int n, int nch, const float4* chm, int u, const P4& q,
+                                           dkey& best) {
+  const int lr = lane_id() & 15;
+  const int c = u * kChunk + lr;
+  bool cp = u >= 0 && c < nch;
+  float clb = 3.4e38f;
+  if (cp) clb = box_lb(ldg(chm + 2 * c), ldg(chm + 2 * c + 1), q);
+  for (;;) {
+    const bool cand = cp && !(clb > dk_d(best));
+    const dkey m1 = row_min(cand ? dk(clb, lr) : kIdent);
+    const bool ev1 = m1 != kIdent;
+    if (!__ballot(ev1)) break;
+    const int p1 = ev1 ? dk_key(m1) : -1;
+    const dkey m2 = row_min(cand && lr != p1 ? dk(clb, lr) : kIdent);
+    const bool ev2 = m2 != kIdent;
+    const int p2 = ev2 ? dk_key(m2) : -1;
+    if (lr == p1 || lr == p2) cp = false;
+    const int j1 = (u * kChunk + p1) * kChunk + lr, j2 = (u * kChunk + p2) * kChunk + lr;
+    const bool ok1 = ev1 && j1 < n, ok2 = ev2 && j2 < n;
+    const P4 a1 = ld4(sorted + (ok1 ? j1 : 0)), a2 = ld4(sorted + (ok2 ? j2 : 0));
+    const float d1 = d2f(q, a1), d2 = d2f(q, a2);
+    const dkey v = dmin(ok1 && d1 < 25.f ? dk(d1, __float_as_int(a1.i)) : kIdent,
+                        ok2 && d2 < 25.f ? dk(d2, __float_as_int(a2.i)) : kIdent);
+    best = dmin(best, row_min(v));
+  }
+}
+
+// Exact 1-NN (d < 25) of the row's query in the Morton-ordered copy; -1 = none.
+__device__ __forceinline__ int nn16(const P4* sorted, int n, const float4* chm, const float4* sum, const P4& q,
+                                    bool act) {
+  const int lr = lane_id() & 15;
+  const int nch = (n + kChunk - 1) / kChunk, nsu = act && n > 0 ? (nch + kChunk - 1) / kChunk : 0;
+  dkey ub = kIdent;
+  float slb[4];  // window 0: this lane's super-chunks lr + 16 kk, kept for the visits below
+  const int kmax = (int)wave_umax((uint32_t)((nsu + 15) >> 4));
+#pragma unroll
+  for (int kk = 0; kk < 4; kk++) slb[kk] = 3.4e38f;
+  for (int k = 0; k < kmax; k++) {
+    const int u = lr + 16 * k;
+    if (u < nsu) {
+      const float lb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
+      ub = dmin(ub, dk(lb, u));
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++)
+        if (k == kk) slb[kk] = lb;
+    }
+  }
+  ub = row_min(ub);
+  const bool go = nsu > 0 && dk_d(ub) < 25.f;
+  const int u0 = go ? dk_key(ub) : -1;
+  dkey best = dk(25.f, kNone);
+  nn16_super(sorted, n, nch, chm, u0, q, best);
+  // the other super-chunks, 64 per window (four per lane), in bound order while <= best
+  const int wmax = (int)wave_umax((uint32_t)(go ? (nsu + 63) >> 6 : 0));
+  for (int win = 0; win < wmax; win++) {
+    bool sp[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      const int u = win * 64 + kk * 16 + lr;
+      sp[kk] = go && u < nsu && u != u0;
+      if (win > 0) slb[kk] = sp[kk] ? box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q) : 3.4e38f;
+    }
+    for (;;) {
+      dkey m = kIdent;
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++)
+        if (sp[kk] && !(slb[kk] > dk_d(best))) m = dmin(m, dk(slb[kk], win * 64 + kk * 16 + lr));
+      m = row_min(m);
+      const bool want = m != kIdent;
+      if (!__ballot(want)) break;
+      const int uu = want ? dk_key(m) : -1;
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++)
+        if (want && uu == win * 64 + kk * 16 + lr) sp[kk] = false;
+      nn16_super(sorted, n, nch, chm, uu, q, best);
+    }
+  }
+  const int bi = dk_key(best);
+  return bi == kNone ? -1 : bi;
+}
+
+// Does a chunk with label range [lmin, lmax] and bound lb still need a visit?
+__device__ __forceinline__ bool ls16_need(bool corner, bool up, int lmin, int lmax, int cid, float lb, float b2,
+                                          float b3) {
+  if (corner) return (up ? lmax > cid : lmin < cid) && !(lb > b2);
+  const bool n2 = (up ? lmin <= cid : lmax >= cid) && !(lb > b2);
+  const bool n3 = (up ? lmax > cid : lmin < cid) && !(lb > b3);
+  return n2 || n3;
+}
+
+// The scan-line searches of the row (corner: b2; surf: b2, b3) around `closest` in the target
+// cloud L (scan-line order, labels non-decreasing), windows of 16 chunks up and down.
+__device__ __forceinline__ void ls16(const P4* L, const float4* chm, int n, int closest, int cid, const P4& sel,
+                                     bool corner, bool act, dkey& b2, dkey& b3) {
+  const int lr = lane_id() & 15;
+  const int nch = (n + kChunk - 1) / kChunk;
+  const int hc = act ? closest / kChunk : 0;
+  bool up_open = act, dn_open = act;
+  for (int win = 0;; win++) {
+    const int cu = hc + 16 * win + lr, cd = hc - 16 * win - lr;
+    const bool uin = up_open && cu < nch, din = dn_open && cd >= 0;
+    if (!__ballot(uin || din)) break;
+    float4 ulo = make_float4(0.f, 0.f, 0.f, 0.f), uhi = ulo, dlo = ulo, dhi = ulo;
+    if (uin) { ulo = ldg(chm + 2 * cu); uhi = ldg(chm + 2 * cu + 1); }
+    if (din) { dlo = ldg(chm + 2 * cd); dhi = ldg(chm + 2 * cd + 1); }
+    // the first chunk holding a label past the nearby range is where that walk breaks
+    const uint32_t ufl = row_bits(__ballot(uin && (int)uhi.w > cid + 2));
+    const uint32_t dfl = row_bits(__ballot(din && (int)dlo.w < cid - 2));
+    const int ulast = ufl ? (int)__builtin_ctz(ufl) : 15, dlast = dfl ? (int)__builtin_ctz(dfl) : 15;
+    bool upend = uin && lr <= ulast, dpend = din && lr <= dlast;
+    const float ulb = upend ? box_lb(ulo, uhi, sel) : 3.4e38f, dlb = dpend ? box_lb(dlo, dhi, sel) : 3.4e38f;
+    for (;;) {
+      const float bd2 = dk_d(b2), bd3 = dk_d(b3);
+      const bool nu = upend && ls16_need(corner, true, (int)ulo.w, (int)uhi.w, cid, ulb, bd2, bd3);
+      const bool nd = dpend && ls16_need(corner, false, (int)dlo.w, (int)dhi.w, cid, dlb, bd2, bd3);
+      const dkey cu1 = nu ? dk(ulb, 2 * lr) : kIdent, cd1 = nd ? dk(dlb, 2 * lr + 1) : kIdent;
+      const dkey m1 = row_min(dmin(cu1, cd1));
+      const bool ev1 = m1 != kIdent;
+      if (!__ballot(ev1)) break;
+      const int k1 = ev1 ? dk_key(m1) : -1;
+      const dkey m2 = row_min(dmin(2 * lr == k1 ? kIdent : cu1, 2 * lr + 1 == k1 ? kIdent : cd1));
+      const bool ev2 = m2 != kIdent;
+      const int k2 = ev2 ? dk_key(m2) : -1;
+      if (k1 == 2 * lr || k2 == 2 * lr) upend = false;
+      if (k1 == 2 * lr + 1 || k2 == 2 * lr + 1) dpend = false;
+      dkey v2 = kIdent, v3 = kIdent;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const bool ev = h == 0 ? ev1 : ev2;
+        const int key = h == 0 ? k1 : k2;
+        const bool up = (key & 1) == 0;
+        const int pl = key >> 1;
+        const int c = up ? hc + 16 * win + pl : hc - 16 * win - pl;
+        const int j = c * kChunk + lr;
+        const bool valid = ev && j >= 0 && j < n && (up ? j > closest : j < closest);
+        const P4 p = ld4(L + (valid ? j : 0));
+        const int pid = int(p.i);
+        // the walk's break inside this chunk: up, the first point past cid + 2; down, the last below cid - 2
+        const uint32_t bm = row_bits(__ballot(valid && (up ? pid > cid + 2 : pid < cid - 2)));
+        bool v = valid;
+        if (bm) v = v && (up ? lr < (int)__builtin_ctz(bm) : lr > 31 - (int)__builtin_clz(bm));
+        const float d = d2f(sel, p);
+        const int rk = up ? j - closest : n + closest - j;
+        if (v && d < 25.f) {
+          if (corner) {
+            if (up ? pid > cid : pid < cid) v2 = dmin(v2, dk(d, rk));
+          } else {
+            if (up ? pid <= cid : pid >= cid) v2 = dmin(v2, dk(d, rk));
+            else v3 = dmin(v3, dk(d, rk));
+          }
+        }
+      }
+      b2 = dmin(b2, row_min(v2));
+      b3 = dmin(b3, row_min(v3));
+    }
+    up_open = up_open && !ufl;
+    dn_open = dn_open && !dfl;
+  }
+}
+
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_odom_assoc16(OdomArgs a, int r, int qblocks) {
+  int c, qb;
+  if (a.cn >= 8) {
+    const int b = blockIdx.x, x = b & 7, rr = b >> 3;
+    c = 8 * (rr / qblocks) + x;
+    qb = rr % qblocks;
+  } else {
+    c = blockIdx.x / qblocks;
+    qb = blockIdx.x % qblocks;
+  }
+  if (c >= a.cn) return;
+  c += a.c0;
+  int k;
+  if (!pair_of(a, c, r, &k)) return;
+  if (a.gate && !a.gate[k]) return;  // not optimized: no association (laserOdometry.cpp:417)
+  const int lane = lane_id(), lr = lane & 15;
+  const int w = (qb * kW + (int)(threadIdx.x >> 6)) * 4 + (lane >> 4);  // this row's query
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  if (__ballot(w < ns + nf) == 0ull) return;  // whole waves leave; nothing below synchronizes the workgroup
+  const bool has = w < ns + nf;
+  const bool corner = w < ns;
+  const int t = corner ? w : w - ns;
+  const P4 qp = has ? ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
+                                 : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t)
+                    : P4{0.f, 0.f, 0.f, 0.f};
+  const int q = __float_as_int(qp.i);
+  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
+  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
+  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
+  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
+  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
+  double x[7];
+  const double* st = a.state + (size_t)c * 16;
+  for (int e = 0; e < 7; e++) x[e] = st[e];
+  const P4 cur{qp.x, qp.y, qp.z, 0.f};
+  const P4 sel = transform_to_start(cur, x);
+  const int closest = nn16(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, has);
+  const bool act = has && closest >= 0;
+  const P4 pa = ld4(L + (act ? closest : 0));
+  const int cid = act ? int(pa.i) : 0;
+  dkey b2 = dk(25.f, kNone), b3 = dk(25.f, kNone);
+  ls16(L, ix.chunk + mo, nL, act ? closest : 0, cid, sel, corner, act, b2, b3);
+  auto idx_of = [&](dkey b) { const int kk = dk_key(b); return kk < nL ? closest + kk : closest - (kk - nL); };
+  bool found = false;
+  double v = 0.0;  // this lane's record entry (lanes 0..8 of the row)
+  if (act && corner && dk_key(b2) != kNone) {  // LidarEdgeFactor(curr, a, b)
+    const P4 pb = ld4(L + idx_of(b2));
+    const float e9[9] = {cur.x, cur.y, cur.z, pa.x, pa.y, pa.z, pb.x, pb.y, pb.z};
+    for (int e = 0; e < 9; e++) if (lr == e) v = e9[e];
+    found = true;
+  } else if (act && !corner && dk_key(b2) != kNone && dk_key(b3) != kNone) {  // LidarPlaneFactor(curr, j, l, m)
+    const P4 pl = ld4(L + idx_of(b2)), pm = ld4(L + idx_of(b3));
+    const D3 j{pa.x, pa.y, pa.z};
+    const D3 nrm = plane_normal(j, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
+    const double e9[9] = {cur.x, cur.y, cur.z, j.x, j.y, j.z, nrm.x, nrm.y, nrm.z};
+    for (int e = 0; e < 9; e++) if (lr == e) v = e9[e];
+    found = true;
+  }
+  if (!has) return;
+  const int slot = corner ? q : a.cap_sharp + q;
+  double* rec = a.blk + ((size_t)c * (a.cap_sharp + a.cap_flat) + slot) * 9;
+  if (found && lr < 9) rec[lr] = v;
+  if (lr == 0) a.blk_kind[(size_t)c * (a.cap_sharp + a.cap_flat) + slot] = found ? (corner ? 0 : 1) : -1;
 }
 
 // ------------------------------------------------------------------ phase 2: LM solve
@@ -1021,7 +1275,13 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
     (void)hipEventRecord(fork, st);
     for (int g = 1; g < G; g++) (void)hipStreamWaitEvent(streams[g], fork, 0);
   }
-  const int qblocks = (a0.cap_sharp + a0.cap_flat + kAssocWaves - 1) / kAssocWaves;
+  // queries (waves) per association workgroup: LISLAM_ASSOC_WAVES = 1, 2 (default) or 4
+  static const int kw_env = getenv("LISLAM_ASSOC_WAVES") ? atoi(getenv("LISLAM_ASSOC_WAVES")) : 2;
+  const int kw = (kw_env == 1 || kw_env == 2) ? kw_env : 4;
+  const int qblocks = (a0.cap_sharp + a0.cap_flat + kw - 1) / kw;
+  // LISLAM_ASSOC16 = 0 selects the one-query-per-wave kernel; default: four queries per wave
+  static const bool rows16 = !(getenv("LISLAM_ASSOC16") && atoi(getenv("LISLAM_ASSOC16")) == 0);
+  const int qblocks16 = (a0.cap_sharp + a0.cap_flat + 8 - 1) / 8;  // 2 waves x 4 rows
   const int rounds = min(a0.chain_len, a0.S - 1);
   auto timed = [&](int kernel, hipStream_t s, auto&& launch) {
     hipEvent_t b = nullptr, e = nullptr;
@@ -1039,7 +1299,10 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
         const hipStream_t s = streams[g];
         const int cb = a.cn >= 8 ? (a.cn + 7) / 8 * 8 : a.cn;
         timed(4, s, [&] {
-          hipLaunchKernelGGL(k_odom_assoc, dim3(qblocks * cb), dim3(64 * kAssocWaves), 0, s, a, r, qblocks);
+          if (rows16) hipLaunchKernelGGL(k_odom_assoc16<2>, dim3(qblocks16 * cb), dim3(128), 0, s, a, r, qblocks16);
+          else if (kw == 1) hipLaunchKernelGGL(k_odom_assoc<1>, dim3(qblocks * cb), dim3(64), 0, s, a, r, qblocks);
+          else if (kw == 2) hipLaunchKernelGGL(k_odom_assoc<2>, dim3(qblocks * cb), dim3(128), 0, s, a, r, qblocks);
+          else hipLaunchKernelGGL(k_odom_assoc<4>, dim3(qblocks * cb), dim3(256), 0, s, a, r, qblocks);
         });
         timed(5, s, [&] { hipLaunchKernelGGL(k_odom_lm, dim3(a.cn), dim3(kLmThreads), 0, s, a, r, outer); });
       }
