@@ -365,9 +365,9 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
     o.init_state = b->d_init;
   }
-  // chain groups: LISLAM_ODOM_GROUPS (default 1) streams, so one group's solves overlap another's
+  // chain groups: LISLAM_ODOM_GROUPS (default 2) streams, so one group's solves overlap another's
   // association (a solve occupies one workgroup per chain, far from filling the device)
-  static const int groups_env = getenv("LISLAM_ODOM_GROUPS") ? atoi(getenv("LISLAM_ODOM_GROUPS")) : 1;
+  static const int groups_env = getenv("LISLAM_ODOM_GROUPS") ? atoi(getenv("LISLAM_ODOM_GROUPS")) : 2;
   const int G = std::max(1, std::min(groups_env, (int)lislam_batch::kMaxGroups));
   b->odo_stream[0] = c->stream;
   for (int g = 1; g < G; g++) {

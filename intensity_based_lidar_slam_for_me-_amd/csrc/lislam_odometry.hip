@@ -149,12 +149,22 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
   const int n = a.n_feat[s * 4 + (which == 0 ? 1 : which == 1 ? 3 : which == 2 ? 0 : 2)];
   if (!query) chunk_boxes(pts, n, true, ix.chunk + (size_t)s * ix.nchunk * 2, ix.super + (size_t)s * ix.nsuper * 2);
   if (n == 0) return;
-  // cloud AABB
+  // cloud AABB: from the super-chunk boxes just written (targets), from the points (queries)
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  for (int j = threadIdx.x; j < n; j += 64 * kW) {
-    const float4 p = ldg(pts + j);
-    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  if (!query) {
+    const float4* sb = ix.super + (size_t)s * ix.nsuper * 2;
+    const int nsu = ((n + kChunk - 1) / kChunk + kChunk - 1) / kChunk;
+    for (int u = threadIdx.x; u < nsu; u += 64 * kW) {
+      const float4 l = ldg(sb + 2 * u), h = ldg(sb + 2 * u + 1);
+      mn[0] = fminf(mn[0], l.x); mn[1] = fminf(mn[1], l.y); mn[2] = fminf(mn[2], l.z);
+      mx[0] = fmaxf(mx[0], h.x); mx[1] = fmaxf(mx[1], h.y); mx[2] = fmaxf(mx[2], h.z);
+    }
+  } else {
+    for (int j = threadIdx.x; j < n; j += 64 * kW) {
+      const float4 p = ldg(pts + j);
+      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+    }
   }
   for (int d = 0; d < 3; d++)
     for (int o = 32; o > 0; o >>= 1) {
@@ -215,12 +225,65 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     return;
   }
   float4* sorted = ix.sorted + (size_t)s * ix.cap;
-  emit([&](int i, int o) {
-    const float4 p = ldg(pts + o);
-    stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
-  });
-  __syncthreads();
-  chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
+  if (!in_regs) {
+    emit([&](int i, int o) {
+      const float4 p = ldg(pts + o);
+      stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+    });
+    __syncthreads();
+    chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
+    return;
+  }
+  // Registers: sorted position i = 1024 wave + 64 t + lane, so a chunk (16 positions) is a 16-lane
+  // row of one slot and a super-chunk (256) is the four slots t = 4 v .. 4 v + 3 of one wave:
+  // both boxes are reduced from the gathered points without reading the sorted copy back.
+  float4* nch_out = ix.nn_chunk + (size_t)s * ix.nchunk * 2;
+  float4* nsu_out = ix.nn_super + (size_t)s * ix.nsuper * 2;
+  auto rmin = [](float v) {
+    v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, true)));
+    v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, true)));
+    v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, true)));
+    return fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, true)));
+  };
+  float slo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, shi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};  // super box (row leaders)
+#pragma unroll
+  for (int t = 0; t < kKeysPerLane; t++) {
+    const int i = wave * 1024 + t * 64 + lane;
+    float4 p = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 0.f);
+    float q[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    if (i < n) {
+      const int o = (int)(uint32_t)key[t];
+      p = ldg(pts + o);
+      stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+      q[0] = p.x; q[1] = p.y; q[2] = p.z;
+    }
+    const float lo0 = rmin(p.x), lo1 = rmin(p.y), lo2 = rmin(p.z);
+    const float hi0 = -rmin(-q[0]), hi1 = -rmin(-q[1]), hi2 = -rmin(-q[2]);
+    const int c = i >> 4;  // chunk of this row
+    if ((lane & 15) == 0 && i < n) {
+      stg4(nch_out + 2 * c, make_float4(lo0, lo1, lo2, 0.f));
+      stg4(nch_out + 2 * c + 1, make_float4(hi0, hi1, hi2, 0.f));
+    }
+    slo[0] = fminf(slo[0], lo0); slo[1] = fminf(slo[1], lo1); slo[2] = fminf(slo[2], lo2);
+    shi[0] = fmaxf(shi[0], hi0); shi[1] = fmaxf(shi[1], hi1); shi[2] = fmaxf(shi[2], hi2);
+    if ((t & 3) == 3) {  // super-chunk (wave * 4 + t / 4): combine the four row leaders 0, 16, 32, 48
+      float r[6] = {slo[0], slo[1], slo[2], -shi[0], -shi[1], -shi[2]};
+#pragma unroll
+      for (int e = 0; e < 6; e++) {
+        float v = r[e];
+        v = fminf(v, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (16 << 10) | 0x1f)));  // lane ^ 16
+        v = fminf(v, __shfl_xor(v, 32));
+        r[e] = v;
+      }
+      const int u = (wave * 1024 + (t - 3) * 64) >> 8;
+      if (lane == 0 && u * kSuper < n) {
+        stg4(nsu_out + 2 * u, make_float4(r[0], r[1], r[2], 0.f));
+        stg4(nsu_out + 2 * u + 1, make_float4(-r[3], -r[4], -r[5], 0.f));
+      }
+      slo[0] = slo[1] = slo[2] = 3.4e38f;
+      shi[0] = shi[1] = shi[2] = -3.4e38f;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ association helpers
