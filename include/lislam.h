@@ -321,11 +321,23 @@ int lislam_voxel_grid(lislam_ctx* ctx, const float* pts, int32_t n, float leaf, 
  * out_pose = q_w_curr, t_w_curr; summary[3] = planes, iterations, termination (-1: built). */
 int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const double* odom, double* state,
                        double* out_pose, int32_t* summary);
+/* The same stage with mapOptimization's corner ikd-Tree (corner_ikdtree_, KD_TREE(0.3, 0.6, 0.8),
+ * mapOptimization.cpp:195,479,505): the sensor-frame corner cloud (pc_corner, stride 4) goes in
+ * at the ground cloud's keyframe pose, Build while that tree is empty, else Add_Points with
+ * downsampling (create corner_map with downsample_size 0.8).  corner_map may be null. */
+int lislam_mapopt_step_corner(lislam_map* m, lislam_map* corner_map, const float* ground, int32_t n,
+                              const float* corner, int32_t nc, const double* odom, double* state, double* out_pose,
+                              int32_t* summary);
 /* The same stage fed from a batch without a host round trip: GroundPointOut of `scan`
  * (lislam_batch_ground) followed by its less-flat cloud, concatenated on the device
  * (mapOptimization.cpp:136-150).  The map's context must be the batch's. */
 int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
                         double* out_pose, int32_t* summary);
+/* As lislam_batch_mapopt, with mapOptimization's corner ikd-Tree (corner_map, see
+ * lislam_mapopt_step_corner) fed the scan's less-sharp cloud (/laser_cloud_less_sharp, the
+ * pc_corner topic, mapOptimizationNode.cpp:63). corner_map NULL = lislam_batch_mapopt. */
+int lislam_batch_mapopt_corner(lislam_batch* b, lislam_map* m, lislam_map* corner_map, int32_t scan,
+                               const double* odom, double* state, double* out_pose, int32_t* summary);
 /* laserMapping::process optimization (laserMapping.cpp:620-850) against a corner map and a surf
  * map: the downsampled current corner / surf clouds (stride 4), pose x (in/out), two outer
  * passes of association + Ceres(4 it).  stats[4] = corner / surf blocks of each pass. */

@@ -267,22 +267,37 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
 // device (the 4th field is not read by the ground-map stage), then lislam_mapopt_step.
 int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
                         double* out_pose, int32_t* summary) {
+  return lislam_batch_mapopt_corner(b, m, nullptr, scan, odom, state, out_pose, summary);
+}
+
+// With the corner ikd-Tree: pc_corner is the scan's less-sharp cloud (/laser_cloud_less_sharp,
+// mapOptimizationNode.cpp:63), staged behind the plane cloud in the same device buffer.
+int lislam_batch_mapopt_corner(lislam_batch* b, lislam_map* m, lislam_map* cm, int32_t scan, const double* odom,
+                               double* state, double* out_pose, int32_t* summary) {
   if (!b || !m || !odom || !state || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   const void *g = nullptr, *lf = nullptr;
   int ng = 0, nlf = 0;
   size_t eg = 0, elf = 0;
+  const void* ls = nullptr;
+  int nls = 0;
+  size_t els = 0;
   int rc = output_source(b, LISLAM_OUT_GROUND, scan, &g, &ng, &eg);
   if (rc) return rc;
   if ((rc = output_source(b, LISLAM_OUT_LESS_FLAT, scan, &lf, &nlf, &elf))) return rc;
-  const size_t bytes = (size_t)(ng + nlf) * 16;
+  if (cm && (rc = output_source(b, LISLAM_OUT_LESS_SHARP, scan, &ls, &nls, &els))) return rc;
+  const size_t bytes = (size_t)(ng + nlf + nls) * 16;
   if ((rc = rc_wire(b, std::max<size_t>(bytes, 16)))) return fail(c, rc, "lislam_batch_mapopt: staging allocation");
   uint8_t* dst = static_cast<uint8_t*>(b->wire);
   if (ng) HIPCHK(c, hipMemcpyAsync(dst, g, (size_t)ng * 16, hipMemcpyDeviceToDevice, c->stream));
   if (nlf) HIPCHK(c, hipMemcpyAsync(dst + (size_t)ng * 16, lf, (size_t)nlf * 16, hipMemcpyDeviceToDevice, c->stream));
+  if (nls)
+    HIPCHK(c, hipMemcpyAsync(dst + (size_t)(ng + nlf) * 16, ls, (size_t)nls * 16, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return lislam_mapopt_step(m, reinterpret_cast<const float*>(dst), ng + nlf, odom, state, out_pose, summary);
+  return lislam_mapopt_step_corner(m, cm, reinterpret_cast<const float*>(dst), ng + nlf,
+                                   reinterpret_cast<const float*>(dst + (size_t)(ng + nlf) * 16), nls, odom, state,
+                                   out_pose, summary);
 }
 
 int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,

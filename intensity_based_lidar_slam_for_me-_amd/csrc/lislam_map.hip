@@ -1518,7 +1518,40 @@ int lislam_voxel_grid(lislam_ctx* c, const float* pts, int32_t n, float leaf, fl
 
 int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const double* odom, double* state,
                        double* out_pose, int32_t* summary) {
-  if (!m || n < 0 || (n > 0 && !ground) || !odom || !state) return LISLAM_ERR_ARG;
+  return lislam_mapopt_step_corner(m, nullptr, ground, n, nullptr, 0, odom, state, out_pose, summary);
+}
+
+// pc_corner into the corner ikd-Tree at the keyframe pose (device pose): Build while the tree is
+// empty (mapOptimization.cpp:193-195), else Add_Points(downsample) (:477-479).
+static int corner_map_update(lislam_map* cm, const float* corner, int nc, const double* pose) {
+  lislam_ctx* c = cm->ctx;
+  hipStream_t st = stream_of(c);
+  MapScratch& sc = cm->sc;
+  MRC(stage_points(c, sc, sc.vout, corner, nc, 4));
+  MCHK(c, sc.vin.reserve((size_t)std::max(nc, 1) * 16));
+  hipLaunchKernelGGL(k_transform, dim3(blocks(nc)), dim3(256), 0, st, sc.vout.as<float>(), 4, (const int*)nullptr, nc,
+                     pose, sc.vin.as<float>());
+  if (cm->n == 0) {
+    MCHK(c, cm->tmp.reserve((size_t)std::max(nc, 1) * 16));
+    hipLaunchKernelGGL(k_pack_points, dim3(blocks(nc)), dim3(256), 0, st, sc.vin.as<float>(), nc, 4, 0, cm->tmp.as<float4>());
+    cm->next_id = nc;
+    MRC(rebuild(cm, nc));
+  } else {
+    MCHK(c, cm->newp.reserve((size_t)std::max(nc, 1) * 16));
+    hipLaunchKernelGGL(k_pack_points, dim3(blocks(nc)), dim3(256), 0, st, sc.vin.as<float>(), nc, 4, cm->next_id,
+                       cm->newp.as<float4>());
+    cm->next_id += nc;
+    MRC(add_packed(cm, nc, true, nullptr));
+  }
+  MCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+int lislam_mapopt_step_corner(lislam_map* m, lislam_map* cm, const float* ground, int32_t n, const float* corner,
+                              int32_t nc, const double* odom, double* state, double* out_pose, int32_t* summary) {
+  if (!m || n < 0 || (n > 0 && !ground) || !odom || !state || nc < 0 || (nc > 0 && !corner) ||
+      (cm && (cm->ctx != m->ctx || cm == m)))
+    return LISLAM_ERR_ARG;
   lislam_ctx* c = m->ctx;
   hipSetDevice(c->device);
   MapScratch& sc = m->sc;
@@ -1539,6 +1572,7 @@ int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const doub
     hipLaunchKernelGGL(k_pack_points, dim3(blocks(n)), dim3(256), 0, st, sc.vin.as<float>(), n, 4, 0, m->tmp.as<float4>());
     m->next_id = n;
     MRC(rebuild(m, n));
+    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 16));
     MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
   } else {
     // VoxelGrid(0.8) (:368-370) of the xyz cloud (PointXYZ: intensity lane zeroed)
@@ -1575,6 +1609,7 @@ int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const doub
                        m->newp.as<float4>());
     m->next_id += hn;
     MRC(add_packed(m, hn, true, nullptr));
+    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 24));  // the same keyframe pose as the ground cloud
     MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
     MCHK(c, hipMemcpyAsync(state, dp, 56, hipMemcpyDefault, st));
   }

@@ -134,22 +134,32 @@ def voxel_grid(ctx, points, leaf: float) -> np.ndarray:
 
 class MapOptimization:
     """Ground-map stage of the mapOptimization node (ikd-Tree map of downsample 0.4,
-    mapOptimization.cpp:504)."""
+    mapOptimization.cpp:504) and, with corner=True, its corner ikd-Tree (downsample 0.8,
+    :505), which takes pc_corner at the same keyframe pose (:193-195, :477-479)."""
 
-    def __init__(self, ctx, downsample_size: float = 0.4, cell_size: float = 0.0):
+    def __init__(self, ctx, downsample_size: float = 0.4, cell_size: float = 0.0, corner: bool = False,
+                 corner_downsample: float = 0.8):
         self.map = IkdMap(ctx, downsample_size, cell_size)
+        self.corner_map = IkdMap(ctx, corner_downsample, cell_size) if corner else None
         self.state = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)  # q_wmap_wodom, t_wmap_wodom
 
-    def callback(self, ground, odom):
-        """One frame: ground = GroundPointOut (sensor frame, (n, 4)), odom = q_wodom_curr, t_wodom_curr.
+    def callback(self, ground, odom, pc_corner=None):
+        """One frame: ground = GroundPointOut (sensor frame, (n, 4)), odom = q_wodom_curr, t_wodom_curr,
+        pc_corner = the corner cloud (sensor frame, (m, 4); with corner=True).
         Returns (q_w_curr, t_w_curr (7,), summary (planes, iterations, termination; -1 = built))."""
         g = np.ascontiguousarray(ground, np.float32).reshape(-1, 4)
         od = np.ascontiguousarray(odom, np.float64)
         pose = np.zeros(7)
         summ = np.zeros(3, np.int32)
         ctx = self.map.ctx
-        nat.check(ctx.lib.lislam_mapopt_step(self.map.h, nat.ptr(g), g.shape[0], nat.ptr(od), nat.ptr(self.state),
-                                             nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_mapopt_step")
+        if self.corner_map is None:
+            nat.check(ctx.lib.lislam_mapopt_step(self.map.h, nat.ptr(g), g.shape[0], nat.ptr(od), nat.ptr(self.state),
+                                                 nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_mapopt_step")
+            return pose, summ
+        c = np.ascontiguousarray(pc_corner if pc_corner is not None else np.zeros((0, 4)), np.float32).reshape(-1, 4)
+        nat.check(ctx.lib.lislam_mapopt_step_corner(self.map.h, self.corner_map.h, nat.ptr(g), g.shape[0], nat.ptr(c),
+                                                    c.shape[0], nat.ptr(od), nat.ptr(self.state), nat.ptr(pose),
+                                                    nat.ptr(summ)), ctx.h, "lislam_mapopt_step_corner")
         return pose, summ
 
     def laser_odometry_handler(self, odom) -> np.ndarray:
@@ -171,14 +181,21 @@ class MapOptimization:
 
     def callback_batch(self, batch, scan: int, odom):
         """The same frame fed from a batch on the device: GroundPointOut of `scan` (batch.ground
-        first) + its less-flat cloud, as mapOptimizationCallback assembles them (:136-150)."""
+        first) + its less-flat cloud, as mapOptimizationCallback assembles them (:136-150); with
+        corner=True the scan's less-sharp cloud is pc_corner (mapOptimizationNode.cpp:63)."""
         od = np.ascontiguousarray(odom, np.float64)
         pose = np.zeros(7)
         summ = np.zeros(3, np.int32)
         ctx = self.map.ctx
-        nat.check(ctx.lib.lislam_batch_mapopt(batch.h, self.map.h, scan, nat.ptr(od), nat.ptr(self.state),
-                                              nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_batch_mapopt")
+        cm = self.corner_map.h if self.corner_map is not None else None
+        nat.check(ctx.lib.lislam_batch_mapopt_corner(batch.h, self.map.h, cm, scan, nat.ptr(od), nat.ptr(self.state),
+                                                     nat.ptr(pose), nat.ptr(summ)), ctx.h, "lislam_batch_mapopt_corner")
         return pose, summ
+
+    def close(self):
+        self.map.close()
+        if self.corner_map is not None:
+            self.corner_map.close()
 
 
 def laser_mapping(corner_map: IkdMap, surf_map: IkdMap, corner, surf, x0):

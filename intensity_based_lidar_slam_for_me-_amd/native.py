@@ -34,12 +34,12 @@ EXPORTED_SYMBOLS = (
     "lislam_batch_download", "lislam_eval_factors", "lislam_eval_factors_raw", "lislam_set_tie_order",
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
     "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
-    "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_laser_mapping",
+    "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_mapopt_step_corner", "lislam_laser_mapping",
     "lislam_map_set_timing", "lislam_map_kernel_times",
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
     "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
     "lislam_lmap_create", "lislam_lmap_destroy", "lislam_lmap_step", "lislam_lmap_counts", "lislam_lmap_points",
-    "lislam_batch_odometry_gated", "lislam_odom_step_gated", "lislam_batch_mapopt", "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
+    "lislam_batch_odometry_gated", "lislam_odom_step_gated", "lislam_batch_mapopt", "lislam_batch_mapopt_corner", "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
 )
 
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
@@ -160,6 +160,7 @@ def load(path: str = LIB_PATH):
     L.lislam_pose_solve.argtypes = [vp, vp, vp, _i32, vp, _i32, vp]
     L.lislam_voxel_grid.argtypes = [vp, vp, _i32, ctypes.c_float, vp, _i32p]
     L.lislam_mapopt_step.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
+    L.lislam_mapopt_step_corner.argtypes = [vp, vp, vp, _i32, vp, _i32, vp, vp, vp, vp]
     L.lislam_laser_mapping.argtypes = [vp, vp, vp, _i32, vp, _i32, vp, vp]
     L.lislam_orb_detect.argtypes = [vp, vp, vp, vp, _i32, _i32, _i32, vp, vp, vp, _i32, _i32p]
     L.lislam_orb_match.argtypes = [vp, vp, _i32, vp, _i32, vp, _i32p]
@@ -177,6 +178,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_odometry_gated.argtypes = [vp, _i32, _i32, vp]
     L.lislam_odom_step_gated.argtypes = [vp, vp, _i32, vp, vp, vp]
     L.lislam_batch_mapopt.argtypes = [vp, vp, _i32, vp, vp, vp, vp]
+    L.lislam_batch_mapopt_corner.argtypes = [vp, vp, vp, _i32, vp, vp, vp, vp]
     L.lislam_loop_icp.argtypes = [vp, ctypes.POINTER(IcpConfig), vp, _i32, vp, vp, vp, _i32, vp, vp, vp, vp, vp]
     L.lislam_odom_fuser_create.argtypes = [vp, ctypes.POINTER(vp)]
     L.lislam_odom_fuser_destroy.argtypes = [vp]

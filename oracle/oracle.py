@@ -54,6 +54,8 @@ def lib():
         L.oracle_map_associate.argtypes = [vp, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f64p, _f64p, _i32p]
         L.oracle_map_solve.argtypes = [_f64p, _i32p, ctypes.c_int, _f64p, ctypes.c_int, _i32p]
         L.oracle_mapopt_step.argtypes = [vp, _f32p, ctypes.c_int, _f64p, _f64p, _f64p, _i32p]
+        L.oracle_mapopt_step_corner.argtypes = [vp, vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _f64p, _f64p,
+                                                _i32p]
         L.oracle_laser_mapping.argtypes = [vp, vp, _f32p, ctypes.c_int, _f32p, ctypes.c_int, _f64p, _i32p]
         L.oracle_orb_detect.argtypes = [_u8p, vp, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _u8p, _f32p,
                                         ctypes.c_int]
@@ -375,6 +377,18 @@ def mapopt_step(m: IkdMap, ground, odom, state):
     pose = np.zeros(7)
     summ = np.zeros(3, np.int32)
     lib().oracle_mapopt_step(m.h, g.reshape(-1), g.shape[0], np.ascontiguousarray(odom, np.float64), st, pose, summ)
+    return pose, st, summ
+
+
+def mapopt_step_corner(m: IkdMap, cm: IkdMap, ground, corner, odom, state):
+    """mapOptimization step with its corner ikd-Tree (mapOptimization.cpp:193-195, :477-479):
+    as mapopt_step, and pc_corner is added to cm at the keyframe pose."""
+    g, c = _xyz4(ground), _xyz4(corner)
+    st = np.array(state, np.float64)
+    pose = np.zeros(7)
+    summ = np.zeros(3, np.int32)
+    lib().oracle_mapopt_step_corner(m.h, cm.h, g.reshape(-1), g.shape[0], c.reshape(-1), c.shape[0],
+                                    np.ascontiguousarray(odom, np.float64), st, pose, summ)
     return pose, st, summ
 
 

@@ -562,9 +562,21 @@ void oracle_map_solve(const double* rec, const int* kind, int n, double* x, int 
 // Add_Points(downsample) of the voxelized cloud at the keyframe pose (:453-475).
 // out_pose = q_w_curr, t_w_curr after the step; summary = planes, iterations, termination.
 int oracle_voxel_grid(const float* xyzi, int n, float leaf, int canonical, float* out, int* n_out);
+void oracle_mapopt_step_corner(void* h, void* hc, const float* ground, int n, const float* corner, int nc,
+                               const double* odom, double* state, double* out_pose, int* summary);
+
 void oracle_mapopt_step(void* h, const float* ground, int n, const double* odom, double* state, double* out_pose,
                         int* summary) {
+  oracle_mapopt_step_corner(h, nullptr, ground, n, nullptr, 0, odom, state, out_pose, summary);
+}
+
+// With mapOptimization's corner ikd-Tree (corner_ikdtree_, KD_TREE(0.3, 0.6, 0.8),
+// mapOptimization.cpp:505): pc_corner transformed by the same keyframe pose as the ground cloud,
+// Build on the first keyframe (:193-195), Add_Points(downsample) afterwards (:477-479).
+void oracle_mapopt_step_corner(void* h, void* hc, const float* ground, int n, const float* corner, int nc,
+                               const double* odom, double* state, double* out_pose, int* summary) {
   IkdMap* m = static_cast<IkdMap*>(h);
+  IkdMap* cm = static_cast<IkdMap*>(hc);
   const double* qo = odom;
   const double* to = odom + 4;
   double* qm = state;
@@ -582,10 +594,18 @@ void oracle_mapopt_step(void* h, const float* ground, int n, const double* odom,
     dst.assign((size_t)cnt * 4, 0.f);
     for (int i = 0; i < cnt; i++) to_world(pose, src + (size_t)i * 4, &dst[(size_t)i * 4]);
   };
+  auto corner_update = [&](const double* pose) {
+    if (!cm || nc <= 0) return;
+    std::vector<float> w;
+    transformed(corner, nc, pose, w);
+    if (cm->live() == 0) cm->build(w.data(), nc, 4);
+    else cm->add_points(w.data(), nc, 4, true);
+  };
   if (m->live() == 0) {
     std::vector<float> w;
     transformed(ground, n, x, w);
     m->build(w.data(), n, 4);
+    corner_update(x);
     for (int e = 0; e < 7; e++) out_pose[e] = x[e];
     return;
   }
@@ -620,6 +640,7 @@ void oracle_mapopt_step(void* h, const float* ground, int n, const double* odom,
   std::vector<float> w;
   transformed(vox.data(), nv, conv ? x : x0, w);
   m->add_points(w.data(), nv, 4, true);
+  corner_update(conv ? x : x0);
   for (int e = 0; e < 7; e++) out_pose[e] = x[e];
 }
 

@@ -232,6 +232,60 @@ def test_mapopt_sequence(pkg, oracle, ctx, synth):
     go.map.close()
 
 
+def test_mapopt_corner_map(pkg, oracle, ctx, synth):
+    """mapOptimization with its corner ikd-Tree (KD_TREE(0.3, 0.6, 0.8), mapOptimization.cpp:505):
+    pc_corner (the scan's less-sharp cloud) Built on the first keyframe (:193-195), then
+    Add_Points(downsample) at the keyframe pose (:477-479).  Poses, summaries and both maps' live
+    points against the oracle, frame by frame."""
+    go = pkg.mapping.MapOptimization(ctx, 0.4, 0.2, corner=True)
+    om, ocm = oracle.IkdMap(0.4), oracle.IkdMap(0.8)
+    ostate = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    for k in range(5):
+        scan = synth.make_scan(20 + k)
+        flat = scan.reshape(-1, 4)
+        ground = _f32(flat[np.abs(flat[:, :3]).sum(1) > 0])
+        corner = oracle.scan_registration(scan).less_sharp
+        q, t = synth.ground_truth_pose(20 + k).as_qt()
+        odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=40 + k)
+        pg, sg = go.callback(ground, odom, corner)
+        po, ostate, so = oracle.mapopt_step_corner(om, ocm, ground, corner, odom, ostate)
+        assert np.max(np.abs(pg - po)) < POSE_TOL, (k, pg, po)
+        assert list(sg) == list(so), (k, sg, so)
+        assert go.map.size() == om.size(), k
+        assert go.corner_map.size() == ocm.size(), (k, go.corner_map.size(), ocm.size())
+        gp, op = _by_id(go.corner_map.points()), ocm.points()
+        assert np.array_equal(gp[:, 3].view(np.int32), op[:, 3].view(np.int32)), k
+        np.testing.assert_allclose(gp[:, :3], op[:, :3], atol=1e-4)
+    assert go.corner_map.size() > 0
+    go.close()
+
+
+def test_mapopt_corner_fed_from_batch(pkg, oracle, ctx, synth):
+    """lislam_batch_mapopt_corner: the scan's less-sharp cloud on the device is pc_corner."""
+    S = 3
+    scans = synth.make_sequence(S, start=40)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.ground(S)
+    go = pkg.mapping.MapOptimization(ctx, 0.4, 0.2, corner=True)
+    om, ocm = oracle.IkdMap(0.4), oracle.IkdMap(0.8)
+    ostate = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    for k in range(S):
+        g_ref, _, _ = oracle.ground_extract(scans[k])
+        f = oracle.scan_registration(scans[k])
+        merged = np.concatenate([g_ref, f.less_flat]).astype(np.float32)
+        q, t = synth.ground_truth_pose(40 + k).as_qt()
+        odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=60 + k)
+        pg, sg = go.callback_batch(b, k, odom)
+        po, ostate, so = oracle.mapopt_step_corner(om, ocm, merged, f.less_sharp, odom, ostate)
+        assert np.max(np.abs(pg - po)) < POSE_TOL, (k, pg, po)
+        assert list(sg) == list(so), (k, sg, so)
+        assert go.corner_map.size() == ocm.size(), k
+    go.close()
+    b.close()
+
+
 def test_laser_mapping(pkg, oracle, ctx, synth):
     M = synth.make_corridor_map(300_000, spacing=0.05)
     E = synth.make_edge_map(40)

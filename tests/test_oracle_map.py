@@ -158,3 +158,40 @@ def test_map_solve_recovers_perturbed_pose(oracle, synth):
     x, summ = oracle.map_solve(rec, kind, x0, 10)
     assert summ[1] in (0, 1)
     assert np.linalg.norm(x[4:] - truth[4:]) < np.linalg.norm(x0[4:] - truth[4:])
+
+
+def test_mapopt_corner_map_oracle(oracle, synth):
+    """The corner ikd-Tree of mapOptimization (oracle): Build on the first keyframe with the
+    corner cloud at the keyframe pose, Add_Points(downsample 0.8) afterwards; the ground stage is
+    unchanged by it (same poses as mapopt_step)."""
+    m1, m2, cm = oracle.IkdMap(0.4), oracle.IkdMap(0.4), oracle.IkdMap(0.8)
+    s1 = s2 = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    sizes, total = [], 0
+    for k in range(3):
+        scan = synth.make_scan(20 + k, 16, 512)
+        flat = scan.reshape(-1, 4)
+        ground = np.ascontiguousarray(flat[np.abs(flat[:, :3]).sum(1) > 0], np.float32)
+        corner = oracle.scan_registration(scan).less_sharp
+        q, t = synth.ground_truth_pose(20 + k).as_qt()
+        odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=40 + k)
+        p1, s1, u1 = oracle.mapopt_step(m1, ground, odom, s1)
+        p2, s2, u2 = oracle.mapopt_step_corner(m2, cm, ground, corner, odom, s2)
+        assert np.array_equal(p1, p2) and np.array_equal(u1, u2) and m1.size() == m2.size()
+        if k == 0:  # Build keeps every point (no downsampling), transformed by the pose
+            assert cm.size() == len(corner)
+            pts = cm.points()
+            qv, tv = p2[:4], p2[4:]
+            R = _rot(qv)
+            np.testing.assert_allclose(pts[:, :3], corner[:, :3].astype(np.float64) @ R.T + tv, atol=1e-4)
+        total += len(corner)
+        sizes.append(cm.size())
+    # Add_Points(downsample) keeps one point per 0.8 m box among the map's points and the new
+    # ones (ikd_Tree.cpp Add_Points): the map can shrink below the raw first keyframe
+    assert 0 < sizes[1] < sizes[0] + total and 0 < sizes[2] <= total, sizes
+
+
+def _rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
