@@ -102,8 +102,10 @@ __device__ __forceinline__ void unpack(const double* acc, double* cost, double* 
 __device__ __forceinline__ void quat_plus(const double* x, const double* d, double* xp) {
   const double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
   if (nd > 0.0) {
-    const double sdd = sin(nd) / nd;
-    const DQ r = qmul(DQ{sdd * d[0], sdd * d[1], sdd * d[2], cos(nd)}, DQ{x[0], x[1], x[2], x[3]});
+    double sn, cs;
+    sincos(nd, &sn, &cs);
+    const double sdd = sn / nd;
+    const DQ r = qmul(DQ{sdd * d[0], sdd * d[1], sdd * d[2], cs}, DQ{x[0], x[1], x[2], x[3]});
     xp[0] = r.x; xp[1] = r.y; xp[2] = r.z; xp[3] = r.w;
   } else {
     for (int k = 0; k < 4; k++) xp[k] = x[k];
@@ -123,36 +125,49 @@ __device__ __forceinline__ double grad_max_norm(const double* x, const double* g
 }
 
 // (S A S + diag/radius) y = S g by Cholesky (the normal equations of Ceres' augmented DENSE_QR
-// system [J S; sqrt(diag/radius)] y = [r; 0]).
+// system [J S; sqrt(diag/radius)] y = [r; 0]).  The factor overwrites the packed lower triangle
+// of the scaled matrix in place (row i at i (i + 1) / 2): 21 live doubles instead of 72, so the
+// step fits the registers of a 16-wave workgroup's thread 0.  Each column divides once (1 / l_jj)
+// and the factor and both substitutions multiply by that reciprocal: the serial step is
+// issue- and latency-bound on one lane, and an fp64 division is ~10 dependent instructions.
 __device__ __forceinline__ bool lm_solve(const LM& s, double* y) {
-  double M[36], b[6], L[36];
+  double M[21], b[6], inv[6];
   for (int i = 0; i < 6; i++) {
-    for (int j = 0; j < 6; j++) { M[i * 6 + j] = s.scale[i] * s.A[i * 6 + j] * s.scale[j]; L[i * 6 + j] = 0; }
-    M[i * 6 + i] += s.diag[i] / s.radius;
+    for (int j = 0; j <= i; j++) M[i * (i + 1) / 2 + j] = s.scale[i] * s.A[i * 6 + j] * s.scale[j];
+    M[i * (i + 1) / 2 + i] += s.diag[i] / s.radius;
     b[i] = s.scale[i] * s.g[i];
   }
+#pragma unroll
   for (int j = 0; j < 6; j++) {
-    double d = M[j * 6 + j];
-    for (int k = 0; k < j; k++) d -= L[j * 6 + k] * L[j * 6 + k];
+    double d = M[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) d -= M[j * (j + 1) / 2 + k] * M[j * (j + 1) / 2 + k];
     if (!(d > 0)) return false;
     const double ljj = sqrt(d);
-    L[j * 6 + j] = ljj;
+    inv[j] = 1.0 / ljj;  // one division per column; the column and both substitutions multiply
+    M[j * (j + 1) / 2 + j] = ljj;
+#pragma unroll
     for (int i = j + 1; i < 6; i++) {
-      double v = M[i * 6 + j];
-      for (int k = 0; k < j; k++) v -= L[i * 6 + k] * L[j * 6 + k];
-      L[i * 6 + j] = v / ljj;
+      double v = M[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) v -= M[i * (i + 1) / 2 + k] * M[j * (j + 1) / 2 + k];
+      M[i * (i + 1) / 2 + j] = v * inv[j];
     }
   }
   double z[6];
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     double v = b[i];
-    for (int k = 0; k < i; k++) v -= L[i * 6 + k] * z[k];
-    z[i] = v / L[i * 6 + i];
+#pragma unroll
+    for (int k = 0; k < i; k++) v -= M[i * (i + 1) / 2 + k] * z[k];
+    z[i] = v * inv[i];
   }
+#pragma unroll
   for (int i = 5; i >= 0; i--) {
     double v = z[i];
-    for (int k = i + 1; k < 6; k++) v -= L[k * 6 + i] * y[k];
-    y[i] = v / L[i * 6 + i];
+#pragma unroll
+    for (int k = i + 1; k < 6; k++) v -= M[k * (k + 1) / 2 + i] * y[k];
+    y[i] = v * inv[i];
   }
   for (int i = 0; i < 6; i++)
     if (!isfinite(y[i])) return false;
@@ -216,8 +231,7 @@ __device__ __forceinline__ bool lm_start(LM& s, const double* x0, const double* 
 // After the evaluation at the candidate s.xc (acc): accept / reject, tolerances, next
 // candidate.  Returns whether another candidate must be evaluated.
 __device__ __forceinline__ bool lm_next(LM& s, const double* acc, int max_it) {
-  double ccost, cA[36], cg[6];
-  unpack(acc, &ccost, cA, cg);
+  double ccost = acc[0];
   if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
   bool cont = true;
   double xn = 0, sn = 0;
@@ -229,9 +243,9 @@ __device__ __forceinline__ bool lm_next(LM& s, const double* acc, int max_it) {
     const double rel = (s.cost - ccost) / s.mcc;
     if (rel > 1e-3) {  // min_relative_decrease: accept
       for (int e = 0; e < 7; e++) s.x[e] = s.xc[e];
+      double unused;
+      unpack(acc, &unused, s.A, s.g);
       s.cost = ccost;
-      for (int e = 0; e < 36; e++) s.A[e] = cA[e];
-      for (int e = 0; e < 6; e++) s.g[e] = cg[e];
       const double t3 = 2.0 * rel - 1.0;
       s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
       s.dfac = 2.0;

@@ -1213,6 +1213,224 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
   }
 }
 
+// ---- the same solve with the chain's residual blocks held in LDS across its evaluations
+// k_odom_lm reads every block record from global memory at every evaluation; here one workgroup
+// of 16 waves per chain reads them once, into LDS, compacted to the bits the records carry: the
+// query point and the first matched point are floats in every record (laserOdometry.cpp:554-556,
+// :677-681 take them from float clouds), the third triple is the edge's second point (float) or
+// the plane's unit normal (double).  Blocks past kLmLds (only when cap_sharp + cap_flat exceeds
+// it, H > 64 lines) are evaluated from the global records.  The reduction sums 16-lane rows by
+// DPP, then each wave sums one accumulator entry over the 64 row partials.
+#ifndef LISLAM_LM2_THREADS
+#define LISLAM_LM2_THREADS 512
+#endif
+constexpr int kLm2Threads = LISLAM_LM2_THREADS;
+constexpr int kLm2Waves = kLm2Threads / 64;
+constexpr int kLmLds = 2816;
+
+struct Lm2Shared {
+  float c[3][kLmLds];    // query point
+  float p[3][kLmLds];    // edge point a / plane point j
+  double d[3][kLmLds];   // edge point b / plane normal
+  int8_t kind[kLmLds];
+  double red[kLm2Waves * 4][kAcc];
+  double x[7];
+  double acc[kAcc];
+  int cnt[kLm2Waves][2];
+  int nc, np, flag;
+};
+
+__device__ __forceinline__ void block_accum3(int kd, const D3& c, const D3& p1, const D3& p2, const DQ& q, const D3& t,
+                                             double* acc) {
+  const double ha = 0.1;  // HuberLoss(0.1)
+  const D3 p = qrot(q, c);
+  const D3 lp = p + t;
+  if (kd == 0) {
+    // edge_factor, one residual row at a time (its Jacobian row is 6 live doubles, not 18), and
+    // the six divisions by |a - b| as products with its reciprocal
+    const D3 nu = cross(lp - p1, lp - p2);
+    const D3 de = p1 - p2;
+    const double inv = 1.0 / sqrt(de.x * de.x + de.y * de.y + de.z * de.z);  // one division, six products
+    const double r0 = nu.x * inv, r1 = nu.y * inv, r2 = nu.z * inv;
+    const double sc = huber_scale(ha, r0 * r0 + r1 * r1 + r2 * r2, &acc[0]);
+    const D3 d{(p2.x - p1.x) * inv, (p2.y - p1.y) * inv, (p2.z - p1.z) * inv};
+    const double P[3][3] = {{0, 2 * p.z, -2 * p.y}, {-2 * p.z, 0, 2 * p.x}, {2 * p.y, -2 * p.x, 0}};  // -2[p]x
+#pragma unroll 1
+    for (int k = 0; k < 3; k++) {
+      const double m0 = k == 0 ? 0.0 : k == 1 ? d.z : -d.y;
+      const double m1 = k == 0 ? -d.z : k == 1 ? 0.0 : d.x;
+      const double m2 = k == 0 ? d.y : k == 1 ? -d.x : 0.0;
+      const double rk = k == 0 ? r0 : k == 1 ? r1 : r2;
+      double Js[6];
+#pragma unroll
+      for (int cc = 0; cc < 3; cc++) Js[cc] = (m0 * P[0][cc] + m1 * P[1][cc] + m2 * P[2][cc]) * sc;
+      Js[3] = m0 * sc; Js[4] = m1 * sc; Js[5] = m2 * sc;
+      accum_row(acc, Js, rk * sc);
+    }
+  } else {
+    // plane_factor (p2 = the constructor's unit normal)
+    const double res = dot(lp - p1, p2);
+    const D3 pn = cross(p, p2);
+    double J[6] = {2 * pn.x, 2 * pn.y, 2 * pn.z, p2.x, p2.y, p2.z};
+    const double sc = huber_scale(ha, res * res, &acc[0]);
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++) J[cc] *= sc;
+    accum_row(acc, J, res * sc);
+  }
+}
+
+__device__ __forceinline__ void evaluate2(Lm2Shared& sh, const double* blk, const int* kind, int ns, int cap_sharp,
+                                          int nf) {
+  double acc[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) acc[e] = 0;
+  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
+  const D3 t{sh.x[4], sh.x[5], sh.x[6]};
+  const int total = ns + nf;
+  for (int i = threadIdx.x; i < total; i += kLm2Threads) {
+    int kd;
+    D3 c, p1, p2;
+    if (i < kLmLds) {
+      kd = sh.kind[i];
+      c = D3{sh.c[0][i], sh.c[1][i], sh.c[2][i]};
+      p1 = D3{sh.p[0][i], sh.p[1][i], sh.p[2][i]};
+      p2 = D3{sh.d[0][i], sh.d[1][i], sh.d[2][i]};
+    } else {  // beyond the LDS cache
+      const int idx = i < ns ? i : cap_sharp + (i - ns);
+      kd = kind[idx];
+      const double* rb = blk + (size_t)idx * 9;
+      c = D3{rb[0], rb[1], rb[2]};
+      p1 = D3{rb[3], rb[4], rb[5]};
+      p2 = D3{rb[6], rb[7], rb[8]};
+    }
+    if (kd >= 0) block_accum3(kd, c, p1, p2, q, t, acc);
+  }
+  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) {
+    const double v = row_sum(acc[e]);
+    if ((lane & 15) == 0) sh.red[row][e] = v;
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  for (int e = w; e < kAcc; e += kLm2Waves) {  // wave w: entries w, w + kLm2Waves, ...
+    double v = lane < kLm2Waves * 4 ? sh.red[lane][e] : 0.0;
+    v = row_sum(v);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane == 0) sh.acc[e] = v;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kLm2Threads) void k_odom_lm2(OdomArgs a, int r, int outer) {
+  __shared__ Lm2Shared sh;
+  __shared__ LM lm;
+#ifdef LISLAM_PHASE_PROF
+  unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int c = a.c0 + blockIdx.x;
+  int k;
+  if (!pair_of(a, c, r, &k)) return;
+  double* st = a.state + (size_t)c * 16;
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  const double* blk = a.blk + (size_t)c * (a.cap_sharp + a.cap_flat) * 9;
+  const int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
+  const bool gated_off = a.gate && !a.gate[k];  // use_aloam false: no solve, the pose still accumulates
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  {
+    // the records into LDS, and the correspondence counts (:562/:685)
+    int c0 = 0, c1 = 0;
+    const int total = gated_off ? 0 : ns + nf;
+    for (int i = threadIdx.x; i < total; i += kLm2Threads) {
+      const int idx = i < ns ? i : a.cap_sharp + (i - ns);
+      const int kd = kind[idx];
+      c0 += kd == 0;
+      c1 += kd == 1;
+      if (i < kLmLds) {
+        sh.kind[i] = (int8_t)kd;
+        if (kd >= 0) {
+          const double* rb = blk + (size_t)idx * 9;
+          double v[9];
+#pragma unroll
+          for (int e = 0; e < 9; e++) v[e] = rb[e];
+#pragma unroll
+          for (int e = 0; e < 3; e++) {
+            sh.c[e][i] = (float)v[e];
+            sh.p[e][i] = (float)v[3 + e];
+            sh.d[e][i] = v[6 + e];
+          }
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 += __shfl_xor(c0, o);
+      c1 += __shfl_xor(c1, o);
+    }
+    if (lane == 0) { sh.cnt[w][0] = c0; sh.cnt[w][1] = c1; }
+    if (threadIdx.x == 0)
+      for (int e = 0; e < 7; e++) sh.x[e] = st[e];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int a0 = 0, a1 = 0;
+      for (int v = 0; v < kLm2Waves; v++) { a0 += sh.cnt[v][0]; a1 += sh.cnt[v][1]; }
+      sh.nc = a0;
+      sh.np = a1;
+    }
+    __syncthreads();
+  }
+  const int nc = sh.nc, np = sh.np;
+  LM_PHASE(3);
+  bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
+  if (go) {
+    evaluate2(sh, blk, kind, ns, a.cap_sharp, nf);
+    LM_PHASE(0);
+    if (threadIdx.x == 0) {
+      const bool cont = lm_start(lm, sh.x, sh.acc, a.max_iterations);
+      sh.flag = cont;
+      if (cont)
+        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
+    }
+    __syncthreads();
+    go = sh.flag;
+  }
+  LM_PHASE(2);
+  while (go) {
+    evaluate2(sh, blk, kind, ns, a.cap_sharp, nf);  // cost + J^T J + J^T r at the candidate
+    LM_PHASE(1);
+#ifdef LISLAM_PHASE_PROF
+    if (threadIdx.x == 0) atomicAdd(&g_lm_phase[5], 1ull);
+#endif
+    if (threadIdx.x == 0) {
+      const bool cont = lm_next(lm, sh.acc, a.max_iterations);
+      sh.flag = cont;
+      if (cont)
+        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
+    }
+    __syncthreads();
+    LM_PHASE(2);
+    go = sh.flag;
+  }
+  if (threadIdx.x != 0) return;
+  int* so = a.stats + (size_t)k * 8;
+  so[outer * 2 + 0] = nc;
+  so[outer * 2 + 1] = np;
+  so[4 + outer] = (nc + np) > 0 ? lm.it : 0;
+  so[6 + outer] = (nc + np) > 0 ? lm.term : 1;
+  if ((nc + np) > 0)
+    for (int e = 0; e < 7; e++) st[e] = lm.x[e];
+  if (outer == 1) {
+    DQ qw{st[7], st[8], st[9], st[10]};
+    D3 tw{st[11], st[12], st[13]};
+    tw = tw + qrot(qw, D3{st[4], st[5], st[6]});
+    qw = qmul(qw, DQ{st[0], st[1], st[2], st[3]});
+    st[7] = qw.x; st[8] = qw.y; st[9] = qw.z; st[10] = qw.w; st[11] = tw.x; st[12] = tw.y; st[13] = tw.z;
+    double* op = a.para + (size_t)k * 7;
+    double* ow = a.pose + (size_t)k * 7;
+    for (int e = 0; e < 7; e++) { op[e] = st[e]; ow[e] = st[7 + e]; }
+  }
+}
+
 __global__ void k_odom_init(OdomArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.n_chains) return;
@@ -1345,6 +1563,8 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
   // LISLAM_ASSOC16 = 0 selects the one-query-per-wave kernel; default: four queries per wave
   static const bool rows16 = !(getenv("LISLAM_ASSOC16") && atoi(getenv("LISLAM_ASSOC16")) == 0);
   const int qblocks16 = (a0.cap_sharp + a0.cap_flat + 8 - 1) / 8;  // 2 waves x 4 rows
+  // LISLAM_LM_V1 = 1 selects the solve that re-reads the block records at every evaluation
+  static const bool lm_v1 = getenv("LISLAM_LM_V1") && atoi(getenv("LISLAM_LM_V1")) == 1;
   const int rounds = min(a0.chain_len, a0.S - 1);
   auto timed = [&](int kernel, hipStream_t s, auto&& launch) {
     hipEvent_t b = nullptr, e = nullptr;
@@ -1367,7 +1587,10 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
           else if (kw == 2) hipLaunchKernelGGL(k_odom_assoc<2>, dim3(qblocks * cb), dim3(128), 0, s, a, r, qblocks);
           else hipLaunchKernelGGL(k_odom_assoc<4>, dim3(qblocks * cb), dim3(256), 0, s, a, r, qblocks);
         });
-        timed(5, s, [&] { hipLaunchKernelGGL(k_odom_lm, dim3(a.cn), dim3(kLmThreads), 0, s, a, r, outer); });
+        timed(5, s, [&] {
+          if (lm_v1) hipLaunchKernelGGL(k_odom_lm, dim3(a.cn), dim3(kLmThreads), 0, s, a, r, outer);
+          else hipLaunchKernelGGL(k_odom_lm2, dim3(a.cn), dim3(kLm2Threads), 0, s, a, r, outer);
+        });
       }
     }
   }

@@ -43,8 +43,10 @@ if sys.argv[1] == "lm":  # k_odom_lm: first evaluation + start, later evaluation
         ctx.synchronize()
         L.lislam_debug_lm_phases(buf)
         nwg = 2 * 10 * ((S - 1 + 9) // 10)
-        for i, nm in enumerate(["first eval + start", "evaluations", "steps (thread 0)"]):
-            print(f"{nm:20s} {buf[i] / 100.0 / nwg:9.1f} us per workgroup")
+        names = ["first eval (+ start, v1)", "evaluations", "steps (thread 0)", "record load + counts (v2)"]
+        for i, nm in enumerate(names):
+            print(f"{nm:26s} {buf[i] / 100.0 / nwg:9.1f} us per workgroup")
+        print(f"{'later evaluations':26s} {buf[5] / nwg:9.2f} per workgroup")
         b.close()
     sys.exit(0)
 
