@@ -243,8 +243,16 @@ int lislam_intensity_tracker_destroy(lislam_intensity_tracker* t);
 int lislam_intensity_tracker_step(lislam_intensity_tracker* t, const uint8_t* image, const float* cloud_track,
                                   double* T_s2s, int32_t* stats);
 /* detectfeatures over scans [0, n_scans) of a batch (its a1 images, want_images = 1): scan k is
- * matched against scan k-1 exactly as the tracker would; outputs LISLAM_OUT_ORB_*. */
+ * matched against scan k-1 exactly as the tracker would; outputs LISLAM_OUT_ORB_*.  Asynchronous:
+ * it returns once its work is queued (on a side stream the context stream then waits for); the
+ * sequential re-detection rule (intensity_feature_tracker.cpp:652-687) is decided on the device in
+ * LISLAM_ORB_ROUNDS passes (default 1).  Reading an ORB output first checks that the device
+ * decision converged, and redoes the batch with host-decided rounds if it did not. */
 int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask);
+/* The last lislam_batch_intensity_odometry's cascade, after its outputs were read: info[0] = 1
+ * device-decided and converged, 0 redone with host rounds, -1 host rounds from the start
+ * (LISLAM_ORB_HOST_CASCADE=1 or fewer than 2 scans); info[1] = device decision passes. */
+int lislam_batch_orb_cascade_info(lislam_batch* b, int32_t* info);
 
 /* ---- ground plane (ImageHandler::groundPlaneExtraction, src/image_handler.h_ouster:41-100):
  * z-band screening [-2, -0.45], PCL SACSegmentation(SACMODEL_PLANE, SAC_RANSAC, 0.01, optimized

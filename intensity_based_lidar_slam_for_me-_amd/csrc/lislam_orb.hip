@@ -116,6 +116,7 @@ struct Args {
   int* nkp;               // [S]
   int* overflow;          // [1]
   const int* smap;        // scan of each grid scan index (null: identity from the slot base)
+  const int* scount;      // device count of grid scan indices in use (null: all); the rest exit
 };
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -634,7 +635,7 @@ extern "C" int lislam_debug_sel_phases(unsigned long long* out) {
 #define SEL_PHASE(i)
 #endif
 constexpr int kPatchDw = 2 * 279;  // LDS dwords per wave: 2 angle patches (31 x 9) >= 4 Harris patches (9 x 4)
-__global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
+__device__ __forceinline__ void orb_select_body(const Args& a, int gi) {
   __shared__ SelShared sh;
   __shared__ uint32_t sh_patch[(kSelThreads / 64) * kPatchDw];
 #ifdef LISLAM_PHASE_PROF
@@ -644,7 +645,7 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   // level-major blocks: consecutive blocks (dealt round-robin to the 8 XCDs) are different scans
   // of one level, so the heavy level-0 workgroups spread over every XCD
   const int S = gridDim.x / kL;
-  const int l = blockIdx.x / S, s = a.smap ? a.smap[blockIdx.x % S] : blockIdx.x % S;
+  const int l = blockIdx.x / S, s = a.smap ? a.smap[gi] : gi;
   const int w = g.w[l], h = g.h[l];
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
   const uint8_t* kf = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
@@ -871,11 +872,27 @@ __global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
   if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
 }
 
+// kStrided: the grid's scan indices stride over the scans in use (*a.scount of them); otherwise one
+// scan per grid scan index (the loop costs the body registers, so the common launch has none)
+template <bool kStrided>
+__global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
+  const int S = gridDim.x / kL;
+  const int cnt = a.scount ? *a.scount : S;
+  if (!kStrided) {
+    if ((int)(blockIdx.x % S) < cnt) orb_select_body(a, blockIdx.x % S);
+    return;
+  }
+  for (int gi = blockIdx.x % S; gi < cnt; gi += S) {
+    orb_select_body(a, gi);
+    __syncthreads();
+  }
+}
+
 // levels in order, level-0 coordinates, cloud-track lookup and zero filter (a9)
-__global__ __launch_bounds__(256) void k_orb_finish(Args a) {
+__device__ __forceinline__ void orb_finish_body(const Args& a, int gi) {
   __shared__ SelShared sh;
   const Geom& g = a.g;
-  const int s = a.smap ? a.smap[blockIdx.x] : blockIdx.x;
+  const int s = a.smap ? a.smap[gi] : gi;
   int n = 0;
   for (int l = 0; l < kL; l++) {
     const int cnt = a.lcnt[s * kL + l];
@@ -906,34 +923,49 @@ __global__ __launch_bounds__(256) void k_orb_finish(Args a) {
   if (threadIdx.x == 0) a.nkp[s] = n;
 }
 
-// steered rBRIEF: 32 threads per keypoint, one descriptor byte each
-__global__ __launch_bounds__(256) void k_orb_desc(Args a) {
-  const Geom& g = a.g;
-  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
-  const int k = blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int byte = threadIdx.x & 31;
-  if (k >= a.nkp[s]) return;
-  const float* kp = a.kp + ((size_t)s * g.cap + k) * 6;
-  const int l = (int)kp[5];
-  const float scale = 1.f / g.scale[l];
-  const float ang = kp[3] * (float)(kPi / 180.f);
-  const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
-  const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
-  const uint8_t* base = a.blur + (size_t)s * g.bytes;
-  int v = 0;
-#pragma unroll
-  for (int bit = 0; bit < 8; bit++) {
-    const int p = (byte * 8 + bit) * 2;
-    int t[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const float qx = (float)c_pattern[(p + e) * 2], qy = (float)c_pattern[(p + e) * 2 + 1];
-      const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
-      t[e] = pxc(base, g, l, cy + (int)rintf(y), cx + (int)rintf(x));
-    }
-    v |= (t[0] < t[1]) << bit;
+__global__ __launch_bounds__(256) void k_orb_finish(Args a) {
+  const int cnt = a.scount ? *a.scount : (int)gridDim.x;
+  for (int gi = blockIdx.x; gi < cnt; gi += gridDim.x) {
+    orb_finish_body(a, gi);
+    __syncthreads();
   }
-  a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)v;
+}
+
+// steered rBRIEF: 32 threads per keypoint, one descriptor byte each (keypoints grid-strided over
+// gridDim.x blocks of 8)
+__device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
+  const Geom& g = a.g;
+  const int s = a.smap ? a.smap[gi] : gi;
+  const int byte = threadIdx.x & 31;
+  const int nk = a.nkp[s];
+  const uint8_t* base = a.blur + (size_t)s * g.bytes;
+  for (int k = blockIdx.x * 8 + (threadIdx.x >> 5); k < nk; k += gridDim.x * 8) {
+    const float* kp = a.kp + ((size_t)s * g.cap + k) * 6;
+    const int l = (int)kp[5];
+    const float scale = 1.f / g.scale[l];
+    const float ang = kp[3] * (float)(kPi / 180.f);
+    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
+    int v = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; bit++) {
+      const int p = (byte * 8 + bit) * 2;
+      int t[2];
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const float qx = (float)c_pattern[(p + e) * 2], qy = (float)c_pattern[(p + e) * 2 + 1];
+        const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
+        t[e] = pxc(base, g, l, cy + (int)rintf(y), cx + (int)rintf(x));
+      }
+      v |= (t[0] < t[1]) << bit;
+    }
+    a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_orb_desc(Args a) {
+  const int cnt = a.scount ? *a.scount : (int)gridDim.y;
+  for (int gi = blockIdx.y; gi < cnt; gi += gridDim.y) orb_desc_body(a, gi);
 }
 
 // ------------------------------------------------------------------ matching (a10) + records
@@ -954,6 +986,7 @@ struct PairArgs {
   int* kind;          // [npairs][qcap]
   int* stats;         // [npairs][8]: ok, -, nq, matches, good, iterations, termination, nt
   double* T;          // [npairs][7]
+  const int* pcount;  // device count of pairs in use (null: npairs); the grid's other pairs exit
 };
 
 __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
@@ -971,9 +1004,8 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 constexpr int kXdThreads = 256;
 constexpr int kXdTrains = 2 * kXdThreads;
 
-__global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
+__device__ __forceinline__ void orb_xdist_body(const PairArgs& p, int pi) {
   __shared__ uint4 qt[kQTile * 2];
-  const int pi = blockIdx.x;
   const int pr = p.pslot ? p.pslot[pi] : pi;
   const int qs = p.qscan[pi], ts = p.tscan[pi];
   const int nq = p.qn[qs], nt = p.tn[ts];
@@ -1011,6 +1043,15 @@ __global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
   if (ib < nt && bjb >= 0) atomicMin(&best[bjb], (bdb << 16) | ib);
 }
 
+// the grid's pair indices stride over the pairs in use (*p.pcount of them when given)
+__global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
+    orb_xdist_body(p, pi);
+    __syncthreads();
+  }
+}
+
 // The same result on the matrix cores: Hamming(q, t) = |q| + |t| - 2 <q, t> with the 256
 // descriptor bits as 0/1 int8 vectors and <q, t> from v_mfma_i32_16x16x64_i8 (four k-steps of 64
 // bits; A and B fragments use one and the same lane -> k map, so the dot product does not depend
@@ -1034,10 +1075,9 @@ __device__ __forceinline__ i32x4 expand16(uint32_t b) {  // 16 bits -> 16 bytes 
   return v;
 }
 
-__global__ __launch_bounds__(64 * kXmWaves) void k_orb_xdist_mfma(PairArgs p) {
+__device__ __forceinline__ void orb_xdist_mfma_body(const PairArgs& p, int pi) {
   __shared__ i32x4 qx[kXmQTile * kXmRow / 16];
   __shared__ int qpop[kXmQTile];
-  const int pi = blockIdx.x;
   const int pr = p.pslot ? p.pslot[pi] : pi;
   const int qs = p.qscan[pi], ts = p.tscan[pi];
   const int nq = p.qn[qs], nt = p.tn[ts];
@@ -1105,13 +1145,21 @@ __global__ __launch_bounds__(64 * kXmWaves) void k_orb_xdist_mfma(PairArgs p) {
   if (h == 0 && ti < nt && bj >= 0) atomicMin(&best[bj], (bd << 16) | ti);
 }
 
+// the grid's pair indices stride over the pairs in use (*p.pcount of them when given)
+__global__ __launch_bounds__(64 * kXmWaves) void k_orb_xdist_mfma(PairArgs p) {
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
+    orb_xdist_mfma_body(p, pi);
+    __syncthreads();
+  }
+}
+
 // Selection part: std::sort by distance (stable, query order), the first ceil(frac M), the
 // good-frame test and the front_end_residual records.
-__global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
+__device__ __forceinline__ void orb_match_body(const PairArgs& p, int pi) {
   __shared__ SelShared sh;
   __shared__ int hist[257];
   __shared__ int sM, sG;
-  const int pi = blockIdx.x;
   const int pr = p.pslot ? p.pslot[pi] : pi;
   const int qs = p.qscan[pi], ts = p.tscan[pi];
   const int nq = p.qn[qs], nt = p.tn[ts];
@@ -1183,6 +1231,15 @@ __global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
   }
 }
 
+// the grid's pair indices stride over the pairs in use (*p.pcount of them when given)
+__global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
+    orb_match_body(p, pi);
+    __syncthreads();
+  }
+}
+
 // front_end_residual solve per pair (p2p_calculateRandT): identity start, 20 iterations
 struct LmSh {
   double red[kLmThreads / 16][kAcc];
@@ -1214,10 +1271,15 @@ __device__ void pair_eval(LmSh& sh, const double* rec, int n) {
 }
 
 // best[] rows of the launch's pairs to the "no match" sentinel (one launch for any slot list)
-__global__ __launch_bounds__(256) void k_orb_mfill(PairArgs p, int qcap) {
-  const int pr = p.pslot ? p.pslot[blockIdx.x] : blockIdx.x;
+__device__ __forceinline__ void orb_mfill_body(const PairArgs& p, int qcap, int pi) {
+  const int pr = p.pslot ? p.pslot[pi] : pi;
   int* row = p.mscratch + (size_t)pr * p.bstride;
   for (int j = blockIdx.y * 256 + threadIdx.x; j < qcap; j += gridDim.y * 256) row[j] = kNoMatch;
+}
+
+__global__ __launch_bounds__(256) void k_orb_mfill(PairArgs p, int qcap) {
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) orb_mfill_body(p, qcap, pi);
 }
 
 // Batch outputs: scan 0 is the first frame (stats -1, its keypoint count), scan k > 0 pair
@@ -1238,9 +1300,91 @@ __global__ __launch_bounds__(256) void k_orb_out(int* outS, double* outT, const 
   for (int e = 0; e < 7; e++) t[e] = T[(size_t)(k - 1) * 7 + e];
 }
 
-__global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
+// ---- the re-detection rule of detectfeatures decided on the device (lislam_batch_intensity_odometry)
+// Pair k (query scan k, train scan k-1, buffer slot k-1) first tries frame k's n-feature set against
+// the set frame k-1 ended with; when that fails, both frames re-detect with 2n features and frame k
+// keeps the 2n set (intensity_feature_tracker.cpp:631-687).  cur2[k] = frame k holds the 2n set;
+// pset[k] = the set (0: n, 1: 2n of frame k-1) pair k's current first attempt used; ok1[k] = that
+// attempt succeeded (its stats word).  One decision pass replays the sequential rule over the
+// attempts made so far and lists the pairs whose attempt used the wrong previous set (to redo,
+// grouped by the set they need) and the frames whose 2n set is missing; the final pass (mode 2)
+// lists the re-detecting pairs' 2n-against-2n matches instead, or reports "not converged".
+struct CascadeArgs {
+  int n;
+  const int* stats;   // [n - 1][8] pair buffer stats (slot k - 1 = pair k)
+  int8_t* pset;       // [n]
+  int8_t* cur2;       // [n]
+  int8_t* have2;      // [n] frame's 2n set detected
+  int* e2list;        // [n] frames to detect with 2n features
+  int* e2cnt;         // [1]
+  int* plist;         // [2][3][n] pairs to (re)attempt against the n / 2n previous set; final: [0]
+                      // (each [3][n]: query scans | train scans | slots, stride n)
+  int* pcnt;          // [2]
+  int* redet;         // [n - 1] pair k re-detected (k_orb_out)
+  int* status;        // [2] converged, decision passes
+};
+constexpr int kCascadeMax = 8192;
+
+__global__ __launch_bounds__(256) void k_orb_decide(CascadeArgs cs, int mode) {
+  __shared__ int8_t ok1[kCascadeMax], ps[kCascadeMax], c2[kCascadeMax], h2[kCascadeMax];
+  const int n = cs.n;
+  for (int k = threadIdx.x; k < n; k += 256) {
+    ok1[k] = k >= 1 ? (int8_t)(cs.stats[(size_t)(k - 1) * 8] == 1) : (int8_t)1;
+    ps[k] = mode == 0 ? (int8_t)0 : cs.pset[k];
+    c2[k] = mode == 0 ? (int8_t)0 : cs.cur2[k];
+    h2[k] = mode == 0 ? (int8_t)0 : cs.have2[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int prev = 0;  // frame 0 keeps its n set
+    for (int k = 1; k < n; k++) {
+      if (ps[k] == prev) c2[k] = (int8_t)!ok1[k];
+      prev = c2[k];
+    }
+    int cnt[2] = {0, 0}, ne = 0;
+    bool dirty = false;
+    for (int k = 1; k < n; k++) {
+      const int g = c2[k - 1];
+      if (ps[k] == g) continue;
+      dirty = true;
+      if (mode == 2) break;
+      int* L = cs.plist + (size_t)g * 3 * n;
+      L[cnt[g]] = k; L[n + cnt[g]] = k - 1; L[2 * n + cnt[g]] = k - 1;
+      cnt[g]++;
+      if (g == 1 && !h2[k - 1]) { h2[k - 1] = 1; cs.e2list[ne++] = k - 1; }
+      ps[k] = (int8_t)g;
+    }
+    if (mode == 2) {
+      if (!dirty) {  // converged: the re-detecting pairs, 2n against 2n (frac 0.2)
+        int* L = cs.plist;
+        for (int k = 1; k < n; k++) {
+          const int r = c2[k];
+          cs.redet[k - 1] = r;
+          if (!r) continue;
+          if (!h2[k - 1]) { h2[k - 1] = 1; cs.e2list[ne++] = k - 1; }
+          if (!h2[k]) { h2[k] = 1; cs.e2list[ne++] = k; }
+          L[cnt[0]] = k; L[n + cnt[0]] = k - 1; L[2 * n + cnt[0]] = k - 1;
+          cnt[0]++;
+        }
+      }
+      cs.status[0] = dirty ? 0 : 1;
+    }
+    cs.pcnt[0] = cnt[0];
+    cs.pcnt[1] = cnt[1];
+    *cs.e2cnt = ne;
+    cs.status[1] = mode == 0 ? 1 : cs.status[1] + 1;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += 256) {
+    cs.pset[k] = ps[k];
+    cs.cur2[k] = c2[k];
+    cs.have2[k] = h2[k];
+  }
+}
+
+__device__ __forceinline__ void orb_lm_body(const PairArgs& p, int max_it, int pi) {
   __shared__ LmSh sh;
-  const int pr = p.pslot ? p.pslot[blockIdx.x] : blockIdx.x;
+  const int pr = p.pslot ? p.pslot[pi] : pi;
   int* st = p.stats + pr * 8;
   double* T = p.T + pr * 7;
   const bool good = st[0] == 1;
@@ -1283,6 +1427,14 @@ __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
     for (int e = 0; e < 7; e++) T[e] = lm.x[e];
     st[5] = lm.it;
     st[6] = lm.term;
+  }
+}
+
+__global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
+    orb_lm_body(p, max_it, pi);
+    __syncthreads();
   }
 }
 
@@ -1561,13 +1713,42 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
                        1 + 2 * 2 * (size_t)g.w[0];  // image, scores, two candidate lists
     hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
   }
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
   {
     TimedScope t(c, kT_orb_blur);
     hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
   }
   { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a); }
+  OCHK(c, hipGetLastError());
+  return LISLAM_OK;
+}
+
+// a8 + a9 of engine e (2n features) for the scans of a device list (dlist, *dcount of them, at most
+// nmax), reading the pyramid, FAST / NMS scores and blurred pyramid that engine src (n features)
+// built for the same scans: those depend only on the image and the mask, not on the feature
+// budget, so a re-detection is retainBest + Harris / angles (k_orb_select), the level
+// concatenation (k_orb_finish) and the descriptors (k_orb_desc).
+constexpr int kListSlots = 16;  // grid slots of a device-list launch (scans or pairs in use: a few)
+
+int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img, const float4* d_track,
+                       const int* dlist, const int* dcount, int nmax) {
+  lislam_ctx* c = e->ctx;
+  hipStream_t st = c->stream;
+  if (nmax <= 0) return LISLAM_OK;
+  Args a = e->args(d_img, d_track);
+  a.S = nmax;
+  a.smap = dlist;
+  a.scount = dcount;
+  a.pyr = src->pyr;
+  a.blur = src->blur;
+  a.nms = src->nms;
+  const Geom& g = e->g;
+  // kListSlots grid scan indices stride over the list: the count is only known on the device
+  const int ns = std::min(nmax, kListSlots);
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<true>, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), ns), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -1608,30 +1789,40 @@ struct PairBufs {
 
 // Match pairs (query scan qs[i] of engine qe, train scan ts[i] of te), select frac, test, and
 // (lm) solve; pair i writes buffer slot slots[i] (null: p0 + i).
+// dlist / dcount: the lists are already on the device (dlist = [3][n] query scans | train scans |
+// slots, dcount = how many are in use; n is the grid's upper bound and the lists' stride), decided
+// by an earlier kernel.
 int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int* qs, const int* ts, int n, double frac,
-              PairBufs& pb, int p0, bool lm, const int* slots = nullptr) {
+              PairBufs& pb, int p0, bool lm, const int* slots = nullptr, const int* dlist = nullptr,
+              const int* dcount = nullptr) {
   hipStream_t st = c->stream;
   if (n <= 0) return LISLAM_OK;
-  if (qe->g.cap > pb.qcap || (!slots && p0 + n > pb.maxp) || n > pb.maxp)
+  if (qe->g.cap > pb.qcap || (!slots && !dlist && p0 + n > pb.maxp) || n > pb.maxp)
     return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
-  // one upload of the launch's lists: query scans | train scans | slots (stream-ordered after
-  // the previous launch's kernels, which read the same staging area)
-  std::vector<int> host((size_t)3 * n);
-  std::copy(qs, qs + n, host.begin());
-  std::copy(ts, ts + n, host.begin() + n);
-  if (slots) std::copy(slots, slots + n, host.begin() + 2 * n);
-  OCHK(c, hipMemcpyAsync(pb.args, host.data(), (size_t)(slots ? 3 : 2) * n * 4, hipMemcpyHostToDevice, st));
   PairArgs p;
   p.npairs = n;
-  p.pslot = slots ? pb.args + 2 * n : nullptr;
-  p.qscan = pb.args; p.tscan = pb.args + n;
+  p.pcount = dcount;
+  if (dlist) {
+    p.qscan = dlist; p.tscan = dlist + n; p.pslot = dlist + 2 * n;
+  } else {
+    // one upload of the launch's lists: query scans | train scans | slots (stream-ordered after
+    // the previous launch's kernels, which read the same staging area)
+    std::vector<int> host((size_t)3 * n);
+    std::copy(qs, qs + n, host.begin());
+    std::copy(ts, ts + n, host.begin() + n);
+    if (slots) std::copy(slots, slots + n, host.begin() + 2 * n);
+    OCHK(c, hipMemcpyAsync(pb.args, host.data(), (size_t)(slots ? 3 : 2) * n * 4, hipMemcpyHostToDevice, st));
+    p.pslot = slots ? pb.args + 2 * n : nullptr;
+    p.qscan = pb.args; p.tscan = pb.args + n;
+  }
   p.qdesc = qe->desc; p.tdesc = te->desc;
   p.qp3d = qe->p3d; p.tp3d = te->p3d;
   p.qn = qe->nkp; p.tn = te->nkp;
   p.qcap = qe->g.cap; p.tcap = te->g.cap;
   p.bstride = pb.qcap;
   p.frac = frac;
-  const int b0 = slots ? 0 : p0;  // buffer base (slots index from buffer 0)
+  const int b0 = (slots || dlist) ? 0 : p0;  // buffer base (slots index from buffer 0)
+  const int gp = dlist ? std::min(n, kListSlots) : n;  // grid pair slots (device lists: strided)
   p.mscratch = pb.mscratch + (size_t)b0 * pb.qcap;
   p.mout = pb.mout ? pb.mout + (size_t)b0 * pb.qcap * 3 : nullptr;
   p.rec = pb.rec + (size_t)b0 * pb.qcap * 9;
@@ -1640,15 +1831,15 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   p.T = pb.T + b0 * 7;
   {
     TimedScope t(c, kT_orb_match);
-    hipLaunchKernelGGL(k_orb_mfill, dim3(n, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
+    hipLaunchKernelGGL(k_orb_mfill, dim3(gp, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
     static const bool valu = getenv("LISLAM_XDIST_VALU") != nullptr;  // developer A/B switch
     if (valu)
-      hipLaunchKernelGGL(k_orb_xdist, dim3(n, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
+      hipLaunchKernelGGL(k_orb_xdist, dim3(gp, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
     else
-      hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(n, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
-    hipLaunchKernelGGL(k_orb_match, dim3(n), dim3(kPairThreads), 0, st, p);
+      hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
+    hipLaunchKernelGGL(k_orb_match, dim3(gp), dim3(kPairThreads), 0, st, p);
   }
-  if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(n), dim3(kLmThreads), 0, st, p, 20); }
+  if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(gp), dim3(kLmThreads), 0, st, p, 20); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -1668,10 +1859,20 @@ struct OrbBatch {
   int* outS = nullptr;      // [S][8]
   hipStream_t side = nullptr;  // the batch front end runs here, concurrently with the odometry chain
   hipEvent_t done = nullptr;
+  // the device-decided re-detection cascade (k_orb_decide): state, lists, and its verdict copied
+  // to pinned host memory; `pending` until a reader of the outputs has checked it
+  CascadeArgs cs{};
+  int* h_status = nullptr;   // pinned [2]
+  hipEvent_t settled = nullptr;
+  bool pending = false;
+  int pending_n = 0;
+  int info[2] = {-1, 0};     // lislam_batch_orb_cascade_info
   ~OrbBatch() {
     if (side) (void)hipStreamSynchronize(side);
     if (side) (void)hipStreamDestroy(side);
     if (done) (void)hipEventDestroy(done);
+    if (settled) (void)hipEventDestroy(settled);
+    if (h_status) (void)hipHostFree(h_status);
     delete e1;
     delete e2;
     for (void* p : allocs) (void)hipFree(p);
@@ -1719,6 +1920,18 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     OCHK(c, hipMalloc(&q, (size_t)b->max_scans * 8 * 4));
     ob->allocs.push_back(q);
     ob->outS = static_cast<int*>(q);
+    const size_t S = (size_t)b->max_scans;
+    CascadeArgs& cs = ob->cs;
+    OCHK(c, hipMalloc(&q, S * 3 + 64));
+    ob->allocs.push_back(q);
+    cs.pset = static_cast<int8_t*>(q); cs.cur2 = cs.pset + S; cs.have2 = cs.pset + 2 * S;
+    OCHK(c, hipMalloc(&q, (S * 8 + 8) * 4));
+    ob->allocs.push_back(q);
+    int* qi = static_cast<int*>(q);
+    cs.e2list = qi; cs.plist = qi + S; cs.redet = qi + 7 * S; cs.e2cnt = qi + 8 * S; cs.pcnt = qi + 8 * S + 2;
+    cs.status = qi + 8 * S + 4;
+    OCHK(c, hipHostMalloc((void**)&ob->h_status, 2 * sizeof(int), hipHostMallocDefault));
+    OCHK(c, hipEventCreateWithFlags(&ob->settled, hipEventDisableTiming));
   }
   *out = ob;
   return LISLAM_OK;
@@ -1800,7 +2013,80 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
   return LISLAM_OK;
 }
 
+// The same cascade with every decision on the device: no host synchronization.  The first
+// attempts of all pairs, then `rounds` passes of (re-detections the last decision listed, the
+// re-attempts, decision), then the final 2n-against-2n matches.  After the first attempts every
+// pair to redo follows a failed pair, so pass 0 only re-attempts against 2n sets; later passes
+// (a re-attempt that failed again, flipping the next pair's previous set) need both groups.  One
+// pass resolves the bench sequence (its re-detections are isolated); a sequence whose re-attempts
+// flip further ends "not converged", and orb_settle redoes the batch with host rounds
+// (batch_intensity_odometry) before anything reads it.  LISLAM_ORB_ROUNDS sets the passes
+// (default 1).
+int cascade_rounds() {
+  const char* e = getenv("LISLAM_ORB_ROUNDS");
+  const int r = e ? atoi(e) : 1;
+  return r < 1 ? 1 : r > 64 ? 64 : r;
+}
+
+int batch_intensity_odometry_dev(lislam_batch* b, OrbBatch* ob, int n_scans) {
+  lislam_ctx* c = b->ctx;
+  hipStream_t st = c->stream;
+  const uint8_t* img = b->fa.img_int;
+  const float4* trk = reinterpret_cast<const float4*>(b->fa.track);
+  ORC(engine_detect_slots(ob->e1, img, trk, 0, n_scans));
+  const int np = n_scans - 1;
+  std::vector<int> qs(np), ts(np);
+  for (int k = 1; k < n_scans; k++) { qs[k - 1] = k; ts[k - 1] = k - 1; }
+  ORC(run_pairs(c, ob->e1, ob->e1, qs.data(), ts.data(), np, 0.3, ob->pb, 0, true));
+  CascadeArgs cs = ob->cs;
+  cs.n = n_scans;
+  cs.stats = ob->pb.stats;
+  hipLaunchKernelGGL(k_orb_decide, dim3(1), dim3(256), 0, st, cs, 0);
+  const int rounds = cascade_rounds();
+  for (int r = 0; r < rounds; r++) {
+    ORC(engine_select_from(ob->e2, ob->e1, img, trk, cs.e2list, cs.e2cnt, n_scans));
+    for (int g2 = r == 0 ? 1 : 0; g2 < 2; g2++)
+      ORC(run_pairs(c, ob->e1, g2 ? ob->e2 : ob->e1, nullptr, nullptr, n_scans, 0.3, ob->pb, 0, true, nullptr,
+                    cs.plist + (size_t)g2 * 3 * n_scans, cs.pcnt + g2));
+    hipLaunchKernelGGL(k_orb_decide, dim3(1), dim3(256), 0, st, cs, r + 1 < rounds ? 1 : 2);
+  }
+  ORC(engine_select_from(ob->e2, ob->e1, img, trk, cs.e2list, cs.e2cnt, n_scans));
+  ORC(run_pairs(c, ob->e2, ob->e2, nullptr, nullptr, n_scans, 0.2, ob->pb, 0, true, nullptr, cs.plist, cs.pcnt));
+  hipLaunchKernelGGL(k_orb_out, dim3(cdiv(n_scans, 256)), dim3(256), 0, st, ob->outS, ob->outT, ob->pb.stats, ob->pb.T,
+                     cs.redet, ob->e1->nkp, n_scans);
+  OCHK(c, hipGetLastError());
+  OCHK(c, hipMemcpyAsync(ob->h_status, cs.status, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+  OCHK(c, hipEventRecord(ob->settled, st));
+  ob->pending = true;
+  ob->pending_n = n_scans;
+  return LISLAM_OK;
+}
+
+bool orb_host_cascade() {  // LISLAM_ORB_HOST_CASCADE = 1: decide between rounds on the host
+  static const bool v = getenv("LISLAM_ORB_HOST_CASCADE") && atoi(getenv("LISLAM_ORB_HOST_CASCADE")) == 1;
+  return v;
+}
+
 }  // namespace
+
+// Before the outputs of a device-decided cascade are read: wait for its verdict (the reader
+// synchronizes anyway) and, if it did not converge in kCascadeRounds passes, redo the batch with
+// host rounds.
+int orb_settle(lislam_batch* b) {
+  OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
+  if (!ob || !ob->pending) return LISLAM_OK;
+  lislam_ctx* c = b->ctx;
+  OCHK(c, hipEventSynchronize(ob->settled));
+  ob->pending = false;
+  ob->info[0] = ob->h_status[0];
+  ob->info[1] = ob->h_status[1];
+  if (ob->h_status[0] == 1) return LISLAM_OK;
+  const hipStream_t main_stream = c->stream;
+  c->stream = ob->side;
+  const int rc = batch_intensity_odometry(b, ob, ob->pending_n);
+  c->stream = main_stream;
+  return rc;
+}
 
 extern "C" {
 
@@ -1820,7 +2106,11 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
   const hipStream_t main_stream = c->stream;
   OCHK(c, hipStreamWaitEvent(ob->side, b->ev_images, 0));
   c->stream = ob->side;
-  const int rc = batch_intensity_odometry(b, ob, n_scans);
+  ob->pending = false;  // a newer batch replaces results nobody read
+  ob->info[0] = -1;
+  ob->info[1] = 0;
+  const int rc = (orb_host_cascade() || n_scans < 2 || n_scans > kCascadeMax) ? batch_intensity_odometry(b, ob, n_scans)
+                                                                               : batch_intensity_odometry_dev(b, ob, n_scans);
   c->stream = main_stream;
   OCHK(c, hipEventRecord(ob->done, ob->side));
   OCHK(c, hipStreamWaitEvent(main_stream, ob->done, 0));
@@ -1973,9 +2263,20 @@ int lislam_orb_match(lislam_ctx* c, const uint8_t* qdesc, int32_t nq, const uint
 }  // extern "C"
 
 // Outputs of lislam_batch_intensity_odometry for lislam_batch_download.
+extern "C" int lislam_batch_orb_cascade_info(lislam_batch* b, int32_t* info) {
+  if (!b || !info) return LISLAM_ERR_ARG;
+  OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
+  if (!ob) return LISLAM_ERR_STATE;
+  ORC(orb_settle(b));
+  info[0] = ob->info[0];
+  info[1] = ob->info[1];
+  return LISLAM_OK;
+}
+
 int lislam_orb_batch_output(lislam_batch* b, int what, int scan, const void** src, int* cnt, size_t* esz) {
   OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
   if (!ob) return LISLAM_ERR_STATE;
+  ORC(orb_settle(b));
   const Geom& g = ob->e1->g;
   switch (what) {
     case LISLAM_OUT_ORB_T: *src = ob->outT + (size_t)scan * 7; *cnt = 7; *esz = 8; return LISLAM_OK;

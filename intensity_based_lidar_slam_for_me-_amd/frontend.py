@@ -212,6 +212,14 @@ class Batch:
         nat.check(rc, self.ctx.h, "lislam_batch_intensity_odometry")
         self._mask_keep = m
 
+    def orb_cascade_info(self):
+        """(converged on the device: 1 / redone with host rounds: 0 / host rounds only: -1, device
+        decision passes) of the last intensity_odometry (lislam_batch_orb_cascade_info)."""
+        info = np.zeros(2, np.int32)
+        rc = self.ctx.lib.lislam_batch_orb_cascade_info(self.h, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        nat.check(rc, self.ctx.h, "lislam_batch_orb_cascade_info")
+        return int(info[0]), int(info[1])
+
     def ground(self, n: int):
         """groundPlaneExtraction of scans [0, n) of the batch (results: ground_result)."""
         nat.check(self.ctx.lib.lislam_batch_ground(self.h, n), self.ctx.h, "lislam_batch_ground")

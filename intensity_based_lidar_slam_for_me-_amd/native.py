@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_mapopt_step_corner", "lislam_laser_mapping",
     "lislam_map_set_timing", "lislam_map_kernel_times",
     "lislam_orb_detect", "lislam_orb_match", "lislam_intensity_tracker_create", "lislam_intensity_tracker_destroy",
-    "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_ground", "lislam_ground_extract",
+    "lislam_intensity_tracker_step", "lislam_batch_intensity_odometry", "lislam_batch_orb_cascade_info", "lislam_batch_ground", "lislam_ground_extract",
     "lislam_lmap_create", "lislam_lmap_destroy", "lislam_lmap_step", "lislam_lmap_counts", "lislam_lmap_points",
     "lislam_batch_odometry_gated", "lislam_odom_step_gated", "lislam_batch_mapopt", "lislam_batch_mapopt_corner", "lislam_loop_icp", "lislam_odom_fuser_create", "lislam_odom_fuser_destroy", "lislam_odom_fuse",
 )
@@ -168,6 +168,7 @@ def load(path: str = LIB_PATH):
     L.lislam_intensity_tracker_destroy.argtypes = [vp]
     L.lislam_intensity_tracker_step.argtypes = [vp, vp, vp, vp, vp]
     L.lislam_batch_intensity_odometry.argtypes = [vp, _i32, _i32, vp]
+    L.lislam_batch_orb_cascade_info.argtypes = [vp, _i32p]
     L.lislam_batch_ground.argtypes = [vp, _i32]
     L.lislam_lmap_create.argtypes = [vp, ctypes.c_float, ctypes.c_float, ctypes.POINTER(vp)]
     L.lislam_lmap_destroy.argtypes = [vp]

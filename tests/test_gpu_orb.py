@@ -4,6 +4,8 @@ Keypoints (positions, angles, responses, octaves), descriptors, cloud points and
 integer / byte / same-order float work and must be bit-exact; T_s2s within the north-star pose
 tolerance 1e-4 (measured agreement ~1e-15).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -124,3 +126,45 @@ def test_batch_intensity_odometry_matches_tracker(pkg, oracle, ctx, frames):
     rkp, _, _ = oracle.orb_detect(si[2], stt[2], 1000, mask)
     assert np.array_equal(kp, rkp)
     b.close()
+
+
+def test_batch_redetection_cascade_on_device(pkg, oracle, ctx, frames):
+    """The re-detection rule decided on the device (k_orb_decide, no host synchronization): runs of
+    repeated frames make first attempts fail back to back, so a pair's previous set depends on the
+    pair before it, over several decision passes (intensity_feature_tracker.cpp:631-687)."""
+    scans, _, _ = frames
+    order = [0, 1, 1, 1, 2, 3, 3, 4, 4, 4, 4, 5, 5]
+    seq = scans[order].copy()
+    seq[5, ..., 3] = 0  # a blank intensity image: its pairs fail against both its sets, so a
+    #                     re-attempt fails again and the next pair's previous set flips in a later pass
+    n = seq.shape[0]
+    feats = [oracle.scan_registration(s) for s in seq]
+    si = np.stack([f.img_intensity for f in feats])
+    stt = np.stack([f.cloud_track for f in feats])
+    mask = oracle.hand_held_mask()
+    rst, rT = oracle.intensity_odometry(si, stt, 1000, mask)
+    assert int(np.sum(rst[1:, 1] == 1)) >= 3  # several re-detections in this sequence
+    b = pkg.Batch(ctx, n)
+    b.upload(seq)
+    b.extract(n)
+    nat = pkg.native
+    seen = set()
+    # one device pass (the default: this sequence needs more, so the batch is redone with host
+    # rounds when its outputs are read), then enough passes to converge on the device
+    for rounds in ("1", "8"):
+        os.environ["LISLAM_ORB_ROUNDS"] = rounds
+        try:
+            for _ in range(2):  # a second batch call over the same scans replaces the first's results
+                b.intensity_odometry(n, 1000, mask)
+        finally:
+            del os.environ["LISLAM_ORB_ROUNDS"]
+        for k in range(1, n):
+            st = b.download(nat.OUT_ORB_STATS, k)
+            T = b.download(nat.OUT_ORB_T, k)
+            assert list(st[:5]) == list(rst[k, :5]) and st[7] == rst[k, 7], (rounds, k, st, rst[k])
+            assert np.max(np.abs(T - rT[k])) < POSE_TOL, (rounds, k, T, rT[k])
+        seen.add((rounds, b.orb_cascade_info()))
+    b.close()
+    print("cascade info", sorted(seen))
+    info = dict(seen)
+    assert info["8"][0] == 1 and info["1"][0] == 0, seen  # converged on the device / redone with host rounds
