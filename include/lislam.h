@@ -141,7 +141,8 @@ int lislam_batch_odometry(lislam_batch* b, int32_t n_scans, int32_t chain_len);
  * optimized only when use_aloam[k] != 0 — the sharp cloud's frame_id is "skip_intensity", i.e.
  * the intensity tracker skipped scan k (scanRegistration.cpp:603-609; LISLAM_OUT_ORB_STATS[0] ==
  * 0).  Otherwise para keeps the previous estimate and the pose accumulates it (:716-717).
- * use_aloam[n_scans]: host or device memory.  lislam_batch_odometry = every use_aloam set. */
+ * use_aloam[n_scans]: host or device memory; a host array is copied before the call returns, so
+ * it may be freed then.  lislam_batch_odometry = every use_aloam set. */
 int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_len, const int32_t* use_aloam);
 /* Enable per-kernel HIP-event timing: every following extract / odometry call records events on
  * the stream (no host synchronization). */

@@ -218,6 +218,8 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (b->ground) lislam_free_ground(b->ground);
   if (b->wire) hipFree(b->wire);
   if (b->ev_images) hipEventDestroy(b->ev_images);
+  if (b->stage_ev) hipEventDestroy(b->stage_ev);
+  if (b->h_stage) hipHostFree(b->h_stage);
   delete b;
   return LISLAM_OK;
 }
@@ -367,18 +369,40 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   lislam_ctx* c = b->ctx;
   OdomArgs o = b->oa;
   o.gate = nullptr;
-  if (use_aloam) {
-    HIPCHK(c, hipMemcpyAsync(b->d_gate, use_aloam, sizeof(int) * n_scans, hipMemcpyDefault, c->stream));
-    o.gate = b->d_gate;
-  }
   o.S = n_scans;
   o.chain_len = chain_len;
   o.n_chains = n_scans > 1 ? (n_scans - 1 + chain_len - 1) / chain_len : 0;
   o.init_state = nullptr;
   o.dbg = getenv("LISLAM_ASSOC_DEBUG") ? atoi(getenv("LISLAM_ASSOC_DEBUG")) : 0;
-  if (init_host) {
-    HIPCHK(c, hipMemcpyAsync(b->d_init, init_host, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
-    o.init_state = b->d_init;
+  if (use_aloam || init_host) {
+    // the caller's arrays -> pinned staging -> device, so they may be freed on return
+    const size_t init_bytes = sizeof(double) * 14 * (size_t)b->max_scans;
+    if (!b->h_stage) {
+      HIPCHK(c, hipHostMalloc(&b->h_stage, init_bytes + sizeof(int) * (size_t)b->max_scans, hipHostMallocDefault));
+      HIPCHK(c, hipEventCreateWithFlags(&b->stage_ev, hipEventDisableTiming));
+    }
+    if (b->stage_busy) HIPCHK(c, hipEventSynchronize(b->stage_ev));  // the previous upload has been read
+    double* hi = static_cast<double*>(b->h_stage);
+    int* hg = reinterpret_cast<int*>(static_cast<char*>(b->h_stage) + init_bytes);
+    if (use_aloam) {
+      hipPointerAttribute_t attr{};
+      const bool on_device = hipPointerGetAttributes(&attr, use_aloam) == hipSuccess && attr.type == hipMemoryTypeDevice;
+      (void)hipGetLastError();  // an unregistered host pointer reports an error here
+      if (on_device) {
+        HIPCHK(c, hipMemcpyAsync(b->d_gate, use_aloam, sizeof(int) * n_scans, hipMemcpyDeviceToDevice, c->stream));
+      } else {
+        std::memcpy(hg, use_aloam, sizeof(int) * n_scans);
+        HIPCHK(c, hipMemcpyAsync(b->d_gate, hg, sizeof(int) * n_scans, hipMemcpyHostToDevice, c->stream));
+      }
+      o.gate = b->d_gate;
+    }
+    if (init_host) {
+      std::memcpy(hi, init_host, sizeof(double) * 14 * o.n_chains);
+      HIPCHK(c, hipMemcpyAsync(b->d_init, hi, sizeof(double) * 14 * o.n_chains, hipMemcpyHostToDevice, c->stream));
+      o.init_state = b->d_init;
+    }
+    HIPCHK(c, hipEventRecord(b->stage_ev, c->stream));
+    b->stage_busy = true;
   }
   // chain groups: LISLAM_ODOM_GROUPS (default 2) streams, so one group's solves overlap another's
   // association (a solve occupies one workgroup per chain, far from filling the device)

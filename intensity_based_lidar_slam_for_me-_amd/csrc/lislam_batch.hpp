@@ -20,6 +20,12 @@ struct lislam_batch {
   OdomArgs oa{};
   double* d_init = nullptr;
   int* d_gate = nullptr;  // [max_scans] use_aloam of lislam_batch_odometry_gated
+  // pinned staging of the odometry's host inputs (init states, use_aloam): the caller's arrays
+  // are copied here before the asynchronous upload, so they may be freed on return; stage_ev
+  // guards the staging against the next call until the previous upload has run
+  void* h_stage = nullptr;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_busy = false;
   bool timing = false;
   // per-call event sets recorded on the stream while timing is on; read back (and released)
   // by lislam_batch_kernel_times, so the timed region never blocks on the host.
