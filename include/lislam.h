@@ -130,6 +130,14 @@ int lislam_batch_create(lislam_ctx* ctx, int32_t max_scans, lislam_batch** out);
 int lislam_batch_destroy(lislam_batch* b);
 /* Copy n_scans clouds from host memory (contiguous, n_scans*n_scans_cfg*width points). */
 int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout);
+/* The same ingest without blocking the host: the bytes go to the device on the batch's copy
+ * stream in chunks of 16 scans, and each chunk is parsed (k_unpack_layout) on the context stream
+ * as soon as it has landed, after whatever the context stream was doing before (the previous
+ * batch's extraction still reading the input buffer).  So the transfer of the next batch overlaps
+ * the processing of the current one.  `points` must stay valid and unchanged until the context
+ * stream has passed the upload (lislam_synchronize, or any download); pinned memory makes the
+ * copies asynchronous. */
+int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout);
 /* Device pointer of the packed float4 (x,y,z,intensity) input buffer [max_scans][H*W]. */
 int lislam_batch_input_device_ptr(lislam_batch* b, void** dptr);
 /* a1..a7 for scans [0, n_scans) of the batch. */

@@ -219,6 +219,13 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (b->wire) hipFree(b->wire);
   if (b->ev_images) hipEventDestroy(b->ev_images);
   if (b->stage_ev) hipEventDestroy(b->stage_ev);
+  if (b->copy_stream) {
+    hipStreamSynchronize(b->copy_stream);
+    hipStreamDestroy(b->copy_stream);
+  }
+  for (hipEvent_t e : b->chunk_landed) hipEventDestroy(e);
+  for (hipEvent_t e : b->chunk_parsed) hipEventDestroy(e);
+  if (b->ring) hipFree(b->ring);
   if (b->h_stage) hipHostFree(b->h_stage);
   delete b;
   return LISLAM_OK;
@@ -261,6 +268,56 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return LISLAM_OK;
+}
+
+int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
+  if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  static const lislam_point_layout kPacked{16, 0, 4, 8, 12};
+  const lislam_point_layout* lay = (!layout || is_packed(layout)) ? &kPacked : layout;
+  if (lay->point_step < 4 || std::max({lay->off_x, lay->off_y, lay->off_z, lay->off_intensity}) + 4 > lay->point_step)
+    return fail(c, LISLAM_ERR_ARG, "bad point layout");
+  const size_t scan_bytes = (size_t)b->N * lay->point_step;
+  const size_t need = (size_t)b->max_scans * scan_bytes;
+  if (b->ring_bytes < need) {
+    // a new staging area: everything queued on either stream may still use the old one
+    if (b->copy_stream) HIPCHK(c, hipStreamSynchronize(b->copy_stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (b->ring) hipFree(b->ring);
+    b->ring = nullptr;
+    b->ring_bytes = 0;
+    if (hipMalloc(&b->ring, need) != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "staging allocation failed");
+    b->ring_bytes = need;
+    std::fill(b->chunk_used.begin(), b->chunk_used.end(), 0);
+  }
+  if (!b->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
+  constexpr int kChunk = 16;
+  const int nchunks = (n_scans + kChunk - 1) / kChunk;
+  while ((int)b->chunk_landed.size() < nchunks) {
+    hipEvent_t e1 = nullptr, e2 = nullptr;
+    HIPCHK(c, hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    b->chunk_landed.push_back(e1);
+    b->chunk_parsed.push_back(e2);
+    b->chunk_used.push_back(0);
+  }
+  const lislam::WireLayout L{lay->point_step, lay->off_x, lay->off_y, lay->off_z, lay->off_intensity};
+  for (int k = 0; k < nchunks; k++) {
+    const int s0 = k * kChunk, ns = std::min(kChunk, n_scans - s0);
+    uint8_t* dst = static_cast<uint8_t*>(b->ring) + (size_t)s0 * scan_bytes;
+    // the chunk's staging bytes are free once the previous upload's parse of them has run
+    if (b->chunk_used[k]) HIPCHK(c, hipStreamWaitEvent(b->copy_stream, b->chunk_parsed[k], 0));
+    HIPCHK(c, hipMemcpyAsync(dst, static_cast<const uint8_t*>(points) + (size_t)s0 * scan_bytes, (size_t)ns * scan_bytes,
+                             hipMemcpyHostToDevice, b->copy_stream));
+    HIPCHK(c, hipEventRecord(b->chunk_landed[k], b->copy_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, b->chunk_landed[k], 0));
+    lislam::launch_unpack_layout(dst, ns * b->N, L, const_cast<lislam::P4*>(b->fa.pts) + (size_t)s0 * b->N, c->stream);
+    HIPCHK(c, hipEventRecord(b->chunk_parsed[k], c->stream));
+    b->chunk_used[k] = 1;
+  }
+  HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
 

@@ -45,7 +45,14 @@ struct lislam_batch {
   void* orb = nullptr;  // ORB engine of lislam_batch_intensity_odometry (lislam_orb.hip)
   void* ground = nullptr;
   void* wire = nullptr;        // device staging of PointCloud2 bytes (lislam_batch_upload / download_cloud)
-  size_t wire_bytes = 0;  // ground-plane engine of lislam_batch_ground (lislam_ground.hip)
+  size_t wire_bytes = 0;
+  // lislam_batch_upload_async: the copy stream, a whole-batch staging area, and per 16-scan chunk
+  // the "landed" (copy stream) and "parsed" (context stream) events
+  hipStream_t copy_stream = nullptr;
+  void* ring = nullptr;
+  size_t ring_bytes = 0;
+  std::vector<hipEvent_t> chunk_landed, chunk_parsed;
+  std::vector<char> chunk_used;
   hipEvent_t get_event() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e = nullptr;

@@ -1459,6 +1459,11 @@ __global__ void k_unpack_layout(const uint8_t* raw, int n, WireLayout L, P4* out
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = raw + (size_t)i * L.step;
+  if (((L.step | L.ox | L.oy | L.oz | L.oi) & 3u) == 0) {  // 4-byte aligned fields (every ROS layout): dword loads
+    const float* f = reinterpret_cast<const float*>(p);
+    st4(out + i, P4{f[L.ox >> 2], f[L.oy >> 2], f[L.oz >> 2], f[L.oi >> 2]});
+    return;
+  }
   st4(out + i, P4{ld_f32_bytes(p + L.ox), ld_f32_bytes(p + L.oy), ld_f32_bytes(p + L.oz), ld_f32_bytes(p + L.oi)});
 }
 // every byte of a point is written: the four fields, zeros elsewhere

@@ -183,6 +183,12 @@ class Batch:
         rc = self.ctx.lib.lislam_batch_upload(self.h, nat.ptr(a), n, ctypes.byref(layout or PACKED_XYZI))
         nat.check(rc, self.ctx.h, "lislam_batch_upload")
 
+    def upload_async(self, ptr, n: int, layout: nat.PointLayout | None = None):
+        """lislam_batch_upload_async of n scans at host address ptr (a ctypes pointer to pinned
+        memory that stays valid until the context stream has passed the upload)."""
+        rc = self.ctx.lib.lislam_batch_upload_async(self.h, ptr, n, ctypes.byref(layout or PACKED_XYZI))
+        nat.check(rc, self.ctx.h, "lislam_batch_upload_async")
+
     def extract(self, n: int):
         nat.check(self.ctx.lib.lislam_batch_extract(self.h, n), self.ctx.h, "lislam_batch_extract")
 

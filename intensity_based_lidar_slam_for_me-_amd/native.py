@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "lislam_ctx_create", "lislam_ctx_destroy", "lislam_last_error", "lislam_synchronize",
     "lislam_set_stream", "lislam_get_stream", "lislam_scan_registration", "lislam_odom_create",
     "lislam_odom_destroy", "lislam_odom_step", "lislam_batch_create", "lislam_batch_destroy",
-    "lislam_batch_upload", "lislam_batch_download_cloud", "lislam_batch_input_device_ptr", "lislam_batch_extract",
+    "lislam_batch_upload", "lislam_batch_upload_async", "lislam_batch_download_cloud", "lislam_batch_input_device_ptr", "lislam_batch_extract",
     "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
     "lislam_batch_download", "lislam_eval_factors", "lislam_eval_factors_raw", "lislam_set_tie_order",
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
@@ -137,6 +137,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_create.argtypes = [vp, _i32, ctypes.POINTER(vp)]
     L.lislam_batch_destroy.argtypes = [vp]
     L.lislam_batch_upload.argtypes = [vp, vp, _i32, ctypes.POINTER(PointLayout)]
+    L.lislam_batch_upload_async.argtypes = [vp, vp, _i32, ctypes.POINTER(PointLayout)]
     L.lislam_batch_input_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
     L.lislam_batch_extract.argtypes = [vp, _i32]
     L.lislam_batch_odometry.argtypes = [vp, _i32, _i32]
