@@ -22,6 +22,20 @@ def short(name):
     return name.split("(")[0].replace("lislam::", "")
 
 
+# rocprof kernel (base name, no "void", namespaces or template arguments) -> the bench's logical
+# kernel (native.KERNELS / the ORB timers); kernels of one logical name are summed per step
+LOGICAL = [("k_front_", "k_scan_front"), ("k_scan_lines", "k_scan_lines"), ("k_scan_compact", "k_scan_compact"),
+           ("k_target_index", "k_target_index"), ("k_odom_assoc", "k_odom_assoc"), ("k_odom_lm", "k_odom_lm")]
+
+
+def logical(name):
+    base = short(name).replace("void ", "").split("::")[-1].split("<")[0]
+    for pre, lg in LOGICAL:
+        if base.startswith(pre):
+            return lg
+    return None
+
+
 def pmc(path):
     agg = {}
     for r in csv.DictReader(open(path)):
@@ -50,6 +64,21 @@ for k in fetch:
     out["kernels"][k] = {"launches_profiled": nf, "fetch_kib_per_launch": f / nf, "write_kib_per_launch": w / nw,
                          "traffic_bytes_per_launch": per,
                          "avg_ns": float(s.get("AverageNs", 0) or 0), "calls": int(s.get("Calls", 0) or 0)}
+# per logical kernel: traffic per launch of the logical kernel (its rocprof kernels' traffic per
+# step / its launches per step), what bench.py's roofline line looks up
+steps_pmc = 1  # profile_round.sh's PMC passes run one step
+lg = {}
+for k in fetch:
+    name = logical(k)
+    if not name:
+        continue
+    f, nf = fetch[k]
+    w, nw = write.get(k, [0.0, 1])
+    a = lg.setdefault(name, [0.0, 0])
+    a[0] += (2 * f + w) * 1024
+    a[1] += nf
+out["kernels_logical"] = {k: {"launches_profiled": v[1], "traffic_bytes_per_launch": v[0] / max(1, v[1])}
+                          for k, v in lg.items()}
 # The roofline's launch time: bench.py measures the dominant kernel in its final isolated stage
 # pass (no other stream active); the same launches are the last `isolated_launches` of that kernel
 # in the kernel trace, so rocprof's average over them is the cross-check of the line's avg_launch_ms.
@@ -58,7 +87,7 @@ dom, n_iso = rl["kernel"], int(rl.get("isolated_launches", 0))
 durs = []
 trace_csv = os.path.join(src, "trace", "trace_kernel_trace.csv")
 if n_iso and os.path.exists(trace_csv):
-    rows = [r for r in csv.DictReader(open(trace_csv)) if short(r["Kernel_Name"]).endswith(dom)]
+    rows = [r for r in csv.DictReader(open(trace_csv)) if logical(r["Kernel_Name"]) == dom]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[-n_iso:]]
 if durs:
