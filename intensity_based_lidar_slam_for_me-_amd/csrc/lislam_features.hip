@@ -982,7 +982,7 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
 // where the state lives.
 template <int kS>
 __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int line, LineLists& ll, uint64_t* lmask,
-                                              P4* stage, P4* ring, uint32_t* vel, uint16_t* vidx) {
+                                              float* curvl, P4* stage, P4* ring, uint32_t* vel, uint16_t* vidx) {
   const int lane = lane_id();
   const int N = a.N, H = a.H;
   const int* lo = a.line_off + (size_t)s * (H + 1);
@@ -998,7 +998,6 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   // curvature (scanRegistration.cpp:397-412) and neighbour links (suppress).  Every point of the
   // line (and the 64 before / after it) is loaded once: slot t's neighbours come from an LDS ring
   // of three 64-point slots (t - 1, t, t + 1), the next slot's load in flight meanwhile.
-  float cr[kS];
   uint32_t linkb = 0;
   auto ld_slot = [&](int t) -> P4 {  // cloud point off + 64 t + lane (zero outside the cloud)
     const int i = off + 64 * t + lane;
@@ -1010,7 +1009,6 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   P4 nxt = ld_slot(1);
 #pragma unroll
   for (int t = 0; t < kS; t++) {
-    cr[t] = 0.f;
     if (t >= nsl) continue;
     ring_at(t + 1)[lane] = nxt;
     if (t + 1 < nsl) nxt = ld_slot(t + 2);
@@ -1034,7 +1032,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         c = dX * dX + dY * dY + dZ * dZ;
       }
       curv[i] = c;
-      cr[t] = c;
+      curvl[k] = c;
       if (k + 1 < len) {
         const P4 p0 = nb(0), p1 = nb(1);
         const float dx = p1.x - p0.x, dy = p1.y - p0.y, dz = p1.z - p0.z;
@@ -1053,11 +1051,18 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   wave_sync<true>();
   PHASE(0);
 
+  // The six segments are walked one at a time in a window of kW register slots: window slot u,
+  // lane l holds line point wb + 64 u + l (wb = the segment's start rounded down to a slot), which
+  // covers the segment and the 5 points a pick past its end can mark.  Marks below wb fall into
+  // earlier segments, which no later walk reads.  The window's curvature comes from LDS (curvl);
+  // the per-lane slot bitmasks of the whole line (pick / lsh / shp / flt) are shifted in and out.
+  constexpr int kSeg = (64 * kS - 11 + 5) / 6;  // longest segment of a line of 64 kS points
+  constexpr int kW = (68 + kSeg + 63) / 64;
   // Suppression (scanRegistration.cpp:481-504) of pick ind, ind itself included: forward marks
   // ind+1.. while link[ind], link[ind+1], ... hold (at most 5), backward ind-1.. while
   // link[ind-1], ... hold.
   uint32_t pick = 0, lsh = 0, shp = 0, flt = 0;  // per-lane slot bitmasks
-  auto mark = [&](int ind) {
+  auto mark = [&](int ind, int wb, uint32_t& pw) {
     const int ti = ind >> 6, b = ind & 63;
     const uint64_t Wm = lmask[ti], W0 = lmask[ti + 1], W1 = lmask[ti + 2];
     const uint32_t fwd5 = (uint32_t)((b == 0 ? W0 : ((W0 >> b) | (W1 << (64 - b)))) & 31u);       // link[ind .. ind+4]
@@ -1067,10 +1072,9 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
     const int nb = bz ? 4 - (31 - (int)__builtin_clz(bz)) : 5;
     const int k0 = ind - nb, k1 = ind + nf;
 #pragma unroll
-    for (int t = 0; t < kS; t++) {
-      if (t < (k0 >> 6) || t > (k1 >> 6)) continue;
-      const int k = lane + 64 * t;
-      if (k >= k0 && k <= k1) pick |= 1u << t;
+    for (int u = 0; u < kW; u++) {
+      const int k = wb + 64 * u + lane;
+      if (k >= k0 && k <= k1) pw |= 1u << u;
     }
   };
 
@@ -1081,19 +1085,26 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
     for (int j = 0; j < 6; j++) {
       const int sp = sI + (eI - sI) * j / 6;
       const int ep = sI + (eI - sI) * (j + 1) / 6 - 1;
-      const int t0 = sp >> 6, t1 = ep >> 6;
+      const int t0 = sp >> 6, wb = 64 * t0;
+      uint64_t kw[kW];
+      uint32_t es = 0, ef = 0;  // window slots passing the sharp (> 0.1) / flat (< 0.1) test
+#pragma unroll
+      for (int u = 0; u < kW; u++) {
+        const int k = wb + 64 * u + lane;
+        const bool in = k >= sp && k <= ep;
+        const float c = in ? curvl[k] : 0.f;
+        kw[u] = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)k;
+        if (in && (double)c > 0.1) es |= 1u << u;
+        if (in && (double)c < 0.1) ef |= 1u << u;
+      }
+      uint32_t pw = (pick >> t0) & ((1u << kW) - 1u), lw = 0, sw = 0, fw = 0;
       // ---- sharp picks: largest (curvature, index) first (:450-506); at most 20 per segment
       for (int largest = 1; largest <= 20; largest++) {
+        const uint32_t ok = es & ~pw;
         uint64_t best = 0;
 #pragma unroll
-        for (int t = 0; t < kS; t++) {
-          if (t < t0 || t > t1) continue;
-          const int k = lane + 64 * t;
-          if (k >= sp && k <= ep && !((pick >> t) & 1u) && (double)cr[t] > 0.1) {
-            const uint64_t key = ((uint64_t)__float_as_uint(cr[t]) << 32) | (uint32_t)k;
-            best = key > best ? key : best;
-          }
-        }
+        for (int u = 0; u < kW; u++)
+          if ((ok >> u) & 1u) best = kw[u] > best ? kw[u] : best;
         best = wave_max_u64(best);
         if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
         const int ind = (int)(uint32_t)best;
@@ -1102,36 +1113,36 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
           ll.less_sharp[n_lsharp] = ind;
         }
         if (lane == (ind & 63)) {
-          lsh |= 1u << (ind >> 6);
-          if (largest <= 2) shp |= 1u << (ind >> 6);
+          const uint32_t bit = 1u << ((ind - wb) >> 6);
+          lw |= bit;
+          if (largest <= 2) sw |= bit;
         }
         if (largest <= 2) n_sharp++;
         n_lsharp++;
-        mark(ind);
+        mark(ind, wb, pw);
       }
       PHASE(2);
       // ---- flat picks: smallest (curvature, index) first (:511-568); the 4th pick ends the walk
       // unmarked
       for (int smallest = 1; smallest <= 4; smallest++) {
+        const uint32_t ok = ef & ~pw;
         uint64_t best = ~0ull;
 #pragma unroll
-        for (int t = 0; t < kS; t++) {
-          if (t < t0 || t > t1) continue;
-          const int k = lane + 64 * t;
-          if (k >= sp && k <= ep && !((pick >> t) & 1u) && (double)cr[t] < 0.1) {
-            const uint64_t key = ((uint64_t)__float_as_uint(cr[t]) << 32) | (uint32_t)k;
-            best = key < best ? key : best;
-          }
-        }
+        for (int u = 0; u < kW; u++)
+          if ((ok >> u) & 1u) best = kw[u] < best ? kw[u] : best;
         best = wave_min_u64(best);
         if (best == ~0ull) break;
         const int ind = (int)(uint32_t)best;
         if (lane == 0) ll.flat[n_flat] = ind;
-        if (lane == (ind & 63)) flt |= 1u << (ind >> 6);
+        if (lane == (ind & 63)) fw |= 1u << ((ind - wb) >> 6);
         n_flat++;
         if (smallest == 4) break;
-        mark(ind);
+        mark(ind, wb, pw);
       }
+      pick |= pw << t0;
+      lsh |= lw << t0;
+      shp |= sw << t0;
+      flt |= fw << t0;
       PHASE(3);
     }
   }
@@ -1152,6 +1163,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   for (int k = lane; k < n_sharp; k += 64) st4(o_sharp + k, ld4(cloud + off + ll.sharp[k]));
   for (int k = lane; k < n_lsharp; k += 64) st4(o_lsharp + k, ld4(cloud + off + ll.less_sharp[k]));
   for (int k = lane; k < n_flat; k += 64) st4(o_flat + k, ld4(cloud + off + ll.flat[k]));
+  wave_sync<true>();  // the pick lists are dead: their LDS becomes the voxel phase's (LineLds)
   // less-flat points (:570-577): label <= 0 inside the six segments, in index order
   uint32_t lfl = 0;
   int nlist = 0;
@@ -1373,26 +1385,43 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
 
 // kS: register slots per lane of the fast path (lines up to 64 kS points); longer lines (input
 // that is not ring-ordered) run line_body on global scratch.
+// The wave's LDS is one union over the line's three phases, so that it bounds occupancy as little
+// as possible: (sel) the curvature ring, the line's curvature, the walks' link masks and pick lists; (vox) the
+// VoxelGrid's std::sort order (introsort_order: the list elements and the partition's index
+// scratch); (stage) the centroid windows.  line_body_reg drains the wave's LDS traffic at each
+// phase change (wave_sync).
 template <int kS>
-__global__ __launch_bounds__(64) void k_scan_lines(FeatureArgs a) {
-  __shared__ LineLists ll;
-  __shared__ P4 stage[64];
-  __shared__ P4 ring[3 * 64];
-  __shared__ uint64_t lmask[kS + 2];
-  // the VoxelGrid's std::sort order (introsort_order): the list elements, and the partition's
-  // index scratch, which fits the curvature ring (dead by then) up to 16 slots
-  __shared__ uint32_t vel[64 * kS];
-  constexpr int kIdx = 2 * (32 * kS + 1);
-  constexpr bool kIdxInRing = kIdx * 2 <= (int)sizeof(P4) * 3 * 64;
-  __shared__ uint16_t vidx_own[kIdxInRing ? 1 : kIdx];
-  uint16_t* vidx = kIdxInRing ? reinterpret_cast<uint16_t*>(ring) : vidx_own;
+struct LineLds {
+  static constexpr int kIdx = 2 * (32 * kS + 1);
+  union {
+    struct {
+      P4 ring[3 * 64];
+      LineLists ll;
+      uint64_t lmask[kS + 2];
+      float curv[64 * kS];
+    } sel;
+    struct {
+      uint32_t vel[64 * kS];
+      uint16_t vidx[kIdx];
+    } vox;
+    P4 stage[64];
+  };
+};
+
+#ifndef LISLAM_LINES_WPE
+#define LISLAM_LINES_WPE 1
+#endif
+
+template <int kS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LISLAM_LINES_WPE))) void k_scan_lines(FeatureArgs a) {
+  __shared__ LineLds<kS> m;
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
   if (len <= 64 * kS)
-    line_body_reg<kS>(a, s, line, ll, lmask, stage, ring, vel, vidx);
-  else
-    line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, ll, stage);
+    line_body_reg<kS>(a, s, line, m.sel.ll, m.sel.lmask, m.sel.curv, m.stage, m.sel.ring, m.vox.vel, m.vox.vidx);
+  else  // the pick lists are dead before the centroid windows are staged
+    line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, m.sel.ll, m.stage);
 }
 
 #ifdef LISLAM_PHASE_PROF
