@@ -1235,6 +1235,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       // keys then become (voxel, position after the loop, line position) for the stable sort
       // below.  Voxel indices below 2^21 pack with the 11-bit line position directly; otherwise a
       // first sort of (voxel, list position) numbers the voxels densely for the element.
+      int sort_to = 64 * kS;  // the bitonic network's last level (none when key[] is already sorted)
       if (a.voxel_ties == LISLAM_TIES_REFERENCE) {
         uint32_t vmax = 0u;
 #pragma unroll
@@ -1258,12 +1259,43 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         if (packed) {
           wave_sync<true>();
           introsort_order_lds<kS>(vel, [](uint32_t e) { return e >> 11; }, nlist, vidx, vidx + 32 * kS + 1);
+          // std::__final_insertion_sort: the loop leaves blocks of at most 16 elements (or
+          // heap-sorted ranges) in key order, and the insertion sort stably sorts each block.  An
+          // element's final position is therefore its position, minus the greater keys among the
+          // 15 positions before it, plus the smaller keys among the 15 after it (earlier blocks
+          // hold no greater key and later blocks no smaller one, so the window needs no block
+          // bounds).  The permutation is written back in place, then read in sorted order.
+#pragma unroll 1
+          for (int t = 0; t < kS; t++) {  // final positions, into the (dead) partition scratch
+            if (64 * t >= nlist) break;
+            const int j = lane + 64 * t;
+            if (j < nlist) {
+              const uint32_t k = vel[j] >> 11;
+              int mv = 0;
+#pragma unroll
+              for (int d = 1; d <= 15; d++) {
+                if (j - d >= 0 && (vel[j - d] >> 11) > k) mv--;
+                if (j + d < nlist && (vel[j + d] >> 11) < k) mv++;
+              }
+              vidx[j] = (uint16_t)(j + mv);
+            }
+          }
+          wave_sync<true>();
+          uint32_t el[kS];
+#pragma unroll
+          for (int t = 0; t < kS; t++) el[t] = lane + 64 * t < nlist ? vel[lane + 64 * t] : 0u;
+          wave_sync<true>();
+#pragma unroll
+          for (int t = 0; t < kS; t++)
+            if (lane + 64 * t < nlist) vel[vidx[lane + 64 * t]] = el[t];
+          wave_sync<true>();
 #pragma unroll
           for (int t = 0; t < kS; t++) {
             const int j = lane + 64 * t;
             const uint32_t e = j < nlist ? vel[j] : 0u;
             key[t] = j < nlist ? ((uint64_t)(e >> 11) << 32) | ((uint32_t)j << 16) | (e & 0x7ffu) : ~0ull;
           }
+          sort_to = 1;
         } else {
           reg_bitonic<kS>(key);
           uint32_t prev_hi = 0xffffffffu;
@@ -1295,7 +1327,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         wave_sync<true>();
       }
       PHASE(6);
-      reg_bitonic<kS>(key);
+      for (int k = 2; k <= sort_to; k <<= 1) reg_bitonic_level<kS>(key, k, k >> 1, 0);  // reg_bitonic
       PHASE(7);
       // centroids in sorted order (sums in input order within a voxel): window t = sorted
       // positions 64 t .. 64 t + 63, staged in LDS; the voxel still open at the end of a window
