@@ -232,6 +232,7 @@ __global__ __launch_bounds__(64 * kFrontWaves) void k_front_scatter(FeatureArgs 
 // Optional per-phase cycle accounting (built only with -DLISLAM_PHASE_PROF, scripts/phase_prof.py).
 #ifdef LISLAM_PHASE_PROF
 __device__ unsigned long long g_phase_cycles[16];
+__device__ unsigned long long* g_line_log;  // k_scan_lines per-wave timeline (lislam_debug_line_log)
 #define PHASE_BEGIN uint64_t t_ph = __builtin_readcyclecounter()
 #define PHASE(i)                                                     \
   do {                                                               \
@@ -1447,6 +1448,9 @@ struct LineLds {
 template <int kS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LISLAM_LINES_WPE))) void k_scan_lines(FeatureArgs a) {
   __shared__ LineLds<kS> m;
+#ifdef LISLAM_PHASE_PROF
+  const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int s = blockIdx.x / a.H, line = blockIdx.x % a.H;
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
@@ -1454,9 +1458,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LISLAM_LINES
     line_body_reg<kS>(a, s, line, m.sel.ll, m.sel.lmask, m.sel.curv, m.stage, m.sel.ring, m.vox.vel, m.vox.vidx);
   else  // the pick lists are dead before the centroid windows are staged
     line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, m.sel.ll, m.stage);
+#ifdef LISLAM_PHASE_PROF
+  if (g_line_log && lane_id() == 0) {  // per-wave start / end (100 MHz), line length
+    unsigned long long* o = g_line_log + (size_t)blockIdx.x * 4;
+    o[0] = t_wave0;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+    o[2] = (unsigned long long)len;
+    o[3] = 0;
+  }
+#endif
 }
 
 #ifdef LISLAM_PHASE_PROF
+extern "C" int lislam_debug_line_log(unsigned long long* dev_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_line_log), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : -2;
+}
 extern "C" int lislam_debug_phase_cycles(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(g_phase_cycles)) != hipSuccess) return -2;
   static const unsigned long long zero[16] = {0};

@@ -217,6 +217,89 @@ __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
     *(__attribute__((address_space(1))) uint8_t*)dst = (uint8_t)word[0];
 }
 
+// The whole pyramid of a scan in one workgroup (levels 0 and 1 fit LDS together): level l-1's ROI
+// stays in LDS while level l is resized from it, ping-ponging between a level-0-sized buffer (even
+// levels) and a level-1-sized one (odd levels), and each padded level is written to HBM once, from
+// LDS, with dword stores (a dword never spans rows: strides are 16-byte multiples).  Same pixels as
+// k_orb_level: border pixels take their reflect-101 ROI pixel, ROI pixels the INTER_LINEAR_EXACT
+// fixed-point resize (hval) of level l-1.  A thread owns a column of the level (its horizontal
+// taps in registers) and walks the rows; the row taps (levels >= 1 have <= 64 rows) sit one per
+// lane and are read with readlane.
+constexpr int kPyrThreads = 1024;
+constexpr int kPyrLds = 112 * 1024;
+__host__ __device__ __forceinline__ int pyr_split(const Geom& g) { return (g.w[0] * g.h[0] + 15) & ~15; }
+__global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kPyrLds];
+  const Geom& g = a.g;
+  const int s = a.smap ? a.smap[blockIdx.x] : blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  uint8_t* const even = lds;
+  uint8_t* const odd = lds + pyr_split(g);
+  uint8_t* const base = a.pyr + (size_t)s * g.bytes;
+  {
+    const uint32_t* img = reinterpret_cast<const uint32_t*>(a.img + (size_t)s * g.W * g.H);
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(even);
+    const int nd = g.W * g.H / 4;
+    for (int d = threadIdx.x; d < nd; d += kPyrThreads) e32[d] = __builtin_nontemporal_load(img + d);
+  }
+  __syncthreads();
+  for (int l = 0; l < kL; l++) {
+    uint8_t* const cur = (l & 1) ? odd : even;
+    const uint8_t* const prev = (l & 1) ? even : odd;
+    const int w = g.w[l], h = g.h[l];
+    if (l > 0) {
+      const int wp = g.w[l - 1], hl = g.h[l - 1] - 1;
+      const int* lim = a.t.lim + l * 4;
+      const int lx0 = lim[0], lx1 = lim[1], ly0 = lim[2], ly1 = lim[3];
+      // row taps of this level: lane y holds yo[y], yc[y] (rows outside [ly0, ly1) clamp)
+      const int yo_l = lane < h && lane >= ly0 && lane < ly1 ? a.t.yo[l * a.t.ys + lane] : 0;
+      const int yc_l = lane < h && lane >= ly0 && lane < ly1 ? (int)a.t.yc[l * a.t.ys + lane] : 0;
+      const int xlast = a.t.xo[l * a.t.xs + w - 1];
+      for (int x = threadIdx.x; x < w; x += kPyrThreads) {
+        int o0 = 0, o1 = 0;
+        uint32_t w0 = 256u, w1 = 0u;  // hval = w0 * pr[o0] + w1 * pr[o1]
+        if (x >= lx0 && x < lx1) {
+          o0 = a.t.xo[l * a.t.xs + x];
+          o1 = o0 + 1;
+          w1 = a.t.xc[l * a.t.xs + x];
+          w0 = 256u - w1;
+        } else if (x >= lx1) {
+          o0 = o1 = xlast;
+        }
+        for (int y = 0; y < h; y++) {
+          uint32_t v;
+          if (y < ly0 || y >= ly1) {
+            const uint8_t* pr = prev + (y < ly0 ? 0 : hl) * wp;
+            v = min(255u, (w0 * pr[o0] + w1 * pr[o1] + 128u) >> 8);
+          } else {
+            const int ya = __builtin_amdgcn_readlane(yo_l, y);
+            const uint32_t cy = (uint32_t)__builtin_amdgcn_readlane(yc_l, y);
+            const uint8_t* pa = prev + ya * wp;
+            const uint8_t* pb = pa + wp;
+            const uint32_t ha = w0 * pa[o0] + w1 * pa[o1], hb = w0 * pb[o0] + w1 * pb[o1];
+            v = min(255u, (ha * (256u - cy) + hb * cy + 32768u) >> 16);
+          }
+          cur[y * w + x] = (uint8_t)v;
+        }
+      }
+      __syncthreads();  // level l complete; the next level writes the buffer read above
+    }
+    // the padded level: 256 dword columns x 4 row phases per pass, columns' reflections hoisted
+    const int ndr = g.stride[l] / 4, rows = h + 2 * kB;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(base + g.off[l]);
+    for (int dc = threadIdx.x & 255; dc < ndr; dc += 256) {
+      int cx[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) cx[k] = reflect101(4 * dc + k - kB, w);
+      for (int rr = threadIdx.x >> 8; rr < rows; rr += kPyrThreads / 256) {
+        const uint8_t* src = cur + reflect101(rr - kB, h) * w;
+        dst[rr * ndr + dc] = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 |
+                             (uint32_t)src[cx[3]] << 24;
+      }
+    }
+  }
+}
+
 // Stage `rows` (<= kMaxRows) rows of nd dwords (source rows 4-byte aligned, sstride bytes apart)
 // into LDS rows of nd dwords: every load of a thread is issued before its first store.
 template <int kMaxRows>
@@ -1703,9 +1786,16 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   const Geom& g = e->g;
   {
     TimedScope t(c, kT_orb_pyramid);
-    for (int l = 0; l < kL; l++)
-      hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256 * kLevelPx), n), dim3(256), 0, st,
-                         a, l, 0);
+    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB); larger
+    // images run the level-by-level kernel.  LISLAM_ORB_PYR_LEVELS=1 forces the latter (A/B).
+    static const bool by_level = getenv("LISLAM_ORB_PYR_LEVELS") && atoi(getenv("LISLAM_ORB_PYR_LEVELS")) == 1;
+    if (!by_level && g.W % 4 == 0 && g.h[1] <= 64 && pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds) {
+      hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(kPyrThreads), 0, st, a);
+    } else {
+      for (int l = 0; l < kL; l++)
+        hipLaunchKernelGGL(k_orb_level, dim3(cdiv(g.stride[l] * (g.h[l] + 2 * kB), 256 * kLevelPx), n), dim3(256), 0,
+                           st, a, l, 0);
+    }
   }
   {
     TimedScope t(c, kT_orb_fast);

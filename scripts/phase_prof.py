@@ -50,6 +50,61 @@ if sys.argv[1] == "lm":  # k_odom_lm: first evaluation + start, later evaluation
         b.close()
     sys.exit(0)
 
+if sys.argv[1] == "lines":  # per-wave timeline of one k_scan_lines launch
+    import numpy as np
+    import torch
+
+    pkg = g.package()
+    L = pkg.native.load(OUT)
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+    scans = pkg.synth.make_sequence(S)
+    with pkg.Context() as ctx:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        ctx.synchronize()
+        H = 64
+        log = torch.zeros(S * H * 4, dtype=torch.int64, device="cuda")
+        L.lislam_debug_line_log(ctypes.c_void_p(log.data_ptr()))
+        buf = (ctypes.c_ulonglong * 16)()
+        L.lislam_debug_phase_cycles(buf)
+        b.extract(S)
+        ctx.synchronize()
+        L.lislam_debug_line_log(ctypes.c_void_p(0))
+        L.lislam_debug_phase_cycles(buf)
+        a = log.view(-1, 4).cpu().numpy()
+        t0 = a[:, 0].min()
+        st, en = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0
+        d = en - st
+        print(f"waves {len(a)}  span {en.max():.1f} us  duration us: p50 {np.median(d):.1f} p90 "
+              f"{np.percentile(d, 90):.1f} p99 {np.percentile(d, 99):.1f} max {d.max():.1f}  mean {d.mean():.1f}")
+        print(f"start us: p50 {np.median(st):.1f} p90 {np.percentile(st, 90):.1f} max {st.max():.1f}")
+        print(f"sum of wave durations {d.sum() / 1e3:.1f} ms; waves alive at t: " +
+              " ".join(f"{t:.0f}:{int(((st <= t) & (en > t)).sum())}" for t in np.linspace(0, en.max(), 12)))
+        order = np.argsort(-d)[:12]
+        print("longest waves (us, len, start):", [(round(float(d[i]), 1), int(a[i, 2]), round(float(st[i]), 1))
+                                                  for i in order])
+        sc = np.arange(len(a)) // H
+        print("by scan (30-scan bins): mean / p90 us:",
+              [(int(b0), round(float(d[(sc >= b0) & (sc < b0 + 30)].mean()), 1),
+                round(float(np.percentile(d[(sc >= b0) & (sc < b0 + 30)], 90)), 1)) for b0 in range(0, S, 30)])
+        print("by line (8-line bins): mean us:",
+              [(int(l0), round(float(d[(np.arange(len(a)) % H >= l0) & (np.arange(len(a)) % H < l0 + 8)].mean()), 1))
+               for l0 in range(0, H, 8)])
+        sb = np.linspace(0, st.max() + 1e-6, 9)
+        print("by start time: mean us:", [(round(float(x0)), round(float(d[(st >= x0) & (st < x1)].mean()), 1))
+                                          for x0, x1 in zip(sb, sb[1:]) if ((st >= x0) & (st < x1)).any()])
+        lens = a[:, 2]
+        for lo_, hi_ in ((0, 600), (600, 800), (800, 950), (950, 1024), (1024, 5000)):
+            m = (lens >= lo_) & (lens < hi_)
+            if m.any():
+                print(f"len [{lo_},{hi_}): {m.sum()} waves, mean {d[m].mean():.1f} us, max {d[m].max():.1f} us")
+        tot = sum(buf[i] for i in range(len(PHASES)))
+        for i, nm in enumerate(PHASES):
+            print(f"{nm:28s} {buf[i] / (S * H):10.0f} cycles/line {100.0 * buf[i] / max(tot, 1):5.1f}%")
+        b.close()
+    sys.exit(0)
+
 if sys.argv[1] == "waves":  # per-wave timeline of one association launch (round R, outer pass 1)
     import numpy as np
     import torch
