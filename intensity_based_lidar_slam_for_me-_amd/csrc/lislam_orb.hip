@@ -284,17 +284,80 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
       }
       __syncthreads();  // level l complete; the next level writes the buffer read above
     }
-    // the padded level: 256 dword columns x 4 row phases per pass, columns' reflections hoisted
+    // the padded level: 256 dword columns x 4 row phases per pass, columns' reflections hoisted.
+    // The blurred copy (k_orb_blur's output) takes the same bytes except where a dword holds ROI
+    // columns of a ROI row: those come from the blur pass below.
     const int ndr = g.stride[l] / 4, rows = h + 2 * kB;
     uint32_t* dst = reinterpret_cast<uint32_t*>(base + g.off[l]);
+    uint32_t* bdst = a.blur ? reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]) : nullptr;
     for (int dc = threadIdx.x & 255; dc < ndr; dc += 256) {
       int cx[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) cx[k] = reflect101(4 * dc + k - kB, w);
+      const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
       for (int rr = threadIdx.x >> 8; rr < rows; rr += kPyrThreads / 256) {
         const uint8_t* src = cur + reflect101(rr - kB, h) * w;
-        dst[rr * ndr + dc] = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 |
-                             (uint32_t)src[cx[3]] << 24;
+        const uint32_t v = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 |
+                           (uint32_t)src[cx[3]] << 24;
+        dst[rr * ndr + dc] = v;
+        if (bdst && !(roi_dw && rr >= kB && rr < kB + h)) bdst[rr * ndr + dc] = v;
+      }
+    }
+    if (bdst) {
+      // GaussianBlur(ROI, 7x7, sigma 2, BORDER_REFLECT_101) of the dwords holding ROI columns, in
+      // k_orb_blur's float order: per row, 4 row sums of 7 taps (a sliding window of 7 rows in
+      // registers), then the symmetric column sum.  A thread owns a dword column holding ROI
+      // columns and one of nseg row segments, nseg as large as one pass of the workgroup allows.
+      const int dlo = kB / 4, ndw = (kB + w - 1) / 4 - dlo + 1;
+      const int nseg = max(1, min(h, kPyrThreads / ndw));
+      for (int item = threadIdx.x; item < ndw * nseg; item += kPyrThreads) {
+        const int dc = dlo + item % ndw, seg = item / ndw;
+        const int ra = seg * h / nseg, rb = (seg + 1) * h / nseg;
+        const int c4 = 4 * dc;  // padded column of byte 0
+        if (ra >= rb) continue;
+        int cs[10];  // ROI columns of padded columns c4 - 3 .. c4 + 6
+#pragma unroll
+        for (int i = 0; i < 10; i++) cs[i] = reflect101(c4 - 3 + i - kB, w);
+        float rs[7][4];
+        auto rowsum = [&](int r, float* out) {
+          const uint8_t* src = cur + reflect101(r, h) * w;
+          float b[10];
+#pragma unroll
+          for (int i = 0; i < 10; i++) b[i] = (float)src[cs[i]];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            float v = g.gk[0] * b[j];
+#pragma unroll
+            for (int t = 1; t < 7; t++) v += g.gk[t] * b[j + t];
+            out[j] = v;
+          }
+        };
+#pragma unroll
+        for (int k = 0; k < 6; k++) rowsum(ra - 3 + k, rs[k + 1]);
+        for (int r = ra; r < rb; r++) {
+#pragma unroll
+          for (int k = 0; k < 6; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) rs[k][j] = rs[k + 1][j];
+          rowsum(r + 3, rs[6]);
+          const uint8_t* src = cur + r * w;
+          uint32_t o = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int cr = c4 + j - kB;
+            uint32_t ob;
+            if (cr >= 0 && cr < w) {
+              float v = g.gk[3] * rs[3][j];
+#pragma unroll
+              for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t][j] + rs[3 - t][j]);
+              ob = (uint32_t)min(255, max(0, (int)rintf(v)));
+            } else {
+              ob = src[cs[j + 3]];
+            }
+            o |= ob << (8 * j);
+          }
+          bdst[(r + kB) * ndr + dc] = o;
+        }
       }
     }
   }
@@ -1784,12 +1847,14 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     a.smap = e->smap;
   }
   const Geom& g = e->g;
+  // LISLAM_ORB_PYR_LEVELS=1 forces the level-by-level pyramid and the separate blur (A/B)
+  static const bool by_level = getenv("LISLAM_ORB_PYR_LEVELS") && atoi(getenv("LISLAM_ORB_PYR_LEVELS")) == 1;
+  const bool fused = !by_level && g.W % 4 == 0 && g.h[1] <= 64 && pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
   {
     TimedScope t(c, kT_orb_pyramid);
-    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB); larger
-    // images run the level-by-level kernel.  LISLAM_ORB_PYR_LEVELS=1 forces the latter (A/B).
-    static const bool by_level = getenv("LISLAM_ORB_PYR_LEVELS") && atoi(getenv("LISLAM_ORB_PYR_LEVELS")) == 1;
-    if (!by_level && g.W % 4 == 0 && g.h[1] <= 64 && pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds) {
+    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB), which
+    // also writes the blurred copy; larger images run the level-by-level kernel and k_orb_blur
+    if (fused) {
       hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(kPyrThreads), 0, st, a);
     } else {
       for (int l = 0; l < kL; l++)
@@ -1805,7 +1870,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
-  {
+  if (!fused) {
     TimedScope t(c, kT_orb_blur);
     hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
   }
