@@ -1226,7 +1226,10 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
 #endif
 constexpr int kLm2Threads = LISLAM_LM2_THREADS;
 constexpr int kLm2Waves = kLm2Threads / 64;
-constexpr int kLmLds = 2816;
+#ifndef LISLAM_LM_LDS
+#define LISLAM_LM_LDS 2816
+#endif
+constexpr int kLmLds = LISLAM_LM_LDS;
 
 struct Lm2Shared {
   float c[3][kLmLds];    // query point
