@@ -17,7 +17,7 @@
 //   k_orb_blur      1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2 separable float
 //                   Gaussian (row sums then the symmetric column sum, the FilterEngine order) on
 //                   the ROI, border copy
-//   k_orb_fastnms   1 WG per band of 8 level rows, staged in LDS: FAST-9/16 segment test +
+//   k_orb_fastnms   1 WG per band of 4 level rows, staged in LDS: FAST-9/16 segment test +
 //                   cornerScore<16> into an LDS score tile, then 3x3 non-max suppression, mask,
 //                   border
 //   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
@@ -60,7 +60,10 @@ constexpr int kPairThreads = 1024;
 constexpr int kLmThreads = 256;
 constexpr int kQTile = 1024;  // queries per LDS tile in k_orb_xdist (32 KiB)
 constexpr int kNoMatch = 0x7f7f7f7f;
-constexpr int kFastBand = 8;   // ROI rows per k_orb_fastnms workgroup
+#ifndef LISLAM_FAST_BAND
+#define LISLAM_FAST_BAND 4
+#endif
+constexpr int kFastBand = LISLAM_FAST_BAND;  // ROI rows per k_orb_fastnms workgroup
 constexpr int kBlurBand = 8;   // padded rows per k_orb_blur workgroup  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
 
 constexpr int kNPatch = 749;  // pixels of the ICAngles circular patch (half size 15; checked on the host)
