@@ -55,7 +55,10 @@ constexpr int kB = 23;  // pyramid border: max(edgeThreshold 1, max(22, 4)) + 1
 constexpr int kL = 8;   // nlevels
 constexpr int kHalf = 15;
 constexpr int kFastT = 20;
-constexpr int kSelThreads = 1024;
+#ifndef LISLAM_SEL_THREADS
+#define LISLAM_SEL_THREADS 512
+#endif
+constexpr int kSelThreads = LISLAM_SEL_THREADS;  // k_orb_select workgroup
 constexpr int kPairThreads = 1024;
 constexpr int kLmThreads = 256;
 constexpr int kQTile = 1024;  // queries per LDS tile in k_orb_xdist (32 KiB)
