@@ -1441,12 +1441,15 @@ struct LineLds {
   };
 };
 
+// Waves per SIMD asked of the 1024-point lines (kS = 16): 5 caps them at 96 VGPRs (44 B of
+// scratch per lane) for one more resident wave than the 113-VGPR build: 2.02 -> 1.96 ms per 300
+// scans isolated (profiles/r02v_experiments.txt).  Other line lengths keep the default.
 #ifndef LISLAM_LINES_WPE
-#define LISLAM_LINES_WPE 1
+#define LISLAM_LINES_WPE 5
 #endif
 
 template <int kS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LISLAM_LINES_WPE))) void k_scan_lines(FeatureArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kS == 16 ? LISLAM_LINES_WPE : 1))) void k_scan_lines(FeatureArgs a) {
   __shared__ LineLds<kS> m;
 #ifdef LISLAM_PHASE_PROF
   const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();
