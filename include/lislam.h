@@ -156,8 +156,10 @@ int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_
  * the stream (no host synchronization). */
 int lislam_batch_set_timing(lislam_batch* b, int32_t enable);
 /* Kernels timed by lislam_batch_kernel_times, in this order. */
-#define LISLAM_NUM_KERNELS 6 /* k_scan_front, k_scan_lines, k_scan_compact, k_target_index,
-                                k_odom_assoc, k_odom_lm (the latter includes k_odom_init) */
+#define LISLAM_NUM_KERNELS 7 /* k_scan_front, k_scan_lines, k_scan_compact, k_target_index,
+                                k_odom_assoc, k_odom_lm (the latter includes k_odom_init),
+                                k_odom_chain (the persistent engine of few long chains: association
+                                and solve of every round in one launch) */
 /* Synchronize, then return, over the calls recorded since the previous read, the average ms
  * per call spent in each kernel (ms_per_call[6]) and the launches per call of each kernel
  * (launches_per_call[6], may be null); calls[2] (may be null) = extract / odometry calls
@@ -206,6 +208,20 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
  * LISLAM_TIES_REFERENCE (the default) replays that order exactly (bit-exact centroids);
  * LISLAM_TIES_INDEX sums them in input order (faster; centroids differ by float rounding, poses by
  * up to 1e-4 on the bench data, tests/test_oracle.py).  Applies to later extractions of ctx. */
+/* Odometry schedule of lislam_batch_odometry (results are the same): LISLAM_ENGINE_OFF issues one
+ * association and one solve launch per round (chains advance together, one workgroup per chain's
+ * solve); LISLAM_ENGINE_ON runs every round of every chain inside ONE persistent launch
+ * (k_odom_chain: a device ticket queue orders the association and solve items, no host round trip
+ * between scans) — the schedule of few long chains, e.g. the reference's single continuous chain;
+ * LISLAM_ENGINE_AUTO (default) picks ON when every chain's workgroups fit the device at once. */
+#define LISLAM_ENGINE_OFF 0
+#define LISLAM_ENGINE_AUTO 1
+#define LISLAM_ENGINE_ON 2
+int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
+/* Synchronize; status = 1 if the last engine launch of the batch gave up (one of its bounded
+ * device waits expired: its outputs are invalid), else 0. */
+int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
+
 #define LISLAM_TIES_REFERENCE 0
 #define LISLAM_TIES_INDEX 1
 int lislam_set_tie_order(lislam_ctx* ctx, int32_t order);

@@ -191,6 +191,8 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.para, (size_t)S * 7);
   rc |= dalloc(b, &o.pose, (size_t)S * 7);
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
+  rc |= dalloc(b, &o.eng_ctl, (size_t)8 + 6 * (size_t)S);
+  rc |= dalloc(b, &o.warm, (size_t)S * (b->cap_sharp + b->cap_flat) * 4);
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
   rc |= dalloc(b, &b->d_gate, (size_t)S);
   if (rc != LISLAM_OK) {
@@ -478,6 +480,17 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   }
   o.c0 = 0;
   o.cn = o.n_chains;
+  if (lislam::use_chain_engine(o, c->odom_engine)) {
+    // few long chains: one persistent launch sequences every round on the device
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ev) { e0 = b->get_event(); HIPCHK(c, hipEventRecord(e0, c->stream)); }
+    lislam::launch_odometry_chain(o, c->stream);
+    b->engine_ran = true;
+    if (ev) { e1 = b->get_event(); HIPCHK(c, hipEventRecord(e1, c->stream)); ev->push_back({6, e0, e1}); }
+    HIPCHK(c, hipGetLastError());
+    return LISLAM_OK;
+  }
+  b->engine_ran = false;
   launch_odometry(o, b->odo_stream, G, b->odo_fork, b->odo_join, ev, &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
@@ -495,6 +508,17 @@ int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_
   if (b->extracted < n_scans) return fail(b->ctx, LISLAM_ERR_STATE, "extract %d scans before odometry", n_scans);
   hipSetDevice(b->ctx->device);
   return run_odometry(b, n_scans, chain_len, nullptr, use_aloam);
+}
+
+int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
+  if (!b || !status) return LISLAM_ERR_ARG;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  unsigned w[2] = {0, 0};
+  if (b->engine_ran) HIPCHK(c, hipMemcpy(w, b->oa.eng_ctl, sizeof(w), hipMemcpyDeviceToHost));
+  *status = w[1] ? 1 : 0;  // the engine's abort word (a bounded wait expired)
+  return LISLAM_OK;
 }
 
 int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls) {
@@ -814,6 +838,12 @@ int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const dou
   if (e == hipSuccess && jac) e = hipMemcpy(jac, dj, (size_t)n * 18 * sizeof(double), hipMemcpyDeviceToHost);
   cleanup();
   if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors: %s", hipGetErrorString(e));
+  return LISLAM_OK;
+}
+
+int lislam_set_odometry_schedule(lislam_ctx* c, int32_t mode) {
+  if (!c || mode < LISLAM_ENGINE_OFF || mode > LISLAM_ENGINE_ON) return LISLAM_ERR_ARG;
+  c->odom_engine = mode;
   return LISLAM_OK;
 }
 

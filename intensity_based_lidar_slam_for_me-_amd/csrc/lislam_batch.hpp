@@ -38,6 +38,7 @@ struct lislam_batch {
   hipEvent_t odo_fork = nullptr, odo_join[kMaxGroups] = {};
   std::vector<hipEvent_t> pool;
   int extracted = 0;
+  bool engine_ran = false;  // the last odometry call ran the chain engine (lislam_batch_odometry_status)
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
   // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
   // queued on the context stream after it.

@@ -37,6 +37,7 @@ struct lislam_ctx {
   void* map_scratch = nullptr;     // device scratch of the stateless mapping entry points
   lislam_ktimer mtimer;            // mapping-kernel timing
   int voxel_ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order
+  int odom_engine = LISLAM_ENGINE_AUTO;     // lislam_set_odometry_schedule
 };
 
 // kernel ids of lislam_map_kernel_times (LISLAM_CTX_NUM_KERNELS in include/lislam.h)

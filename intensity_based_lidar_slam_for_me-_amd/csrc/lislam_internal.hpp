@@ -100,6 +100,10 @@ struct OdomArgs {
   int* stats;      // [S][8] corners/planes for outer 0/1, LM iterations 0/1, terminations 0/1
   int dbg;         // ablation switch for profiling (0 in production): 1 skip 1-NN, 2 skip line search
   const int* gate;  // [S] use_aloam per scan (laserOdometry.cpp:403-417), or null = every scan
+  // chain engine (k_odom_chain): control words (zeroed before every launch) and the per-query
+  // association of the first outer pass, the second pass's starting bounds
+  unsigned* eng_ctl;  // [8 + 6 S]
+  int* warm;          // [n_chains][cap_sharp + cap_flat][4]
 };
 
 // Batched evaluation of the cost functors (lislam_eval_factors).
@@ -136,6 +140,13 @@ struct OdoTimed {
 void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups, hipEvent_t fork,
                      const hipEvent_t* join, std::vector<OdoTimed>* ev, hipEvent_t (*get_event)(void*),
                      void* ev_owner);
+// The same schedule as ONE persistent launch (k_odom_chain, lislam_odometry.hip): every round of
+// the a.n_chains chains, association and solve, sequenced on the device.  Returns the grid size.
+int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
+// Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
+// lislam_set_odometry_schedule (LISLAM_ENGINE_*); AUTO = the environment's LISLAM_ENGINE (0 off,
+// 2 on) if set, else on when every chain's workgroups fit the device at once.
+bool use_chain_engine(const OdomArgs& a, int mode);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
 // AutoDiffCostFunction<F, R, 4, 3>::Evaluate of the functors of lidarFeaturePointsFunction.hpp:

@@ -26,6 +26,9 @@
 
 namespace lislam {
 
+// a value every lane holds alike (LDS broadcasts), as a scalar: branches on it stay uniform
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 constexpr int kLmThreads = 512;
 constexpr int kLmWaves = kLmThreads / 64;
 constexpr double kDistSq = 25.0;   // DISTANCE_SQ_THRESHOLD (laserOdometry.cpp:89)
@@ -1176,7 +1179,7 @@ __global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int o
         for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
-    go = sh.flag;
+    go = uni(sh.flag);
   }
   LM_PHASE(0);
   while (go) {
@@ -1395,7 +1398,7 @@ __global__ __launch_bounds__(kLm2Threads) void k_odom_lm2(OdomArgs a, int r, int
         for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
     }
     __syncthreads();
-    go = sh.flag;
+    go = uni(sh.flag);
   }
   LM_PHASE(2);
   while (go) {
@@ -1531,6 +1534,745 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
     if (a.jt)
       for (int cc = 0; cc < 3; cc++) a.jt[((size_t)i * 3 + k) * 3 + cc] = (k < R && kd != 4) ? G[k][cc] : 0.0;
   }
+}
+
+// ================================================================== the chain engine
+// The whole odometry schedule of a few long chains (the reference's continuous para_q / para_t
+// carry, laserOdometry.cpp:130-135,716-717) as ONE persistent launch.  The schedule is a ticket
+// queue: for every round r and outer pass o (:417), and every chain c, I association items (32
+// queries each: 8 waves x four 16-lane rows, the searches of k_odom_assoc16) then one solve item
+// (the Ceres-semantics LM of k_odom_lm2, on one workgroup).  A workgroup takes the next ticket
+// with one atomic add and waits, polling one word, until the ticket's inputs exist:
+//   association (c, r, o)  needs the solve before it (lm_gen[c] >= 2 r + o): x = para_q / para_t;
+//   solve (c, r, o)        needs its I association items (assoc_done[c][2 r + o] == I).
+// Every dependency of a ticket is a lower ticket, taken earlier by a running workgroup, so the
+// queue drains whatever the residency (one resident workgroup runs it all, serially): there is
+// no grid barrier to deadlock.  Every spin is bounded (2 s) and raises the abort word, which every
+// waiting workgroup also polls, so the grid always drains.
+// Hand-offs (MI355X_MICROARCH.md, visibility): the payloads (records, x) are stored write-through
+// (relaxed agent-scope atomic stores = global_store sc1), every storing wave drains vmcnt, ONE
+// lane signals with an agent-scope atomic; the consumer polls relaxed, then every load of the
+// payload is an agent-scope (sc1) load.
+// The solve evaluates each block in the form J^T J = G^T M G, J^T r = G^T v with G = [-2 [p]x, I]
+// (p = R c, the local parameterization of EigenQuaternionParameterization): M = w (|u|^2 I - u u^T)
+// and v = w (u x r) for LidarEdgeFactor (r = (lp - a) x u, u = (a - b) / |a - b|, the functor's
+// (lp - a) x (lp - b) / |a - b| rearranged), M = w n n^T and v = w r n for LidarPlaneFactor
+// (r = (lp - j) . n); w = the Huber corrector's rho'.  28 sums per thread: cost, M, T = [p]x M,
+// U = T [p]x, v, p x v; H = [[-4 U, 2 T], [2 T^T, M]], g = [2 p x v, v].
+#ifndef LISLAM_ENG_THREADS
+#define LISLAM_ENG_THREADS 512  // 256 VGPRs: the fp64 evaluation's 28 sums + block state spill at 128
+#endif
+constexpr int kEngThreads = LISLAM_ENG_THREADS;
+constexpr int kEngWaves = kEngThreads / 64;
+constexpr int kEngQ = kEngWaves * 4;  // queries per association item (four per wave)
+#ifndef LISLAM_ENG_LDS
+#define LISLAM_ENG_LDS 2304           // 64 lines: 12 * 64 sharp + 24 * 64 flat queries
+#endif
+constexpr int kEngLds = LISLAM_ENG_LDS;
+constexpr int kRecWords = 8;          // u64 words per record: c.xy, c.z a.x, a.yz, kind, u/n xyz, -
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1d(double* p, double v) { st_sc1((uint64_t*)p, (uint64_t)__double_as_longlong(v)); }
+__device__ __forceinline__ double ld_sc1d(const double* p) { return __longlong_as_double((long long)ld_sc1((const uint64_t*)p)); }
+__device__ __forceinline__ unsigned ld_rlx(unsigned* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(unsigned* p, unsigned v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned add_rlx(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double uniform_d(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// control words: [0] ticket, [1] abort, [2] error, [3] -, [4, 4 + C) lm_gen, then assoc_done[C][2 R]
+struct EngCtl {
+  unsigned* w;
+  int C, R, I;
+  __device__ unsigned* ticket() const { return w; }
+  __device__ unsigned* abort_w() const { return w + 1; }
+  __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
+  __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
+};
+
+// Developer trace of the engine (null in production): per workgroup {ticket, stage, LM passes,
+// time}, stored system-scope into host-pinned memory so the host can read it while the kernel runs.
+__device__ unsigned* g_eng_trace = nullptr;
+extern "C" int lislam_debug_engine_trace(int n_wgs, unsigned** host_out) {
+  static unsigned* h = nullptr;
+  static int cap = 0;
+  if (n_wgs <= 0) {
+    unsigned* z = nullptr;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_eng_trace), &z, sizeof(z)) == hipSuccess ? 0 : -2;
+  }
+  if (n_wgs > cap) {
+    if (h) (void)hipHostFree(h);
+    if (hipHostMalloc((void**)&h, sizeof(unsigned) * 256 * n_wgs, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return -2;
+    cap = n_wgs;
+  }
+  for (int i = 0; i < 256 * n_wgs; i++) h[i] = 0xffffffffu;
+  unsigned* d = nullptr;
+  if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return -2;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_eng_trace), &d, sizeof(d)) != hipSuccess) return -2;
+  *host_out = h;
+  return 0;
+}
+__device__ __forceinline__ void eng_trace(int slot, unsigned v) {
+  unsigned* t = g_eng_trace;
+  if (t) __hip_atomic_store(t + (blockIdx.x * 16 + slot) * 16, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // a 64-B line each
+}
+
+// One lane: wait until *p >= target; false = aborted (2 s bound, or another workgroup's abort).
+// Arguments by value: a struct passed by reference would live in scratch, and values loaded from
+// scratch count as divergent, which would put the ticket loop's barriers in divergent control flow.
+__device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (ld_rlx(p) >= target) return true;
+    if (ld_rlx(abort_w)) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+      st_rlx(abort_w, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+struct EngShared {
+  float cf[6][kEngLds];   // query point c, first matched point a (edge) / j (plane)
+  double ud[3][kEngLds];  // edge: u = (a - b) / |a - b|; plane: unit normal
+  int8_t kd[kEngLds];     // 0 edge, 1 plane, -1 none
+  double red[kEngWaves * 4][kAcc];
+  double acc[kAcc];
+  double x[7];
+  int cnt[kEngWaves][2];
+  unsigned ticket;
+  int flag, nc, np;
+};
+
+// x (para_q, para_t) a ticket of (c, r, o) starts from: the chain's initial state for its first
+// pass, else the last solve's (write-through) result.  Thread 0 -> sh.x.
+__device__ __forceinline__ void eng_load_x(const OdomArgs& a, int c, int r, int o, double* x) {
+  if (r == 0 && o == 0) {
+    if (a.init_state) {
+      for (int e = 0; e < 7; e++) x[e] = a.init_state[(size_t)c * 14 + e];
+    } else {
+      for (int e = 0; e < 7; e++) x[e] = e == 3 ? 1.0 : 0.0;
+    }
+  } else {
+    const double* st = a.state + (size_t)c * 16;
+    for (int e = 0; e < 7; e++) x[e] = ld_sc1d(st + e);
+  }
+}
+
+// One association item: queries [item * 64, item * 64 + 64) of pair k (Morton order, corner
+// queries first), four per wave.  Record w of the chain = query w's residual block.
+__device__ __forceinline__ void eng_assoc(const OdomArgs& a, const EngShared& sh, int k, int item, uint64_t* rec) {
+  const int lane = lane_id(), lr = lane & 15;
+  const int w = item * kEngQ + (int)(threadIdx.x >> 6) * 4 + (lane >> 4);
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  if (__ballot(w < ns + nf) == 0ull) return;
+  const bool has = w < ns + nf;
+  const bool corner = w < ns;
+  const int t = corner ? w : w - ns;
+  const P4 qp = has ? ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
+                                 : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t)
+                    : P4{0.f, 0.f, 0.f, 0.f};
+  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
+  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
+  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
+  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
+  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
+  double x[7];
+#pragma unroll
+  for (int e = 0; e < 7; e++) x[e] = sh.x[e];
+  const P4 cur{qp.x, qp.y, qp.z, 0.f};
+  const P4 sel = transform_to_start(cur, x);
+  const int closest = nn16(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, has);
+  const bool act = has && closest >= 0;
+  const P4 pa = ld4(L + (act ? closest : 0));
+  const int cid = act ? int(pa.i) : 0;
+  dkey b2 = dk(25.f, kNone), b3 = dk(25.f, kNone);
+  ls16(L, ix.chunk + mo, nL, act ? closest : 0, cid, sel, corner, act, b2, b3);
+  auto idx_of = [&](dkey b) { const int kk = dk_key(b); return kk < nL ? closest + kk : closest - (kk - nL); };
+  int kind = -1;
+  D3 u{0.0, 0.0, 0.0};
+  if (act && corner && dk_key(b2) != kNone) {  // LidarEdgeFactor(curr, a, b)
+    const P4 pb = ld4(L + idx_of(b2));
+    const D3 de{(double)pa.x - (double)pb.x, (double)pa.y - (double)pb.y, (double)pa.z - (double)pb.z};
+    const double inv = 1.0 / sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
+    u = D3{de.x * inv, de.y * inv, de.z * inv};
+    kind = 0;
+  } else if (act && !corner && dk_key(b2) != kNone && dk_key(b3) != kNone) {  // LidarPlaneFactor(curr, j, l, m)
+    const P4 pl = ld4(L + idx_of(b2)), pm = ld4(L + idx_of(b3));
+    u = plane_normal(D3{pa.x, pa.y, pa.z}, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
+    kind = 1;
+  }
+  if (!has || lr >= 7) return;
+  uint64_t v;
+  auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
+  switch (lr) {
+    case 0: v = pk(cur.x, cur.y); break;
+    case 1: v = pk(cur.z, pa.x); break;
+    case 2: v = pk(pa.y, pa.z); break;
+    case 3: v = (uint64_t)(uint32_t)kind; break;
+    case 4: v = (uint64_t)__double_as_longlong(u.x); break;
+    case 5: v = (uint64_t)__double_as_longlong(u.y); break;
+    default: v = (uint64_t)__double_as_longlong(u.z); break;
+  }
+  if (lr == 3 || kind >= 0) st_sc1(rec + (size_t)w * kRecWords + lr, v);
+}
+
+// One block's 28 sums (see the engine comment) at p = R c, lp = p + t (R, t uniform).  Each row
+// of T is folded into the sums (and into U) as soon as it exists, to keep few doubles live.
+__device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
+                                          double (&s)[kAcc]) {
+  const D3 p{fma(R[0], c.x, fma(R[1], c.y, R[2] * c.z)), fma(R[3], c.x, fma(R[4], c.y, R[5] * c.z)),
+             fma(R[6], c.x, fma(R[7], c.y, R[8] * c.z))};
+  double m00, m01, m02, m11, m12, m22, v0, v1, v2;
+  {
+    const D3 e{(p.x + t.x) - pa.x, (p.y + t.y) - pa.y, (p.z + t.z) - pa.z};
+    double r0 = 0, r1 = 0, r2 = 0, rp = 0, s2;
+    if (kd == 0) {
+      r0 = fma(e.y, u.z, -e.z * u.y); r1 = fma(e.z, u.x, -e.x * u.z); r2 = fma(e.x, u.y, -e.y * u.x);
+      s2 = fma(r0, r0, fma(r1, r1, r2 * r2));
+    } else {
+      rp = fma(e.x, u.x, fma(e.y, u.y, e.z * u.z));
+      s2 = rp * rp;
+    }
+    double w = 1.0;
+    if (s2 > 0.01) {  // HuberLoss(0.1): rho = 2 a sqrt(s) - a^2, rho' = a / sqrt(s)
+      const double rr = sqrt(s2);
+      s[0] += 0.5 * (0.2 * rr - 0.01);
+      w = fmax(2.2250738585072014e-308, 0.1 / rr);
+    } else {
+      s[0] += 0.5 * s2;
+    }
+    const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
+    if (kd == 0) {
+      const double wuu = w * fma(u.x, u.x, fma(u.y, u.y, u.z * u.z));
+      m00 = fma(-wx, u.x, wuu); m01 = -wx * u.y; m02 = -wx * u.z;
+      m11 = fma(-wy, u.y, wuu); m12 = -wy * u.z; m22 = fma(-wz, u.z, wuu);
+      // v = w (u x r)
+      v0 = w * fma(u.y, r2, -u.z * r1); v1 = w * fma(u.z, r0, -u.x * r2); v2 = w * fma(u.x, r1, -u.y * r0);
+    } else {
+      m00 = wx * u.x; m01 = wx * u.y; m02 = wx * u.z; m11 = wy * u.y; m12 = wy * u.z; m22 = wz * u.z;
+      v0 = rp * wx; v1 = rp * wy; v2 = rp * wz;
+    }
+  }
+  s[1] += m00; s[2] += m01; s[3] += m02; s[4] += m11; s[5] += m12; s[6] += m22;
+  s[22] += v0; s[23] += v1; s[24] += v2;
+  s[25] += fma(p.y, v2, -p.z * v1); s[26] += fma(p.z, v0, -p.x * v2); s[27] += fma(p.x, v1, -p.y * v0);
+  // T = [p]x M row by row; U = T [p]x (symmetric): U[i][0] = T[i][1] pz - T[i][2] py,
+  // U[i][1] = T[i][2] px - T[i][0] pz, U[i][2] = T[i][0] py - T[i][1] px
+  {
+    const double t0 = fma(-p.z, m01, p.y * m02), t1 = fma(-p.z, m11, p.y * m12), t2 = fma(-p.z, m12, p.y * m22);
+    s[7] += t0; s[8] += t1; s[9] += t2;
+    s[16] += fma(t1, p.z, -t2 * p.y);
+    s[17] += fma(t2, p.x, -t0 * p.z);
+    s[18] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(p.z, m00, -p.x * m02), t1 = fma(p.z, m01, -p.x * m12), t2 = fma(p.z, m02, -p.x * m22);
+    s[10] += t0; s[11] += t1; s[12] += t2;
+    s[19] += fma(t2, p.x, -t0 * p.z);
+    s[20] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(-p.y, m00, p.x * m01), t1 = fma(-p.y, m01, p.x * m11), t2 = fma(-p.y, m02, p.x * m12);
+    s[13] += t0; s[14] += t1; s[15] += t2;
+    s[21] += fma(t0, p.y, -t1 * p.x);
+  }
+}
+
+// The 28 sums of every thread -> sh.acc in lislam_lm.hpp's layout (cost, H upper, g).  Inside each
+// 16-lane row a reduce-scatter: xor 1 / xor 2 (quad_perm) halve the values each lane carries
+// (lane i of an 8-lane group keeps part(i), part(7 - i) == part(i)), the half- and full-row mirrors
+// then pair lanes holding the same part; lanes 0..3 of each row write their 7 sums to LDS.
+__device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
+  const int lane = lane_id(), i8 = lane & 7;
+  const int part = (i8 & 4) ? (~i8 & 3) : (i8 & 3);
+  const bool h1 = part & 1, h2 = (part >> 1) & 1;
+  double h[14], o[7];
+#pragma unroll
+  for (int q = 0; q < 14; q++) {
+    const double snd = h1 ? s[q] : s[q + 14];
+    const double kp = h1 ? s[q + 14] : s[q];
+    h[q] = kp + dpp_d<0xB1>(snd);
+  }
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const double snd = h2 ? h[q] : h[q + 7];
+    const double kp = h2 ? h[q + 7] : h[q];
+    o[q] = kp + dpp_d<0x4E>(snd);
+  }
+#pragma unroll
+  for (int q = 0; q < 7; q++) o[q] += dpp_d<0x141>(o[q]);
+#pragma unroll
+  for (int q = 0; q < 7; q++) o[q] += dpp_d<0x140>(o[q]);
+  if ((lane & 15) < 4) {  // part p holds sums 14 (p & 1) + 7 (p >> 1) + [0, 7)
+    const int row = threadIdx.x >> 4, base = 14 * (part & 1) + 7 * (part >> 1);
+#pragma unroll
+    for (int q = 0; q < 7; q++) sh.red[row][base + q] = o[q];
+  }
+  __syncthreads();
+  const int wv = threadIdx.x >> 6;
+  for (int e = wv; e < kAcc; e += kEngWaves) {
+    double v = lane < kEngWaves * 4 ? sh.red[lane][e] : 0.0;
+    v = row_sum(v);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane == 0) {
+      // sum index e -> acc index (H upper row-major over (theta 0..2, t 0..2), then g)
+      int ai;
+      double sc;
+      if (e == 0) { ai = 0; sc = 1.0; }
+      else if (e <= 6) {  // M -> H_tt
+        const int ij[6][2] = {{3, 3}, {3, 4}, {3, 5}, {4, 4}, {4, 5}, {5, 5}};
+        const int i = ij[e - 1][0], j = ij[e - 1][1];
+        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = 1.0;
+      } else if (e <= 15) {  // T -> H_theta,t = 2 T
+        const int i = (e - 7) / 3, j = 3 + (e - 7) % 3;
+        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = 2.0;
+      } else if (e <= 21) {  // U -> H_theta,theta = -4 U
+        const int ij[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+        const int i = ij[e - 16][0], j = ij[e - 16][1];
+        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = -4.0;
+      } else if (e <= 24) { ai = 22 + 3 + (e - 22); sc = 1.0; }  // v -> g_t
+      else { ai = 22 + (e - 25); sc = 2.0; }                      // p x v -> g_theta
+      sh.acc[ai] = sc * v;
+    }
+  }
+  __syncthreads();
+}
+
+// One evaluation at sh.x over `total` records (LDS for i < kEngLds, write-through records beyond).
+__device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec, int total) {
+  double s[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) s[e] = 0.0;
+  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
+  D3 t{sh.x[4], sh.x[5], sh.x[6]};
+  // rotation matrix of q (the columns are q rotating the unit vectors: qrot's arithmetic)
+  double R[9];
+  {
+    const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
+    R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
+  }
+#pragma unroll
+  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);  // identical in every lane: scalar registers
+  t = D3{uniform_d(t.x), uniform_d(t.y), uniform_d(t.z)};
+  for (int i = threadIdx.x; i < total; i += kEngThreads) {
+    int kd;
+    D3 c, pa, u;
+    if (i < kEngLds) {
+      kd = sh.kd[i];
+      if (kd < 0) continue;
+      c = D3{sh.cf[0][i], sh.cf[1][i], sh.cf[2][i]};
+      pa = D3{sh.cf[3][i], sh.cf[4][i], sh.cf[5][i]};
+      u = D3{sh.ud[0][i], sh.ud[1][i], sh.ud[2][i]};
+    } else {
+      const uint64_t* rw = rec + (size_t)i * kRecWords;
+      kd = (int)(uint32_t)ld_sc1(rw + 3);
+      if (kd < 0) continue;
+      const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2);
+      c = D3{__uint_as_float((uint32_t)w0), __uint_as_float((uint32_t)(w0 >> 32)), __uint_as_float((uint32_t)w1)};
+      pa = D3{__uint_as_float((uint32_t)(w1 >> 32)), __uint_as_float((uint32_t)w2), __uint_as_float((uint32_t)(w2 >> 32))};
+      u = D3{ld_sc1d((const double*)(rw + 4)), ld_sc1d((const double*)(rw + 5)), ld_sc1d((const double*)(rw + 6))};
+    }
+    eng_block(kd, c, pa, u, R, t, s);
+  }
+  eng_reduce(s, sh);
+}
+
+// ---- the step logic of lislam_lm.hpp (Ceres 1.14 LM, same decisions) for thread 0, lean:
+// A held packed (21), the Cholesky's column reciprocals from rsqrt (no sqrt + division per column),
+// the model cost change from the solve (m = 0.5 (y.Sg + y.(D/radius)y), the same quantity as
+// -(step.Sg + 0.5 step'SAS step) since (SAS + D/radius) y = Sg), EigenQuaternionParameterization's
+// sin|d|/|d| and cos|d| as series in |d|^2 below |d| = 0.5 (library sincos above), and the
+// gradient test's rotation part only when its translation part is not already above 1e-10.
+struct EngLM {
+  double x[7], xc[7], A[21], g[6], scale[6], diag[6];
+  double cost, radius, dfac, mcc;
+  int reuse, it, invalid, term;
+};
+
+__device__ __forceinline__ double rsqrt_d(double d) {  // 1 / sqrt(d), d > 0, to ~1 ulp
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d, y * y, 1.5);
+  y = y * fma(-0.5 * d, y * y, 1.5);
+  return y;
+}
+__device__ __noinline__ void sincos_slow(double n2, double* sdd, double* cs) {
+  const double nd = sqrt(n2);
+  double sn;
+  sincos(nd, &sn, cs);
+  *sdd = sn / nd;
+}
+// x' = [sin|d| d/|d|, cos|d|] (x) x (quaternion part of the state plus)
+__device__ __forceinline__ void eng_quat_plus(const double* x, const double* d, double* xp) {
+  const double n2 = fma(d[0], d[0], fma(d[1], d[1], d[2] * d[2]));
+  if (!(n2 > 0.0)) {
+    for (int k = 0; k < 4; k++) xp[k] = x[k];
+    return;
+  }
+  double sdd, cs;
+  if (n2 <= 0.25) {  // Taylor series in n2 to x^16 (truncation < 1e-19)
+    sdd = fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, 2.8114572543455206e-15, -7.6471637318198164e-13),
+          1.6059043836821613e-10), -2.5052108385441720e-08), 2.7557319223985893e-06), -1.9841269841269841e-04),
+          8.3333333333333333e-03), -1.6666666666666666e-01), 1.0);
+    cs = fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, 4.7794773323873853e-14, -1.1470745597729725e-11),
+         2.0876756987868099e-09), -2.7557319223985888e-07), 2.4801587301587302e-05), -1.3888888888888889e-03),
+         4.1666666666666664e-02), -0.5), 1.0);
+  } else {
+    sincos_slow(n2, &sdd, &cs);
+  }
+  const DQ r = qmul(DQ{sdd * d[0], sdd * d[1], sdd * d[2], cs}, DQ{x[0], x[1], x[2], x[3]});
+  xp[0] = r.x; xp[1] = r.y; xp[2] = r.z; xp[3] = r.w;
+}
+// grad_max_norm(x, g) <= 1e-10: max_k |x_k - (x (+) -g)_k|
+__device__ __forceinline__ bool eng_grad_small(const double* x, const double* g) {
+  double mx = 0.0;
+  for (int k = 0; k < 3; k++) mx = fmax(mx, fabs(x[4 + k] - (x[4 + k] + -g[3 + k])));
+  if (mx > 1e-10) return false;  // the rotation part only raises the maximum
+  const double ng[3] = {-g[0], -g[1], -g[2]};
+  double xp[4];
+  eng_quat_plus(x, ng, xp);
+  for (int k = 0; k < 4; k++) mx = fmax(mx, fabs(x[k] - xp[k]));
+  return mx <= 1e-10;
+}
+// packed upper index of (i, j), i <= j
+__device__ __forceinline__ constexpr int pu(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
+
+// Propose the next candidate into s.xc; false = stop (s.term set).
+__device__ __forceinline__ bool eng_propose(EngLM& s, int max_it) {
+  double A[21], sc[6], g[6];
+#pragma unroll
+  for (int e = 0; e < 21; e++) A[e] = s.A[e];
+#pragma unroll
+  for (int e = 0; e < 6; e++) { sc[e] = s.scale[e]; g[e] = s.g[e]; }
+  double b[6];
+#pragma unroll
+  for (int e = 0; e < 6; e++) b[e] = sc[e] * g[e];
+  while (s.it < max_it) {
+    s.it++;
+    if (!s.reuse)
+#pragma unroll
+      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(sc[e] * sc[e] * A[pu(e, e)], 1e-6), 1e32);
+    s.reuse = 1;
+    const double ir = 1.0 / s.radius;
+    double Dr[6];
+#pragma unroll
+    for (int e = 0; e < 6; e++) Dr[e] = s.diag[e] * ir;
+    // Cholesky of S A S + D / radius, lower factor L[i][j] at pu(j, i), reciprocals of L[j][j]
+    double L[21], inv[6];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      double d = fma(sc[j] * A[pu(j, j)], sc[j], Dr[j]);
+#pragma unroll
+      for (int k = 0; k < j; k++) d = fma(-L[pu(k, j)], L[pu(k, j)], d);
+      ok = ok && d > 0.0;
+      inv[j] = rsqrt_d(d > 0.0 ? d : 1.0);
+#pragma unroll
+      for (int i = j + 1; i < 6; i++) {
+        double v = sc[j] * A[pu(j, i)] * sc[i];
+#pragma unroll
+        for (int k = 0; k < j; k++) v = fma(-L[pu(k, i)], L[pu(k, j)], v);
+        L[pu(j, i)] = v * inv[j];
+      }
+    }
+    double y[6], z[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      double v = b[i];
+#pragma unroll
+      for (int k = 0; k < i; k++) v = fma(-L[pu(k, i)], z[k], v);
+      z[i] = v * inv[i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+      double v = z[i];
+#pragma unroll
+      for (int k = i + 1; k < 6; k++) v = fma(-L[pu(i, k)], y[k], v);
+      y[i] = v * inv[i];
+    }
+    double mcc = 0.0, yb = 0.0, yd = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) { ok = ok && isfinite(y[i]); yb = fma(y[i], b[i], yb); yd = fma(y[i] * Dr[i], y[i], yd); }
+    if (ok) mcc = 0.5 * (yb + yd);
+    if (!ok || !(mcc > 0.0)) {  // invalid step: rejected-step radius update, solve again
+      if (++s.invalid >= 5) { s.term = 2; return false; }
+      s.radius /= s.dfac;
+      s.dfac *= 2.0;
+      continue;
+    }
+    s.invalid = 0;
+    double delta[6], x[7], xc[7];
+#pragma unroll
+    for (int k = 0; k < 6; k++) delta[k] = -y[k] * sc[k];
+#pragma unroll
+    for (int k = 0; k < 7; k++) x[k] = s.x[k];
+    eng_quat_plus(x, delta, xc);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xc[4 + k] = x[4 + k] + delta[3 + k];
+#pragma unroll
+    for (int k = 0; k < 7; k++) s.xc[k] = xc[k];
+    s.mcc = mcc;
+    return true;
+  }
+  s.term = 0;  // NO_CONVERGENCE: max_num_iterations
+  return false;
+}
+
+// After the evaluation at x0 (first) or at the candidate s.xc (acc, lislam_lm.hpp layout):
+// lm_start / lm_next.  Returns whether a candidate (s.xc) must be evaluated.
+__device__ __noinline__ bool eng_step(EngLM& s, const double* x0, const double* acc, bool first, int max_it) {
+  if (first) {
+    for (int e = 0; e < 7; e++) s.x[e] = x0[e];
+    s.cost = acc[0];
+    for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
+    for (int e = 0; e < 6; e++) s.g[e] = acc[22 + e];
+    for (int e = 0; e < 6; e++) s.scale[e] = 1.0 / (1.0 + sqrt(acc[1 + pu(e, e)]));  // jacobi scaling
+    s.radius = 1e4; s.dfac = 2.0; s.reuse = 0; s.mcc = 0;
+    s.it = 0; s.invalid = 0; s.term = 0;
+    if (!isfinite(s.cost)) { s.term = 2; return false; }
+    double x[7], g[6];
+    for (int e = 0; e < 7; e++) x[e] = s.x[e];
+    for (int e = 0; e < 6; e++) g[e] = s.g[e];
+    if (eng_grad_small(x, g)) { s.term = 1; return false; }
+    return eng_propose(s, max_it);
+  }
+  double ccost = acc[0];
+  if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
+  double x[7], xc[7], xn = 0, sn = 0;
+  for (int e = 0; e < 7; e++) { x[e] = s.x[e]; xc[e] = s.xc[e]; }
+  for (int e = 0; e < 7; e++) { xn = fma(x[e], x[e], xn); sn = fma(x[e] - xc[e], x[e] - xc[e], sn); }
+  xn = sqrt(xn); sn = sqrt(sn);
+  const double cost = s.cost;
+  if (sn <= 1e-8 * (xn + 1e-8)) { s.term = 1; return false; }             // parameter_tolerance
+  if (fabs(cost - ccost) <= 1e-6 * cost) { s.term = 1; return false; }     // function_tolerance
+  const double rel = (cost - ccost) / s.mcc;
+  if (rel > 1e-3) {  // min_relative_decrease: accept
+    for (int e = 0; e < 7; e++) s.x[e] = xc[e];
+    for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
+    double g[6];
+    for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
+    s.cost = ccost;
+    const double t3 = 2.0 * rel - 1.0;
+    s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
+    s.dfac = 2.0;
+    s.reuse = 0;
+    if (eng_grad_small(xc, g)) { s.term = 1; return false; }                // gradient_tolerance
+  } else {  // reject
+    s.radius /= s.dfac;
+    s.dfac *= 2.0;
+    s.reuse = 1;
+  }
+  if (s.radius <= 1e-32) { s.term = 1; return false; }
+  return eng_propose(s, max_it);
+}
+
+// The solve item of (c, r, o) on pair k: records -> LDS, LM, outputs; publishes lm_gen[c].
+__device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
+                                          int r, int outer, const uint64_t* rec, bool wave0) {
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  const bool gated_off = a.gate && !a.gate[k];
+  const int total = gated_off ? 0 : ns + nf;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  {
+    int c0 = 0, c1 = 0;
+    for (int i = threadIdx.x; i < total; i += kEngThreads) {
+      const uint64_t* rw = rec + (size_t)i * kRecWords;
+      const int kd = (int)(uint32_t)ld_sc1(rw + 3);
+      c0 += kd == 0;
+      c1 += kd == 1;
+      if (i < kEngLds) {
+        sh.kd[i] = (int8_t)kd;
+        if (kd >= 0) {
+          const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2);
+          sh.cf[0][i] = __uint_as_float((uint32_t)w0); sh.cf[1][i] = __uint_as_float((uint32_t)(w0 >> 32));
+          sh.cf[2][i] = __uint_as_float((uint32_t)w1); sh.cf[3][i] = __uint_as_float((uint32_t)(w1 >> 32));
+          sh.cf[4][i] = __uint_as_float((uint32_t)w2); sh.cf[5][i] = __uint_as_float((uint32_t)(w2 >> 32));
+          sh.ud[0][i] = ld_sc1d((const double*)(rw + 4));
+          sh.ud[1][i] = ld_sc1d((const double*)(rw + 5));
+          sh.ud[2][i] = ld_sc1d((const double*)(rw + 6));
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 += __shfl_xor(c0, o);
+      c1 += __shfl_xor(c1, o);
+    }
+    if (lane == 0) { sh.cnt[wv][0] = c0; sh.cnt[wv][1] = c1; }
+    __syncthreads();
+  }
+  int nc = 0, np = 0;
+  for (int v = 0; v < kEngWaves; v++) { nc += sh.cnt[v][0]; np += sh.cnt[v][1]; }
+  nc = uni(nc);
+  np = uni(np);
+  bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
+  for (bool first = true; go; first = false) {
+    eng_evaluate(sh, rec, total);  // cost + J^T J + J^T r at x, then at each candidate
+    if (wave0) {
+      if (lane == 0) {
+        eng_trace(2, (unsigned)lm.it + (first ? 100u : 0u));
+        const bool cont = eng_step(lm, sh.x, sh.acc, first, a.max_iterations);
+        sh.flag = cont;
+        if (cont)
+          for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
+      }
+    }
+    __syncthreads();
+    go = uni(sh.flag);
+  }
+  if (!wave0) return;
+  if (lane != 0) return;
+  int* so = a.stats + (size_t)k * 8;
+  so[outer * 2 + 0] = nc;
+  so[outer * 2 + 1] = np;
+  so[4 + outer] = (nc + np) > 0 ? lm.it : 0;
+  so[6 + outer] = (nc + np) > 0 ? lm.term : 1;
+  double xs[7], pw[7];
+  double* st = a.state + (size_t)c * 16;
+  if (r == 0 && outer == 0) {  // the chain's pose at its first scan
+    if (a.init_state) {
+      for (int e = 0; e < 7; e++) pw[e] = a.init_state[(size_t)c * 14 + 7 + e];
+    } else {
+      for (int e = 0; e < 7; e++) pw[e] = e == 3 ? 1.0 : 0.0;
+    }
+  } else {
+    for (int e = 0; e < 7; e++) pw[e] = ld_sc1d(st + 7 + e);
+  }
+  eng_load_x(a, c, r, outer, xs);  // the pass's starting point (unchanged without blocks)
+  if ((nc + np) > 0)
+    for (int e = 0; e < 7; e++) xs[e] = lm.x[e];
+  if (outer == 1) {
+    // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr (:716-717)
+    DQ qw{pw[0], pw[1], pw[2], pw[3]};
+    D3 tw{pw[4], pw[5], pw[6]};
+    tw = tw + qrot(qw, D3{xs[4], xs[5], xs[6]});
+    qw = qmul(qw, DQ{xs[0], xs[1], xs[2], xs[3]});
+    pw[0] = qw.x; pw[1] = qw.y; pw[2] = qw.z; pw[3] = qw.w; pw[4] = tw.x; pw[5] = tw.y; pw[6] = tw.z;
+    double* op = a.para + (size_t)k * 7;
+    double* ow = a.pose + (size_t)k * 7;
+    for (int e = 0; e < 7; e++) { op[e] = xs[e]; ow[e] = pw[e]; }
+  }
+  for (int e = 0; e < 7; e++) { st_sc1d(st + e, xs[e]); st_sc1d(st + 7 + e, pw[e]); }
+  drain_stores();
+  st_rlx(ctl.lm_gen(c), (unsigned)(2 * r + outer + 1));
+  eng_trace(1, 5u);
+}
+
+// Control flow around the workgroup barriers.  Every branch tests a wave-uniform scalar: LDS
+// broadcasts go through readfirstlane, and single-lane work (ticket, waits, signals) sits in
+// `if (wave0) { if (lane == 0) ... }` — the divergent part closed inside a uniform branch.  The
+// loop takes its next ticket at the bottom and tests it at the top.  (A `for (;;)` opening with
+// `if (threadIdx.x == 0)` let the compiler rotate the divergent block into the latch, so wave 0's
+// other lanes reached the next barrier ahead of lane 0 and the waves' barrier counts diverged.)
+__global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl ctl) {
+  __shared__ EngShared sh;
+  __shared__ EngLM lm;
+  const unsigned per_ro = (unsigned)ctl.C * (ctl.I + 1);
+  const unsigned total = per_ro * 2u * ctl.R;
+  const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
+  const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
+  const bool lead = lane_id() == 0;
+  if (wave0) {
+    if (lead) {
+      sh.ticket = add_rlx(ctl.ticket(), 1u);
+      eng_trace(0, sh.ticket);
+    }
+  }
+  __syncthreads();
+  unsigned tk = (unsigned)uni((int)sh.ticket);
+  while (tk < total) {
+    const int ro = uni((int)(tk / per_ro)), rem = (int)(tk % per_ro);
+    const int r = ro >> 1, o = ro & 1, c = uni(rem / (ctl.I + 1)), item = uni(rem % (ctl.I + 1));
+    int k;
+    const bool live = pair_of(a, c, r, &k);
+    uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
+    if (wave0) {
+      if (lead) {
+        bool ok = true;
+        if (live) {
+          ok = item < ctl.I ? eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w())
+                            : eng_wait(ctl.assoc_done(c, ro), (unsigned)ctl.I, ctl.abort_w());
+          eng_trace(1, ok ? 2u : 99u);
+          if (ok) eng_load_x(a, c, r, o, sh.x);
+          if (ok && c == 0 && r == 0 && o == 0 && item == 0 && !a.init_state) {  // scan 0 of the batch: first frame
+            for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
+            for (int e = 0; e < 8; e++) a.stats[e] = 0;
+          }
+        }
+        sh.flag = ok;
+      }
+    }
+    __syncthreads();
+    const bool ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
+    if (ok && live) {
+      if (item < ctl.I) {
+        const bool gated_off = a.gate && !a.gate[k];  // not optimized: no association (:417)
+        if (!gated_off) eng_assoc(a, sh, k, item, rec);
+        drain_stores();
+        __syncthreads();
+        if (wave0) {
+          if (lead) { add_rlx(ctl.assoc_done(c, ro), 1u); eng_trace(1, 4u); }
+        }
+      } else {
+        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0);
+        __syncthreads();
+      }
+    }
+    if (wave0) {
+      if (lead) {
+        sh.ticket = add_rlx(ctl.ticket(), 1u);
+        eng_trace(0, sh.ticket);
+      }
+    }
+    __syncthreads();
+    tk = ok ? (unsigned)uni((int)sh.ticket) : total;
+  }
+}
+
+bool use_chain_engine(const OdomArgs& a, int mode) {
+  static const int env = getenv("LISLAM_ENGINE") ? atoi(getenv("LISLAM_ENGINE")) : 1;
+  if (mode == 1) mode = env;
+  if (mode == 0 || a.n_chains < 1 || !a.eng_ctl) return false;
+  if (mode == 2) return true;
+  const int I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
+  return a.n_chains * (I + 1) <= 256;
+}
+
+int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
+  if (a.n_chains <= 0) return 0;
+  EngCtl ctl;
+  ctl.w = a.eng_ctl;
+  ctl.C = a.n_chains;
+  ctl.R = min(a.chain_len, a.S - 1);
+  ctl.I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
+  const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
+  (void)hipMemsetAsync(a.eng_ctl, 0, words * sizeof(unsigned), st);
+  // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)
+  const char* cap_env = getenv("LISLAM_ENGINE_WGS");
+  const int cap = cap_env ? atoi(cap_env) : 0;
+  int grid = ctl.C * (ctl.I + 1);
+  if (cap > 0) grid = min(grid, cap);
+  hipLaunchKernelGGL(k_odom_chain, dim3(grid), dim3(kEngThreads), 0, st, a, ctl);
+  return grid;
 }
 
 void launch_factors_raw(const RawFactorArgs& a, hipStream_t st) {

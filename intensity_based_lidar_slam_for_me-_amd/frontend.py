@@ -45,6 +45,12 @@ class Context:
         nat.check(self.lib.lislam_synchronize(self.h), self.h, "lislam_synchronize")
 
     TIES_REFERENCE, TIES_INDEX = 0, 1
+    ENGINE_OFF, ENGINE_AUTO, ENGINE_ON = 0, 1, 2  # lislam_set_odometry_schedule
+
+    def set_odometry_schedule(self, mode: int):
+        """lislam_set_odometry_schedule: ENGINE_OFF (per-round launches), ENGINE_ON (one persistent
+        launch, k_odom_chain) or ENGINE_AUTO.  Results are the same."""
+        nat.check(self.lib.lislam_set_odometry_schedule(self.h, int(mode)), self.h, "lislam_set_odometry_schedule")
 
     def set_tie_order(self, order: int):
         """Order of equal voxels in the a7 VoxelGrid (lislam_set_tie_order): TIES_REFERENCE
@@ -204,6 +210,13 @@ class Batch:
             raise ValueError("use_aloam needs one flag per scan")
         nat.check(self.ctx.lib.lislam_batch_odometry_gated(self.h, n, chain_len, nat.ptr(u)), self.ctx.h,
                   "lislam_batch_odometry_gated")
+
+    def odometry_status(self) -> int:
+        """1 if the last engine launch gave up (a bounded device wait expired), else 0."""
+        st = ctypes.c_int32(0)
+        nat.check(self.ctx.lib.lislam_batch_odometry_status(self.h, ctypes.byref(st)), self.ctx.h,
+                  "lislam_batch_odometry_status")
+        return int(st.value)
 
     def skip_flags(self, n: int) -> np.ndarray:
         """use_aloam per scan from the ORB front end's results (intensity_odometry first): 1 where

@@ -23,7 +23,8 @@ OUT_PARA, OUT_POSE, OUT_STATS = 11, 12, 13
 OUT_ORB_T, OUT_ORB_STATS, OUT_ORB_KEYPOINTS, OUT_ORB_POINTS, OUT_ORB_DESCRIPTORS = 14, 15, 16, 17, 18
 OUT_GROUND, OUT_GROUND_PLANE, OUT_GROUND_INFO = 19, 20, 21
 
-KERNELS = ("k_scan_front", "k_scan_lines", "k_scan_compact", "k_target_index", "k_odom_assoc", "k_odom_lm")
+KERNELS = ("k_scan_front", "k_scan_lines", "k_scan_compact", "k_target_index", "k_odom_assoc", "k_odom_lm",
+           "k_odom_chain")
 
 EXPORTED_SYMBOLS = (
     "lislam_ctx_create", "lislam_ctx_destroy", "lislam_last_error", "lislam_synchronize",
@@ -31,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "lislam_odom_destroy", "lislam_odom_step", "lislam_batch_create", "lislam_batch_destroy",
     "lislam_batch_upload", "lislam_batch_upload_async", "lislam_batch_download_cloud", "lislam_batch_input_device_ptr", "lislam_batch_extract",
     "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
-    "lislam_batch_download", "lislam_eval_factors", "lislam_eval_factors_raw", "lislam_set_tie_order",
+    "lislam_batch_download", "lislam_eval_factors", "lislam_eval_factors_raw", "lislam_set_tie_order", "lislam_set_odometry_schedule", "lislam_batch_odometry_status",
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
     "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_mapopt_step_corner", "lislam_laser_mapping",
@@ -148,6 +149,8 @@ def load(path: str = LIB_PATH):
     L.lislam_eval_factors.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp]
     L.lislam_eval_factors_raw.argtypes = [vp, _i32, vp, vp, vp, vp, vp, vp, vp]
     L.lislam_set_tie_order.argtypes = [vp, _i32]
+    L.lislam_set_odometry_schedule.argtypes = [vp, _i32]
+    L.lislam_batch_odometry_status.argtypes = [vp, ctypes.POINTER(_i32)]
     i64, i64p = ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)
     L.lislam_map_create.argtypes = [vp, ctypes.POINTER(MapConfig), ctypes.POINTER(vp)]
     L.lislam_map_destroy.argtypes = [vp]

@@ -1,0 +1,139 @@
+"""The reference's continuous odometry chain (laserOdometry.cpp:130-135,716-717: para_q / para_t
+carried from scan to scan, one node over the whole stream) on the GPU, against the oracle's chain
+over the same scans.  Two schedules compute it (include/lislam.h, lislam_set_odometry_schedule):
+per-round launches and the persistent engine (k_odom_chain); both must equal the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4  # BASELINE.json north_star: <= 1e-4 m / <= 1e-4 rad
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(n_scans=64, width=1024)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def stream61(pkg, oracle, synth):
+    scans = synth.make_sequence(61, start=100)
+    feats = [oracle.scan_registration(s) for s in scans]
+    return scans, feats
+
+
+def check_chain(pkg, b, feats, pose, rel, st, k0=0):
+    worst = 0.0
+    for j in range(1, len(feats)):
+        k = k0 + j
+        para = b.download(pkg.native.OUT_PARA, k)
+        pw = b.download(pkg.native.OUT_POSE, k)
+        d = max(np.max(np.abs(para - rel[j])), np.max(np.abs(pw - pose[j])))
+        worst = max(worst, d)
+        assert d < POSE_TOL, (k, para, rel[j], pw, pose[j])
+        gst = b.download(pkg.native.OUT_STATS, k)
+        assert np.array_equal(gst[:6], st[j][:6]), (k, gst, st[j])  # correspondences + LM iterations
+    return worst
+
+
+def test_continuous_chain_60_pairs_engine(pkg, oracle, ctx, stream61):
+    """One continuous chain over 61 scans (60 pairs) through the persistent engine."""
+    scans, feats = stream61
+    S = len(scans)
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.odometry(S, S - 1)
+    pose, rel, st = oracle.odometry_chain(feats)
+    worst = check_chain(pkg, b, feats, pose, rel, st)
+    print(f"continuous chain of {S - 1} pairs: max |pose - oracle| = {worst:.3g}")
+    b.close()
+    ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+
+
+def test_continuous_chain_60_pairs_round_launches(pkg, oracle, ctx, stream61):
+    """The same chain through the per-round launches (k_odom_assoc16 + k_odom_lm2)."""
+    scans, feats = stream61
+    S = len(scans)
+    ctx.set_odometry_schedule(ctx.ENGINE_OFF)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.odometry(S, S - 1)
+    pose, rel, st = oracle.odometry_chain(feats)
+    check_chain(pkg, b, feats, pose, rel, st)
+    b.close()
+    ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+
+
+@pytest.mark.parametrize("chain_len", [1, 3, 7])
+def test_schedules_agree(pkg, synth, ctx, chain_len):
+    """Engine and per-round launches: the same correspondences and poses (to fp64 rounding of the
+    two evaluation forms) for several chains per batch."""
+    S = 8
+    scans = synth.make_sequence(S, start=20)
+    out = {}
+    for mode in (ctx.ENGINE_OFF, ctx.ENGINE_ON):
+        ctx.set_odometry_schedule(mode)
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, chain_len)
+        out[mode] = [(b.download(pkg.native.OUT_PARA, k), b.download(pkg.native.OUT_POSE, k),
+                      b.download(pkg.native.OUT_STATS, k)) for k in range(S)]
+        b.close()
+    ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+    for k in range(S):
+        (p0, w0, s0), (p1, w1, s1) = out[ctx.ENGINE_OFF][k], out[ctx.ENGINE_ON][k]
+        assert np.max(np.abs(p0 - p1)) < 1e-9, k
+        assert np.max(np.abs(w0 - w1)) < 1e-9, k
+        assert np.array_equal(s0, s1), (k, s0, s1)
+
+
+@pytest.mark.parametrize("wgs", [1, 5])
+def test_engine_drains_with_few_workgroups(pkg, oracle, synth, ctx, wgs):
+    """The ticket queue needs no co-residency: a grid of 1 (every ticket in turn) or 5 workgroups
+    computes the same chain."""
+    S = 5
+    scans = synth.make_sequence(S, start=40)
+    feats = [oracle.scan_registration(s) for s in scans]
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    os.environ["LISLAM_ENGINE_WGS"] = str(wgs)
+    try:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, S - 1)
+        ctx.synchronize()
+    finally:
+        del os.environ["LISLAM_ENGINE_WGS"]
+        ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+    pose, rel, st = oracle.odometry_chain(feats)
+    check_chain(pkg, b, feats, pose, rel, st)
+    b.close()
+
+
+def test_engine_gated_chain(pkg, oracle, synth, ctx):
+    """The reference's default gating inside the engine: unflagged scans skip association and solve
+    and accumulate the carried estimate (laserOdometry.cpp:403-417,716-717)."""
+    S = 8
+    scans = synth.make_sequence(S, start=50)
+    feats = [oracle.scan_registration(s) for s in scans]
+    use = np.array([0, 1, 0, 0, 1, 1, 0, 1], np.int32)
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.odometry(S, S - 1, use_aloam=use)
+    ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+    pose, rel, st = oracle.odometry_chain(feats, use_aloam=use)
+    for k in range(1, S):
+        assert np.max(np.abs(b.download(pkg.native.OUT_PARA, k) - rel[k])) < POSE_TOL, k
+        assert np.max(np.abs(b.download(pkg.native.OUT_POSE, k) - pose[k])) < POSE_TOL, k
+        assert np.array_equal(b.download(pkg.native.OUT_STATS, k)[:4], st[k][:4]), k
+    b.close()
