@@ -213,7 +213,7 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
  * solve); LISLAM_ENGINE_ON runs every round of every chain inside ONE persistent launch
  * (k_odom_chain: a device ticket queue orders the association and solve items, no host round trip
  * between scans) — the schedule of few long chains, e.g. the reference's single continuous chain;
- * LISLAM_ENGINE_AUTO (default) picks ON when every chain's workgroups fit the device at once. */
+ * LISLAM_ENGINE_AUTO (default) picks ON for at most 4 chains. */
 #define LISLAM_ENGINE_OFF 0
 #define LISLAM_ENGINE_AUTO 1
 #define LISLAM_ENGINE_ON 2

@@ -193,6 +193,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
   rc |= dalloc(b, &o.eng_ctl, (size_t)8 + 6 * (size_t)S);
   rc |= dalloc(b, &o.warm, (size_t)S * (b->cap_sharp + b->cap_flat) * 4);
+  rc |= dalloc(b, &o.eng_part, (size_t)S * ((b->cap_sharp + b->cap_flat) / 8 + 2) * 32);  // >= the engine's items
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
   rc |= dalloc(b, &b->d_gate, (size_t)S);
   if (rc != LISLAM_OK) {

@@ -104,6 +104,7 @@ struct OdomArgs {
   // association of the first outer pass, the second pass's starting bounds
   unsigned* eng_ctl;  // [8 + 6 S]
   int* warm;          // [n_chains][cap_sharp + cap_flat][4]
+  double* eng_part;   // [n_chains][items][32]: each association item's share of the first evaluation
 };
 
 // Batched evaluation of the cost functors (lislam_eval_factors).
@@ -145,7 +146,7 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
 // lislam_set_odometry_schedule (LISLAM_ENGINE_*); AUTO = the environment's LISLAM_ENGINE (0 off,
-// 2 on) if set, else on when every chain's workgroups fit the device at once.
+// 2 on) if set, else on for at most 4 chains.
 bool use_chain_engine(const OdomArgs& a, int mode);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 

@@ -447,7 +447,8 @@ __device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)
 // chunk bounds of every other super-chunk whose bound is not above the best (eight super-chunks
 // per round trip), then those chunks (eight per round trip).  Returns the original index of the
 // lexicographically smallest (distance, index), or -1.
-__device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* chm, const float4* sum, const P4& q) {
+__device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* chm, const float4* sum, const P4& q,
+                                       dkey seed = kIdent) {
   const int lane = lane_id();
   if (n <= 0) return -1;
   const int nch = (n + kChunk - 1) / kChunk, nsu = (nch + kChunk - 1) / kChunk;
@@ -481,7 +482,7 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
   bool cpend[2] = {c[0] >= 0 && c[0] < nch, false};
   float4 slo = make_float4(0.f, 0.f, 0.f, 0.f), shi = slo;
   if (cpend[0]) { slo = ldg(chm + 2 * c[0]); shi = ldg(chm + 2 * c[0] + 1); }
-  dkey best = dk(25.f, kNone);
+  dkey best = dmin(dk(25.f, kNone), seed);  // seed: a known point (d < 25) only tightens the pruning
   {  // the nearest super-chunk, all 256 points in one round trip
     dkey v = kIdent;
     P4 p[4];
@@ -1536,6 +1537,48 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
   }
 }
 
+// Developer profile of the engine (null in production): per ticket 8 u64 = s_memrealtime (100
+// MHz) at claim, inputs ready, records loaded (solve), done; summed evaluation and step ticks and
+// the evaluation count (solve).  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
+// lislam_debug_engine_prof_read copies it out.
+__device__ unsigned long long* g_eng_prof = nullptr;
+__device__ unsigned g_eng_prof_n = 0;  // tickets the buffer holds (writes past it are dropped)
+static unsigned long long* s_eng_prof = nullptr;
+static int s_eng_prof_n = 0;
+extern "C" int lislam_debug_engine_prof(int n_tickets) {
+  if (s_eng_prof) { (void)hipFree(s_eng_prof); s_eng_prof = nullptr; }
+  s_eng_prof_n = 0;
+  unsigned long long* d = nullptr;
+  if (n_tickets > 0) {
+    if (hipMalloc((void**)&d, sizeof(unsigned long long) * 8 * n_tickets) != hipSuccess) return -2;
+    if (hipMemset(d, 0, sizeof(unsigned long long) * 8 * n_tickets) != hipSuccess) return -2;
+    s_eng_prof = d;
+    s_eng_prof_n = n_tickets;
+  }
+  const unsigned n = (unsigned)s_eng_prof_n;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_eng_prof_n), &n, sizeof(n)) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_eng_prof), &d, sizeof(d)) == hipSuccess ? 0 : -2;
+}
+extern "C" int lislam_debug_engine_prof_read(unsigned long long* out, int n_tickets) {
+  if (!s_eng_prof || n_tickets > s_eng_prof_n) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpy(out, s_eng_prof, sizeof(unsigned long long) * 8 * n_tickets, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+__device__ __forceinline__ void eng_prof(unsigned tk, int slot, unsigned long long v, bool add = false) {
+  unsigned long long* p = g_eng_prof;
+  if (!p || tk >= g_eng_prof_n) return;
+  if (add) p[(size_t)tk * 8 + slot] += v;
+  else p[(size_t)tk * 8 + slot] = v;
+}
+__device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+// per-query record of one pair (developer): [outer][query] = {1-NN ticks, line-search ticks, closest, kind}
+__device__ int* g_eng_qlog = nullptr;
+__device__ int g_eng_qlog_pair = -1;
+extern "C" int lislam_debug_engine_qlog(int* dev_buf, int pair) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_eng_qlog), &dev_buf, sizeof(dev_buf)) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_eng_qlog_pair), &pair, sizeof(pair)) == hipSuccess ? 0 : -2;
+}
+
 // ================================================================== the chain engine
 // The whole odometry schedule of a few long chains (the reference's continuous para_q / para_t
 // carry, laserOdometry.cpp:130-135,716-717) as ONE persistent launch.  The schedule is a ticket
@@ -1564,7 +1607,11 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
 #endif
 constexpr int kEngThreads = LISLAM_ENG_THREADS;
 constexpr int kEngWaves = kEngThreads / 64;
-constexpr int kEngQ = kEngWaves * 4;  // queries per association item (four per wave)
+#ifndef LISLAM_ENG_ROWS16
+constexpr int kEngQ = kEngWaves;      // queries per association item: one per wave (64 lanes)
+#else
+constexpr int kEngQ = kEngWaves * 4;  // four per wave (16-lane rows, k_odom_assoc16's searches)
+#endif
 #ifndef LISLAM_ENG_LDS
 #define LISLAM_ENG_LDS 2304           // 64 lines: 12 * 64 sharp + 24 * 64 flat queries
 #endif
@@ -1601,6 +1648,7 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 struct EngCtl {
   unsigned* w;
   int C, R, I;
+  int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
@@ -1610,6 +1658,7 @@ struct EngCtl {
 // Developer trace of the engine (null in production): per workgroup {ticket, stage, LM passes,
 // time}, stored system-scope into host-pinned memory so the host can read it while the kernel runs.
 __device__ unsigned* g_eng_trace = nullptr;
+__device__ unsigned g_eng_trace_n = 0;  // workgroups the buffer holds
 extern "C" int lislam_debug_engine_trace(int n_wgs, unsigned** host_out) {
   static unsigned* h = nullptr;
   static int cap = 0;
@@ -1626,13 +1675,15 @@ extern "C" int lislam_debug_engine_trace(int n_wgs, unsigned** host_out) {
   for (int i = 0; i < 256 * n_wgs; i++) h[i] = 0xffffffffu;
   unsigned* d = nullptr;
   if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return -2;
+  const unsigned n = (unsigned)n_wgs;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_eng_trace_n), &n, sizeof(n)) != hipSuccess) return -2;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_eng_trace), &d, sizeof(d)) != hipSuccess) return -2;
   *host_out = h;
   return 0;
 }
 __device__ __forceinline__ void eng_trace(int slot, unsigned v) {
   unsigned* t = g_eng_trace;
-  if (t) __hip_atomic_store(t + (blockIdx.x * 16 + slot) * 16, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // a 64-B line each
+  if (t && blockIdx.x < g_eng_trace_n) __hip_atomic_store(t + (blockIdx.x * 16 + slot) * 16, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // a 64-B line each
 }
 
 // One lane: wait until *p >= target; false = aborted (2 s bound, or another workgroup's abort).
@@ -1655,12 +1706,13 @@ struct EngShared {
   float cf[6][kEngLds];   // query point c, first matched point a (edge) / j (plane)
   double ud[3][kEngLds];  // edge: u = (a - b) / |a - b|; plane: unit normal
   int8_t kd[kEngLds];     // 0 edge, 1 plane, -1 none
-  double red[kEngWaves * 4][kAcc];
+  double red[kEngWaves * 4][32];  // kAcc sums (+ 2 counts) per 16-lane row
   double acc[kAcc];
   double x[7];
   int cnt[kEngWaves][2];
   unsigned ticket;
-  int flag, nc, np;
+  int flag, nc, np, pref;
+  unsigned sink;
 };
 
 // x (para_q, para_t) a ticket of (c, r, o) starts from: the chain's initial state for its first
@@ -1678,12 +1730,148 @@ __device__ __forceinline__ void eng_load_x(const OdomArgs& a, int c, int r, int 
   }
 }
 
+// One association item, one query per wave (the 64-lane searches of k_odom_assoc: every round
+// trip looks at 64 candidates): queries [item * kEngQ, item * kEngQ + kEngQ) of pair k.  Faster
+// than four 16-lane rows per wave when one chain's ~2000 queries are all the GPU runs (latency
+// bound: 16.5 vs 34.9 us per round as separate launches).
+__device__ __forceinline__ void eng_assoc64(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, int* warm,
+                                            int outer, unsigned tk) {
+  const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
+  const int lane = lane_id();
+  const int ql = (int)(threadIdx.x >> 6);
+  const int w = item * kEngQ + ql;
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  if (lane == 0) sh.kd[ql] = -1;
+  if (w >= ns + nf) return;  // wave-uniform
+  const bool corner = w < ns;
+  const int t = corner ? w : w - ns;
+  const P4 qp = ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
+                           : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t);
+  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
+  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
+  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
+  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
+  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
+  double x[7];
+#pragma unroll
+  for (int e = 0; e < 7; e++) x[e] = sh.x[e];
+  const P4 cur{qp.x, qp.y, qp.z, 0.f};
+  const P4 sel = transform_to_start(cur, x);
+  // Second outer pass: the first pass's closest / second / third points seed the searches (the
+  // pose moved little).  A seed is one of the candidates of the minimum it seeds, so every result
+  // is unchanged; only the pruning starts tighter.
+  int wi[3] = {-1, -1, -1};
+  P4 wp[3];
+  if (outer == 1) {
+#pragma unroll
+    for (int e = 0; e < 3; e++) {
+      wi[e] = (int)__hip_atomic_load((gu32*)(warm + (size_t)w * 4 + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wp[e] = ld4(L + (wi[e] >= 0 && wi[e] < nL ? wi[e] : 0));
+    }
+  }
+  dkey seed = kIdent;
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    const float d = d2f(sel, wp[e]);
+    if (wi[e] >= 0 && wi[e] < nL && d < 25.f) seed = dmin(seed, dk(d, wi[e]));
+  }
+  const bool qlog = g_eng_qlog && g_eng_qlog_pair == k;
+  const unsigned long long tq1 = (threadIdx.x == 0 || qlog) ? rt_now() : 0ull;
+  const int closest = nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, seed);
+  const unsigned long long tq2 = (threadIdx.x == 0 || qlog) ? rt_now() : 0ull;
+  int kind = -1;
+  D3 u{0.0, 0.0, 0.0};
+  P4 pa{0.f, 0.f, 0.f, 0.f};
+  int i2 = -1, i3 = -1;
+  if (closest >= 0) {
+    pa = ld4(L + closest);
+    const int cid = int(pa.i);
+    dkey s2 = dk(25.f, kNone), s3 = dk(25.f, kNone);
+#pragma unroll
+    for (int e = 0; e < 3; e++) {  // seeds of the walks (:467-520 / :589-646) under this closest
+      const int j = wi[e];
+      if (j < 0 || j >= nL || j == closest) continue;
+      const int lab = int(wp[e].i);
+      const bool up = j > closest;
+      if (up ? lab > cid + 2 : lab < cid - 2) continue;  // past the walk's break
+      const float d = d2f(sel, wp[e]);
+      if (!(d < 25.f)) continue;
+      const dkey kd2 = dk(d, up ? j - closest : nL + closest - j);
+      const bool other = up ? lab > cid : lab < cid;  // another scan line
+      if (corner) {
+        if (other) s2 = dmin(s2, kd2);
+      } else {
+        if (other) s3 = dmin(s3, kd2);
+        else s2 = dmin(s2, kd2);
+      }
+    }
+    LineSearch ls{L, ix.chunk + mo, nL, (nL + kChunk - 1) / kChunk, closest, cid, sel, s2, s3};
+    if (corner) {  // LidarEdgeFactor(curr, a, b)
+      line_search<true>(ls);
+      if (dk_key(ls.b2) != kNone) {
+        i2 = rank_to_index(ls, dk_key(ls.b2));
+        const P4 pb = ld4(L + i2);
+        const D3 de{(double)pa.x - (double)pb.x, (double)pa.y - (double)pb.y, (double)pa.z - (double)pb.z};
+        const double inv = 1.0 / sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
+        u = D3{de.x * inv, de.y * inv, de.z * inv};
+        kind = 0;
+      }
+    } else {        // LidarPlaneFactor(curr, j, l, m)
+      line_search<false>(ls);
+      if (dk_key(ls.b2) != kNone) i2 = rank_to_index(ls, dk_key(ls.b2));
+      if (dk_key(ls.b3) != kNone) i3 = rank_to_index(ls, dk_key(ls.b3));
+      if (i2 >= 0 && i3 >= 0) {
+        const P4 pl = ld4(L + i2), pm = ld4(L + i3);
+        u = plane_normal(D3{pa.x, pa.y, pa.z}, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
+        kind = 1;
+      }
+    }
+  }
+  if (qlog && lane == 0) {
+    int* ql = g_eng_qlog + ((size_t)outer * (a.cap_sharp + a.cap_flat) + w) * 4;
+    ql[0] = (int)(tq2 - tq1);
+    ql[1] = (int)(rt_now() - tq2);
+    ql[2] = closest;
+    ql[3] = kind + (corner ? 10 : 20);
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long tq3 = rt_now();
+    eng_prof(tk, 4, tq1 - tq0);  // query load, transform, seeds
+    eng_prof(tk, 5, tq2 - tq1);  // 1-NN
+    eng_prof(tk, 6, tq3 - tq2);  // line searches + record
+  }
+  if (outer == 0 && lane < 3)  // seeds of the second pass (write-through: another workgroup reads them)
+    __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), (unsigned)(lane == 0 ? closest : lane == 1 ? i2 : i3),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    sh.kd[ql] = (int8_t)kind;
+    sh.cf[0][ql] = cur.x; sh.cf[1][ql] = cur.y; sh.cf[2][ql] = cur.z;
+    sh.cf[3][ql] = pa.x; sh.cf[4][ql] = pa.y; sh.cf[5][ql] = pa.z;
+    sh.ud[0][ql] = u.x; sh.ud[1][ql] = u.y; sh.ud[2][ql] = u.z;
+  }
+  if (lane >= 7 || (lane != 3 && kind < 0)) return;
+  auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
+  uint64_t v;
+  switch (lane) {
+    case 0: v = pk(cur.x, cur.y); break;
+    case 1: v = pk(cur.z, pa.x); break;
+    case 2: v = pk(pa.y, pa.z); break;
+    case 3: v = (uint64_t)(uint32_t)kind; break;
+    case 4: v = (uint64_t)__double_as_longlong(u.x); break;
+    case 5: v = (uint64_t)__double_as_longlong(u.y); break;
+    default: v = (uint64_t)__double_as_longlong(u.z); break;
+  }
+  st_sc1(rec + (size_t)w * kRecWords + lane, v);
+}
+
 // One association item: queries [item * 64, item * 64 + 64) of pair k (Morton order, corner
 // queries first), four per wave.  Record w of the chain = query w's residual block.
-__device__ __forceinline__ void eng_assoc(const OdomArgs& a, const EngShared& sh, int k, int item, uint64_t* rec) {
+__device__ __forceinline__ void eng_assoc(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, unsigned tk) {
   const int lane = lane_id(), lr = lane & 15;
-  const int w = item * kEngQ + (int)(threadIdx.x >> 6) * 4 + (lane >> 4);
+  const int ql = (int)(threadIdx.x >> 6) * 4 + (lane >> 4);  // this row's slot in the item
+  const int w = item * kEngQ + ql;
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  if (lr == 0) sh.kd[ql] = -1;  // the item's blocks are staged in LDS for its first evaluation
   if (__ballot(w < ns + nf) == 0ull) return;
   const bool has = w < ns + nf;
   const bool corner = w < ns;
@@ -1701,12 +1889,19 @@ __device__ __forceinline__ void eng_assoc(const OdomArgs& a, const EngShared& sh
   for (int e = 0; e < 7; e++) x[e] = sh.x[e];
   const P4 cur{qp.x, qp.y, qp.z, 0.f};
   const P4 sel = transform_to_start(cur, x);
+  const unsigned long long t0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int closest = nn16(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, has);
+  const unsigned long long t1 = threadIdx.x == 0 ? rt_now() : 0ull;
   const bool act = has && closest >= 0;
   const P4 pa = ld4(L + (act ? closest : 0));
   const int cid = act ? int(pa.i) : 0;
   dkey b2 = dk(25.f, kNone), b3 = dk(25.f, kNone);
   ls16(L, ix.chunk + mo, nL, act ? closest : 0, cid, sel, corner, act, b2, b3);
+  if (threadIdx.x == 0) {
+    const unsigned long long t2 = rt_now();
+    eng_prof(tk, 4, t1 - t0);
+    eng_prof(tk, 5, t2 - t1);
+  }
   auto idx_of = [&](dkey b) { const int kk = dk_key(b); return kk < nL ? closest + kk : closest - (kk - nL); };
   int kind = -1;
   D3 u{0.0, 0.0, 0.0};
@@ -1720,6 +1915,12 @@ __device__ __forceinline__ void eng_assoc(const OdomArgs& a, const EngShared& sh
     const P4 pl = ld4(L + idx_of(b2)), pm = ld4(L + idx_of(b3));
     u = plane_normal(D3{pa.x, pa.y, pa.z}, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
     kind = 1;
+  }
+  if (has && lr == 0) {
+    sh.kd[ql] = (int8_t)kind;
+    sh.cf[0][ql] = cur.x; sh.cf[1][ql] = cur.y; sh.cf[2][ql] = cur.z;
+    sh.cf[3][ql] = pa.x; sh.cf[4][ql] = pa.y; sh.cf[5][ql] = pa.z;
+    sh.ud[0][ql] = u.x; sh.ud[1][ql] = u.y; sh.ud[2][ql] = u.z;
   }
   if (!has || lr >= 7) return;
   uint64_t v;
@@ -1802,11 +2003,37 @@ __device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, con
 // 16-lane row a reduce-scatter: xor 1 / xor 2 (quad_perm) halve the values each lane carries
 // (lane i of an 8-lane group keeps part(i), part(7 - i) == part(i)), the half- and full-row mirrors
 // then pair lanes holding the same part; lanes 0..3 of each row write their 7 sums to LDS.
-__device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
+// sum index e of eng_block -> index in lislam_lm.hpp's acc (H upper row-major over (theta 0..2,
+// t 0..2), then g) and its scale: cost; M -> H_tt; T -> H_theta,t = 2 T; U -> H_theta,theta = -4 U;
+// v -> g_t; p x v -> g_theta = 2 p x v
+__constant__ int kAccMap[kAcc] = {0, 16, 17, 18, 19, 20, 21, 4, 5, 6, 9, 10, 11, 13, 14, 15,
+                                  1, 2, 3, 7, 8, 12, 25, 26, 27, 22, 23, 24};
+__device__ __forceinline__ int acc_index(int e, double* scale) {
+  *scale = e == 0 ? 1.0 : e <= 6 ? 1.0 : e <= 15 ? 2.0 : e <= 21 ? -4.0 : e <= 24 ? 1.0 : 2.0;
+  return kAccMap[e];
+}
+
+// Sum of a double over the four 16-lane rows of the wave (every lane gets its column's sum):
+// v_permlane16_swap / v_permlane32_swap pair rows (0,1)(2,3), then halves, without LDS.
+__device__ __forceinline__ double rows_sum(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  auto lo16 = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  auto hi16 = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  v = __longlong_as_double((long long)(((uint64_t)hi16[0] << 32) | lo16[0])) +
+      __longlong_as_double((long long)(((uint64_t)hi16[1] << 32) | lo16[1]));
+  const uint64_t w = (uint64_t)__double_as_longlong(v);
+  auto lo32 = __builtin_amdgcn_permlane32_swap((uint32_t)w, (uint32_t)w, false, false);
+  auto hi32 = __builtin_amdgcn_permlane32_swap((uint32_t)(w >> 32), (uint32_t)(w >> 32), false, false);
+  return __longlong_as_double((long long)(((uint64_t)hi32[0] << 32) | lo32[0])) +
+         __longlong_as_double((long long)(((uint64_t)hi32[1] << 32) | lo32[1]));
+}
+
+// Inside each 16-lane row: o[7] = the row's sums 14 (part & 1) + 7 (part >> 1) + [0, 7).
+__device__ __forceinline__ int row_reduce_scatter28(const double (&s)[kAcc], double (&o)[7]) {
   const int lane = lane_id(), i8 = lane & 7;
   const int part = (i8 & 4) ? (~i8 & 3) : (i8 & 3);
   const bool h1 = part & 1, h2 = (part >> 1) & 1;
-  double h[14], o[7];
+  double h[14];
 #pragma unroll
   for (int q = 0; q < 14; q++) {
     const double snd = h1 ? s[q] : s[q + 14];
@@ -1823,58 +2050,78 @@ __device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
   for (int q = 0; q < 7; q++) o[q] += dpp_d<0x141>(o[q]);
 #pragma unroll
   for (int q = 0; q < 7; q++) o[q] += dpp_d<0x140>(o[q]);
-  if ((lane & 15) < 4) {  // part p holds sums 14 (p & 1) + 7 (p >> 1) + [0, 7)
-    const int row = threadIdx.x >> 4, base = 14 * (part & 1) + 7 * (part >> 1);
+  return part;
+}
+
+__device__ __forceinline__ int part_base(int part) { return 14 * (part & 1) + 7 * (part >> 1); }
+
+__device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  double o[7];
+  const int part = row_reduce_scatter28(s, o);
 #pragma unroll
-    for (int q = 0; q < 7; q++) sh.red[row][base + q] = o[q];
+  for (int q = 0; q < 7; q++) o[q] = rows_sum(o[q]);  // the wave's sums of part(lane)
+  if (lane < 4) {
+    const int base = part_base(part);
+#pragma unroll
+    for (int q = 0; q < 7; q++) sh.red[wv][base + q] = o[q];
   }
   __syncthreads();
-  const int wv = threadIdx.x >> 6;
-  for (int e = wv; e < kAcc; e += kEngWaves) {
-    double v = lane < kEngWaves * 4 ? sh.red[lane][e] : 0.0;
-    v = row_sum(v);
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if (lane == 0) {
-      // sum index e -> acc index (H upper row-major over (theta 0..2, t 0..2), then g)
-      int ai;
-      double sc;
-      if (e == 0) { ai = 0; sc = 1.0; }
-      else if (e <= 6) {  // M -> H_tt
-        const int ij[6][2] = {{3, 3}, {3, 4}, {3, 5}, {4, 4}, {4, 5}, {5, 5}};
-        const int i = ij[e - 1][0], j = ij[e - 1][1];
-        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = 1.0;
-      } else if (e <= 15) {  // T -> H_theta,t = 2 T
-        const int i = (e - 7) / 3, j = 3 + (e - 7) % 3;
-        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = 2.0;
-      } else if (e <= 21) {  // U -> H_theta,theta = -4 U
-        const int ij[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
-        const int i = ij[e - 16][0], j = ij[e - 16][1];
-        ai = 1 + i * 6 - i * (i - 1) / 2 + (j - i); sc = -4.0;
-      } else if (e <= 24) { ai = 22 + 3 + (e - 22); sc = 1.0; }  // v -> g_t
-      else { ai = 22 + (e - 25); sc = 2.0; }                      // p x v -> g_theta
-      sh.acc[ai] = sc * v;
-    }
+  if (threadIdx.x < kAcc) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < kEngWaves; w++) v += sh.red[w][threadIdx.x];
+    double sc;
+    const int ai = acc_index(threadIdx.x, &sc);
+    sh.acc[ai] = sc * v;
   }
   __syncthreads();
 }
 
-// One evaluation at sh.x over `total` records (LDS for i < kEngLds, write-through records beyond).
-__device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec, int total) {
+// R (row-major rotation matrix of sh.x's quaternion: qrot of the unit vectors) and t, in scalar
+// registers (every lane holds them alike).
+__device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) {
+  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
+  const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
+  R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
+#pragma unroll
+  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);
+  t = D3{uniform_d(sh.x[4]), uniform_d(sh.x[5]), uniform_d(sh.x[6])};
+}
+
+// The item's share of the solve's first evaluation (at the x its association used): wave 0, lanes
+// 0..31 one staged block each; the 28 sums + the corner / plane counts -> part[0..29] (write-through).
+__device__ __forceinline__ void eng_item_partials(const EngShared& sh, double* part) {
+  const int lane = lane_id();
   double s[kAcc];
 #pragma unroll
   for (int e = 0; e < kAcc; e++) s[e] = 0.0;
-  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
-  D3 t{sh.x[4], sh.x[5], sh.x[6]};
-  // rotation matrix of q (the columns are q rotating the unit vectors: qrot's arithmetic)
   double R[9];
-  {
-    const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
-    R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
-  }
+  D3 t;
+  eng_rt(sh, R, t);
+  const int kd = lane < kEngQ ? (int)sh.kd[lane] : -1;
+  if (kd >= 0)
+    eng_block(kd, D3{sh.cf[0][lane], sh.cf[1][lane], sh.cf[2][lane]}, D3{sh.cf[3][lane], sh.cf[4][lane], sh.cf[5][lane]},
+              D3{sh.ud[0][lane], sh.ud[1][lane], sh.ud[2][lane]}, R, t, s);
+  double o[7];
+  const int p = row_reduce_scatter28(s, o);
 #pragma unroll
-  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);  // identical in every lane: scalar registers
-  t = D3{uniform_d(t.x), uniform_d(t.y), uniform_d(t.z)};
+  for (int q = 0; q < 7; q++) o[q] = rows_sum(o[q]);
+  const int nc = __popcll(__ballot(kd == 0)), np = __popcll(__ballot(kd == 1));
+  if (lane < 4)
+#pragma unroll
+    for (int q = 0; q < 7; q++) st_sc1d(part + part_base(p) + q, o[q]);
+  if (lane == 0) { st_sc1d(part + 28, (double)nc); st_sc1d(part + 29, (double)np); }
+}
+
+// One evaluation at sh.x over `total` records (LDS for i < kEngLds, write-through records beyond).
+__device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec, int total, unsigned tk) {
+  double s[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) s[e] = 0.0;
+  double R[9];
+  D3 t;
+  eng_rt(sh, R, t);
   for (int i = threadIdx.x; i < total; i += kEngThreads) {
     int kd;
     D3 c, pa, u;
@@ -1895,7 +2142,9 @@ __device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec,
     }
     eng_block(kd, c, pa, u, R, t, s);
   }
+  const unsigned long long t_red = threadIdx.x == 0 ? rt_now() : 0ull;
   eng_reduce(s, sh);
+  if (threadIdx.x == 0) eng_prof(tk, 7, rt_now() - t_red, true);
 }
 
 // ---- the step logic of lislam_lm.hpp (Ceres 1.14 LM, same decisions) for thread 0, lean:
@@ -1957,55 +2206,66 @@ __device__ __forceinline__ bool eng_grad_small(const double* x, const double* g)
 // packed upper index of (i, j), i <= j
 __device__ __forceinline__ constexpr int pu(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
 
-// Propose the next candidate into s.xc; false = stop (s.term set).
-__device__ __forceinline__ bool eng_propose(EngLM& s, int max_it) {
-  double A[21], sc[6], g[6];
+// Developer sub-phase profile of the step (lane 0 of the solve): accumulated ticks of the lm_next
+// logic, the factorization and the rest of propose; read and cleared by lislam_debug_step_prof.
+__device__ unsigned long long g_step_acc[4];
+extern "C" int lislam_debug_step_prof(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_acc), sizeof(g_step_acc)) != hipSuccess) return -2;
+  static const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_step_acc), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+
+// Propose the next candidate into s.xc; false = stop (s.term set).  The scaled, regularized matrix
+// is factored in place (21 doubles) and rebuilt from s.A only for another try at a smaller radius.
+__device__ __forceinline__ bool eng_propose(__attribute__((address_space(3))) EngLM& s, int max_it) {
+  double sc[6], b[6];
 #pragma unroll
-  for (int e = 0; e < 21; e++) A[e] = s.A[e];
-#pragma unroll
-  for (int e = 0; e < 6; e++) { sc[e] = s.scale[e]; g[e] = s.g[e]; }
-  double b[6];
-#pragma unroll
-  for (int e = 0; e < 6; e++) b[e] = sc[e] * g[e];
+  for (int e = 0; e < 6; e++) { sc[e] = s.scale[e]; b[e] = sc[e] * s.g[e]; }
   while (s.it < max_it) {
     s.it++;
     if (!s.reuse)
 #pragma unroll
-      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(sc[e] * sc[e] * A[pu(e, e)], 1e-6), 1e32);
+      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(sc[e] * sc[e] * s.A[pu(e, e)], 1e-6), 1e32);
     s.reuse = 1;
     const double ir = 1.0 / s.radius;
     double Dr[6];
 #pragma unroll
     for (int e = 0; e < 6; e++) Dr[e] = s.diag[e] * ir;
-    // Cholesky of S A S + D / radius, lower factor L[i][j] at pu(j, i), reciprocals of L[j][j]
+    // L (lower factor, L[i][j] at pu(j, i)) overwrites S A S + D / radius; inv = 1 / L[j][j]
     double L[21], inv[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+#pragma unroll
+      for (int i = j; i < 6; i++) L[pu(j, i)] = sc[j] * s.A[pu(j, i)] * sc[i];
     bool ok = true;
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-      double d = fma(sc[j] * A[pu(j, j)], sc[j], Dr[j]);
+      double d = L[pu(j, j)] + Dr[j];
 #pragma unroll
       for (int k = 0; k < j; k++) d = fma(-L[pu(k, j)], L[pu(k, j)], d);
       ok = ok && d > 0.0;
       inv[j] = rsqrt_d(d > 0.0 ? d : 1.0);
 #pragma unroll
       for (int i = j + 1; i < 6; i++) {
-        double v = sc[j] * A[pu(j, i)] * sc[i];
+        double v = L[pu(j, i)];
 #pragma unroll
         for (int k = 0; k < j; k++) v = fma(-L[pu(k, i)], L[pu(k, j)], v);
         L[pu(j, i)] = v * inv[j];
       }
     }
-    double y[6], z[6];
+    double y[6];
+    if (g_eng_prof) g_step_acc[1] += __builtin_amdgcn_s_memrealtime() - tf0;
 #pragma unroll
     for (int i = 0; i < 6; i++) {
       double v = b[i];
 #pragma unroll
-      for (int k = 0; k < i; k++) v = fma(-L[pu(k, i)], z[k], v);
-      z[i] = v * inv[i];
+      for (int k = 0; k < i; k++) v = fma(-L[pu(k, i)], y[k], v);
+      y[i] = v * inv[i];
     }
 #pragma unroll
     for (int i = 5; i >= 0; i--) {
-      double v = z[i];
+      double v = y[i];
 #pragma unroll
       for (int k = i + 1; k < 6; k++) v = fma(-L[pu(i, k)], y[k], v);
       y[i] = v * inv[i];
@@ -2039,98 +2299,148 @@ __device__ __forceinline__ bool eng_propose(EngLM& s, int max_it) {
 }
 
 // After the evaluation at x0 (first) or at the candidate s.xc (acc, lislam_lm.hpp layout):
-// lm_start / lm_next.  Returns whether a candidate (s.xc) must be evaluated.
-__device__ __noinline__ bool eng_step(EngLM& s, const double* x0, const double* acc, bool first, int max_it) {
+// lm_start / lm_next, then one propose.  Returns whether a candidate (s.xc) must be evaluated.
+typedef __attribute__((address_space(3))) EngLM LdsLM;
+typedef const __attribute__((address_space(3))) double LdsD;
+// The state and the evaluation stay in LDS, addressed as LDS (ds_read / ds_write): through the
+// generic pointers a call receives they would be flat accesses, each waiting on both counters.
+__device__ __noinline__ bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool first, int max_it) {
+  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+  bool cont = true;
   if (first) {
-    for (int e = 0; e < 7; e++) s.x[e] = x0[e];
+    double x[7], g[6];
+    for (int e = 0; e < 7; e++) { x[e] = x0[e]; s.x[e] = x[e]; }
     s.cost = acc[0];
     for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
-    for (int e = 0; e < 6; e++) s.g[e] = acc[22 + e];
+    for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
     for (int e = 0; e < 6; e++) s.scale[e] = 1.0 / (1.0 + sqrt(acc[1 + pu(e, e)]));  // jacobi scaling
     s.radius = 1e4; s.dfac = 2.0; s.reuse = 0; s.mcc = 0;
     s.it = 0; s.invalid = 0; s.term = 0;
-    if (!isfinite(s.cost)) { s.term = 2; return false; }
-    double x[7], g[6];
-    for (int e = 0; e < 7; e++) x[e] = s.x[e];
-    for (int e = 0; e < 6; e++) g[e] = s.g[e];
-    if (eng_grad_small(x, g)) { s.term = 1; return false; }
-    return eng_propose(s, max_it);
+    if (!isfinite(s.cost)) { s.term = 2; cont = false; }
+    else if (eng_grad_small(x, g)) { s.term = 1; cont = false; }
+  } else {
+    double ccost = acc[0];
+    if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
+    double xc[7], xn = 0, sn = 0;
+    for (int e = 0; e < 7; e++) {
+      const double xe = s.x[e];
+      xc[e] = s.xc[e];
+      xn = fma(xe, xe, xn);
+      sn = fma(xe - xc[e], xe - xc[e], sn);
+    }
+    xn = sqrt(xn); sn = sqrt(sn);
+    const double cost = s.cost;
+    if (sn <= 1e-8 * (xn + 1e-8)) { s.term = 1; cont = false; }                  // parameter_tolerance
+    else if (fabs(cost - ccost) <= 1e-6 * cost) { s.term = 1; cont = false; }    // function_tolerance
+    else {
+      const double rel = (cost - ccost) / s.mcc;
+      if (rel > 1e-3) {  // min_relative_decrease: accept
+        double g[6];
+        for (int e = 0; e < 7; e++) s.x[e] = xc[e];
+        for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
+        for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
+        s.cost = ccost;
+        const double t3 = 2.0 * rel - 1.0;
+        s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
+        s.dfac = 2.0;
+        s.reuse = 0;
+        if (eng_grad_small(xc, g)) { s.term = 1; cont = false; }                 // gradient_tolerance
+      } else {  // reject
+        s.radius /= s.dfac;
+        s.dfac *= 2.0;
+        s.reuse = 1;
+      }
+      if (cont && s.radius <= 1e-32) { s.term = 1; cont = false; }
+    }
   }
-  double ccost = acc[0];
-  if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
-  double x[7], xc[7], xn = 0, sn = 0;
-  for (int e = 0; e < 7; e++) { x[e] = s.x[e]; xc[e] = s.xc[e]; }
-  for (int e = 0; e < 7; e++) { xn = fma(x[e], x[e], xn); sn = fma(x[e] - xc[e], x[e] - xc[e], sn); }
-  xn = sqrt(xn); sn = sqrt(sn);
-  const double cost = s.cost;
-  if (sn <= 1e-8 * (xn + 1e-8)) { s.term = 1; return false; }             // parameter_tolerance
-  if (fabs(cost - ccost) <= 1e-6 * cost) { s.term = 1; return false; }     // function_tolerance
-  const double rel = (cost - ccost) / s.mcc;
-  if (rel > 1e-3) {  // min_relative_decrease: accept
-    for (int e = 0; e < 7; e++) s.x[e] = xc[e];
-    for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
-    double g[6];
-    for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
-    s.cost = ccost;
-    const double t3 = 2.0 * rel - 1.0;
-    s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
-    s.dfac = 2.0;
-    s.reuse = 0;
-    if (eng_grad_small(xc, g)) { s.term = 1; return false; }                // gradient_tolerance
-  } else {  // reject
-    s.radius /= s.dfac;
-    s.dfac *= 2.0;
-    s.reuse = 1;
+  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+  const bool r = cont && eng_propose(s, max_it);
+  if (g_eng_prof) {
+    g_step_acc[0] += ts1 - ts0;
+    g_step_acc[2] += __builtin_amdgcn_s_memrealtime() - ts1;
+    g_step_acc[3] += 1;
   }
-  if (s.radius <= 1e-32) { s.term = 1; return false; }
-  return eng_propose(s, max_it);
+  return r;
 }
 
 // The solve item of (c, r, o) on pair k: records -> LDS, LM, outputs; publishes lm_gen[c].
 __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
-                                          int r, int outer, const uint64_t* rec, bool wave0) {
+                                          int r, int outer, const uint64_t* rec, bool wave0, unsigned tk) {
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const bool gated_off = a.gate && !a.gate[k];
   const int total = gated_off ? 0 : ns + nf;
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  {
-    int c0 = 0, c1 = 0;
-    for (int i = threadIdx.x; i < total; i += kEngThreads) {
-      const uint64_t* rw = rec + (size_t)i * kRecWords;
-      const int kd = (int)(uint32_t)ld_sc1(rw + 3);
-      c0 += kd == 0;
-      c1 += kd == 1;
-      if (i < kEngLds) {
-        sh.kd[i] = (int8_t)kd;
-        if (kd >= 0) {
-          const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2);
-          sh.cf[0][i] = __uint_as_float((uint32_t)w0); sh.cf[1][i] = __uint_as_float((uint32_t)(w0 >> 32));
-          sh.cf[2][i] = __uint_as_float((uint32_t)w1); sh.cf[3][i] = __uint_as_float((uint32_t)(w1 >> 32));
-          sh.cf[4][i] = __uint_as_float((uint32_t)w2); sh.cf[5][i] = __uint_as_float((uint32_t)(w2 >> 32));
-          sh.ud[0][i] = ld_sc1d((const double*)(rw + 4));
-          sh.ud[1][i] = ld_sc1d((const double*)(rw + 5));
-          sh.ud[2][i] = ld_sc1d((const double*)(rw + 6));
-        }
+  const int lane = lane_id();
+  // the first evaluation at x (sh.x, the items' x): the sum of the items' shares
+  {  // entry e = tid % 32 of items tid / 32, tid / 32 + 16, ...: all loads in flight, then 16 rows in LDS
+    const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const double* part = a.eng_part + (size_t)c * ctl.I * 32 + e;
+    double t = 0.0;
+    for (int it0 = g; it0 < ctl.I; it0 += 16 * 24) {  // 24 loads in flight per thread (384 items per pass)
+      double v[24];
+#pragma unroll
+      for (int j = 0; j < 24; j++) {
+        const int it = it0 + 16 * j;
+        v[j] = (e < 30 && it < ctl.I) ? ld_sc1d(part + (size_t)it * 32) : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < 24; j++) t += v[j];
+    }
+    if (e < 30) sh.red[g][e] = t;
+    __syncthreads();
+    if (threadIdx.x < 30) {
+      double sum = 0.0;
+      for (int r2 = 0; r2 < 16; r2++) sum += sh.red[r2][threadIdx.x];
+      if (threadIdx.x < kAcc) {
+        double sc;
+        const int ai = acc_index(threadIdx.x, &sc);
+        sh.acc[ai] = sc * sum;
+      } else {
+        sh.cnt[0][threadIdx.x - kAcc] = (int)sum;
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      c0 += __shfl_xor(c0, o);
-      c1 += __shfl_xor(c1, o);
-    }
-    if (lane == 0) { sh.cnt[wv][0] = c0; sh.cnt[wv][1] = c1; }
     __syncthreads();
   }
-  int nc = 0, np = 0;
-  for (int v = 0; v < kEngWaves; v++) { nc += sh.cnt[v][0]; np += sh.cnt[v][1]; }
-  nc = uni(nc);
-  np = uni(np);
+  const int nc = uni(sh.cnt[0][0]), np = uni(sh.cnt[0][1]);
   bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
-  for (bool first = true; go; first = false) {
-    eng_evaluate(sh, rec, total);  // cost + J^T J + J^T r at x, then at each candidate
+  unsigned long long t_ev = 0;
+  if (threadIdx.x == 0) { t_ev = rt_now(); eng_prof(tk, 2, t_ev); }
+  if (go) {
+    if (wave0) {  // the first step on lane 0 ...
+      if (lane == 0) {
+        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, true, a.max_iterations);
+        sh.flag = cont;
+        if (cont)
+          for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
+        eng_prof(tk, 5, rt_now() - t_ev, true);
+      }
+    } else {      // ... while the other waves bring the blocks into LDS for the candidates' evaluations
+      for (int i = threadIdx.x - 64; i < min(total, kEngLds); i += kEngThreads - 64) {
+        const uint64_t* rw = rec + (size_t)i * kRecWords;
+        const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2), w3 = ld_sc1(rw + 3);
+        const uint64_t w4 = ld_sc1(rw + 4), w5 = ld_sc1(rw + 5), w6 = ld_sc1(rw + 6);
+        sh.kd[i] = (int8_t)(int)(uint32_t)w3;
+        sh.cf[0][i] = __uint_as_float((uint32_t)w0); sh.cf[1][i] = __uint_as_float((uint32_t)(w0 >> 32));
+        sh.cf[2][i] = __uint_as_float((uint32_t)w1); sh.cf[3][i] = __uint_as_float((uint32_t)(w1 >> 32));
+        sh.cf[4][i] = __uint_as_float((uint32_t)w2); sh.cf[5][i] = __uint_as_float((uint32_t)(w2 >> 32));
+        sh.ud[0][i] = __longlong_as_double((long long)w4);
+        sh.ud[1][i] = __longlong_as_double((long long)w5);
+        sh.ud[2][i] = __longlong_as_double((long long)w6);
+      }
+    }
+    __syncthreads();
+    go = uni(sh.flag);
+    if (threadIdx.x == 0) t_ev = rt_now();
+  }
+  while (go) {
+    eng_evaluate(sh, rec, total, tk);  // cost + J^T J + J^T r at each candidate
     if (wave0) {
       if (lane == 0) {
-        eng_trace(2, (unsigned)lm.it + (first ? 100u : 0u));
-        const bool cont = eng_step(lm, sh.x, sh.acc, first, a.max_iterations);
+        const unsigned long long t_st = rt_now();
+        eng_prof(tk, 4, t_st - t_ev, true);
+        eng_prof(tk, 6, 1ull, true);
+        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, false, a.max_iterations);
+        t_ev = rt_now();
+        eng_prof(tk, 5, t_ev - t_st, true);
         sh.flag = cont;
         if (cont)
           for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
@@ -2175,6 +2485,39 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
   drain_stores();
   st_rlx(ctl.lm_gen(c), (unsigned)(2 * r + outer + 1));
   eng_trace(1, 5u);
+  eng_prof(tk, 3, rt_now());
+}
+
+// Touch (one dword per 128-B line, plain loads: they allocate in this XCD's L2) every structure the
+// association of pair k reads: the Morton copies, the chunk / super-chunk boxes and the clouds of
+// scan k-1's less-sharp and less-flat sets.  Waves 1.. of a workgroup whose ticket must wait.
+__device__ __forceinline__ void eng_prefetch(const OdomArgs& a, EngShared& sh, int k, int t0, int nt) {
+  unsigned acc = 0;
+  auto touch = [&](const void* base, size_t bytes) {
+    const __attribute__((address_space(1))) unsigned* p = (const __attribute__((address_space(1))) unsigned*)base;
+    for (size_t o = (size_t)t0 * 32; o < bytes / 4; o += (size_t)nt * 32) acc ^= p[o];
+  };
+  for (int which = 0; which < 2; which++) {
+    const TargetIndex& ix = which ? a.idx_lf : a.idx_ls;
+    const int nL = a.n_feat[(k - 1) * 4 + (which ? 3 : 1)];
+    const int nch = (nL + kChunk - 1) / kChunk, nsu = (nch + kChunk - 1) / kChunk;
+    const P4* L = which ? a.less_flat + (size_t)(k - 1) * a.N : a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp;
+    touch(ix.nn_super + (size_t)(k - 1) * ix.nsuper * 2, (size_t)nsu * 32);
+    touch(ix.nn_chunk + (size_t)(k - 1) * ix.nchunk * 2, (size_t)nch * 32);
+    touch(ix.chunk + (size_t)(k - 1) * ix.nchunk * 2, (size_t)nch * 32);
+    touch(ix.sorted + (size_t)(k - 1) * ix.cap, (size_t)nL * 16);
+    touch(L, (size_t)nL * 16);
+  }
+  if (acc == 0x9e3779b9u) sh.sink = acc;  // keeps the loads
+}
+
+// An association ticket whose solve has not finished yet: its waves 1.. prefetch meanwhile.
+__device__ __forceinline__ int eng_wants_prefetch(const EngCtl& ctl, unsigned t, unsigned per_ro) {
+  if (!ctl.prefetch) return 0;
+  const int ro = (int)(t / per_ro), rem = (int)(t % per_ro);
+  const int c = rem / (ctl.I + 1), item = rem % (ctl.I + 1);
+  if (item >= ctl.I || ro >= 2 * ctl.R || ro == 0) return 0;
+  return ld_rlx(ctl.lm_gen(c)) < (unsigned)ro ? 1 : 0;
 }
 
 // Control flow around the workgroup barriers.  Every branch tests a wave-uniform scalar: LDS
@@ -2193,8 +2536,11 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
   const bool lead = lane_id() == 0;
   if (wave0) {
     if (lead) {
-      sh.ticket = add_rlx(ctl.ticket(), 1u);
-      eng_trace(0, sh.ticket);
+      const unsigned t = add_rlx(ctl.ticket(), 1u);
+      sh.ticket = t;
+      sh.pref = eng_wants_prefetch(ctl, t, per_ro);
+      eng_trace(0, t);
+      if (t < total) eng_prof(t, 0, rt_now());
     }
   }
   __syncthreads();
@@ -2205,6 +2551,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     int k;
     const bool live = pair_of(a, c, r, &k);
     uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
+    if (!wave0 && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
     if (wave0) {
       if (lead) {
         bool ok = true;
@@ -2212,6 +2559,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
           ok = item < ctl.I ? eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w())
                             : eng_wait(ctl.assoc_done(c, ro), (unsigned)ctl.I, ctl.abort_w());
           eng_trace(1, ok ? 2u : 99u);
+          eng_prof(tk, 1, rt_now());
           if (ok) eng_load_x(a, c, r, o, sh.x);
           if (ok && c == 0 && r == 0 && o == 0 && item == 0 && !a.init_state) {  // scan 0 of the batch: first frame
             for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
@@ -2226,21 +2574,34 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     if (ok && live) {
       if (item < ctl.I) {
         const bool gated_off = a.gate && !a.gate[k];  // not optimized: no association (:417)
-        if (!gated_off) eng_assoc(a, sh, k, item, rec);
+#ifndef LISLAM_ENG_ROWS16
+        if (!gated_off)
+          eng_assoc64(a, sh, k, item, rec, a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4, o, tk);
+#else
+        if (!gated_off) eng_assoc(a, sh, k, item, rec, tk);
+#endif
+        else if (threadIdx.x < kEngQ) sh.kd[threadIdx.x] = -1;
         drain_stores();
         __syncthreads();
         if (wave0) {
-          if (lead) { add_rlx(ctl.assoc_done(c, ro), 1u); eng_trace(1, 4u); }
+          const unsigned long long tp0 = lead ? rt_now() : 0ull;
+          eng_item_partials(sh, a.eng_part + ((size_t)c * ctl.I + item) * 32);
+          if (lead) eng_prof(tk, 7, rt_now() - tp0);
+          drain_stores();
+          if (lead) { add_rlx(ctl.assoc_done(c, ro), 1u); eng_trace(1, 4u); eng_prof(tk, 3, rt_now()); }
         }
       } else {
-        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0);
+        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0, tk);
         __syncthreads();
       }
     }
     if (wave0) {
       if (lead) {
-        sh.ticket = add_rlx(ctl.ticket(), 1u);
-        eng_trace(0, sh.ticket);
+        const unsigned t = add_rlx(ctl.ticket(), 1u);
+        sh.ticket = t;
+        sh.pref = eng_wants_prefetch(ctl, t, per_ro);
+        eng_trace(0, t);
+        if (t < total) eng_prof(t, 0, rt_now());
       }
     }
     __syncthreads();
@@ -2248,13 +2609,14 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
   }
 }
 
+extern "C" int lislam_debug_engine_items(int cap_queries) { return (cap_queries + kEngQ - 1) / kEngQ; }
+
 bool use_chain_engine(const OdomArgs& a, int mode) {
   static const int env = getenv("LISLAM_ENGINE") ? atoi(getenv("LISLAM_ENGINE")) : 1;
   if (mode == 1) mode = env;
   if (mode == 0 || a.n_chains < 1 || !a.eng_ctl) return false;
   if (mode == 2) return true;
-  const int I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
-  return a.n_chains * (I + 1) <= 256;
+  return a.n_chains <= 4;  // few long chains (the continuous chain, a rank's shard); many short: rounds
 }
 
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
@@ -2264,6 +2626,8 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
   ctl.I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
+  const char* pf = getenv("LISLAM_ENGINE_PREFETCH");
+  ctl.prefetch = pf ? atoi(pf) : 1;
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   (void)hipMemsetAsync(a.eng_ctl, 0, words * sizeof(unsigned), st);
   // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)

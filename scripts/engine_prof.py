@@ -1,0 +1,95 @@
+"""Developer tool (GPU box): phase profile of the chain engine on one continuous chain — per round
+and outer pass, from the device's own clock (s_memrealtime, 10 ns ticks): association span,
+association -> solve hand-off, record load, evaluations, steps, solve -> association hand-off.
+usage: python scripts/engine_prof.py [S]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, _R)
+import __graft_entry__ as g  # noqa: E402
+
+pkg = g.package()
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+cache = f"/tmp/lislam_chain_scans_{S}.npy"
+if os.path.exists(cache):
+    scans = np.load(cache)
+else:
+    scans = pkg.synth.make_sequence(S)
+    np.save(cache, scans)
+if len(sys.argv) > 2:
+    os.environ["LISLAM_ENGINE_PREFETCH"] = sys.argv[2]
+with pkg.Context() as ctx:
+    lib = ctx.lib
+    lib.lislam_debug_engine_prof.argtypes = [ctypes.c_int]
+    lib.lislam_debug_engine_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    b = pkg.Batch(ctx, S)
+    b.upload(scans)
+    b.extract(S)
+    b.odometry(S, S - 1)
+    ctx.synchronize()
+    I = lib.lislam_debug_engine_items(12 * 64 + 24 * 64)
+    R = S - 1
+    T = 2 * R * (I + 1)
+    assert lib.lislam_debug_engine_prof(T) == 0
+    b.odometry(S, S - 1)
+    ctx.synchronize()
+    sp = np.zeros(4, np.uint64)
+    lib.lislam_debug_step_prof.argtypes = [ctypes.c_void_p]
+    buf = np.zeros((T, 8), np.uint64)
+    assert lib.lislam_debug_engine_prof_read(buf.ctypes.data, T) == 0
+    assert lib.lislam_debug_step_prof(sp.ctypes.data) == 0
+    lib.lislam_debug_engine_prof(0)
+    p = buf.reshape(2 * R, I + 1, 8).astype(np.int64)
+    us = 0.01
+    items, lm = p[:, :I], p[:, I]
+    valid = items[:, :, 3] > 0  # items that ran (all live ones)
+    a_start = np.where(valid, items[:, :, 1], np.iinfo(np.int64).max).min(1)
+    a_end = np.where(valid, items[:, :, 3], 0).max(1)
+    a_med = np.array([np.median(items[i, valid[i], 3] - items[i, valid[i], 1]) for i in range(2 * R)])
+    lm_ready, lm_loaded, lm_done = lm[:, 1], lm[:, 2], lm[:, 3]
+    ev, st, npass = lm[:, 4], lm[:, 5], lm[:, 6]
+    span = (lm_done[-1] - a_start[0]) * us
+    print(f"chain of {R} pairs: {span / 1e3:.2f} ms on the device clock, {span / (2 * R):.1f} us per outer pass")
+    rows = {
+        "association span (first ready -> last done)": (a_end - a_start) * us,
+        "association item median (ready -> done)": a_med * us,
+        "hand-off assoc -> solve (last item done -> solve ready)": (lm_ready - a_end) * us,
+        "solve record load": (lm_loaded - lm_ready) * us,
+        "solve evaluations (sum)": ev * us,
+        "solve steps (sum)": st * us,
+        "solve evaluations: reductions (sum)": lm[:, 7] * us,
+        "solve total (ready -> done)": (lm_done - lm_ready) * us,
+        "hand-off solve -> assoc (solve done -> next first item ready)": (a_start[1:] - lm_done[:-1]) * us,
+    }
+    w0 = items[:, :, 5] > 0
+    med = lambda col: np.array([np.median(items[i, w0[i], col]) for i in range(2 * R)]) * us
+    rows["association wave 0: query load + transform + seeds"] = med(4)
+    rows["association wave 0: 1-NN (nn_wave)"] = med(5)
+    rows["association wave 0: line searches + record"] = med(6)
+    rows["association item: first-evaluation share (wave 0)"] = med(7)
+    rows["association wave 0: 1-NN, outer 1 (seeded)"] = med(5)[1::2]
+    rows["association wave 0: line searches, outer 1 (seeded)"] = med(6)[1::2]
+    rows["association span, outer pass 0"] = ((a_end - a_start) * us)[0::2]
+    rows["association span, outer pass 1 (seeded)"] = ((a_end - a_start) * us)[1::2]
+    rows["association item median, outer 0"] = (a_med * us)[0::2]
+    rows["association item median, outer 1"] = (a_med * us)[1::2]
+    late = np.array([np.sum(valid[i] & (items[i, :, 1] - a_start[i] > 300)) for i in range(2 * R)])  # > 3 us after
+    spread = np.array([np.percentile(items[i, valid[i], 1] - a_start[i], 90) for i in range(2 * R)]) * us
+    done_last = np.array([np.max(items[i, valid[i], 3] - items[i, valid[i], 1]) for i in range(2 * R)]) * us
+    rows["association items ready > 3 us after the first (count)"] = late
+    rows["association ready-time spread p90 (us)"] = spread
+    rows["association slowest item (ready -> done)"] = done_last
+    claim_ready = np.array([np.median(items[i, valid[i], 1] - items[i, valid[i], 0]) for i in range(2 * R)]) * us
+    rows["association item claim -> ready median"] = claim_ready
+    for k, v in rows.items():
+        print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")
+    print(f"  evaluations per solve: mean {np.mean(npass):.2f}")
+    n = max(int(sp[3]), 1)
+    print(f"  step sub-phases per step: lm_next logic {sp[0] * us / n:.2f} us, factorization {sp[1] * us / n:.2f} us, "
+          f"propose total {sp[2] * us / n:.2f} us ({n} steps)")
+    b.close()

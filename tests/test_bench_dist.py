@@ -76,12 +76,14 @@ def test_bench_gpus_flag_starts_the_ranks():
 
 @pytest.mark.timeout(200)
 def test_bench_config4_total_scans_shards():
-    """Config 4: 1000 scans split into contiguous shards of ceil(1000 / N); chains restart at
-    every shard boundary."""
+    """Config 4: 1000 scans split into contiguous shards of ceil(1000 / N); the chain restarts at
+    every shard boundary: one continuous chain per shard, or chains of --chain."""
     d = _bench("--gpus", "3", "--dry-run", "--total-scans", "1000")
     assert d["scaling"] == "strong"
     assert d["shards"] == [[0, 334], [334, 334], [668, 332]]
-    assert d["chains_per_shard"] == [34, 34, 34]  # ceil((334 - 1) / 10), ceil(331 / 10)
+    assert d["chains_per_shard"] == [1, 1, 1]  # one continuous chain per shard (the default)
+    d10 = _bench("--gpus", "3", "--dry-run", "--total-scans", "1000", "--chain", "10")
+    assert d10["chains_per_shard"] == [34, 34, 34]  # ceil((334 - 1) / 10), ceil(331 / 10)
     d1 = _bench("--dry-run", "--total-scans", "1000")
     assert d1["n_gpus"] == 1 and d1["shards"] == [[0, 1000]]
 
