@@ -202,12 +202,6 @@ int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst
 int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,
                                 int32_t cap, int32_t* n);
 
-/* Order of equal keys in the scan-line VoxelGrid(0.2) of the less-flat cloud (a7,
- * scanRegistration.cpp:583-586): PCL 1.10's VoxelGrid sorts (voxel, point) pairs with std::sort
- * by voxel alone, so a voxel's points are summed in the order libstdc++'s introsort leaves them.
- * LISLAM_TIES_REFERENCE (the default) replays that order exactly (bit-exact centroids);
- * LISLAM_TIES_INDEX sums them in input order (faster; centroids differ by float rounding, poses by
- * up to 1e-4 on the bench data, tests/test_oracle.py).  Applies to later extractions of ctx. */
 /* Odometry schedule of lislam_batch_odometry (results are the same): LISLAM_ENGINE_OFF issues one
  * association and one solve launch per round (chains advance together, one workgroup per chain's
  * solve); LISLAM_ENGINE_ON runs every round of every chain inside ONE persistent launch
@@ -222,6 +216,16 @@ int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
  * device waits expired: its outputs are invalid), else 0. */
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
 
+/* Order of equal sort keys in the two std::sort calls of the feature extraction:
+ * - each segment's sort by curvature (scanRegistration.cpp:445), which decides which of two
+ *   points of equal curvature the sharp / flat walks (:450-568) reach first;
+ * - the scan-line VoxelGrid(0.2) of the less-flat cloud (a7, :583-586): PCL 1.10's VoxelGrid
+ *   sorts (voxel, point) pairs with std::sort by voxel alone, so a voxel's points are summed in
+ *   the order libstdc++'s introsort leaves them.
+ * LISLAM_TIES_REFERENCE (the default) replays libstdc++'s order exactly in both (bit-exact
+ * selections and centroids); LISLAM_TIES_INDEX breaks ties by point index (faster; centroids
+ * differ by float rounding, poses by up to 1e-4 on the bench data, tests/test_oracle.py).
+ * Applies to later extractions of ctx. */
 #define LISLAM_TIES_REFERENCE 0
 #define LISLAM_TIES_INDEX 1
 int lislam_set_tie_order(lislam_ctx* ctx, int32_t order);

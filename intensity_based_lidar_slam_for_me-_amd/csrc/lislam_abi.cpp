@@ -407,9 +407,15 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   if (!b || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
+  // a pending ORB cascade may still need the current images (its host-round redo): settle it
+  // before they are overwritten
+  if (b->orb) {
+    const int rc = orb_settle(b);
+    if (rc != LISLAM_OK) return rc;
+  }
   FeatureArgs f = b->fa;
   f.S = n_scans;
-  f.voxel_ties = c->voxel_ties;
+  f.ties = c->ties;
   hipEvent_t* ev = nullptr;
   if (b->timing) {
     b->ext_ev.emplace_back();
@@ -850,7 +856,7 @@ int lislam_set_odometry_schedule(lislam_ctx* c, int32_t mode) {
 
 int lislam_set_tie_order(lislam_ctx* c, int32_t order) {
   if (!c || (order != LISLAM_TIES_REFERENCE && order != LISLAM_TIES_INDEX)) return LISLAM_ERR_ARG;
-  c->voxel_ties = order;
+  c->ties = order;
   return LISLAM_OK;
 }
 

@@ -79,3 +79,7 @@ int lislam_ground_batch_output(lislam_batch* b, int what, int scan, const void**
 void lislam_free_orb(void* p);
 // Device source of the ORB outputs (LISLAM_OUT_ORB_*) of one scan (lislam_orb.hip).
 int lislam_orb_batch_output(lislam_batch* b, int what, int scan, const void** src, int* cnt, size_t* esz);
+// Resolves a pending device-decided ORB cascade (lislam_orb.hip): waits for its verdict and, if it
+// did not converge, redoes the batch from the images it was given.  lislam_batch_extract calls it
+// before it overwrites those images.
+int orb_settle(lislam_batch* b);

@@ -36,7 +36,7 @@ struct lislam_ctx {
   lislam_batch* single = nullptr;  // 2-scan batch behind lislam_scan_registration / odom_step
   void* map_scratch = nullptr;     // device scratch of the stateless mapping entry points
   lislam_ktimer mtimer;            // mapping-kernel timing
-  int voxel_ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order
+  int ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order
   int odom_engine = LISLAM_ENGINE_AUTO;     // lislam_set_odometry_schedule
 };
 

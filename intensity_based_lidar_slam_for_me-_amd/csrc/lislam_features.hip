@@ -654,6 +654,25 @@ __device__ __forceinline__ void introsort_order_lds(uint32_t* a, KeyOf kof, int 
   }
 }
 
+// std::sort's final positions after its introsort loop (std::__final_insertion_sort, see the
+// VoxelGrid below): element el[j] ends at j minus the greater keys among the 15 positions before
+// it plus the smaller keys among the 15 after it.  pos[el[j]] <- that position (pos is distinct
+// from el; the elements are 0 .. n-1).
+template <bool kLds, typename ElemPtr, typename KeyOf, typename PosPtr>
+__device__ __forceinline__ void final_positions(ElemPtr el, KeyOf kof, int n, PosPtr pos) {
+  for (int j = lane_id(); j < n; j += 64) {
+    const uint32_t e = el[j];
+    const uint32_t k = kof(e);
+    int mv = 0;
+#pragma unroll
+    for (int d = 1; d <= 15; d++) {
+      if (j - d >= 0 && kof(el[j - d]) > k) mv--;
+      if (j + d < n && kof(el[j + d]) < k) mv++;
+    }
+    pos[e] = j + mv;
+  }
+  wave_sync<kLds>();
+}
 
 struct LineCounts {
   int sharp, less_sharp, flat, less_flat;
@@ -753,18 +772,58 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
     for (int j = 0; j < 6; j++) {
       const int sp = sI + (eI - sI) * j / 6;
       const int ep = sI + (eI - sI) * (j + 1) / 6 - 1;
-      // ---- sharp picks: largest curvature first (:450-506); at most 20 per segment
-      for (int largest = 1; largest <= 20; largest++) {
-        uint64_t best = 0;
+      // keys (curvature, index) until a pick meets a tie (TIES_REFERENCE), then (std::sort's
+      // position, index): the segment's sort replayed in the key buffer, which the walks leave
+      // unused (line_body_reg documents the scheme)
+      const bool want_replay = a.ties == LISLAM_TIES_REFERENCE;
+      bool by_pos = false;  // keys are sorted positions (after a replay)
+      // [n] elements, then [n + 2] index scratch / positions (past the curvature when it is LDS)
+      uint32_t* seg_el = reinterpret_cast<uint32_t*>(keys) + (kLds ? len : 0);
+      uint32_t* seg_pos = seg_el + (ep - sp + 1);
+      auto key_of = [&](int k) -> uint64_t {
+        const uint32_t hi = by_pos ? seg_pos[k - sp] : __float_as_uint(curvL[k]);
+        return ((uint64_t)hi << 32) | (uint32_t)k;
+      };
+      auto walk_best = [&](bool largest) {
+        uint64_t best = largest ? 0ull : ~0ull;
         for (int k = sp + lane; k <= ep; k += 64) {
           const float c = curvL[k];
-          if (picked[k] == 0 && (double)c > 0.1) {
-            const uint64_t key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)k;
-            best = key > best ? key : best;
+          if (picked[k] == 0 && (largest ? (double)c > 0.1 : (double)c < 0.1)) {
+            const uint64_t key = key_of(k);
+            best = largest ? (key > best ? key : best) : (key < best ? key : best);
           }
         }
-        best = wave_max_u64(best);
+        return largest ? wave_max_u64(best) : wave_min_u64(best);
+      };
+      auto tie_at = [&](bool largest, uint64_t best) {
+        const uint32_t bc = (uint32_t)(best >> 32);
+        bool t = false;
+        for (int k = sp + lane; k <= ep; k += 64) {
+          const float c = curvL[k];
+          if (picked[k] == 0 && (largest ? (double)c > 0.1 : (double)c < 0.1) && __float_as_uint(c) == bc &&
+              k != (int)(uint32_t)best)
+            t = true;
+        }
+        return __ballot(t) != 0ull;
+      };
+      auto replay = [&]() {
+        const int n = ep - sp + 1;
+        for (int i = lane; i < n; i += 64) seg_el[i] = (uint32_t)i;
+        wave_sync<kLds>();
+        auto kof = [&](uint32_t e) { return __float_as_uint(curvL[sp + (int)e]); };
+        introsort_order<kLds>(seg_el, kof, n, seg_pos, seg_pos + (n / 2 + 1));
+        wave_sync<kLds>();
+        final_positions<kLds>(seg_el, kof, n, seg_pos);
+        by_pos = true;
+      };
+      // ---- sharp picks: largest key first (:450-506); at most 20 per segment
+      for (int largest = 1; largest <= 20; largest++) {
+        uint64_t best = walk_best(true);
         if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
+        if (want_replay && !by_pos && tie_at(true, best)) {
+          replay();
+          best = walk_best(true);
+        }
         const int ind = (int)(uint32_t)best;
         if (lane == 0) {
           if (largest <= 2) {
@@ -782,18 +841,14 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
         suppress<kLds>(link, ind, picked);
       }
       PHASE(2);
-      // ---- flat picks: smallest curvature first (:511-568); the 4th pick ends the walk unmarked
+      // ---- flat picks: smallest key first (:511-568); the 4th pick ends the walk unmarked
       for (int smallest = 1; smallest <= 4; smallest++) {
-        uint64_t best = ~0ull;
-        for (int k = sp + lane; k <= ep; k += 64) {
-          const float c = curvL[k];
-          if (picked[k] == 0 && (double)c < 0.1) {
-            const uint64_t key = ((uint64_t)__float_as_uint(c) << 32) | (uint32_t)k;
-            best = key < best ? key : best;
-          }
-        }
-        best = wave_min_u64(best);
+        uint64_t best = walk_best(false);
         if (best == ~0ull) break;
+        if (want_replay && !by_pos && tie_at(false, best)) {
+          replay();
+          best = walk_best(false);
+        }
         const int ind = (int)(uint32_t)best;
         if (lane == 0) {
           label[ind] = -1;
@@ -873,7 +928,7 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
           el[k] = ((uint64_t)(uint32_t)(i0 + i1 * mul1 + i2 * mul2) << 32) | (uint32_t)list[k];
         }
         wave_sync<kLds>();
-        if (a.voxel_ties == LISLAM_TIES_REFERENCE)
+        if (a.ties == LISLAM_TIES_REFERENCE)
           introsort_order<kLds>(el, [](uint64_t e) { return (uint32_t)(e >> 32); }, nlist, lidx, ridx);
         // keys (voxel, position after the introsort loop) and the list in that order.  Key k
         // occupies bytes 8 k .. 8 k + 7 < 8 len, below the elements; the padding keys beyond the
@@ -1099,15 +1154,60 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         if (in && (double)c < 0.1) ef |= 1u << u;
       }
       uint32_t pw = (pick >> t0) & ((1u << kW) - 1u), lw = 0, sw = 0, fw = 0;
-      // ---- sharp picks: largest (curvature, index) first (:450-506); at most 20 per segment
-      for (int largest = 1; largest <= 20; largest++) {
-        const uint32_t ok = es & ~pw;
+      // Equal curvatures (TIES_REFERENCE): the walks reach them in std::sort's order.  While no
+      // pick meets a tie the keys stay (curvature, index); the first pick whose extreme curvature
+      // is shared by another candidate replays the segment's sort (introsort_order_lds on the
+      // dead curvature ring) and re-keys the window by sorted position, a refinement of the
+      // curvature order, so the picks made so far stand.
+      bool by_pos = a.ties != LISLAM_TIES_REFERENCE;  // true: no replay wanted / already done
+      auto tie_at = [&](uint32_t ok, uint64_t best) {
+        const uint32_t bc = (uint32_t)(best >> 32);
+        bool t = false;
+#pragma unroll
+        for (int u = 0; u < kW; u++)
+          if (((ok >> u) & 1u) && (uint32_t)(kw[u] >> 32) == bc && kw[u] != best) t = true;
+        return __ballot(t) != 0ull;
+      };
+      auto replay = [&]() {
+        const int n = ep - sp + 1;
+        uint32_t* sel = reinterpret_cast<uint32_t*>(ring);
+        uint16_t* sidx = reinterpret_cast<uint16_t*>(sel + kSeg);
+        for (int i = lane; i < n; i += 64) sel[i] = (uint32_t)i;
+        wave_sync<true>();
+        auto kof = [&](uint32_t e) { return __float_as_uint(curvl[sp + (int)e]); };
+        introsort_order_lds<kS>(sel, kof, n, sidx, sidx + (n / 2 + 1));
+        wave_sync<true>();
+        final_positions<true>(sel, kof, n, sidx);
+#pragma unroll
+        for (int u = 0; u < kW; u++) {
+          const int k = wb + 64 * u + lane;
+          kw[u] = k >= sp && k <= ep ? ((uint64_t)sidx[k - sp] << 32) | (uint32_t)k : 0ull;
+        }
+        by_pos = true;
+      };
+      auto max_key = [&](uint32_t ok) {
         uint64_t best = 0;
 #pragma unroll
         for (int u = 0; u < kW; u++)
           if ((ok >> u) & 1u) best = kw[u] > best ? kw[u] : best;
-        best = wave_max_u64(best);
+        return wave_max_u64(best);
+      };
+      auto min_key = [&](uint32_t ok) {
+        uint64_t best = ~0ull;
+#pragma unroll
+        for (int u = 0; u < kW; u++)
+          if ((ok >> u) & 1u) best = kw[u] < best ? kw[u] : best;
+        return wave_min_u64(best);
+      };
+      // ---- sharp picks: largest key first (:450-506); at most 20 per segment
+      for (int largest = 1; largest <= 20; largest++) {
+        const uint32_t ok = es & ~pw;
+        uint64_t best = max_key(ok);
         if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
+        if (!by_pos && tie_at(ok, best)) {
+          replay();
+          best = max_key(ok);
+        }
         const int ind = (int)(uint32_t)best;
         if (lane == 0) {
           if (largest <= 2) ll.sharp[n_sharp] = ind;
@@ -1123,16 +1223,15 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         mark(ind, wb, pw);
       }
       PHASE(2);
-      // ---- flat picks: smallest (curvature, index) first (:511-568); the 4th pick ends the walk
-      // unmarked
+      // ---- flat picks: smallest key first (:511-568); the 4th pick ends the walk unmarked
       for (int smallest = 1; smallest <= 4; smallest++) {
         const uint32_t ok = ef & ~pw;
-        uint64_t best = ~0ull;
-#pragma unroll
-        for (int u = 0; u < kW; u++)
-          if ((ok >> u) & 1u) best = kw[u] < best ? kw[u] : best;
-        best = wave_min_u64(best);
+        uint64_t best = min_key(ok);
         if (best == ~0ull) break;
+        if (!by_pos && tie_at(ok, best)) {
+          replay();
+          best = min_key(ok);
+        }
         const int ind = (int)(uint32_t)best;
         if (lane == 0) ll.flat[n_flat] = ind;
         if (lane == (ind & 63)) fw |= 1u << ((ind - wb) >> 6);
@@ -1237,7 +1336,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       // below.  Voxel indices below 2^21 pack with the 11-bit line position directly; otherwise a
       // first sort of (voxel, list position) numbers the voxels densely for the element.
       int sort_to = 64 * kS;  // the bitonic network's last level (none when key[] is already sorted)
-      if (a.voxel_ties == LISLAM_TIES_REFERENCE) {
+      if (a.ties == LISLAM_TIES_REFERENCE) {
         uint32_t vmax = 0u;
 #pragma unroll
         for (int t = 0; t < kS; t++)

@@ -53,7 +53,8 @@ struct FeatureArgs {
   int* n_feat;     // [S][4] = sharp, less_sharp, flat, less_flat
   int* feat_loff;  // [S][2][H+1] per-line offsets of less_sharp / less_flat
   int cap_sharp, cap_less_sharp, cap_flat;
-  int voxel_ties;  // a7 VoxelGrid order of equal voxels: LISLAM_TIES_REFERENCE (std::sort) / _INDEX
+  int ties;  // order of equal keys in the segment sorts and the a7 VoxelGrid: LISLAM_TIES_REFERENCE
+            // (libstdc++ std::sort's) / LISLAM_TIES_INDEX
 };
 
 // Spatial index of a feature cloud: chunks of kChunk consecutive points (in the cloud's own,

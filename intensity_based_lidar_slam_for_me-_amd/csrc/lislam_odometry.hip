@@ -2365,7 +2365,7 @@ __device__ __noinline__ bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool first,
 
 // The solve item of (c, r, o) on pair k: records -> LDS, LM, outputs; publishes lm_gen[c].
 __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
-                                          int r, int outer, const uint64_t* rec, bool wave0, unsigned tk) {
+                                          int r, int outer, const uint64_t* rec, bool wave0, unsigned tk, int ieff) {
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const bool gated_off = a.gate && !a.gate[k];
   const int total = gated_off ? 0 : ns + nf;
@@ -2375,12 +2375,12 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
     const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
     const double* part = a.eng_part + (size_t)c * ctl.I * 32 + e;
     double t = 0.0;
-    for (int it0 = g; it0 < ctl.I; it0 += 16 * 24) {  // 24 loads in flight per thread (384 items per pass)
+    for (int it0 = g; it0 < ieff; it0 += 16 * 24) {  // 24 loads in flight per thread (384 items per pass)
       double v[24];
 #pragma unroll
       for (int j = 0; j < 24; j++) {
         const int it = it0 + 16 * j;
-        v[j] = (e < 30 && it < ctl.I) ? ld_sc1d(part + (size_t)it * 32) : 0.0;
+        v[j] = (e < 30 && it < ieff) ? ld_sc1d(part + (size_t)it * 32) : 0.0;
       }
 #pragma unroll
       for (int j = 0; j < 24; j++) t += v[j];
@@ -2488,14 +2488,24 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
   eng_prof(tk, 3, rt_now());
 }
 
+// Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
+__device__ __forceinline__ int eng_live_items(const OdomArgs& a, int k) {
+  if (a.gate && !a.gate[k]) return 0;
+  return uni((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + kEngQ - 1) / kEngQ);
+}
+
 // Touch (one dword per 128-B line, plain loads: they allocate in this XCD's L2) every structure the
 // association of pair k reads: the Morton copies, the chunk / super-chunk boxes and the clouds of
-// scan k-1's less-sharp and less-flat sets.  Waves 1.. of a workgroup whose ticket must wait.
+// scan k-1's less-sharp and less-flat sets.  Waves 1.. of a workgroup whose ticket must wait.  The
+// workgroups of one XCD (dispatched round-robin over the 8 XCDs) split the lines between them:
+// workgroup b touches lines congruent to (b / 8) mod 32.
 __device__ __forceinline__ void eng_prefetch(const OdomArgs& a, EngShared& sh, int k, int t0, int nt) {
   unsigned acc = 0;
+  const size_t part = (blockIdx.x >> 3) & 31;
   auto touch = [&](const void* base, size_t bytes) {
     const __attribute__((address_space(1))) unsigned* p = (const __attribute__((address_space(1))) unsigned*)base;
-    for (size_t o = (size_t)t0 * 32; o < bytes / 4; o += (size_t)nt * 32) acc ^= p[o];
+    const size_t lines = (bytes + 127) / 128;
+    for (size_t l = part + (size_t)t0 * 32; l < lines; l += (size_t)nt * 32) acc ^= p[l * 32];
   };
   for (int which = 0; which < 2; which++) {
     const TargetIndex& ix = which ? a.idx_lf : a.idx_ls;
@@ -2512,11 +2522,13 @@ __device__ __forceinline__ void eng_prefetch(const OdomArgs& a, EngShared& sh, i
 }
 
 // An association ticket whose solve has not finished yet: its waves 1.. prefetch meanwhile.
-__device__ __forceinline__ int eng_wants_prefetch(const EngCtl& ctl, unsigned t, unsigned per_ro) {
+__device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCtl& ctl, unsigned t, unsigned per_ro) {
   if (!ctl.prefetch) return 0;
   const int ro = (int)(t / per_ro), rem = (int)(t % per_ro);
   const int c = rem / (ctl.I + 1), item = rem % (ctl.I + 1);
   if (item >= ctl.I || ro >= 2 * ctl.R || ro == 0) return 0;
+  int k;
+  if (!pair_of(a, c, ro >> 1, &k) || item >= eng_live_items(a, k)) return 0;
   return ld_rlx(ctl.lm_gen(c)) < (unsigned)ro ? 1 : 0;
 }
 
@@ -2538,7 +2550,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     if (lead) {
       const unsigned t = add_rlx(ctl.ticket(), 1u);
       sh.ticket = t;
-      sh.pref = eng_wants_prefetch(ctl, t, per_ro);
+      sh.pref = eng_wants_prefetch(a, ctl, t, per_ro);
       eng_trace(0, t);
       if (t < total) eng_prof(t, 0, rt_now());
     }
@@ -2549,19 +2561,24 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     const int ro = uni((int)(tk / per_ro)), rem = (int)(tk % per_ro);
     const int r = ro >> 1, o = ro & 1, c = uni(rem / (ctl.I + 1)), item = uni(rem % (ctl.I + 1));
     int k;
-    const bool live = pair_of(a, c, r, &k);
+    bool live = pair_of(a, c, r, &k);
+    // items holding queries of pair k: ceil((sharp + flat) / kEngQ), none for a gated-off scan
+    const int ieff = live ? eng_live_items(a, k) : 0;
+    if (item < ctl.I && item >= ieff) live = false;  // an empty item: nothing to wait for or signal
     uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
     if (!wave0 && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
     if (wave0) {
       if (lead) {
         bool ok = true;
         if (live) {
-          ok = item < ctl.I ? eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w())
-                            : eng_wait(ctl.assoc_done(c, ro), (unsigned)ctl.I, ctl.abort_w());
+          // every item after the chain's previous solve; the solve after its pair's live items too
+          // (which imply the first wait, except for a pair without queries: ieff == 0)
+          ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w());
+          if (ok && item == ctl.I) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w());
           eng_trace(1, ok ? 2u : 99u);
           eng_prof(tk, 1, rt_now());
           if (ok) eng_load_x(a, c, r, o, sh.x);
-          if (ok && c == 0 && r == 0 && o == 0 && item == 0 && !a.init_state) {  // scan 0 of the batch: first frame
+          if (ok && c == 0 && r == 0 && o == 0 && item == ctl.I && !a.init_state) {  // scan 0 of the batch: first frame
             for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
             for (int e = 0; e < 8; e++) a.stats[e] = 0;
           }
@@ -2591,7 +2608,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
           if (lead) { add_rlx(ctl.assoc_done(c, ro), 1u); eng_trace(1, 4u); eng_prof(tk, 3, rt_now()); }
         }
       } else {
-        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0, tk);
+        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0, tk, ieff);
         __syncthreads();
       }
     }
@@ -2599,7 +2616,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
       if (lead) {
         const unsigned t = add_rlx(ctl.ticket(), 1u);
         sh.ticket = t;
-        sh.pref = eng_wants_prefetch(ctl, t, per_ro);
+        sh.pref = eng_wants_prefetch(a, ctl, t, per_ro);
         eng_trace(0, t);
         if (t < total) eng_prof(t, 0, rt_now());
       }

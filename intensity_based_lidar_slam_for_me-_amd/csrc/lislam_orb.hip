@@ -2230,9 +2230,10 @@ bool orb_host_cascade() {  // LISLAM_ORB_HOST_CASCADE = 1: decide between rounds
 
 }  // namespace
 
-// Before the outputs of a device-decided cascade are read: wait for its verdict (the reader
-// synchronizes anyway) and, if it did not converge in kCascadeRounds passes, redo the batch with
-// host rounds.
+// Before the outputs of a device-decided cascade are read, and before lislam_batch_extract
+// overwrites the images it read: wait for its verdict (the reader synchronizes anyway) and, if it
+// did not converge in LISLAM_ORB_ROUNDS passes, redo the batch with host rounds from the same
+// images (the redo finishes before this returns).
 int orb_settle(lislam_batch* b) {
   OrbBatch* ob = static_cast<OrbBatch*>(b->orb);
   if (!ob || !ob->pending) return LISLAM_OK;
@@ -2243,6 +2244,7 @@ int orb_settle(lislam_batch* b) {
   ob->info[1] = ob->h_status[1];
   if (ob->h_status[0] == 1) return LISLAM_OK;
   const hipStream_t main_stream = c->stream;
+  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_images, 0));
   c->stream = ob->side;
   const int rc = batch_intensity_odometry(b, ob, ob->pending_n);
   c->stream = main_stream;

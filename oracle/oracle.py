@@ -211,17 +211,19 @@ class ScanFeatures:
     less_flat: np.ndarray
 
 
-TIES_REFERENCE, TIES_CANONICAL = 0, 3  # oracle_scanreg.cpp: bit 0 segment sort, bit 1 VoxelGrid by index
-TIES_GPU = 1  # index order in the segment sorts, std::sort's order in the VoxelGrid (the HIP path)
+# oracle_scanreg.cpp: bit 0 segment sort, bit 1 VoxelGrid by index.  TIES_REFERENCE (libstdc++'s
+# std::sort order in both) is the reference and the HIP path's default (LISLAM_TIES_REFERENCE);
+# TIES_CANONICAL (index order in both) is the HIP path's LISLAM_TIES_INDEX.
+TIES_REFERENCE, TIES_CANONICAL = 0, 3
 
 
 def scan_registration(scan: np.ndarray, min_range: float = 0.3, canonical: bool | None = None,
                       ties: int | None = None) -> ScanFeatures:
     """scanRegistration a1-a7 of one organized scan.  Tie order of equal sort keys: `ties`
     (TIES_*), or canonical=True (index order throughout) / False (the reference's std::sort
-    throughout); the default is the HIP path's TIES_GPU."""
+    throughout); the default is the reference's TIES_REFERENCE."""
     if ties is None:
-        ties = TIES_GPU if canonical is None else (TIES_CANONICAL if canonical else TIES_REFERENCE)
+        ties = TIES_CANONICAL if canonical else TIES_REFERENCE
     scan = np.ascontiguousarray(scan, dtype=np.float32)
     H, W = scan.shape[:2]
     N = H * W

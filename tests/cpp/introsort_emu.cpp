@@ -2,12 +2,20 @@
 // compute it (lislam_device.hpp introsort_order): every partition step of std::__introsort_loop is
 // evaluated with prefix counts instead of the two-pointer walk, the heap-sort fallback runs
 // serially, and the final insertion sort — stable for equal keys — becomes a stable sort by key.
+// The device finishes with a window rank instead of the insertion sort (final_positions in
+// lislam_features.hip): an element's final position is its position after the loop, minus the
+// greater keys among the 15 before it, plus the smaller keys among the 15 after it.
 // This file checks that formulation against std::sort itself on many arrays with heavy ties (the
 // situation of PCL VoxelGrid's std::sort of (voxel, point) pairs by voxel,
-// scanRegistration.cpp:574-578).  Prints "introsort ok" and exits 0 on success.
+// scanRegistration.cpp:574-578), and on scan-line segments sorted by curvature the way
+// scanRegistration.cpp:445 sorts them (std::sort of point indices with comp(i, j) =
+// curvature[i] < curvature[j], float curvatures with many equal values; the device keys are the
+// floats' bits, which order non-negative floats alike).  Prints "introsort ok" and exits 0.
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cmath>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -107,7 +115,8 @@ static void heap_sort(E* first, long len) {
   }
 }
 
-static std::vector<E> emulate(std::vector<E> a) {
+// The introsort loop only (blocks of at most 16 elements left for the final insertion sort).
+static std::vector<E> introsort_loop(std::vector<E> a) {
   const int n = (int)a.size();
   if (n == 0) return a;
   int lg = 0;
@@ -128,8 +137,40 @@ static std::vector<E> emulate(std::vector<E> a) {
       r.l = cut;
     }
   }
+  return a;
+}
+
+static std::vector<E> emulate(std::vector<E> a) {
+  a = introsort_loop(a);
   std::stable_sort(a.begin(), a.end());  // the final insertion sort never reorders equal keys
   return a;
+}
+
+// The device's finish: every element's final position from a +-15 window rank.
+static std::vector<E> window_rank(const std::vector<E>& a) {
+  const int n = (int)a.size();
+  std::vector<E> out(n);
+  for (int j = 0; j < n; j++) {
+    int mv = 0;
+    for (int d = 1; d <= 15; d++) {
+      if (j - d >= 0 && a[j - d].key > a[j].key) mv--;
+      if (j + d < n && a[j + d].key < a[j].key) mv++;
+    }
+    out[j + mv] = a[j];
+  }
+  return out;
+}
+
+static bool same_order(const std::vector<E>& got, const std::vector<E>& ref) {
+  for (size_t i = 0; i < ref.size(); i++)
+    if (got[i].id != ref[i].id || got[i].key != ref[i].key) return false;
+  return true;
+}
+
+static uint32_t fbits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
 }
 
 int main() {
@@ -153,10 +194,40 @@ int main() {
       std::vector<E> ref = a;
       std::sort(ref.begin(), ref.end());
       const std::vector<E> got = emulate(a);
+      const std::vector<E> win = window_rank(introsort_loop(a));
+      cases++;
+      if (!same_order(got, ref) || !same_order(win, ref)) {
+        if (bad < 10) std::fprintf(stderr, "n=%d mode=%d differs\n", n, mode);
+        bad++;
+      }
+    }
+  }
+  // scan-line segments (scanRegistration.cpp:440-445): indices sp..ep sorted by float curvature,
+  // curvatures with ties (snapped / duplicated points give exactly equal sums)
+  for (int n = 1; n <= 400; n += (n < 40 ? 1 : 3)) {
+    for (int mode = 0; mode < 4; mode++) {
+      std::vector<float> curv(n);
+      for (int i = 0; i < n; i++) {
+        switch (mode) {
+          case 0: curv[i] = 0.01f * (float)(rng() % 5); break;              // a few values, 0 included
+          case 1: curv[i] = (rng() % 3 == 0) ? 0.f : (float)(rng() % 1000) * 1e-3f; break;  // many zeros
+          case 2: curv[i] = (float)((i / 4) % 7) * 0.125f; break;             // duplicated runs
+          default: curv[i] = std::ldexp((float)(rng() % 64), -(int)(rng() % 8)); break;
+        }
+      }
+      const int sp = 5;
+      std::vector<int> ind(sp + n);
+      for (int i = 0; i < sp + n; i++) ind[i] = i;
+      std::vector<float> curv_full(sp + n, 0.f);
+      for (int i = 0; i < n; i++) curv_full[sp + i] = curv[i];
+      std::sort(ind.begin() + sp, ind.end(), [&](int i, int j) { return curv_full[i] < curv_full[j]; });
+      std::vector<E> a(n);
+      for (int i = 0; i < n; i++) a[i] = E{fbits(curv[i]), (uint32_t)i};
+      const std::vector<E> win = window_rank(introsort_loop(a));
       cases++;
       for (int i = 0; i < n; i++)
-        if (got[i].id != ref[i].id || got[i].key != ref[i].key) {
-          if (bad < 10) std::fprintf(stderr, "n=%d mode=%d differs at %d\n", n, mode, i);
+        if ((int)win[i].id + sp != ind[sp + i]) {
+          if (bad < 10) std::fprintf(stderr, "segment n=%d mode=%d differs at %d\n", n, mode, i);
           bad++;
           break;
         }
@@ -169,9 +240,9 @@ int main() {
     std::vector<E> ref = a;
     std::sort(ref.begin(), ref.end());
     const std::vector<E> got = emulate(a);
+    const std::vector<E> win = window_rank(introsort_loop(a));
     cases++;
-    for (int i = 0; i < n; i++)
-      if (got[i].id != ref[i].id) { bad++; std::fprintf(stderr, "killer n=%d differs\n", n); break; }
+    if (!same_order(got, ref) || !same_order(win, ref)) { bad++; std::fprintf(stderr, "killer n=%d differs\n", n); }
   }
   if (bad) {
     std::fprintf(stderr, "%d of %d cases differ\n", bad, cases);

@@ -168,3 +168,38 @@ def test_batch_redetection_cascade_on_device(pkg, oracle, ctx, frames):
     print("cascade info", sorted(seen))
     info = dict(seen)
     assert info["8"][0] == 1 and info["1"][0] == 0, seen  # converged on the device / redone with host rounds
+
+
+def test_cascade_settles_before_the_images_are_overwritten(pkg, oracle, ctx, frames):
+    """A device cascade that does not converge is redone with host rounds from the images it was
+    given.  If the batch is extracted again before its ORB outputs are read (bench.py's pipelined
+    loop does this), lislam_batch_extract settles the cascade first, so the outputs still describe
+    the first sequence, not the new images."""
+    scans, _, _ = frames
+    order = [0, 1, 1, 1, 2, 3, 3, 4, 4, 4, 4, 5, 5]
+    seq = scans[order].copy()
+    seq[5, ..., 3] = 0
+    n = seq.shape[0]
+    feats = [oracle.scan_registration(s) for s in seq]
+    mask = oracle.hand_held_mask()
+    rst, rT = oracle.intensity_odometry(np.stack([f.img_intensity for f in feats]),
+                                        np.stack([f.cloud_track for f in feats]), 1000, mask)
+    b = pkg.Batch(ctx, n)
+    b.upload(seq)
+    b.extract(n)
+    os.environ["LISLAM_ORB_ROUNDS"] = "1"  # one device pass: this sequence needs the host redo
+    try:
+        b.intensity_odometry(n, 1000, mask)
+    finally:
+        del os.environ["LISLAM_ORB_ROUNDS"]
+    other = scans[[5, 4, 3, 2, 1, 0, 0, 1, 2, 3, 4, 5, 5]].copy()
+    b.upload(other)
+    b.extract(n)  # overwrites the images the cascade was given
+    nat = pkg.native
+    for k in range(1, n):
+        st = b.download(nat.OUT_ORB_STATS, k)
+        T = b.download(nat.OUT_ORB_T, k)
+        assert list(st[:5]) == list(rst[k, :5]) and st[7] == rst[k, 7], (k, st, rst[k])
+        assert np.max(np.abs(T - rT[k])) < POSE_TOL, (k, T, rT[k])
+    assert b.orb_cascade_info()[0] == 0  # it was redone with host rounds
+    b.close()

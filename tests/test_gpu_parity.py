@@ -379,6 +379,58 @@ def test_voxel_grid_std_sort_order_heavy_ties(pkg, oracle, synth, contexts, quan
     b.close()
 
 
+@pytest.mark.parametrize("kind", ["snapped", "duplicated"])
+def test_segment_sort_std_sort_order_ties(pkg, oracle, synth, contexts, kind):
+    """Equal curvatures in a segment (scanRegistration.cpp:445): the sharp / flat walks reach
+    them in the order libstdc++'s std::sort leaves them, which the kernel replays (introsort
+    order + window rank) once a pick meets a tie.  Snapped coordinates (0.1 m grid) and runs
+    of identical points (curvature exactly 0) make many curvatures tie; the labels, sharp, less-sharp and flat
+    clouds are bit-exact against the oracle's reference order (ties=0), and the oracle's
+    index-order segments (ties=1) pick differently on these inputs.  The global-scratch path
+    (a doubled 2048-point line) is covered too.  TIES_INDEX matches the index-order oracle."""
+    ctx = contexts(64, 1024)
+    scans = synth.make_sequence(2, start=40).copy()
+    xyz = scans[..., :3]
+    nz = np.abs(xyz).sum(-1) > 0
+    if kind == "snapped":
+        xyz[nz] = np.round(xyz[nz] / 0.1) * 0.1
+    else:  # runs of 16 identical points: curvature exactly 0 inside each run
+        scans[:] = scans[:, :, (np.arange(scans.shape[2]) // 16) * 16]
+    b = pkg.Batch(ctx, 2)
+    b.upload(scans)
+    b.extract(2)
+    moved = 0
+    for k in range(2):
+        ref = oracle.scan_registration(scans[k], ties=0)
+        assert_features_equal(pkg, b, k, ref)
+        seg_index = oracle.scan_registration(scans[k], ties=1)
+        moved += int(np.sum(ref.label != seg_index.label))
+    assert moved > 0  # the segment tie order decides picks on these inputs
+    try:
+        ctx.set_tie_order(ctx.TIES_INDEX)
+        b.extract(2)
+        for k in range(2):
+            assert_features_equal(pkg, b, k, oracle.scan_registration(scans[k], canonical=True))
+    finally:
+        ctx.set_tie_order(ctx.TIES_REFERENCE)
+    b.close()
+    ctx2 = contexts(16, 1024)
+    s2 = _tied_long_lines(synth)  # lines of 2048 points: the global-scratch line path
+    b = pkg.Batch(ctx2, 1)
+    b.upload(s2[None])
+    b.extract(1)
+    assert_features_equal(pkg, b, 0, oracle.scan_registration(s2, ties=0))
+    b.close()
+
+
+def _tied_long_lines(synth):
+    s = synth.make_scan(9, 16, 1024).copy()
+    s[8:] = s[:8]
+    nz = np.abs(s[..., :3]).sum(-1) > 0
+    s[..., :3][nz] = np.round(s[..., :3][nz] / 0.1) * 0.1
+    return s
+
+
 def test_tie_order_index_mode(pkg, oracle, synth, contexts):
     """lislam_set_tie_order(LISLAM_TIES_INDEX): the VoxelGrid sums a voxel's points in input order,
     bit-exact against the oracle's index-order mode (canonical); the reference order is the

@@ -106,7 +106,9 @@ def test_voxel_grid_vs_python(oracle):
 def test_introsort_order_formulation_vs_std_sort():
     """The prefix-count formulation of std::sort's tie order that the HIP kernels use
     (lislam_features.hip introsort_order), restated on the host in tests/cpp/introsort_emu.cpp,
-    against std::sort itself on 1360 arrays with heavy ties (and heap-sort fallback inputs)."""
+    against std::sort itself on 1360 arrays with heavy ties (and heap-sort fallback inputs), and the
+    device's window-rank finish (final_positions) on those and on 640 curvature segments sorted
+    the way scanRegistration.cpp:445 sorts them (float keys, many equal)."""
     import subprocess
     import tempfile
 
