@@ -16,9 +16,13 @@
  * argument-dependent lookup).  Create(...) returns a lislam::CostFunction whose Evaluate()
  * computes the residuals and the Jacobians w.r.t. the raw parameter blocks — what
  * ceres::AutoDiffCostFunction<F, R, 4, 3> returns — on the GPU through lislam_eval_factors_raw.
- * lislam::EvaluateBlocks() evaluates many Create()d blocks in one launch (the per-iteration
- * residual pass of a solve), and lislam_normal_equations / lislam_pose_solve (lislam.h) reduce and
- * solve them without leaving the device.
+ * Ceres calls Evaluate() once per residual block per evaluation pass, all at one parameter point:
+ * the first call at a new (q, t) evaluates EVERY live Create()d block at that point in one launch
+ * (lidarFeaturePointsFunction.hpp:49-54,183-190,282-288 are the per-block functors this batches),
+ * and the pass's other calls are served from that result (lislam::FactorLaunches() counts the
+ * launches).  lislam::EvaluateBlocks() evaluates a given list of blocks in one launch, and
+ * lislam_normal_equations / lislam_pose_solve (lislam.h) reduce and solve them without leaving
+ * the device.
  *
  * Create() takes no context (the reference signature has none): the blocks evaluate on the
  * context given to lislam::SetFactorContext().  The reference passes s = 1 at every call site
@@ -34,7 +38,9 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <limits>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -146,14 +152,70 @@ class CostFunction {
 };
 #endif
 
+class DeviceCostFunction;
+
+namespace detail {
+/* Every live DeviceCostFunction, packed as lislam_eval_factors_raw records, and the outputs of the
+ * last parameter point they were evaluated at.  One per process (the blocks evaluate on the one
+ * SetFactorContext() context); the mutex serializes Ceres' evaluation threads. */
+struct FactorRegistry {
+  std::mutex mu;
+  std::vector<DeviceCostFunction*> blocks;  // slot i = blocks[i]
+  std::vector<int32_t> kinds;
+  std::vector<double> recs;                  // [n][12]
+  unsigned long long generation = 0;         // bumped by every Create() / destruction
+  bool cached = false;
+  unsigned long long cached_generation = 0;
+  double cq[4] = {0, 0, 0, 0}, ct[3] = {0, 0, 0};
+  std::vector<double> res, jq, jt;           // [n][3], [n][3][4], [n][3][3]
+  long long launches = 0;
+};
+inline FactorRegistry& factor_registry() {
+  static FactorRegistry r;
+  return r;
+}
+}  // namespace detail
+
+/* lislam_eval_factors_raw launches made by DeviceCostFunction::Evaluate so far. */
+inline long long FactorLaunches() {
+  detail::FactorRegistry& g = detail::factor_registry();
+  std::lock_guard<std::mutex> lock(g.mu);
+  return g.launches;
+}
+
 /* One residual block evaluated on the GPU: the functor's data packed as a
- * lislam_eval_factors_raw record (kind, 12 doubles). */
+ * lislam_eval_factors_raw record (kind, 12 doubles), registered for the batched evaluation. */
 class DeviceCostFunction : public CostFunction {
  public:
   DeviceCostFunction(int kind, int residuals, const double* rec12) : kind_(kind), residuals_(residuals) {
     for (int k = 0; k < 12; k++) rec_[k] = rec12[k];
     init(residuals, kind == 4 ? std::vector<int32_t>{4} : std::vector<int32_t>{4, 3});
+    detail::FactorRegistry& g = detail::factor_registry();
+    std::lock_guard<std::mutex> lock(g.mu);
+    slot_ = g.blocks.size();
+    g.blocks.push_back(this);
+    g.kinds.push_back(kind);
+    g.recs.insert(g.recs.end(), rec_, rec_ + 12);
+    g.generation++;
   }
+  ~DeviceCostFunction() override {
+    detail::FactorRegistry& g = detail::factor_registry();
+    std::lock_guard<std::mutex> lock(g.mu);
+    const size_t last = g.blocks.size() - 1;
+    if (slot_ != last) {  // the last block moves into this slot
+      DeviceCostFunction* m = g.blocks[last];
+      g.blocks[slot_] = m;
+      g.kinds[slot_] = g.kinds[last];
+      std::memcpy(&g.recs[slot_ * 12], &g.recs[last * 12], 12 * sizeof(double));
+      m->slot_ = slot_;
+    }
+    g.blocks.pop_back();
+    g.kinds.pop_back();
+    g.recs.resize(last * 12);
+    g.generation++;
+  }
+  DeviceCostFunction(const DeviceCostFunction&) = delete;
+  DeviceCostFunction& operator=(const DeviceCostFunction&) = delete;
   int kind() const { return kind_; }
   const double* record() const { return rec_; }
 
@@ -164,13 +226,32 @@ class DeviceCostFunction : public CostFunction {
       return false;
     }
     static const double zero_t[3] = {0.0, 0.0, 0.0};
-    const double* t = kind_ == 4 ? zero_t : parameters[1];
-    double r[3], jq[12], jt[9];
-    const int32_t kd = kind_;
+    const double* q = parameters[0];
+    detail::FactorRegistry& g = detail::factor_registry();
+    std::lock_guard<std::mutex> lock(g.mu);
+    // the ground factor has no t block (its residual ignores t): any cached t serves it
+    const double* t = kind_ == 4 ? (g.cached ? g.ct : zero_t) : parameters[1];
+    if (!g.cached || g.cached_generation != g.generation || std::memcmp(g.cq, q, sizeof(g.cq)) != 0 ||
+        std::memcmp(g.ct, t, sizeof(g.ct)) != 0) {
+      // a new parameter point: every registered block at (q, t), one launch
+      const size_t n = g.blocks.size();
+      g.res.resize(n * 3);
+      g.jq.resize(n * 12);
+      g.jt.resize(n * 9);
+      g.cached = false;
+      if (lislam_eval_factors_raw(ctx, (int32_t)n, g.kinds.data(), g.recs.data(), q, t, g.res.data(), g.jq.data(),
+                                  g.jt.data()) != LISLAM_OK)
+        return false;
+      g.launches++;
+      std::memcpy(g.cq, q, sizeof(g.cq));
+      if (t != g.ct) std::memcpy(g.ct, t, sizeof(g.ct));
+      g.cached_generation = g.generation;
+      g.cached = true;
+    }
     const bool want_q = jacobians && jacobians[0], want_t = jacobians && kind_ != 4 && jacobians[1];
-    if (lislam_eval_factors_raw(ctx, 1, &kd, rec_, parameters[0], t, r, want_q ? jq : nullptr,
-                                want_t ? jt : nullptr) != LISLAM_OK)
-      return false;
+    const double* r = &g.res[slot_ * 3];
+    const double* jq = &g.jq[slot_ * 12];
+    const double* jt = &g.jt[slot_ * 9];
     for (int i = 0; i < residuals_; i++) {
       residuals[i] = r[i];
       if (want_q)
@@ -184,6 +265,7 @@ class DeviceCostFunction : public CostFunction {
  private:
   int kind_, residuals_;
   double rec_[12];
+  size_t slot_ = 0;
 };
 
 /* Evaluate many Create()d blocks at one (q, t) in a single launch: residuals[n][3] and raw

@@ -87,6 +87,10 @@ int lislam_ctx_destroy(lislam_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     lislam_free_map_scratch(c->map_scratch);
   }
+  if (c->factor_buf) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->factor_buf);
+  }
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return LISLAM_OK;
@@ -820,30 +824,51 @@ int lislam_odom_step_gated(lislam_odom* od, const lislam_frame* fr, int32_t use_
 }
 
 // ------------------------------------------------------------------------------ functors
+// The context's factor scratch, at least `bytes` (caller holds c->factor_mu).
+static int factor_scratch(lislam_ctx* c, size_t bytes, uint8_t** out) {
+  if (c->factor_bytes < bytes) {
+    if (c->factor_buf) {
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipFree(c->factor_buf);
+      c->factor_buf = nullptr;
+      c->factor_bytes = 0;
+    }
+    const size_t want = std::max(bytes, (size_t)1 << 20);
+    if (hipMalloc(&c->factor_buf, want) != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "factor scratch allocation failed");
+    c->factor_bytes = want;
+  }
+  *out = static_cast<uint8_t*>(c->factor_buf);
+  return LISLAM_OK;
+}
+
 int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const double* pts, const double* q,
                         const double* t, double* residuals, double* jac) {
   if (!c || n < 0 || (n > 0 && (!kind || !pts)) || !q || !t) return LISLAM_ERR_ARG;
   if (n == 0) return LISLAM_OK;
   hipSetDevice(c->device);
-  int* dk = nullptr;
-  double *dp = nullptr, *dx = nullptr, *dr = nullptr, *dj = nullptr;
-  double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
-  auto cleanup = [&]() { hipFree(dk); hipFree(dp); hipFree(dx); hipFree(dr); hipFree(dj); };
-  if (hipMalloc(&dk, n * sizeof(int)) != hipSuccess || hipMalloc(&dp, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
-      hipMalloc(&dx, 7 * sizeof(double)) != hipSuccess || hipMalloc(&dr, (size_t)n * 3 * sizeof(double)) != hipSuccess ||
-      hipMalloc(&dj, (size_t)n * 18 * sizeof(double)) != hipSuccess) {
-    cleanup();
-    return fail(c, LISLAM_ERR_DEVICE, "hipMalloc failed in lislam_eval_factors");
+  std::lock_guard<std::mutex> lock(c->factor_mu);
+  // [x 7][pts n*12][res n*3][jac n*18] doubles, then kinds
+  const size_t nd = 7 + (size_t)n * (12 + 3 + 18);
+  uint8_t* base = nullptr;
+  int rc = factor_scratch(c, nd * 8 + (size_t)n * 4, &base);
+  if (rc) return rc;
+  double* dx = reinterpret_cast<double*>(base);
+  double* dp = dx + 7;
+  double* dr = dp + (size_t)n * 12;
+  double* dj = dr + (size_t)n * 3;
+  int* dk = reinterpret_cast<int*>(dj + (size_t)n * 18);
+  const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
+  hipError_t e = hipMemcpyAsync(dk, kind, n * sizeof(int), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dp, pts, (size_t)n * 12 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dx, x, sizeof(x), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    FactorArgs a{n, dk, dp, dx, dr, dj};
+    launch_factors(a, c->stream);
+    e = hipGetLastError();
   }
-  hipMemcpy(dk, kind, n * sizeof(int), hipMemcpyHostToDevice);
-  hipMemcpy(dp, pts, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice);
-  hipMemcpy(dx, x, sizeof(x), hipMemcpyHostToDevice);
-  FactorArgs a{n, dk, dp, dx, dr, dj};
-  launch_factors(a, c->stream);
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e == hipSuccess && residuals) e = hipMemcpy(residuals, dr, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && jac) e = hipMemcpy(jac, dj, (size_t)n * 18 * sizeof(double), hipMemcpyDeviceToHost);
-  cleanup();
+  if (e == hipSuccess && residuals) e = hipMemcpyAsync(residuals, dr, (size_t)n * 3 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess && jac) e = hipMemcpyAsync(jac, dj, (size_t)n * 18 * sizeof(double), hipMemcpyDefault, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors: %s", hipGetErrorString(e));
   return LISLAM_OK;
 }
@@ -867,17 +892,19 @@ int lislam_eval_factors_raw(lislam_ctx* c, int32_t n, const int32_t* kind, const
     if (kind[i] < 0 || kind[i] > 4) return fail(c, LISLAM_ERR_ARG, "lislam_eval_factors_raw: block %d has kind %d", i, kind[i]);
   if (n == 0) return LISLAM_OK;
   hipSetDevice(c->device);
-  int* dk = nullptr;
-  double *dp = nullptr, *dx = nullptr, *dr = nullptr, *djq = nullptr, *djt = nullptr;
+  std::lock_guard<std::mutex> lock(c->factor_mu);
+  // [x 7][pts n*12][res n*3][jq n*12][jt n*9] doubles, then kinds
+  const size_t nd = 7 + (size_t)n * (12 + 3 + 12 + 9);
+  uint8_t* base = nullptr;
+  const int rc = factor_scratch(c, nd * 8 + (size_t)n * 4, &base);
+  if (rc) return rc;
+  double* dx = reinterpret_cast<double*>(base);
+  double* dp = dx + 7;
+  double* dr = dp + (size_t)n * 12;
+  double* djq = dr + (size_t)n * 3;
+  double* djt = djq + (size_t)n * 12;
+  int* dk = reinterpret_cast<int*>(djt + (size_t)n * 9);
   const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
-  auto cleanup = [&]() { hipFree(dk); hipFree(dp); hipFree(dx); hipFree(dr); hipFree(djq); hipFree(djt); };
-  if (hipMalloc(&dk, n * sizeof(int)) != hipSuccess || hipMalloc(&dp, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
-      hipMalloc(&dx, 7 * sizeof(double)) != hipSuccess || hipMalloc(&dr, (size_t)n * 3 * sizeof(double)) != hipSuccess ||
-      hipMalloc(&djq, (size_t)n * 12 * sizeof(double)) != hipSuccess ||
-      hipMalloc(&djt, (size_t)n * 9 * sizeof(double)) != hipSuccess) {
-    cleanup();
-    return fail(c, LISLAM_ERR_DEVICE, "hipMalloc failed in lislam_eval_factors_raw");
-  }
   hipError_t e = hipMemcpyAsync(dk, kind, n * sizeof(int), hipMemcpyDefault, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(dp, pts, (size_t)n * 12 * sizeof(double), hipMemcpyDefault, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(dx, x, sizeof(x), hipMemcpyHostToDevice, c->stream);
@@ -890,7 +917,6 @@ int lislam_eval_factors_raw(lislam_ctx* c, int32_t n, const int32_t* kind, const
   if (e == hipSuccess && jac_q) e = hipMemcpyAsync(jac_q, djq, (size_t)n * 12 * sizeof(double), hipMemcpyDefault, c->stream);
   if (e == hipSuccess && jac_t) e = hipMemcpyAsync(jac_t, djt, (size_t)n * 9 * sizeof(double), hipMemcpyDefault, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  cleanup();
   if (e != hipSuccess) return fail(c, LISLAM_ERR_DEVICE, "lislam_eval_factors_raw: %s", hipGetErrorString(e));
   return LISLAM_OK;
 }

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -38,6 +39,12 @@ struct lislam_ctx {
   lislam_ktimer mtimer;            // mapping-kernel timing
   int ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order
   int odom_engine = LISLAM_ENGINE_AUTO;     // lislam_set_odometry_schedule
+  // lislam_eval_factors(_raw): one grow-only device buffer for the blocks, the parameters and the
+  // outputs, reused across calls; the mutex serializes callers (Ceres evaluates residual blocks
+  // from num_threads threads)
+  std::mutex factor_mu;
+  void* factor_buf = nullptr;
+  size_t factor_bytes = 0;
 };
 
 // kernel ids of lislam_map_kernel_times (LISLAM_CTX_NUM_KERNELS in include/lislam.h)

@@ -1521,9 +1521,10 @@ int lislam_mapopt_step(lislam_map* m, const float* ground, int32_t n, const doub
   return lislam_mapopt_step_corner(m, nullptr, ground, n, nullptr, 0, odom, state, out_pose, summary);
 }
 
-// pc_corner into the corner ikd-Tree at the keyframe pose (device pose): Build while the tree is
-// empty (mapOptimization.cpp:193-195), else Add_Points(downsample) (:477-479).
-static int corner_map_update(lislam_map* cm, const float* corner, int nc, const double* pose) {
+// pc_corner into the corner ikd-Tree at the keyframe pose (device pose): Build on the ground map's
+// first keyframe (mapOptimization.cpp:193-195), Add_Points(downsample) on every later one
+// (:477-479) — also when the first keyframe's corner cloud was empty and the tree still is.
+static int corner_map_update(lislam_map* cm, const float* corner, int nc, const double* pose, bool first) {
   lislam_ctx* c = cm->ctx;
   hipStream_t st = stream_of(c);
   MapScratch& sc = cm->sc;
@@ -1531,7 +1532,7 @@ static int corner_map_update(lislam_map* cm, const float* corner, int nc, const 
   MCHK(c, sc.vin.reserve((size_t)std::max(nc, 1) * 16));
   hipLaunchKernelGGL(k_transform, dim3(blocks(nc)), dim3(256), 0, st, sc.vout.as<float>(), 4, (const int*)nullptr, nc,
                      pose, sc.vin.as<float>());
-  if (cm->n == 0) {
+  if (first) {
     MCHK(c, cm->tmp.reserve((size_t)std::max(nc, 1) * 16));
     hipLaunchKernelGGL(k_pack_points, dim3(blocks(nc)), dim3(256), 0, st, sc.vin.as<float>(), nc, 4, 0, cm->tmp.as<float4>());
     cm->next_id = nc;
@@ -1572,7 +1573,7 @@ int lislam_mapopt_step_corner(lislam_map* m, lislam_map* cm, const float* ground
     hipLaunchKernelGGL(k_pack_points, dim3(blocks(n)), dim3(256), 0, st, sc.vin.as<float>(), n, 4, 0, m->tmp.as<float4>());
     m->next_id = n;
     MRC(rebuild(m, n));
-    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 16));
+    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 16, true));
     MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
   } else {
     // VoxelGrid(0.8) (:368-370) of the xyz cloud (PointXYZ: intensity lane zeroed)
@@ -1609,7 +1610,7 @@ int lislam_mapopt_step_corner(lislam_map* m, lislam_map* cm, const float* ground
                        m->newp.as<float4>());
     m->next_id += hn;
     MRC(add_packed(m, hn, true, nullptr));
-    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 24));  // the same keyframe pose as the ground cloud
+    if (cm && nc > 0) MRC(corner_map_update(cm, corner, nc, dp + 24, false));  // the same keyframe pose as the ground cloud
     MCHK(c, hipMemcpyAsync(out_pose, dp + 16, 56, hipMemcpyDefault, st));
     MCHK(c, hipMemcpyAsync(state, dp, 56, hipMemcpyDefault, st));
   }

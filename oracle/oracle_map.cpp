@@ -594,18 +594,20 @@ void oracle_mapopt_step_corner(void* h, void* hc, const float* ground, int n, co
     dst.assign((size_t)cnt * 4, 0.f);
     for (int i = 0; i < cnt; i++) to_world(pose, src + (size_t)i * 4, &dst[(size_t)i * 4]);
   };
-  auto corner_update = [&](const double* pose) {
+  // Build on the ground map's first keyframe, Add_Points(downsample) afterwards, whatever the
+  // corner tree holds (an empty first pc_corner leaves it empty until a later Add_Points)
+  auto corner_update = [&](const double* pose, bool first) {
     if (!cm || nc <= 0) return;
     std::vector<float> w;
     transformed(corner, nc, pose, w);
-    if (cm->live() == 0) cm->build(w.data(), nc, 4);
+    if (first) cm->build(w.data(), nc, 4);
     else cm->add_points(w.data(), nc, 4, true);
   };
   if (m->live() == 0) {
     std::vector<float> w;
     transformed(ground, n, x, w);
     m->build(w.data(), n, 4);
-    corner_update(x);
+    corner_update(x, true);
     for (int e = 0; e < 7; e++) out_pose[e] = x[e];
     return;
   }
@@ -640,7 +642,7 @@ void oracle_mapopt_step_corner(void* h, void* hc, const float* ground, int n, co
   std::vector<float> w;
   transformed(vox.data(), nv, conv ? x : x0, w);
   m->add_points(w.data(), nv, 4, true);
-  corner_update(conv ? x : x0);
+  corner_update(conv ? x : x0, false);
   for (int e = 0; e < 7; e++) out_pose[e] = x[e];
 }
 

@@ -161,6 +161,49 @@ int main() {
       for (int cc = 0; cc < 4; cc++) check(JQ[i * 12 + k * 4 + cc] == jq[k * 4 + cc], "batched J_q", (int)i, 0, 0);
     }
   }
+  // laserOdometry's problem size (64 lines: 768 edge + 1536 plane blocks, laserOdometry.cpp:
+  // 556-700): Ceres evaluates every residual block through Evaluate() at each parameter point of
+  // the solve; the first call at a new point evaluates all registered blocks in ONE launch and the
+  // others are served from it (lislam::FactorLaunches), bit-equal to a per-list EvaluateBlocks.
+  {
+    std::vector<std::unique_ptr<lislam::CostFunction>> prob;
+    std::vector<const lislam::CostFunction*> pb;
+    for (int i = 0; i < 2304; i++) {
+      lislam::CostFunction* f = i < 768 ? LidarEdgeFactor::Create(v3(), v3(), v3(), 1.0)
+                                        : LidarPlaneFactor::Create(v3(), v3(), v3(), v3(), 1.0);
+      prob.emplace_back(f);
+      pb.push_back(f);
+    }
+    const int points = 5;
+    for (int pt = 0; pt < points; pt++) {
+      double qq[4] = {A(rng), A(rng), A(rng), 0.0}, tt[3] = {U(rng), U(rng), U(rng)};
+      qq[3] = std::sqrt(1.0 - qq[0] * qq[0] - qq[1] * qq[1] - qq[2] * qq[2]);
+      const long long before = lislam::FactorLaunches();
+      std::vector<double> R3p(pb.size() * 3), JQp(pb.size() * 12), JTp(pb.size() * 9);
+      if (lislam::EvaluateBlocks(pb, qq, tt, R3p.data(), JQp.data(), JTp.data()) != LISLAM_OK) return 7;
+      const double* params[2] = {qq, tt};
+      for (int pass = 0; pass < 2; pass++) {  // cost-only pass, then with Jacobians (as Ceres does)
+        for (size_t i = 0; i < pb.size(); i++) {
+          double res[3], jq[12], jt[9];
+          double* jacs[2] = {jq, jt};
+          if (!pb[i]->Evaluate(params, res, pass ? jacs : nullptr)) return 8;
+          for (int k = 0; k < pb[i]->num_residuals(); k++) {
+            check(res[k] == R3p[i * 3 + k], "2304-block residual", (int)i, res[k], R3p[i * 3 + k]);
+            if (pass) {
+              for (int cc = 0; cc < 4; cc++) check(jq[k * 4 + cc] == JQp[i * 12 + k * 4 + cc], "2304-block J_q", (int)i, 0, 0);
+              for (int cc = 0; cc < 3; cc++) check(jt[k * 3 + cc] == JTp[i * 9 + k * 3 + cc], "2304-block J_t", (int)i, 0, 0);
+            }
+          }
+        }
+      }
+      const long long used = lislam::FactorLaunches() - before;
+      if (used != 1) {
+        std::fprintf(stderr, "point %d: %lld launches for 2304 blocks x 2 passes (want 1)\n", pt, used);
+        g_fail++;
+      }
+    }
+    std::printf("batched: 2304 blocks, %d parameter points, 1 launch each\n", points);
+  }
   // s != 1 is refused (DISTORTION 0 only)
   if (LidarEdgeFactor::Create(v3(), v3(), v3(), 0.5) != nullptr) {
     std::fprintf(stderr, "Create with s != 1 should return nullptr\n");

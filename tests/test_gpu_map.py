@@ -232,11 +232,14 @@ def test_mapopt_sequence(pkg, oracle, ctx, synth):
     go.map.close()
 
 
-def test_mapopt_corner_map(pkg, oracle, ctx, synth):
+@pytest.mark.parametrize("empty_first", [False, True])
+def test_mapopt_corner_map(pkg, oracle, ctx, synth, empty_first):
     """mapOptimization with its corner ikd-Tree (KD_TREE(0.3, 0.6, 0.8), mapOptimization.cpp:505):
     pc_corner (the scan's less-sharp cloud) Built on the first keyframe (:193-195), then
     Add_Points(downsample) at the keyframe pose (:477-479).  Poses, summaries and both maps' live
-    points against the oracle, frame by frame."""
+    points against the oracle, frame by frame.  empty_first: the first keyframe's pc_corner is
+    empty, so the tree is Built empty and the next cloud goes in through Add_Points (downsampled),
+    not through a Build."""
     go = pkg.mapping.MapOptimization(ctx, 0.4, 0.2, corner=True)
     om, ocm = oracle.IkdMap(0.4), oracle.IkdMap(0.8)
     ostate = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
@@ -245,6 +248,8 @@ def test_mapopt_corner_map(pkg, oracle, ctx, synth):
         flat = scan.reshape(-1, 4)
         ground = _f32(flat[np.abs(flat[:, :3]).sum(1) > 0])
         corner = oracle.scan_registration(scan).less_sharp
+        if empty_first and k == 0:
+            corner = corner[:0]
         q, t = synth.ground_truth_pose(20 + k).as_qt()
         odom = synth.perturb_pose(q, t, 0.02, 0.2, seed=40 + k)
         pg, sg = go.callback(ground, odom, corner)
