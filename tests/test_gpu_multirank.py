@@ -44,3 +44,41 @@ def test_two_ranks_config4_shards_match_oracle(tmp_path, oracle, synth):
                 assert np.max(np.abs(d["pose"][k] - pose[j])) < POSE_TOL, (r, k)
                 assert np.max(np.abs(d["para"][k] - rel[j])) < POSE_TOL, (r, k)
                 assert np.array_equal(d["stats"][k][:4], st[j][:4]), (r, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_eight_ranks_config4_full_shape(tmp_path, oracle, synth):
+    """Config 4 at its full shape on the one GPU: `bench.py --gpus 8 --total-scans 1000` (eight
+    rank processes round-robin on the card, 125 contiguous scans each, one continuous odometry chain
+    per shard).  The line carries n_gpus 8 and total_scans_per_step 1000; every rank's feature counts
+    match the oracle on its whole shard, and its poses / para / stats on the first 16 pairs of its
+    chain (the chain is sequential, so the sample is a prefix)."""
+    T, W, P = 1000, 8, 16
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(W), "--total-scans", str(T),
+                          "--steps", "1", "--warmup", "1", "--cpu-budget", "0", "--sustain-s", "0", "--segmented", "0",
+                          "--workers", "1", "--dump-dir", str(tmp_path)],
+                         capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.strip()][-1])
+    assert line["n_gpus"] == W and line["scaling"] == "strong"
+    assert line["config"]["total_scans_per_step"] == T
+    per = T // W
+    for r in range(W):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        start, n = int(d["start"]), int(d["n"])
+        assert (start, n) == (per * r, per)
+        assert int(d["chain"]) == n - 1  # one continuous chain over the shard
+        print(f"rank {r}: shard [{start}, {start + n}) checking", flush=True)
+        scans = synth.make_sequence(n, start=start)
+        for k in range(n):
+            f = oracle.scan_registration(scans[k])
+            ref = [f.laser_cloud.shape[0], f.sharp.shape[0], f.less_sharp.shape[0], f.flat.shape[0], f.less_flat.shape[0]]
+            assert list(d["counts"][k]) == ref, (r, k)
+        feats = [oracle.scan_registration(s) for s in scans[:P + 1]]
+        pose, rel, st = oracle.odometry_chain(feats)
+        for k in range(1, P + 1):
+            assert np.max(np.abs(d["pose"][k] - pose[k])) < POSE_TOL, (r, k)
+            assert np.max(np.abs(d["para"][k] - rel[k])) < POSE_TOL, (r, k)
+            assert np.array_equal(d["stats"][k][:4], st[k][:4]), (r, k)
