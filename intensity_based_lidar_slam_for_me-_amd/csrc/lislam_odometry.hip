@@ -137,188 +137,117 @@ __device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kKeysPerLane], int P,
 }
 
 // which: 0 less-sharp, 1 less-flat (targets), 2 sharp, 3 flat (queries: permutation only);
-// blockIdx.x -> (scan, w0 / w1 / w2 / w3 of the launch)
-// lf_split: the less-flat clouds of at most lf_split points go to the 8-wave launch (their keys and
-// coordinates fit its registers), larger ones to the 16-wave launch.
+// blockIdx.x -> (scan, w0 / w1 / w2 of the launch)
 template <int kW>
-__global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2, int w3,
-                                                          int lf_split) {
+__global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
   __shared__ uint64_t xch[kW * 8 * 64];
   __shared__ float red[6][kW];
   const int s = blockIdx.x / per_scan, wi = blockIdx.x % per_scan;
-  const int which = wi == 0 ? w0 : wi == 1 ? w1 : wi == 2 ? w2 : w3;
+  const int which = wi == 0 ? w0 : wi == 1 ? w1 : w2;
   const bool query = which >= 2;
   const TargetIndex& ix = (which & 1) ? a.idx_lf : a.idx_ls;
   const float4* pts = reinterpret_cast<const float4*>(
       which == 0 ? a.less_sharp + (size_t)s * a.cap_less_sharp : which == 1 ? a.less_flat + (size_t)s * a.N
       : which == 2 ? a.sharp + (size_t)s * a.cap_sharp : a.flat + (size_t)s * a.cap_flat);
   const int n = a.n_feat[s * 4 + (which == 0 ? 1 : which == 1 ? 3 : which == 2 ? 0 : 2)];
+  if (!query) chunk_boxes(pts, n, true, ix.chunk + (size_t)s * ix.nchunk * 2, ix.super + (size_t)s * ix.nsuper * 2);
   if (n == 0) return;
-  if (which == 1 && (kW == 16 ? n <= lf_split : n > lf_split)) return;  // the other launch's cloud
+  // cloud AABB: from the super-chunk boxes just written (targets), from the points (queries)
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  if (!query) {
+    const float4* sb = ix.super + (size_t)s * ix.nsuper * 2;
+    const int nsu = ((n + kChunk - 1) / kChunk + kChunk - 1) / kChunk;
+    for (int u = threadIdx.x; u < nsu; u += 64 * kW) {
+      const float4 l = ldg(sb + 2 * u), h = ldg(sb + 2 * u + 1);
+      mn[0] = fminf(mn[0], l.x); mn[1] = fminf(mn[1], l.y); mn[2] = fminf(mn[2], l.z);
+      mx[0] = fmaxf(mx[0], h.x); mx[1] = fmaxf(mx[1], h.y); mx[2] = fmaxf(mx[2], h.z);
+    }
+  } else {
+    for (int j = threadIdx.x; j < n; j += 64 * kW) {
+      const float4 p = ldg(pts + j);
+      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+    }
+  }
+  for (int d = 0; d < 3; d++)
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+      mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+    }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int d = 0; d < 3; d++) { red[d][wave] = mn[d]; red[3 + d][wave] = mx[d]; }
+  __syncthreads();
+  for (int d = 0; d < 3; d++) {
+    mn[d] = red[d][0]; mx[d] = red[3 + d][0];
+    for (int w = 1; w < kW; w++) { mn[d] = fminf(mn[d], red[d][w]); mx[d] = fmaxf(mx[d], red[3 + d][w]); }
+  }
+  const float ext = fmaxf(fmaxf(mx[0] - mn[0], mx[1] - mn[1]), fmaxf(mx[2] - mn[2], 1e-6f));
+  const float inv = 1023.0f / ext;  // cubic cells
+  auto key_of = [&](int j) -> uint64_t {
+    if (j >= n) return ~0ull;
+    const float4 p = ldg(pts + j);
+    const uint32_t qx = (uint32_t)fminf(fmaxf((p.x - mn[0]) * inv, 0.f), 1023.f);
+    const uint32_t qy = (uint32_t)fminf(fmaxf((p.y - mn[1]) * inv, 0.f), 1023.f);
+    const uint32_t qz = (uint32_t)fminf(fmaxf((p.z - mn[2]) * inv, 0.f), 1023.f);
+    const uint32_t code = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
+    return ((uint64_t)code << 32) | (uint32_t)j;
+  };
   int P = 1024;
   while (P < n) P <<= 1;
+  uint64_t key[kKeysPerLane];
   const bool in_regs = P <= 1024 * kW;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  gu64* gkeys = (gu64*)(ix.keys + (size_t)s * 2 * ix.cap);
+  if (in_regs) {
+#pragma unroll
+    for (int t = 0; t < kKeysPerLane; t++) key[t] = key_of(wave * 1024 + t * 64 + lane);
+    wg_bitonic<kW>(key, P, xch);
+  } else {
+    for (int j = threadIdx.x; j < P; j += 64 * kW) gkeys[j] = key_of(j);
+    __syncthreads();
+    global_bitonic(gkeys, P);
+  }
+  // sorted position i -> original index
+  auto emit = [&](auto&& f) {
+    if (in_regs) {
+#pragma unroll
+      for (int t = 0; t < kKeysPerLane; t++) {
+        const int i = wave * 1024 + t * 64 + lane;
+        if (i < n) f(i, (int)(uint32_t)key[t]);
+      }
+    } else {
+      for (int i = threadIdx.x; i < n; i += 64 * kW) f(i, (int)(uint32_t)gkeys[i]);
+    }
+  };
+  if (query) {  // association waves take their queries in this order (spatially coherent workgroups)
+    float4* qp = which == 2 ? a.qpts_sharp + (size_t)s * a.cap_sharp : a.qpts_flat + (size_t)s * a.cap_flat;
+    emit([&](int i, int o) {
+      const float4 p = ldg(pts + o);
+      stg4(qp + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+    });
+    return;
+  }
   float4* sorted = ix.sorted + (size_t)s * ix.cap;
-  float4* qp = which == 2 ? a.qpts_sharp + (size_t)s * a.cap_sharp : a.qpts_flat + (size_t)s * a.cap_flat;
-  // 16-lane row minimum (a chunk's 16 points are one row of one slot)
+  if (!in_regs) {
+    emit([&](int i, int o) {
+      const float4 p = ldg(pts + o);
+      stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
+    });
+    __syncthreads();
+    chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
+    return;
+  }
+  // Registers: sorted position i = 1024 wave + 64 t + lane, so a chunk (16 positions) is a 16-lane
+  // row of one slot and a super-chunk (256) is the four slots t = 4 v .. 4 v + 3 of one wave:
+  // both boxes are reduced from the gathered points without reading the sorted copy back.
+  float4* nch_out = ix.nn_chunk + (size_t)s * ix.nchunk * 2;
+  float4* nsu_out = ix.nn_super + (size_t)s * ix.nsuper * 2;
   auto rmin = [](float v) {
     v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, true)));
     v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, true)));
     v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, true)));
     return fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, true)));
   };
-  // the four row leaders (lanes 0, 16, 32, 48) of a slot group -> every lane
-  auto leaders_min = [](float v) {
-    v = fminf(v, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (16 << 10) | 0x1f)));  // lane ^ 16
-    return fminf(v, __shfl_xor(v, 32));
-  };
-  // cloud AABB -> every thread (lane-local partial min / max in, workgroup min / max out)
-  auto wg_aabb = [&](float (&mn)[3], float (&mx)[3]) {
-    for (int d = 0; d < 3; d++)
-      for (int o = 32; o > 0; o >>= 1) {
-        mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
-        mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
-      }
-    if (lane == 0)
-      for (int d = 0; d < 3; d++) { red[d][wave] = mn[d]; red[3 + d][wave] = mx[d]; }
-    __syncthreads();
-    for (int d = 0; d < 3; d++) {
-      mn[d] = red[d][0]; mx[d] = red[3 + d][0];
-      for (int w = 1; w < kW; w++) { mn[d] = fminf(mn[d], red[d][w]); mx[d] = fmaxf(mx[d], red[3 + d][w]); }
-    }
-  };
-  auto morton = [](float x, float y, float z, const float (&mn)[3], float inv) {
-    const uint32_t qx = (uint32_t)fminf(fmaxf((x - mn[0]) * inv, 0.f), 1023.f);
-    const uint32_t qy = (uint32_t)fminf(fmaxf((y - mn[1]) * inv, 0.f), 1023.f);
-    const uint32_t qz = (uint32_t)fminf(fmaxf((z - mn[2]) * inv, 0.f), 1023.f);
-    return spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
-  };
-  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  if (!in_regs) {
-    // clouds beyond the registers: boxes, keys and the gather each read the cloud (global sort)
-    if (!query) chunk_boxes(pts, n, true, ix.chunk + (size_t)s * ix.nchunk * 2, ix.super + (size_t)s * ix.nsuper * 2);
-    for (int j = threadIdx.x; j < n; j += 64 * kW) {
-      const float4 p = ldg(pts + j);
-      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-    }
-    wg_aabb(mn, mx);
-    const float ext = fmaxf(fmaxf(mx[0] - mn[0], mx[1] - mn[1]), fmaxf(mx[2] - mn[2], 1e-6f));
-    const float inv = 1023.0f / ext;  // cubic cells
-    gu64* gkeys = (gu64*)(ix.keys + (size_t)s * 2 * ix.cap);
-    for (int j = threadIdx.x; j < P; j += 64 * kW) {
-      uint64_t k = ~0ull;
-      if (j < n) {
-        const float4 p = ldg(pts + j);
-        k = ((uint64_t)morton(p.x, p.y, p.z, mn, inv) << 32) | (uint32_t)j;
-      }
-      gkeys[j] = k;
-    }
-    __syncthreads();
-    global_bitonic(gkeys, P);
-    for (int i = threadIdx.x; i < n; i += 64 * kW) {
-      const int o = (int)(uint32_t)gkeys[i];
-      const float4 p = ldg(pts + o);
-      stg4((query ? qp : sorted) + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
-    }
-    if (query) return;
-    __syncthreads();
-    chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
-    return;
-  }
-  // ---- registers: the cloud is read once.  Thread (wave, t, lane) holds point
-  // j = 1024 wave + 64 t + lane: a chunk (16 points) is a 16-lane row of one slot and a
-  // super-chunk (256) the four slots 4 v .. 4 v + 3 of one wave, so the scan-line-order boxes
-  // (targets) are row reductions of the loaded points, the AABB and the Morton keys come from
-  // the same registers, and after the sort the gather goes through LDS one coordinate at a time
-  // (the exchange buffer holds 1024 kW floats).
-  float px[kKeysPerLane], py[kKeysPerLane], pz[kKeysPerLane];
-  {
-    float4* cb = ix.chunk + (size_t)s * ix.nchunk * 2;
-    float4* sb = ix.super + (size_t)s * ix.nsuper * 2;
-    float slo[4] = {3.4e38f, 3.4e38f, 3.4e38f, 1e9f}, shi[4] = {-3.4e38f, -3.4e38f, -3.4e38f, -1e9f};
-#pragma unroll
-    for (int t = 0; t < kKeysPerLane; t++) {
-      const int j = wave * 1024 + t * 64 + lane;
-      const bool valid = j < n;
-      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid) p = ldg(pts + j);
-      px[t] = p.x; py[t] = p.y; pz[t] = p.z;
-      if (valid) {
-        mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-        mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-      }
-      if (!query && j - lane < n) {  // chunk boxes of this slot's rows, label = int(intensity)
-        const float l = (float)int(p.w);
-        const float lo0 = rmin(valid ? p.x : 3.4e38f), lo1 = rmin(valid ? p.y : 3.4e38f), lo2 = rmin(valid ? p.z : 3.4e38f);
-        const float lo3 = rmin(valid ? l : 1e9f);
-        const float hi0 = -rmin(valid ? -p.x : 3.4e38f), hi1 = -rmin(valid ? -p.y : 3.4e38f);
-        const float hi2 = -rmin(valid ? -p.z : 3.4e38f), hi3 = -rmin(valid ? -l : 1e9f);
-        if ((lane & 15) == 0 && valid) {
-          stg4(cb + 2 * (j >> 4), make_float4(lo0, lo1, lo2, lo3));
-          stg4(cb + 2 * (j >> 4) + 1, make_float4(hi0, hi1, hi2, hi3));
-        }
-        slo[0] = fminf(slo[0], lo0); slo[1] = fminf(slo[1], lo1); slo[2] = fminf(slo[2], lo2); slo[3] = fminf(slo[3], lo3);
-        shi[0] = fmaxf(shi[0], hi0); shi[1] = fmaxf(shi[1], hi1); shi[2] = fmaxf(shi[2], hi2); shi[3] = fmaxf(shi[3], hi3);
-      }
-      if (!query && (t & 3) == 3) {  // super-chunk wave * 4 + t / 4
-        const int u = (wave * 1024 + (t - 3) * 64) >> 8;
-        if (u * kSuper < n) {
-          float r[8];
-#pragma unroll
-          for (int e = 0; e < 4; e++) { r[e] = leaders_min(slo[e]); r[4 + e] = -leaders_min(-shi[e]); }
-          if (lane == 0) {
-            stg4(sb + 2 * u, make_float4(r[0], r[1], r[2], r[3]));
-            stg4(sb + 2 * u + 1, make_float4(r[4], r[5], r[6], r[7]));
-          }
-        }
-        slo[0] = slo[1] = slo[2] = 3.4e38f; slo[3] = 1e9f;
-        shi[0] = shi[1] = shi[2] = -3.4e38f; shi[3] = -1e9f;
-      }
-    }
-  }
-  wg_aabb(mn, mx);
-  const float ext = fmaxf(fmaxf(mx[0] - mn[0], mx[1] - mn[1]), fmaxf(mx[2] - mn[2], 1e-6f));
-  const float inv = 1023.0f / ext;  // cubic cells
-  uint64_t key[kKeysPerLane];
-#pragma unroll
-  for (int t = 0; t < kKeysPerLane; t++) {
-    const int j = wave * 1024 + t * 64 + lane;
-    key[t] = j < n ? ((uint64_t)morton(px[t], py[t], pz[t], mn, inv) << 32) | (uint32_t)j : ~0ull;
-  }
-  wg_bitonic<kW>(key, P, xch);
-  // the gather: coordinate c of point j -> LDS slot j, then sorted position i reads slot key[i]
-  float* xs = reinterpret_cast<float*>(xch);
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    __syncthreads();  // the sort's (or the previous coordinate's) reads of the exchange are done
-#pragma unroll
-    for (int t = 0; t < kKeysPerLane; t++) {
-      const int j = wave * 1024 + t * 64 + lane;
-      if (j < n) xs[j] = c == 0 ? px[t] : c == 1 ? py[t] : pz[t];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kKeysPerLane; t++) {
-      const int i = wave * 1024 + t * 64 + lane;
-      if (i < n) {
-        const float v = xs[(int)(uint32_t)key[t]];
-        if (c == 0) px[t] = v; else if (c == 1) py[t] = v; else pz[t] = v;
-      }
-    }
-  }
-  if (query) {  // association waves take their queries in this order (spatially coherent workgroups)
-#pragma unroll
-    for (int t = 0; t < kKeysPerLane; t++) {
-      const int i = wave * 1024 + t * 64 + lane;
-      if (i < n) stg4(qp + i, make_float4(px[t], py[t], pz[t], __int_as_float((int)(uint32_t)key[t])));
-    }
-    return;
-  }
-  // the sorted copy and its chunk / super-chunk boxes, from the gathered registers
-  float4* nch_out = ix.nn_chunk + (size_t)s * ix.nchunk * 2;
-  float4* nsu_out = ix.nn_super + (size_t)s * ix.nsuper * 2;
   float slo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, shi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};  // super box (row leaders)
 #pragma unroll
   for (int t = 0; t < kKeysPerLane; t++) {
@@ -327,7 +256,7 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     float q[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
     if (i < n) {
       const int o = (int)(uint32_t)key[t];
-      p = make_float4(px[t], py[t], pz[t], 0.f);
+      p = ldg(pts + o);
       stg4(sorted + i, make_float4(p.x, p.y, p.z, __int_as_float(o)));
       q[0] = p.x; q[1] = p.y; q[2] = p.z;
     }
@@ -343,7 +272,12 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     if ((t & 3) == 3) {  // super-chunk (wave * 4 + t / 4): combine the four row leaders 0, 16, 32, 48
       float r[6] = {slo[0], slo[1], slo[2], -shi[0], -shi[1], -shi[2]};
 #pragma unroll
-      for (int e = 0; e < 6; e++) r[e] = leaders_min(r[e]);
+      for (int e = 0; e < 6; e++) {
+        float v = r[e];
+        v = fminf(v, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (16 << 10) | 0x1f)));  // lane ^ 16
+        v = fminf(v, __shfl_xor(v, 32));
+        r[e] = v;
+      }
       const int u = (wave * 1024 + (t - 3) * 64) >> 8;
       if (lane == 0 && u * kSuper < n) {
         stg4(nsu_out + 2 * u, make_float4(r[0], r[1], r[2], 0.f));
@@ -2738,11 +2672,10 @@ void launch_factors(const FactorArgs& a, hipStream_t st) {
 }
 
 void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st) {
-  // 8 waves (8192 keys and their coordinates in registers): less-sharp, query clouds and less-flat
-  // clouds of at most 8192 points; 16 waves (16384 keys): larger less-flat clouds (a workgroup whose
-  // cloud belongs to the other launch returns at once)
-  hipLaunchKernelGGL(k_target_index<16>, dim3(n_scans), dim3(1024), 0, st, a, 1, 1, 1, 1, 1, 8192);
-  hipLaunchKernelGGL(k_target_index<8>, dim3(4 * n_scans), dim3(512), 0, st, a, 4, 0, 1, 2, 3, 8192);
+  // less-flat clouds: 16 waves (16384 keys in registers, 64 KiB LDS exchange, two workgroups per
+  // CU); less-sharp + query clouds: 8 waves (8192 keys)
+  hipLaunchKernelGGL(k_target_index<16>, dim3(n_scans), dim3(1024), 0, st, a, 1, 1, 1, 1);
+  hipLaunchKernelGGL(k_target_index<8>, dim3(3 * n_scans), dim3(512), 0, st, a, 3, 0, 2, 3);
 }
 
 void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups, hipEvent_t fork,
