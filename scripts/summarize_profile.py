@@ -25,7 +25,8 @@ def short(name):
 # rocprof kernel (base name, no "void", namespaces or template arguments) -> the bench's logical
 # kernel (native.KERNELS / the ORB timers); kernels of one logical name are summed per step
 LOGICAL = [("k_front_", "k_scan_front"), ("k_scan_lines", "k_scan_lines"), ("k_scan_compact", "k_scan_compact"),
-           ("k_target_index", "k_target_index"), ("k_odom_assoc", "k_odom_assoc"), ("k_odom_lm", "k_odom_lm")]
+           ("k_target_index", "k_target_index"), ("k_odom_assoc", "k_odom_assoc"), ("k_odom_lm", "k_odom_lm"),
+           ("k_odom_chain", "k_odom_chain")]
 
 
 def logical(name):
@@ -46,12 +47,26 @@ def pmc(path):
     return agg
 
 
+def pmc_multi(path):  # several counters in one pass: kernel -> counter -> [sum, launches]
+    agg = {}
+    if not os.path.exists(path):
+        return agg
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        a = agg.setdefault(k, {}).setdefault(r["Counter_Name"], [0.0, 0])
+        a[0] += float(r["Counter_Value"])
+        a[1] += 1
+    return agg
+
+
 fetch = pmc(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"))
+sq = pmc_multi(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv"))
 write = pmc(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"))
 stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv")))}
 bench = json.load(open(os.path.join(src, "trace_bench.json")))
 bc = bench["config"]
-out = {"tag": tag, "config": {k: bc[k] for k in ("lines", "width", "scans_per_step_per_gpu", "chain_len")},
+out = {"tag": tag, "config": {k: bc[k] for k in ("lines", "width", "scans_per_step_per_gpu", "chain_len") if k in bc},
+       "workload": bc.get("workload"),
        "correction": "traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE "
                                  "half-count of wide reads, MI355X_MICROARCH.md HBM section)", "kernels": {}}
 for k in fetch:
@@ -79,11 +94,23 @@ for k in fetch:
     a[1] += nf
 out["kernels_logical"] = {k: {"launches_profiled": v[1], "traffic_bytes_per_launch": v[0] / max(1, v[1])}
                           for k, v in lg.items()}
+# SQ counters per launch (summed over the dispatch's shader engines); the fractions of the wave
+# cycles spent waiting (SQ_WAIT_ANY), waiting for instruction issue (SQ_WAIT_INST_ANY) and with an
+# instruction active (SQ_ACTIVE_INST_ANY) name the bound that applies to a latency-bound kernel
+for k, cs in sq.items():
+    name = logical(k) or k
+    per = {c: v[0] / max(1, v[1]) for c, v in cs.items()}
+    wc = per.get("SQ_WAVE_CYCLES", 0.0)
+    if wc > 0:
+        per.update({"wait_any_frac": per.get("SQ_WAIT_ANY", 0.0) / wc,
+                    "wait_inst_any_frac": per.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                    "active_inst_any_frac": per.get("SQ_ACTIVE_INST_ANY", 0.0) / wc})
+    out.setdefault("sq_logical", {})[name] = per
 # The roofline's launch time: bench.py measures the dominant kernel in its final isolated stage
 # pass (no other stream active); the same launches are the last `isolated_launches` of that kernel
 # in the kernel trace, so rocprof's average over them is the cross-check of the line's avg_launch_ms.
-rl = bench["roofline"]
-dom, n_iso = rl["kernel"], int(rl.get("isolated_launches", 0))
+rl = bench.get("roofline") or {}
+dom, n_iso = rl.get("kernel"), int(rl.get("isolated_launches", 0) or 0)
 durs = []
 trace_csv = os.path.join(src, "trace", "trace_kernel_trace.csv")
 if n_iso and os.path.exists(trace_csv):
