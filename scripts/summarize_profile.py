@@ -26,7 +26,8 @@ def short(name):
 # kernel (native.KERNELS / the ORB timers); kernels of one logical name are summed per step
 LOGICAL = [("k_front_", "k_scan_front"), ("k_scan_lines", "k_scan_lines"), ("k_scan_compact", "k_scan_compact"),
            ("k_target_index", "k_target_index"), ("k_odom_assoc", "k_odom_assoc"), ("k_odom_lm", "k_odom_lm"),
-           ("k_odom_chain", "k_odom_chain")]
+           ("k_odom_chain", "k_odom_chain"),
+           ("k_knn", "k_knn"), ("k_fit", "k_fit"), ("k_lm_eval", "k_lm_eval"), ("k_lm_step", "k_lm_step")]
 
 
 def logical(name):
