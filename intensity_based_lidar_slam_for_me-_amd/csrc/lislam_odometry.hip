@@ -1607,16 +1607,16 @@ extern "C" int lislam_debug_engine_qlog(int* dev_buf, int pair) {
 #endif
 constexpr int kEngThreads = LISLAM_ENG_THREADS;
 constexpr int kEngWaves = kEngThreads / 64;
-#ifndef LISLAM_ENG_ROWS16
 constexpr int kEngQ = kEngWaves;      // queries per association item: one per wave (64 lanes)
-#else
-constexpr int kEngQ = kEngWaves * 4;  // four per wave (16-lane rows, k_odom_assoc16's searches)
-#endif
 #ifndef LISLAM_ENG_LDS
 #define LISLAM_ENG_LDS 2304           // 64 lines: 12 * 64 sharp + 24 * 64 flat queries
 #endif
 constexpr int kEngLds = LISLAM_ENG_LDS;
 constexpr int kRecWords = 8;          // u64 words per record: c.xy, c.z a.x, a.yz, kind, u/n xyz, -
+#ifndef LISLAM_REC_UNROLL
+#define LISLAM_REC_UNROLL 2           // records per solve-load round trip and thread
+#endif
+constexpr int kRecUnroll = LISLAM_REC_UNROLL;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
@@ -1711,64 +1711,167 @@ struct EngShared {
   double x[7];
   int cnt[kEngWaves][2];
   unsigned ticket;
-  int flag, nc, np, pref;
+  int flag, flag0, nc, np, pref;
   unsigned sink;
 };
 
-// x (para_q, para_t) a ticket of (c, r, o) starts from: the chain's initial state for its first
-// pass, else the last solve's (write-through) result.  Thread 0 -> sh.x.
+// Word e of x (para_q, para_t) a ticket of (c, r, o) starts from: the chain's initial state for
+// its first pass, else the last solve's (write-through) result.
+__device__ __forceinline__ double eng_x_word(const OdomArgs& a, int c, int r, int o, int e) {
+  if (r == 0 && o == 0) return a.init_state ? a.init_state[(size_t)c * 14 + e] : (e == 3 ? 1.0 : 0.0);
+  return ld_sc1d(a.state + (size_t)c * 16 + e);
+}
 __device__ __forceinline__ void eng_load_x(const OdomArgs& a, int c, int r, int o, double* x) {
-  if (r == 0 && o == 0) {
-    if (a.init_state) {
-      for (int e = 0; e < 7; e++) x[e] = a.init_state[(size_t)c * 14 + e];
-    } else {
-      for (int e = 0; e < 7; e++) x[e] = e == 3 ? 1.0 : 0.0;
-    }
+#pragma unroll
+  for (int e = 0; e < 7; e++) x[e] = eng_x_word(a, c, r, o, e);
+}
+
+// One block's 28 sums (see the engine comment) at p = R c, lp = p + t (R, t uniform).
+// Edge blocks: M (rank 2) and each row of T folded into the sums (and into U) as soon as it exists,
+// to keep few doubles live.  Plane blocks are rank 1: with a = p x n, M = w n n^T, T = [p]x M =
+// w a n^T, U = T [p]x = -w a a^T, v = w r n, p x v = w r a (39 multiply-adds instead of ~90).
+__device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
+                                          double (&s)[kAcc]) {
+  const D3 p{fma(R[0], c.x, fma(R[1], c.y, R[2] * c.z)), fma(R[3], c.x, fma(R[4], c.y, R[5] * c.z)),
+             fma(R[6], c.x, fma(R[7], c.y, R[8] * c.z))};
+  const D3 e{(p.x + t.x) - pa.x, (p.y + t.y) - pa.y, (p.z + t.z) - pa.z};
+  double r0 = 0, r1 = 0, r2 = 0, rp = 0, s2;
+  if (kd == 0) {
+    r0 = fma(e.y, u.z, -e.z * u.y); r1 = fma(e.z, u.x, -e.x * u.z); r2 = fma(e.x, u.y, -e.y * u.x);
+    s2 = fma(r0, r0, fma(r1, r1, r2 * r2));
   } else {
-    const double* st = a.state + (size_t)c * 16;
-    for (int e = 0; e < 7; e++) x[e] = ld_sc1d(st + e);
+    rp = fma(e.x, u.x, fma(e.y, u.y, e.z * u.z));
+    s2 = rp * rp;
+  }
+  double w = 1.0;
+  if (s2 > 0.01) {  // HuberLoss(0.1): rho = 2 a sqrt(s) - a^2, rho' = a / sqrt(s)
+    const double rr = sqrt(s2);
+    s[0] += 0.5 * (0.2 * rr - 0.01);
+    w = fmax(2.2250738585072014e-308, 0.1 / rr);
+  } else {
+    s[0] += 0.5 * s2;
+  }
+  const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
+  if (kd != 0) {
+    const D3 av{fma(p.y, u.z, -p.z * u.y), fma(p.z, u.x, -p.x * u.z), fma(p.x, u.y, -p.y * u.x)};
+    const double ax = w * av.x, ay = w * av.y, az = w * av.z;
+    s[1] = fma(wx, u.x, s[1]); s[2] = fma(wx, u.y, s[2]); s[3] = fma(wx, u.z, s[3]);
+    s[4] = fma(wy, u.y, s[4]); s[5] = fma(wy, u.z, s[5]); s[6] = fma(wz, u.z, s[6]);
+    s[7] = fma(ax, u.x, s[7]); s[8] = fma(ax, u.y, s[8]); s[9] = fma(ax, u.z, s[9]);
+    s[10] = fma(ay, u.x, s[10]); s[11] = fma(ay, u.y, s[11]); s[12] = fma(ay, u.z, s[12]);
+    s[13] = fma(az, u.x, s[13]); s[14] = fma(az, u.y, s[14]); s[15] = fma(az, u.z, s[15]);
+    s[16] = fma(-ax, av.x, s[16]); s[17] = fma(-ax, av.y, s[17]); s[18] = fma(-ax, av.z, s[18]);
+    s[19] = fma(-ay, av.y, s[19]); s[20] = fma(-ay, av.z, s[20]); s[21] = fma(-az, av.z, s[21]);
+    s[22] = fma(rp, wx, s[22]); s[23] = fma(rp, wy, s[23]); s[24] = fma(rp, wz, s[24]);
+    s[25] = fma(rp, ax, s[25]); s[26] = fma(rp, ay, s[26]); s[27] = fma(rp, az, s[27]);
+    return;
+  }
+  double m00, m01, m02, m11, m12, m22, v0, v1, v2;
+  {
+    const double wuu = w * fma(u.x, u.x, fma(u.y, u.y, u.z * u.z));
+    m00 = fma(-wx, u.x, wuu); m01 = -wx * u.y; m02 = -wx * u.z;
+    m11 = fma(-wy, u.y, wuu); m12 = -wy * u.z; m22 = fma(-wz, u.z, wuu);
+    // v = w (u x r)
+    v0 = w * fma(u.y, r2, -u.z * r1); v1 = w * fma(u.z, r0, -u.x * r2); v2 = w * fma(u.x, r1, -u.y * r0);
+  }
+  s[1] += m00; s[2] += m01; s[3] += m02; s[4] += m11; s[5] += m12; s[6] += m22;
+  s[22] += v0; s[23] += v1; s[24] += v2;
+  s[25] += fma(p.y, v2, -p.z * v1); s[26] += fma(p.z, v0, -p.x * v2); s[27] += fma(p.x, v1, -p.y * v0);
+  // T = [p]x M row by row; U = T [p]x (symmetric): U[i][0] = T[i][1] pz - T[i][2] py,
+  // U[i][1] = T[i][2] px - T[i][0] pz, U[i][2] = T[i][0] py - T[i][1] px
+  {
+    const double t0 = fma(-p.z, m01, p.y * m02), t1 = fma(-p.z, m11, p.y * m12), t2 = fma(-p.z, m12, p.y * m22);
+    s[7] += t0; s[8] += t1; s[9] += t2;
+    s[16] += fma(t1, p.z, -t2 * p.y);
+    s[17] += fma(t2, p.x, -t0 * p.z);
+    s[18] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(p.z, m00, -p.x * m02), t1 = fma(p.z, m01, -p.x * m12), t2 = fma(p.z, m02, -p.x * m22);
+    s[10] += t0; s[11] += t1; s[12] += t2;
+    s[19] += fma(t2, p.x, -t0 * p.z);
+    s[20] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(-p.y, m00, p.x * m01), t1 = fma(-p.y, m01, p.x * m11), t2 = fma(-p.y, m02, p.x * m12);
+    s[13] += t0; s[14] += t1; s[15] += t2;
+    s[21] += fma(t0, p.y, -t1 * p.x);
   }
 }
 
+// What an association item loads before its pass's x exists (all waves, while the lead waits):
+// the wave's query point and, in the second outer pass, the first pass's matches of that query
+// (closest / second / third, written by the pass-0 items) and their points.
+struct ItemPre {
+  P4 qp;
+  int wi[3];
+  P4 wp[3];
+};
+__device__ __forceinline__ ItemPre eng_item_pre(const OdomArgs& a, int k, int item, const int* warm, int outer) {
+  ItemPre pre;
+  const int w = item * kEngQ + (int)(threadIdx.x >> 6);
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  const bool has = w < ns + nf;
+  const bool corner = w < ns;
+  const int t = corner ? w : w - ns;
+  pre.qp = has ? ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
+                            : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t)
+               : P4{0.f, 0.f, 0.f, 0.f};
+  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
+  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
+#pragma unroll
+  for (int e = 0; e < 3; e++)
+    pre.wi[e] = (has && outer == 1)
+                    ? (int)__hip_atomic_load((gu32*)(warm + (size_t)w * 4 + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : -1;
+#pragma unroll
+  for (int e = 0; e < 3; e++) pre.wp[e] = ld4(L + (pre.wi[e] >= 0 && pre.wi[e] < nL ? pre.wi[e] : 0));
+  return pre;
+}
+
+// R (row-major rotation matrix of x's quaternion: qrot of the unit vectors) and t, in scalar
+// registers (every lane holds them alike).
+__device__ __forceinline__ void eng_rt_x(const double* xs, double (&R)[9], D3& t) {
+  const DQ q{xs[0], xs[1], xs[2], xs[3]};
+  const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
+  R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
+#pragma unroll
+  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);
+  t = D3{uniform_d(xs[4]), uniform_d(xs[5]), uniform_d(xs[6])};
+}
+__device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) { eng_rt_x(sh.x, R, t); }
+
 // One association item, one query per wave (the 64-lane searches of k_odom_assoc: every round
-// trip looks at 64 candidates): queries [item * kEngQ, item * kEngQ + kEngQ) of pair k.  Faster
-// than four 16-lane rows per wave when one chain's ~2000 queries are all the GPU runs (latency
-// bound: 16.5 vs 34.9 us per round as separate launches).
-__device__ __forceinline__ void eng_assoc64(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, int* warm,
-                                            int outer, unsigned tk) {
+// trip looks at 64 candidates): query item * kEngQ + wave of pair k, at the pass's x (each wave's
+// own copy).  Faster than four 16-lane rows per wave when one chain's ~2000 queries are all the
+// GPU runs (latency bound: 16.5 vs 34.9 us per round as separate launches).  The record goes out
+// write-through; the wave's share of the solve's first evaluation (its block's 28 sums at x and
+// the corner / plane counts) goes to sh.red[wave].
+__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, int* warm,
+                                             int outer, unsigned tk, const ItemPre& pre, const double (&x)[7]) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id();
   const int ql = (int)(threadIdx.x >> 6);
   const int w = item * kEngQ + ql;
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  if (lane == 0) sh.kd[ql] = -1;
-  if (w >= ns + nf) return;  // wave-uniform
+  if (w >= ns + nf) {  // wave-uniform: no query, no share
+    if (lane < 30) sh.red[ql][lane] = 0.0;
+    return;
+  }
   const bool corner = w < ns;
-  const int t = corner ? w : w - ns;
-  const P4 qp = ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
-                           : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t);
+  const P4 qp = pre.qp;
   const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
   const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
   const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
   const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
   const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
-  double x[7];
-#pragma unroll
-  for (int e = 0; e < 7; e++) x[e] = sh.x[e];
   const P4 cur{qp.x, qp.y, qp.z, 0.f};
   const P4 sel = transform_to_start(cur, x);
-  // Second outer pass: the first pass's closest / second / third points seed the searches (the
-  // pose moved little).  A seed is one of the candidates of the minimum it seeds, so every result
-  // is unchanged; only the pruning starts tighter.
-  int wi[3] = {-1, -1, -1};
-  P4 wp[3];
-  if (outer == 1) {
-#pragma unroll
-    for (int e = 0; e < 3; e++) {
-      wi[e] = (int)__hip_atomic_load((gu32*)(warm + (size_t)w * 4 + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      wp[e] = ld4(L + (wi[e] >= 0 && wi[e] < nL ? wi[e] : 0));
-    }
-  }
+  // Second outer pass: the first pass's closest / second / third points (pre.wi / pre.wp, loaded
+  // before x existed) seed the searches (the pose moved little).  A seed is one of the candidates
+  // of the minimum it seeds, so every result is unchanged; only the pruning starts tighter.
+  const int (&wi)[3] = pre.wi;
+  const P4 (&wp)[3] = pre.wp;
   dkey seed = kIdent;
 #pragma unroll
   for (int e = 0; e < 3; e++) {
@@ -1836,166 +1939,42 @@ __device__ __forceinline__ void eng_assoc64(const OdomArgs& a, EngShared& sh, in
   }
   if (threadIdx.x == 0) {
     const unsigned long long tq3 = rt_now();
-    eng_prof(tk, 4, tq1 - tq0);  // query load, transform, seeds
+    eng_prof(tk, 4, tq1 - tq0);  // transform, seeds
     eng_prof(tk, 5, tq2 - tq1);  // 1-NN
     eng_prof(tk, 6, tq3 - tq2);  // line searches + record
   }
   if (outer == 0 && lane < 3)  // seeds of the second pass (write-through: another workgroup reads them)
     __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), (unsigned)(lane == 0 ? closest : lane == 1 ? i2 : i3),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lane == 0) {
-    sh.kd[ql] = (int8_t)kind;
-    sh.cf[0][ql] = cur.x; sh.cf[1][ql] = cur.y; sh.cf[2][ql] = cur.z;
-    sh.cf[3][ql] = pa.x; sh.cf[4][ql] = pa.y; sh.cf[5][ql] = pa.z;
-    sh.ud[0][ql] = u.x; sh.ud[1][ql] = u.y; sh.ud[2][ql] = u.z;
+  if (lane < 7 && (lane == 3 || kind >= 0)) {
+    auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
+    uint64_t v;
+    switch (lane) {
+      case 0: v = pk(cur.x, cur.y); break;
+      case 1: v = pk(cur.z, pa.x); break;
+      case 2: v = pk(pa.y, pa.z); break;
+      case 3: v = (uint64_t)(uint32_t)kind; break;
+      case 4: v = (uint64_t)__double_as_longlong(u.x); break;
+      case 5: v = (uint64_t)__double_as_longlong(u.y); break;
+      default: v = (uint64_t)__double_as_longlong(u.z); break;
+    }
+    st_sc1(rec + (size_t)w * kRecWords + lane, v);
   }
-  if (lane >= 7 || (lane != 3 && kind < 0)) return;
-  auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
-  uint64_t v;
-  switch (lane) {
-    case 0: v = pk(cur.x, cur.y); break;
-    case 1: v = pk(cur.z, pa.x); break;
-    case 2: v = pk(pa.y, pa.z); break;
-    case 3: v = (uint64_t)(uint32_t)kind; break;
-    case 4: v = (uint64_t)__double_as_longlong(u.x); break;
-    case 5: v = (uint64_t)__double_as_longlong(u.y); break;
-    default: v = (uint64_t)__double_as_longlong(u.z); break;
-  }
-  st_sc1(rec + (size_t)w * kRecWords + lane, v);
-}
-
-// One association item: queries [item * 64, item * 64 + 64) of pair k (Morton order, corner
-// queries first), four per wave.  Record w of the chain = query w's residual block.
-__device__ __forceinline__ void eng_assoc(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, unsigned tk) {
-  const int lane = lane_id(), lr = lane & 15;
-  const int ql = (int)(threadIdx.x >> 6) * 4 + (lane >> 4);  // this row's slot in the item
-  const int w = item * kEngQ + ql;
-  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  if (lr == 0) sh.kd[ql] = -1;  // the item's blocks are staged in LDS for its first evaluation
-  if (__ballot(w < ns + nf) == 0ull) return;
-  const bool has = w < ns + nf;
-  const bool corner = w < ns;
-  const int t = corner ? w : w - ns;
-  const P4 qp = has ? ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
-                                 : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t)
-                    : P4{0.f, 0.f, 0.f, 0.f};
-  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
-  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
-  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
-  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
-  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
-  double x[7];
+  // the share of the first evaluation (kind is wave-uniform; every lane computes, lane 0 writes)
+  double sb[kAcc];
 #pragma unroll
-  for (int e = 0; e < 7; e++) x[e] = sh.x[e];
-  const P4 cur{qp.x, qp.y, qp.z, 0.f};
-  const P4 sel = transform_to_start(cur, x);
-  const unsigned long long t0 = threadIdx.x == 0 ? rt_now() : 0ull;
-  const int closest = nn16(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, has);
-  const unsigned long long t1 = threadIdx.x == 0 ? rt_now() : 0ull;
-  const bool act = has && closest >= 0;
-  const P4 pa = ld4(L + (act ? closest : 0));
-  const int cid = act ? int(pa.i) : 0;
-  dkey b2 = dk(25.f, kNone), b3 = dk(25.f, kNone);
-  ls16(L, ix.chunk + mo, nL, act ? closest : 0, cid, sel, corner, act, b2, b3);
-  if (threadIdx.x == 0) {
-    const unsigned long long t2 = rt_now();
-    eng_prof(tk, 4, t1 - t0);
-    eng_prof(tk, 5, t2 - t1);
+  for (int e = 0; e < kAcc; e++) sb[e] = 0.0;
+  if (kind >= 0) {
+    double R[9];
+    D3 t;
+    eng_rt_x(x, R, t);
+    eng_block(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, sb);
   }
-  auto idx_of = [&](dkey b) { const int kk = dk_key(b); return kk < nL ? closest + kk : closest - (kk - nL); };
-  int kind = -1;
-  D3 u{0.0, 0.0, 0.0};
-  if (act && corner && dk_key(b2) != kNone) {  // LidarEdgeFactor(curr, a, b)
-    const P4 pb = ld4(L + idx_of(b2));
-    const D3 de{(double)pa.x - (double)pb.x, (double)pa.y - (double)pb.y, (double)pa.z - (double)pb.z};
-    const double inv = 1.0 / sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
-    u = D3{de.x * inv, de.y * inv, de.z * inv};
-    kind = 0;
-  } else if (act && !corner && dk_key(b2) != kNone && dk_key(b3) != kNone) {  // LidarPlaneFactor(curr, j, l, m)
-    const P4 pl = ld4(L + idx_of(b2)), pm = ld4(L + idx_of(b3));
-    u = plane_normal(D3{pa.x, pa.y, pa.z}, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
-    kind = 1;
-  }
-  if (has && lr == 0) {
-    sh.kd[ql] = (int8_t)kind;
-    sh.cf[0][ql] = cur.x; sh.cf[1][ql] = cur.y; sh.cf[2][ql] = cur.z;
-    sh.cf[3][ql] = pa.x; sh.cf[4][ql] = pa.y; sh.cf[5][ql] = pa.z;
-    sh.ud[0][ql] = u.x; sh.ud[1][ql] = u.y; sh.ud[2][ql] = u.z;
-  }
-  if (!has || lr >= 7) return;
-  uint64_t v;
-  auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
-  switch (lr) {
-    case 0: v = pk(cur.x, cur.y); break;
-    case 1: v = pk(cur.z, pa.x); break;
-    case 2: v = pk(pa.y, pa.z); break;
-    case 3: v = (uint64_t)(uint32_t)kind; break;
-    case 4: v = (uint64_t)__double_as_longlong(u.x); break;
-    case 5: v = (uint64_t)__double_as_longlong(u.y); break;
-    default: v = (uint64_t)__double_as_longlong(u.z); break;
-  }
-  if (lr == 3 || kind >= 0) st_sc1(rec + (size_t)w * kRecWords + lr, v);
-}
-
-// One block's 28 sums (see the engine comment) at p = R c, lp = p + t (R, t uniform).  Each row
-// of T is folded into the sums (and into U) as soon as it exists, to keep few doubles live.
-__device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
-                                          double (&s)[kAcc]) {
-  const D3 p{fma(R[0], c.x, fma(R[1], c.y, R[2] * c.z)), fma(R[3], c.x, fma(R[4], c.y, R[5] * c.z)),
-             fma(R[6], c.x, fma(R[7], c.y, R[8] * c.z))};
-  double m00, m01, m02, m11, m12, m22, v0, v1, v2;
-  {
-    const D3 e{(p.x + t.x) - pa.x, (p.y + t.y) - pa.y, (p.z + t.z) - pa.z};
-    double r0 = 0, r1 = 0, r2 = 0, rp = 0, s2;
-    if (kd == 0) {
-      r0 = fma(e.y, u.z, -e.z * u.y); r1 = fma(e.z, u.x, -e.x * u.z); r2 = fma(e.x, u.y, -e.y * u.x);
-      s2 = fma(r0, r0, fma(r1, r1, r2 * r2));
-    } else {
-      rp = fma(e.x, u.x, fma(e.y, u.y, e.z * u.z));
-      s2 = rp * rp;
-    }
-    double w = 1.0;
-    if (s2 > 0.01) {  // HuberLoss(0.1): rho = 2 a sqrt(s) - a^2, rho' = a / sqrt(s)
-      const double rr = sqrt(s2);
-      s[0] += 0.5 * (0.2 * rr - 0.01);
-      w = fmax(2.2250738585072014e-308, 0.1 / rr);
-    } else {
-      s[0] += 0.5 * s2;
-    }
-    const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
-    if (kd == 0) {
-      const double wuu = w * fma(u.x, u.x, fma(u.y, u.y, u.z * u.z));
-      m00 = fma(-wx, u.x, wuu); m01 = -wx * u.y; m02 = -wx * u.z;
-      m11 = fma(-wy, u.y, wuu); m12 = -wy * u.z; m22 = fma(-wz, u.z, wuu);
-      // v = w (u x r)
-      v0 = w * fma(u.y, r2, -u.z * r1); v1 = w * fma(u.z, r0, -u.x * r2); v2 = w * fma(u.x, r1, -u.y * r0);
-    } else {
-      m00 = wx * u.x; m01 = wx * u.y; m02 = wx * u.z; m11 = wy * u.y; m12 = wy * u.z; m22 = wz * u.z;
-      v0 = rp * wx; v1 = rp * wy; v2 = rp * wz;
-    }
-  }
-  s[1] += m00; s[2] += m01; s[3] += m02; s[4] += m11; s[5] += m12; s[6] += m22;
-  s[22] += v0; s[23] += v1; s[24] += v2;
-  s[25] += fma(p.y, v2, -p.z * v1); s[26] += fma(p.z, v0, -p.x * v2); s[27] += fma(p.x, v1, -p.y * v0);
-  // T = [p]x M row by row; U = T [p]x (symmetric): U[i][0] = T[i][1] pz - T[i][2] py,
-  // U[i][1] = T[i][2] px - T[i][0] pz, U[i][2] = T[i][0] py - T[i][1] px
-  {
-    const double t0 = fma(-p.z, m01, p.y * m02), t1 = fma(-p.z, m11, p.y * m12), t2 = fma(-p.z, m12, p.y * m22);
-    s[7] += t0; s[8] += t1; s[9] += t2;
-    s[16] += fma(t1, p.z, -t2 * p.y);
-    s[17] += fma(t2, p.x, -t0 * p.z);
-    s[18] += fma(t0, p.y, -t1 * p.x);
-  }
-  {
-    const double t0 = fma(p.z, m00, -p.x * m02), t1 = fma(p.z, m01, -p.x * m12), t2 = fma(p.z, m02, -p.x * m22);
-    s[10] += t0; s[11] += t1; s[12] += t2;
-    s[19] += fma(t2, p.x, -t0 * p.z);
-    s[20] += fma(t0, p.y, -t1 * p.x);
-  }
-  {
-    const double t0 = fma(-p.y, m00, p.x * m01), t1 = fma(-p.y, m01, p.x * m11), t2 = fma(-p.y, m02, p.x * m12);
-    s[13] += t0; s[14] += t1; s[15] += t2;
-    s[21] += fma(t0, p.y, -t1 * p.x);
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < kAcc; e++) sh.red[ql][e] = sb[e];
+    sh.red[ql][28] = kind == 0 ? 1.0 : 0.0;
+    sh.red[ql][29] = kind == 1 ? 1.0 : 0.0;
   }
 }
 
@@ -2076,42 +2055,6 @@ __device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
     sh.acc[ai] = sc * v;
   }
   __syncthreads();
-}
-
-// R (row-major rotation matrix of sh.x's quaternion: qrot of the unit vectors) and t, in scalar
-// registers (every lane holds them alike).
-__device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) {
-  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
-  const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
-  R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
-#pragma unroll
-  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);
-  t = D3{uniform_d(sh.x[4]), uniform_d(sh.x[5]), uniform_d(sh.x[6])};
-}
-
-// The item's share of the solve's first evaluation (at the x its association used): wave 0, lanes
-// 0..31 one staged block each; the 28 sums + the corner / plane counts -> part[0..29] (write-through).
-__device__ __forceinline__ void eng_item_partials(const EngShared& sh, double* part) {
-  const int lane = lane_id();
-  double s[kAcc];
-#pragma unroll
-  for (int e = 0; e < kAcc; e++) s[e] = 0.0;
-  double R[9];
-  D3 t;
-  eng_rt(sh, R, t);
-  const int kd = lane < kEngQ ? (int)sh.kd[lane] : -1;
-  if (kd >= 0)
-    eng_block(kd, D3{sh.cf[0][lane], sh.cf[1][lane], sh.cf[2][lane]}, D3{sh.cf[3][lane], sh.cf[4][lane], sh.cf[5][lane]},
-              D3{sh.ud[0][lane], sh.ud[1][lane], sh.ud[2][lane]}, R, t, s);
-  double o[7];
-  const int p = row_reduce_scatter28(s, o);
-#pragma unroll
-  for (int q = 0; q < 7; q++) o[q] = rows_sum(o[q]);
-  const int nc = __popcll(__ballot(kd == 0)), np = __popcll(__ballot(kd == 1));
-  if (lane < 4)
-#pragma unroll
-    for (int q = 0; q < 7; q++) st_sc1d(part + part_base(p) + q, o[q]);
-  if (lane == 0) { st_sc1d(part + 28, (double)nc); st_sc1d(part + 29, (double)np); }
 }
 
 // One evaluation at sh.x over `total` records (LDS for i < kEngLds, write-through records beyond).
@@ -2306,7 +2249,12 @@ typedef __attribute__((address_space(3))) EngLM LdsLM;
 typedef const __attribute__((address_space(3))) double LdsD;
 // The state and the evaluation stay in LDS, addressed as LDS (ds_read / ds_write): through the
 // generic pointers a call receives they would be flat accesses, each waiting on both counters.
-__device__ __noinline__ bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool first, int max_it) {
+#ifdef LISLAM_STEP_NOINLINE
+#define LISLAM_STEP_ATTR __noinline__
+#else
+#define LISLAM_STEP_ATTR __forceinline__  // a call saves / restores 24 callee-saved VGPRs through scratch per step
+#endif
+__device__ LISLAM_STEP_ATTR bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool first, int max_it) {
   const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
   bool cont = true;
   if (first) {
@@ -2388,6 +2336,7 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
       for (int j = 0; j < 24; j++) t += v[j];
     }
     if (e < 30) sh.red[g][e] = t;
+    if (e == 30 && g < 7) sh.x[g] = eng_x_word(a, c, r, outer, g);  // in flight with the shares
     __syncthreads();
     if (threadIdx.x < 30) {
       double sum = 0.0;
@@ -2406,43 +2355,51 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
   bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
   unsigned long long t_ev = 0;
   if (threadIdx.x == 0) { t_ev = rt_now(); eng_prof(tk, 2, t_ev); }
-  if (go) {
-    if (wave0) {  // the first step on lane 0 ...
-      if (lane == 0) {
-        lm.prof = g_eng_prof != nullptr;
-        for (int e = 0; e < 4; e++) lm.pacc[e] = 0;
-        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, true, a.max_iterations);
-        sh.flag = cont;
-        if (cont)
-          for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
-        eng_prof(tk, 5, rt_now() - t_ev, true);
-      }
-    } else {      // ... while the other waves bring the blocks into LDS for the candidates' evaluations
-      for (int i = threadIdx.x - 64; i < min(total, kEngLds); i += kEngThreads - 64) {
-        const uint64_t* rw = rec + (size_t)i * kRecWords;
-        const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2), w3 = ld_sc1(rw + 3);
-        const uint64_t w4 = ld_sc1(rw + 4), w5 = ld_sc1(rw + 5), w6 = ld_sc1(rw + 6);
-        sh.kd[i] = (int8_t)(int)(uint32_t)w3;
-        sh.cf[0][i] = __uint_as_float((uint32_t)w0); sh.cf[1][i] = __uint_as_float((uint32_t)(w0 >> 32));
-        sh.cf[2][i] = __uint_as_float((uint32_t)w1); sh.cf[3][i] = __uint_as_float((uint32_t)(w1 >> 32));
-        sh.cf[4][i] = __uint_as_float((uint32_t)w2); sh.cf[5][i] = __uint_as_float((uint32_t)(w2 >> 32));
-        sh.ud[0][i] = __longlong_as_double((long long)w4);
-        sh.ud[1][i] = __longlong_as_double((long long)w5);
-        sh.ud[2][i] = __longlong_as_double((long long)w6);
+  // One loop, one (inlined) step site: pass 0 is the first step on lane 0 while the other waves
+  // bring the blocks into LDS; every later pass evaluates at the candidate, then steps.
+  for (int pass = 0; go; pass++) {
+    if (pass > 0) {
+      eng_evaluate(sh, rec, total, tk);  // cost + J^T J + J^T r at each candidate
+    } else if (!wave0) {
+      // records -> LDS: every record's seven words in flight before any is stored (the loads
+      // are agent-scope atomics, which the compiler does not batch across loop iterations)
+      constexpr int kStride = kEngThreads - 64;
+      const int n = min(total, kEngLds);
+      for (int i0 = threadIdx.x - 64; i0 < n; i0 += kRecUnroll * kStride) {
+        uint64_t w[kRecUnroll][7];
+#pragma unroll
+        for (int u = 0; u < kRecUnroll; u++) {
+          const int i = i0 + u * kStride;
+          const uint64_t* rw = rec + (size_t)(i < n ? i : 0) * kRecWords;
+#pragma unroll
+          for (int e = 0; e < 7; e++) w[u][e] = i < n ? ld_sc1(rw + e) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kRecUnroll; u++) {
+          const int i = i0 + u * kStride;
+          if (i < n) {
+            sh.kd[i] = (int8_t)(int)(uint32_t)w[u][3];
+            sh.cf[0][i] = __uint_as_float((uint32_t)w[u][0]); sh.cf[1][i] = __uint_as_float((uint32_t)(w[u][0] >> 32));
+            sh.cf[2][i] = __uint_as_float((uint32_t)w[u][1]); sh.cf[3][i] = __uint_as_float((uint32_t)(w[u][1] >> 32));
+            sh.cf[4][i] = __uint_as_float((uint32_t)w[u][2]); sh.cf[5][i] = __uint_as_float((uint32_t)(w[u][2] >> 32));
+            sh.ud[0][i] = __longlong_as_double((long long)w[u][4]);
+            sh.ud[1][i] = __longlong_as_double((long long)w[u][5]);
+            sh.ud[2][i] = __longlong_as_double((long long)w[u][6]);
+          }
+        }
       }
     }
-    __syncthreads();
-    go = uni(sh.flag);
-    if (threadIdx.x == 0) t_ev = rt_now();
-  }
-  while (go) {
-    eng_evaluate(sh, rec, total, tk);  // cost + J^T J + J^T r at each candidate
     if (wave0) {
       if (lane == 0) {
         const unsigned long long t_st = rt_now();
-        eng_prof(tk, 4, t_st - t_ev, true);
-        eng_prof(tk, 6, 1ull, true);
-        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, false, a.max_iterations);
+        if (pass == 0) {
+          lm.prof = g_eng_prof != nullptr;
+          for (int e = 0; e < 4; e++) lm.pacc[e] = 0;
+        } else {
+          eng_prof(tk, 4, t_st - t_ev, true);
+          eng_prof(tk, 6, 1ull, true);
+        }
+        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, pass == 0, a.max_iterations);
         t_ev = rt_now();
         eng_prof(tk, 5, t_ev - t_st, true);
         sh.flag = cont;
@@ -2452,6 +2409,7 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
     }
     __syncthreads();
     go = uni(sh.flag);
+    if (pass == 0 && threadIdx.x == 0) t_ev = rt_now();
   }
   if (!wave0) return;
   if (lane != 0) return;
@@ -2573,19 +2531,28 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     const int ieff = live ? eng_live_items(a, k) : 0;
     if (item < ctl.I && item >= ieff) live = false;  // an empty item: nothing to wait for or signal
     uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
-    if (!wave0 && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
+    int* warm = a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4;
+    const bool is_item = item < ctl.I;
+    // An item of the second outer pass first waits for the first pass's items (its seeds), long
+    // done in the common case; then every wave loads what needs no x while the lead waits for x.
+    if (wave0) {
+      if (lead) sh.flag0 = (live && is_item && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w()) : true;
+    }
+    __syncthreads();
+    bool ok = uni(sh.flag0) != 0;
+    ItemPre pre;
+    if (ok && live && is_item) pre = eng_item_pre(a, k, item, warm, o);
+    if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
     if (wave0) {
       if (lead) {
-        bool ok = true;
-        if (live) {
+        if (ok && live) {
           // every item after the chain's previous solve; the solve after its pair's live items too
           // (which imply the first wait, except for a pair without queries: ieff == 0)
           ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w());
-          if (ok && item == ctl.I) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w());
+          if (ok && !is_item) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w());
           eng_trace(1, ok ? 2u : 99u);
           eng_prof(tk, 1, rt_now());
-          if (ok) eng_load_x(a, c, r, o, sh.x);
-          if (ok && c == 0 && r == 0 && o == 0 && item == ctl.I && !a.init_state) {  // scan 0 of the batch: first frame
+          if (ok && c == 0 && r == 0 && o == 0 && !is_item && !a.init_state) {  // scan 0 of the batch: first frame
             for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
             for (int e = 0; e < 8; e++) a.stats[e] = 0;
           }
@@ -2594,25 +2561,29 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
       }
     }
     __syncthreads();
-    const bool ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
+    ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
     if (ok && live) {
-      if (item < ctl.I) {
-        const bool gated_off = a.gate && !a.gate[k];  // not optimized: no association (:417)
-#ifndef LISLAM_ENG_ROWS16
-        if (!gated_off)
-          eng_assoc64(a, sh, k, item, rec, a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4, o, tk);
-#else
-        if (!gated_off) eng_assoc(a, sh, k, item, rec, tk);
-#endif
-        else if (threadIdx.x < kEngQ) sh.kd[threadIdx.x] = -1;
-        drain_stores();
+      if (is_item) {
+        double x[7];
+        eng_load_x(a, c, r, o, x);  // each wave its own copy: no LDS hop, no barrier
+        eng_item_run(a, sh, k, item, rec, warm, o, tk, pre, x);
+        drain_stores();  // this wave's record (and seed) stores
         __syncthreads();
         if (wave0) {
           const unsigned long long tp0 = lead ? rt_now() : 0ull;
-          eng_item_partials(sh, a.eng_part + ((size_t)c * ctl.I + item) * 32);
-          if (lead) eng_prof(tk, 7, rt_now() - tp0);
+          if (lane_id() < 30) {  // the item's share: the sum of its waves' shares
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < kEngWaves; w++) v += sh.red[w][lane_id()];
+            st_sc1d(a.eng_part + ((size_t)c * ctl.I + item) * 32 + lane_id(), v);
+          }
           drain_stores();
-          if (lead) { add_rlx(ctl.assoc_done(c, ro), 1u); eng_trace(1, 4u); eng_prof(tk, 3, rt_now()); }
+          if (lead) {
+            eng_prof(tk, 7, rt_now() - tp0);
+            add_rlx(ctl.assoc_done(c, ro), 1u);
+            eng_trace(1, 4u);
+            eng_prof(tk, 3, rt_now());
+          }
         }
       } else {
         eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0, tk, ieff);

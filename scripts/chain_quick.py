@@ -12,6 +12,8 @@ sys.path.insert(0, _R)
 import __graft_entry__ as g  # noqa: E402
 
 pkg = g.package()
+if os.environ.get("LISLAM_ALT_LIB"):
+    pkg.native.load(os.environ["LISLAM_ALT_LIB"])  # a developer variant of the library
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 cache = f"/tmp/lislam_chain_scans_{S}.npy"
@@ -26,7 +28,8 @@ with pkg.Context() as ctx:
     b.extract(S)
     ctx.synchronize()
     res = {}
-    for name, mode in (("engine", ctx.ENGINE_ON), ("rounds", ctx.ENGINE_OFF)):
+    modes = (("engine", ctx.ENGINE_ON),) if os.environ.get("CHAIN_ENGINE_ONLY") else (("engine", ctx.ENGINE_ON), ("rounds", ctx.ENGINE_OFF))
+    for name, mode in modes:
         ctx.set_odometry_schedule(mode)
         b.odometry(S, S - 1)
         ctx.synchronize()
@@ -44,6 +47,16 @@ with pkg.Context() as ctx:
                               for k in range(S)])
         st = np.array([b.download(pkg.native.OUT_STATS, k) for k in range(S)])
         res[name + "_st"] = st
+    if "rounds" not in res:
+        ref = os.environ.get("CHAIN_REF")
+        if ref and os.path.exists(ref):
+            z = np.load(ref)
+            print(f"engine vs {ref}: max |para/pose delta| {np.max(np.abs(res['engine'] - z['p'])):.3g}, "
+                  f"stats mismatches {int(np.sum(np.any(res['engine_st'][:, :6] != z['st'][:, :6], axis=1)))}", flush=True)
+        elif ref:
+            np.savez(ref, p=res["engine"], st=res["engine_st"])
+        b.close()
+        sys.exit(0)
     d = np.max(np.abs(res["engine"] - res["rounds"]))
     nst = int(np.sum(np.any(res["engine_st"][:, :6] != res["rounds_st"][:, :6], axis=1)))
     print(f"engine vs rounds: max |para/pose delta| {d:.3g}, stats mismatches {nst}", flush=True)
