@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as g  # noqa: E402
 
-OUT = os.path.join(ROOT, "scripts", "_prof", "liblislam_count.so")
+OUT = os.environ.get("LISLAM_COUNT_LIB", os.path.join(ROOT, "scripts", "_prof", "liblislam_count.so"))
 NAMES = ["nn: candidate super-chunk", "nn: super-chunk rounds", "nn: chunk rounds", "nn: speculative bounds", "ls: windows",
          "ls: first batch", "ls corner: batch rounds", "ls surf: batch rounds", "corner queries", "surf queries",
          "corner with closest", "surf with closest"]
