@@ -435,9 +435,10 @@ __device__ __forceinline__ void nn_eval(const P4* sorted, int n, const int (&ch)
   }
   dkey v = kIdent;
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
+  for (int t = 0; t < 2; t++) {  // selects, not branches: no exec-mask traffic in the round
     const float dd = d2f(q, p[t]);
-    if (ok[t] && dd < 25.f) v = dmin(v, dk(dd, __float_as_int(p[t].i)));
+    const dkey kk = dk(dd, __float_as_int(p[t].i));
+    v = (ok[t] && dd < 25.f && kk < v) ? kk : v;
   }
   best = dmin(best, wave_min(v));
 }
@@ -577,25 +578,23 @@ __device__ __forceinline__ void ls_eval(LineSearch& s, const int (&ch)[2], const
   }
   dkey v2 = kIdent, v3 = kIdent;
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
+  for (int t = 0; t < 2; t++) {  // selects, not branches: no exec-mask traffic in the round
     const int pid = int(p[t].i);
     const bool brk = valid[t] && (up[t] ? pid > s.cid + 2 : pid < s.cid - 2);  // the walk's 'break'
     const uint64_t bm = __ballot(brk);
     if (brk_mask) brk_mask[t] = bm;
     const uint32_t gm = (uint32_t)((bm >> (lane & 48)) & 0xffffull);
-    bool v = valid[t];
-    if (gm) v = v && (up[t] ? l16 < (int)__builtin_ctz(gm) : l16 > 31 - (int)__builtin_clz(gm));
-    if (v) {
-      const float d = d2f(s.sel, p[t]);
-      const int key = up[t] ? j[t] - s.closest : s.n + s.closest - j[t];
-      if (d < 25.f) {
-        if (kCorner) {
-          if (up[t] ? pid > s.cid : pid < s.cid) v2 = dmin(v2, dk(d, key));
-        } else {
-          if (up[t] ? pid <= s.cid : pid >= s.cid) v2 = dmin(v2, dk(d, key));
-          else v3 = dmin(v3, dk(d, key));
-        }
-      }
+    const int first_brk = gm ? (int)__builtin_ctz(gm) : 16, last_brk = gm ? 31 - (int)__builtin_clz(gm) : -1;
+    const bool v = valid[t] && (up[t] ? l16 < first_brk : l16 > last_brk);
+    const float d = d2f(s.sel, p[t]);
+    const dkey kk = dk(d, up[t] ? j[t] - s.closest : s.n + s.closest - j[t]);
+    const bool near = v && d < 25.f;
+    const bool other = up[t] ? pid > s.cid : pid < s.cid;  // another scan line
+    if (kCorner) {
+      v2 = (near && other && kk < v2) ? kk : v2;
+    } else {
+      v2 = (near && !other && kk < v2) ? kk : v2;
+      v3 = (near && other && kk < v3) ? kk : v3;
     }
   }
   if (kCorner) {
@@ -2548,6 +2547,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
         if (ok && live) {
           // every item after the chain's previous solve; the solve after its pair's live items too
           // (which imply the first wait, except for a pair without queries: ieff == 0)
+          if (is_item) eng_prof(tk, 2, rt_now());  // the item's lead starts its wait for x
           ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w());
           if (ok && !is_item) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w());
           eng_trace(1, ok ? 2u : 99u);

@@ -88,6 +88,21 @@ with pkg.Context() as ctx:
     rows["association slowest item (ready -> done)"] = done_last
     claim_ready = np.array([np.median(items[i, valid[i], 1] - items[i, valid[i], 0]) for i in range(2 * R)]) * us
     rows["association item claim -> ready median"] = claim_ready
+    # items ready > 3 us after their pass's first: when they were claimed and began waiting
+    late = []
+    for i in range(1, 2 * R):
+        v = valid[i]
+        rd = items[i, :, 1] - a_start[i]
+        for j in np.nonzero(v & (rd > 300))[0]:
+            late.append(((items[i, j, 0] - a_start[i]) * us, (items[i, j, 2] - a_start[i]) * us, rd[j] * us,
+                         (items[i, j, 3] - items[i, j, 1]) * us, int(j)))
+    if late:
+        la = np.array(late)
+        print(f"  late items: {len(la)} over {2 * R} passes; relative to the pass's first ready (us): "
+              f"claim p50 {np.median(la[:, 0]):.1f}, wait start p50 {np.median(la[:, 1]):.1f}, "
+              f"ready p50 {np.median(la[:, 2]):.1f}, run p50 {np.median(la[:, 3]):.1f}; item index p50 {np.median(la[:, 4]):.0f}")
+        for row in la[np.argsort(-la[:, 2])][:8]:
+            print("   late item: claim %.1f wait %.1f ready %.1f run %.1f item %d" % tuple(row))
     for k, v in rows.items():
         print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")
     print(f"  evaluations per solve: mean {np.mean(npass):.2f}")
