@@ -1648,6 +1648,7 @@ struct EngCtl {
   unsigned* w;
   int C, R, I;
   int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
+  int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at once
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
@@ -1706,6 +1707,9 @@ struct EngShared {
   double ud[3][kEngLds];  // edge: u = (a - b) / |a - b|; plane: unit normal
   int8_t kd[kEngLds];     // 0 edge, 1 plane, -1 none
   double red[kEngWaves * 4][32];  // kAcc sums (+ 2 counts) per 16-lane row
+  double xw[kEngWaves][8];        // each wave's copy of its item's x (the item's queries read it here)
+  P4 prew[kEngWaves][4];          // each wave's ItemPre of its first query: qp, the seeds' points
+  int prei[kEngWaves][4];         // ... and the seeds' indices
   double acc[kAcc];
   double x[7];
   int cnt[kEngWaves][2];
@@ -1806,9 +1810,8 @@ struct ItemPre {
   int wi[3];
   P4 wp[3];
 };
-__device__ __forceinline__ ItemPre eng_item_pre(const OdomArgs& a, int k, int item, const int* warm, int outer) {
+__device__ __forceinline__ ItemPre eng_item_pre(const OdomArgs& a, int k, int w, const int* warm, int outer) {
   ItemPre pre;
-  const int w = item * kEngQ + (int)(threadIdx.x >> 6);
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const bool has = w < ns + nf;
   const bool corner = w < ns;
@@ -1846,17 +1849,11 @@ __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& 
 // GPU runs (latency bound: 16.5 vs 34.9 us per round as separate launches).  The record goes out
 // write-through; the wave's share of the solve's first evaluation (its block's 28 sums at x and
 // the corner / plane counts) goes to sh.red[wave].
-__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, uint64_t* rec, int* warm,
-                                             int outer, unsigned tk, const ItemPre& pre, const double (&x)[7]) {
+__device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int k, int w, uint64_t* rec, int* warm, int outer,
+                                          unsigned tk, const ItemPre& pre, const double (&x)[7]) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id();
-  const int ql = (int)(threadIdx.x >> 6);
-  const int w = item * kEngQ + ql;
-  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  if (w >= ns + nf) {  // wave-uniform: no query, no share
-    if (lane < 30) sh.red[ql][lane] = 0.0;
-    return;
-  }
+  const int ns = a.n_feat[k * 4 + 0];
   const bool corner = w < ns;
   const P4 qp = pre.qp;
   const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
@@ -1959,21 +1956,50 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, i
     }
     st_sc1(rec + (size_t)w * kRecWords + lane, v);
   }
-  // the share of the first evaluation (kind is wave-uniform; every lane computes, lane 0 writes)
-  double sb[kAcc];
-#pragma unroll
-  for (int e = 0; e < kAcc; e++) sb[e] = 0.0;
+  // the share of the first evaluation, added to the wave's row sh.red[wave] (kind is wave-uniform;
+  // every lane computes, lane 0 adds; a wave's LDS accesses stay in order)
   if (kind >= 0) {
+    double sb[kAcc];
+#pragma unroll
+    for (int e = 0; e < kAcc; e++) sb[e] = 0.0;
     double R[9];
     D3 t;
     eng_rt_x(x, R, t);
     eng_block(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, sb);
-  }
-  if (lane == 0) {
+    if (lane == 0) {
+      double* row = sh.red[threadIdx.x >> 6];
 #pragma unroll
-    for (int e = 0; e < kAcc; e++) sh.red[ql][e] = sb[e];
-    sh.red[ql][28] = kind == 0 ? 1.0 : 0.0;
-    sh.red[ql][29] = kind == 1 ? 1.0 : 0.0;
+      for (int e = 0; e < kAcc; e++) row[e] += sb[e];
+      row[28 + kind] += 1.0;
+    }
+  }
+}
+
+// One association item: wave wv of item `item` takes queries (item + m ieff) kEngQ + wv, m = 0,
+// 1, ...: one each while the pair's queries fit ieff items (the common case), more when the pair
+// holds more queries than the engine keeps items in flight (EngCtl::budget), so that no item
+// waits for a workgroup to come free.  The wave's share of the first evaluation (its blocks' 28
+// sums at x, and the corner / plane counts) goes to sh.red[wave].
+__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, int ieff, uint64_t* rec,
+                                             int* warm, int outer, unsigned tk) {
+  const int ql = (int)(threadIdx.x >> 6);
+  const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
+  if (lane_id() < 30) sh.red[ql][lane_id()] = 0.0;
+  for (int m = 0;; m++) {
+    const int w = (item + m * ieff) * kEngQ + ql;
+    if (w >= nq) break;  // wave-uniform
+    ItemPre pre;
+    if (m > 0) {
+      pre = eng_item_pre(a, k, w, warm, outer);
+    } else {  // loaded before x existed, parked in this wave's LDS slots
+      pre.qp = sh.prew[ql][0];
+#pragma unroll
+      for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][1 + e]; pre.wi[e] = sh.prei[ql][e]; }
+    }
+    double x[7];
+#pragma unroll
+    for (int e = 0; e < 7; e++) x[e] = sh.xw[ql][e];
+    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x);
   }
 }
 
@@ -2453,9 +2479,9 @@ __device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, 
 }
 
 // Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
-__device__ __forceinline__ int eng_live_items(const OdomArgs& a, int k) {
+__device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& ctl, int k) {
   if (a.gate && !a.gate[k]) return 0;
-  return uni((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + kEngQ - 1) / kEngQ);
+  return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + kEngQ - 1) / kEngQ, ctl.budget));
 }
 
 // Touch (one dword per 128-B line, plain loads: they allocate in this XCD's L2) every structure the
@@ -2492,7 +2518,7 @@ __device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCt
   const int c = rem / (ctl.I + 1), item = rem % (ctl.I + 1);
   if (item >= ctl.I || ro >= 2 * ctl.R || ro == 0) return 0;
   int k;
-  if (!pair_of(a, c, ro >> 1, &k) || item >= eng_live_items(a, k)) return 0;
+  if (!pair_of(a, c, ro >> 1, &k) || item >= eng_live_items(a, ctl, k)) return 0;
   return ld_rlx(ctl.lm_gen(c)) < (unsigned)ro ? 1 : 0;
 }
 
@@ -2527,7 +2553,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     int k;
     bool live = pair_of(a, c, r, &k);
     // items holding queries of pair k: ceil((sharp + flat) / kEngQ), none for a gated-off scan
-    const int ieff = live ? eng_live_items(a, k) : 0;
+    const int ieff = live ? eng_live_items(a, ctl, k) : 0;
     if (item < ctl.I && item >= ieff) live = false;  // an empty item: nothing to wait for or signal
     uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
     int* warm = a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4;
@@ -2539,8 +2565,12 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     }
     __syncthreads();
     bool ok = uni(sh.flag0) != 0;
-    ItemPre pre;
-    if (ok && live && is_item) pre = eng_item_pre(a, k, item, warm, o);
+    if (ok && live && is_item) {  // each wave parks its first query's loads in its LDS slots
+      const ItemPre pre = eng_item_pre(a, k, item * kEngQ + (int)(threadIdx.x >> 6), warm, o);
+      const int wv = (int)(threadIdx.x >> 6), l = lane_id();
+      if (l < 4) sh.prew[wv][l] = l == 0 ? pre.qp : pre.wp[l == 1 ? 0 : l == 2 ? 1 : 2];
+      if (l < 3) sh.prei[wv][l] = pre.wi[l == 0 ? 0 : l == 1 ? 1 : 2];
+    }
     if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
     if (wave0) {
       if (lead) {
@@ -2564,9 +2594,11 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
     if (ok && live) {
       if (is_item) {
-        double x[7];
-        eng_load_x(a, c, r, o, x);  // each wave its own copy: no LDS hop, no barrier
-        eng_item_run(a, sh, k, item, rec, warm, o, tk, pre, x);
+        {  // each wave its own copy of x (its lanes 0..6 load it): no barrier
+          const int l = lane_id();
+          if (l < 7) sh.xw[threadIdx.x >> 6][l] = eng_x_word(a, c, r, o, l);
+        }
+        eng_item_run(a, sh, k, item, ieff, rec, warm, o, tk);
         drain_stores();  // this wave's record (and seed) stores
         __syncthreads();
         if (wave0) {
@@ -2623,6 +2655,20 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   ctl.I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
   const char* pf = getenv("LISLAM_ENGINE_PREFETCH");
   ctl.prefetch = pf ? atoi(pf) : 1;
+  // Items per (pass, chain): the workgroups resident at once, less the chains' solves (the running
+  // one and the next, already claimed) and one spare, shared by the chains.  More queries than
+  // that are dealt as second queries to the items' waves (eng_item_run).  LISLAM_ENGINE_BUDGET
+  // overrides (tests).
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_odom_chain, kEngThreads, 0);
+    resident = max(1, cus * max(per_cu, 1));
+  }
+  const char* bud = getenv("LISLAM_ENGINE_BUDGET");
+  ctl.budget = bud ? max(1, atoi(bud)) : max(1, (resident - 2 * ctl.C - 1) / ctl.C);
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   (void)hipMemsetAsync(a.eng_ctl, 0, words * sizeof(unsigned), st);
   // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)

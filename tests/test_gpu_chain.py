@@ -137,3 +137,26 @@ def test_engine_gated_chain(pkg, oracle, synth, ctx):
         assert np.max(np.abs(b.download(pkg.native.OUT_POSE, k) - pose[k])) < POSE_TOL, k
         assert np.array_equal(b.download(pkg.native.OUT_STATS, k)[:4], st[k][:4]), k
     b.close()
+
+
+@pytest.mark.parametrize("budget", [1, 37])
+def test_engine_item_budget(pkg, oracle, synth, ctx, budget):
+    """More queries than the engine keeps items in flight: the items' waves take second (and later)
+    queries (EngCtl::budget), with the same correspondences and poses."""
+    S = 5
+    scans = synth.make_sequence(S, start=60)
+    feats = [oracle.scan_registration(s) for s in scans]
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    os.environ["LISLAM_ENGINE_BUDGET"] = str(budget)
+    try:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, S - 1)
+        ctx.synchronize()
+    finally:
+        del os.environ["LISLAM_ENGINE_BUDGET"]
+        ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+    pose, rel, st = oracle.odometry_chain(feats)
+    check_chain(pkg, b, feats, pose, rel, st)
+    b.close()
