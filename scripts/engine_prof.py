@@ -62,6 +62,7 @@ with pkg.Context() as ctx:
         "association item median (ready -> done)": a_med * us,
         "hand-off assoc -> solve (last item done -> solve ready)": (lm_ready - a_end) * us,
         "solve record load": (lm_loaded - lm_ready) * us,
+        "last item done -> solve has every share (gather tail)": (lm_loaded - a_end) * us,
         "solve evaluations (sum)": ev * us,
         "solve steps (sum)": st * us,
         "solve evaluations: reductions (sum)": lm[:, 7] * us,
