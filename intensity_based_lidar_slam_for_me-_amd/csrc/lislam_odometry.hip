@@ -1563,13 +1563,25 @@ extern "C" int lislam_debug_engine_prof_read(unsigned long long* out, int n_tick
   if (hipDeviceSynchronize() != hipSuccess) return -2;
   return hipMemcpy(out, s_eng_prof, sizeof(unsigned long long) * 8 * n_tickets, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
+// LISLAM_ENG_PROF = 0 compiles the engine's developer timestamps out (rt_now() = 0, eng_prof a no-op).
+#ifndef LISLAM_ENG_PROF
+#define LISLAM_ENG_PROF 1
+#endif
 __device__ __forceinline__ void eng_prof(unsigned tk, int slot, unsigned long long v, bool add = false) {
+#if LISLAM_ENG_PROF
   unsigned long long* p = g_eng_prof;
   if (!p || tk >= g_eng_prof_n) return;
   if (add) p[(size_t)tk * 8 + slot] += v;
   else p[(size_t)tk * 8 + slot] = v;
+#endif
 }
-__device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned long long rt_now() {
+#if LISLAM_ENG_PROF
+  return __builtin_amdgcn_s_memrealtime();
+#else
+  return 0ull;
+#endif
+}
 // per-query record of one pair (developer): [outer][query] = {1-NN ticks, line-search ticks, closest, kind}
 __device__ int* g_eng_qlog = nullptr;
 __device__ int g_eng_qlog_pair = -1;
@@ -1833,12 +1845,16 @@ __device__ __forceinline__ ItemPre eng_item_pre(const OdomArgs& a, int k, int w,
 
 // R (row-major rotation matrix of x's quaternion: qrot of the unit vectors) and t, in scalar
 // registers (every lane holds them alike).
+// (Eigen's Quaternion::toRotationMatrix: 22 flops, not three vector rotations; the evaluation only
+// needs R to rounding, the association's TransformToStart keeps the reference's q * v.)
 __device__ __forceinline__ void eng_rt_x(const double* xs, double (&R)[9], D3& t) {
-  const DQ q{xs[0], xs[1], xs[2], xs[3]};
-  const D3 ex = qrot(q, D3{1, 0, 0}), ey = qrot(q, D3{0, 1, 0}), ez = qrot(q, D3{0, 0, 1});
-  R[0] = ex.x; R[1] = ey.x; R[2] = ez.x; R[3] = ex.y; R[4] = ey.y; R[5] = ez.y; R[6] = ex.z; R[7] = ey.z; R[8] = ez.z;
-#pragma unroll
-  for (int e = 0; e < 9; e++) R[e] = uniform_d(R[e]);
+  const double x = uniform_d(xs[0]), y = uniform_d(xs[1]), z = uniform_d(xs[2]), w = uniform_d(xs[3]);
+  const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+  R[3] = txy + twz; R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1.0 - (txx + tyy);
   t = D3{uniform_d(xs[4]), uniform_d(xs[5]), uniform_d(xs[6])};
 }
 __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) { eng_rt_x(sh.x, R, t); }
@@ -2010,11 +2026,21 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, i
 // sum index e of eng_block -> index in lislam_lm.hpp's acc (H upper row-major over (theta 0..2,
 // t 0..2), then g) and its scale: cost; M -> H_tt; T -> H_theta,t = 2 T; U -> H_theta,theta = -4 U;
 // v -> g_t; p x v -> g_theta = 2 p x v
-__constant__ int kAccMap[kAcc] = {0, 16, 17, 18, 19, 20, 21, 4, 5, 6, 9, 10, 11, 13, 14, 15,
-                                  1, 2, 3, 7, 8, 12, 25, 26, 27, 22, 23, 24};
 __device__ __forceinline__ int acc_index(int e, double* scale) {
   *scale = e == 0 ? 1.0 : e <= 6 ? 1.0 : e <= 15 ? 2.0 : e <= 21 ? -4.0 : e <= 24 ? 1.0 : 2.0;
-  return kAccMap[e];
+  // H upper index (lislam_lm.hpp: 1 + pu(i, j)) of the (i, j) each group of sums fills; arithmetic,
+  // not a table in memory (a divergent load on the reduction's critical path)
+  auto pu1 = [](int i, int j) { return 1 + i * 6 - i * (i - 1) / 2 + (j - i); };
+  auto upper = [](int q, int& i, int& j) {  // q-th entry of a 3x3 upper triangle, row-major
+    i = q < 3 ? 0 : q < 5 ? 1 : 2;
+    j = i + q - (i == 0 ? 0 : i == 1 ? 3 : 5);
+  };
+  int i, j;
+  if (e == 0) return 0;
+  if (e <= 6) { upper(e - 1, i, j); return pu1(3 + i, 3 + j); }  // M -> H_tt
+  if (e <= 15) return pu1((e - 7) / 3, 3 + (e - 7) % 3);           // T -> H_theta,t
+  if (e <= 21) { upper(e - 16, i, j); return pu1(i, j); }          // U -> H_theta,theta
+  return e <= 24 ? e + 3 : e - 3;                                   // v -> g_t, p x v -> g_theta
 }
 
 // Sum of a double over the four 16-lane rows of the wave (every lane gets its column's sum):
@@ -2122,7 +2148,7 @@ __device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec,
 // sin|d|/|d| and cos|d| as series in |d|^2 below |d| = 0.5 (library sincos above), and the
 // gradient test's rotation part only when its translation part is not already above 1e-10.
 struct EngLM {
-  double x[7], xc[7], A[21], g[6], scale[6], diag[6];
+  double x[7], xc[7], A[21], g[6], scale[6], iscale[6], diag[6];
   double cost, radius, dfac, mcc;
   int reuse, it, invalid, term;
   int prof;                      // developer profile armed (g_eng_prof): sub-phase ticks into pacc
@@ -2188,25 +2214,29 @@ extern "C" int lislam_debug_step_prof(unsigned long long* out) {
 // Propose the next candidate into s.xc; false = stop (s.term set).  The scaled, regularized matrix
 // is factored in place (21 doubles) and rebuilt from s.A only for another try at a smaller radius.
 __device__ __forceinline__ bool eng_propose(__attribute__((address_space(3))) EngLM& s, int max_it) {
-  double sc[6], b[6];
+  // Ceres solves (S A S + D / radius) y = S g and steps -S y (S the Jacobi scaling, D its clamped
+  // diagonal).  With z = S y that is (A + S^-1 D S^-1 / radius) z = g, step -z, and the model cost
+  // change 0.5 (y.Sg + y.(D / radius) y) = 0.5 (z.g + z.(D' / radius) z), D' = S^-1 D S^-1: the same
+  // system without scaling the matrix (s.diag holds D'; s.scale / s.iscale hold S^2 / S^-2).
+  double b[6];
 #pragma unroll
-  for (int e = 0; e < 6; e++) { sc[e] = s.scale[e]; b[e] = sc[e] * s.g[e]; }
+  for (int e = 0; e < 6; e++) b[e] = s.g[e];
   while (s.it < max_it) {
     s.it++;
     if (!s.reuse)
 #pragma unroll
-      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(sc[e] * sc[e] * s.A[pu(e, e)], 1e-6), 1e32);
+      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(s.scale[e] * s.A[pu(e, e)], 1e-6), 1e32) * s.iscale[e];
     s.reuse = 1;
     const double ir = 1.0 / s.radius;
     double Dr[6];
 #pragma unroll
     for (int e = 0; e < 6; e++) Dr[e] = s.diag[e] * ir;
-    // L (lower factor, L[i][j] at pu(j, i)) overwrites S A S + D / radius; inv = 1 / L[j][j]
+    // L (lower factor, L[i][j] at pu(j, i)) overwrites A + D' / radius; inv = 1 / L[j][j]
     double L[21], inv[6];
 #pragma unroll
     for (int j = 0; j < 6; j++)
 #pragma unroll
-      for (int i = j; i < 6; i++) L[pu(j, i)] = sc[j] * s.A[pu(j, i)] * sc[i];
+      for (int i = j; i < 6; i++) L[pu(j, i)] = s.A[pu(j, i)];
     bool ok = true;
     const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -2253,7 +2283,7 @@ __device__ __forceinline__ bool eng_propose(__attribute__((address_space(3))) En
     s.invalid = 0;
     double delta[6], x[7], xc[7];
 #pragma unroll
-    for (int k = 0; k < 6; k++) delta[k] = -y[k] * sc[k];
+    for (int k = 0; k < 6; k++) delta[k] = -y[k];
 #pragma unroll
     for (int k = 0; k < 7; k++) x[k] = s.x[k];
     eng_quat_plus(x, delta, xc);
@@ -2288,7 +2318,12 @@ __device__ LISLAM_STEP_ATTR bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool fi
     s.cost = acc[0];
     for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
     for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
-    for (int e = 0; e < 6; e++) s.scale[e] = 1.0 / (1.0 + sqrt(acc[1 + pu(e, e)]));  // jacobi scaling
+    for (int e = 0; e < 6; e++) {  // jacobi scaling S = 1 / (1 + sqrt(A_ee)), kept as S^2 and 1 / S^2
+      const double r = 1.0 + sqrt(acc[1 + pu(e, e)]);
+      const double sc = 1.0 / r;
+      s.scale[e] = sc * sc;
+      s.iscale[e] = r * r;
+    }
     s.radius = 1e4; s.dfac = 2.0; s.reuse = 0; s.mcc = 0;
     s.it = 0; s.invalid = 0; s.term = 0;
     if (!isfinite(s.cost)) { s.term = 2; cont = false; }
@@ -2568,8 +2603,13 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     if (ok && live && is_item) {  // each wave parks its first query's loads in its LDS slots
       const ItemPre pre = eng_item_pre(a, k, item * kEngQ + (int)(threadIdx.x >> 6), warm, o);
       const int wv = (int)(threadIdx.x >> 6), l = lane_id();
-      if (l < 4) sh.prew[wv][l] = l == 0 ? pre.qp : pre.wp[l == 1 ? 0 : l == 2 ? 1 : 2];
-      if (l < 3) sh.prei[wv][l] = pre.wi[l == 0 ? 0 : l == 1 ? 1 : 2];
+      P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
+      int wi = pre.wi[0];
+      if (l == 1) { v = pre.wp[0]; wi = pre.wi[1]; }
+      if (l == 2) { v = pre.wp[1]; wi = pre.wi[2]; }
+      if (l == 3) v = pre.wp[2];
+      if (l < 4) sh.prew[wv][l] = v;
+      if (l < 3) sh.prei[wv][l] = wi;
     }
     if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
     if (wave0) {
