@@ -243,7 +243,9 @@ int lislam_eval_factors(lislam_ctx* ctx, int32_t n, const int32_t* kind, const d
  * 208,228-234,252,282-288).  kind[i]: 0 LidarEdgeFactor (pts: curr, a, b), 1 LidarPlaneFactor
  * (curr, j, l, m), 2 LidarPlaneNormFactor (curr, n, d), 3 front_end_residual /
  * FeatureMatchingResidual (curr / src, dst; :21-99), 4 LidarGroundPlaneNormFactor (curr, n, d;
- * q block only, jac_t rows zero; :101-141).  Residual rows past the block's size are zero.  All
+ * q block only, jac_t rows zero; :101-141), 5 LidarEdgeFactor with s != 1 (curr, a, b, s) and
+ * 6 LidarPlaneFactor with s != 1 (curr, j, unit normal, s): DISTORTION 1, Identity.slerp(s, q)
+ * and s t (:155-162,255-262).  Residual rows past the block's size are zero.  All
  * pointers may be host or device memory; outputs are optional.  include/lislam_factors.h wraps
  * this behind the reference's functor structs and their Create(). */
 int lislam_eval_factors_raw(lislam_ctx* ctx, int32_t n, const int32_t* kind, const double* pts, const double* q,

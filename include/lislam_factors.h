@@ -27,7 +27,10 @@
  * Create() takes no context (the reference signature has none): the blocks evaluate on the
  * context given to lislam::SetFactorContext().  The reference passes s = 1 at every call site
  * (DISTORTION 0, laserOdometry.cpp:82,556,679; laserMapping.cpp:718): the device path evaluates
- * identity.slerp(1, q) (= +-q, the same rotation); Create() with s != 1 returns nullptr.
+ * identity.slerp(1, q) (= +-q, the same rotation) with analytic Jacobians.  With DISTORTION 1
+ * (s = the point's relative time in the sweep) LidarEdgeFactor / LidarPlaneFactor interpolate the
+ * pose, Identity.slerp(s, q) and s t: Create() then makes a kind 5 / 6 block that the device
+ * differentiates with a forward-mode dual number, as ceres::AutoDiffCostFunction does.
  *
  * Host-side C++ only (any C++11 compiler); link liblislam.so.  With Ceres available, define
  * LISLAM_WITH_CERES before including this header and lislam::CostFunction derives from
@@ -399,10 +402,16 @@ struct LidarPlaneFactor {  // lidarFeaturePointsFunction.hpp:143-196
   static lislam::CostFunction* Create(const lislam::Vector3d curr_point_, const lislam::Vector3d last_point_j_,
                                       const lislam::Vector3d last_point_l_, const lislam::Vector3d last_point_m_,
                                       const double s_) {
-    if (s_ != 1.0) return nullptr;  // DISTORTION 0 only (see the header comment)
     double rec[12];
     lislam::detail::put3(rec, curr_point_);
     lislam::detail::put3(rec + 3, last_point_j_);
+    if (s_ != 1.0) {  // DISTORTION 1: (curr, j, the constructor's unit normal, s), kind 6
+      const LidarPlaneFactor f(curr_point_, last_point_j_, last_point_l_, last_point_m_, s_);
+      lislam::detail::put3(rec + 6, f.ljm_norm);
+      rec[9] = s_;
+      rec[10] = rec[11] = 0.0;
+      return new lislam::DeviceCostFunction(6, 1, rec);
+    }
     lislam::detail::put3(rec + 6, last_point_l_);
     lislam::detail::put3(rec + 9, last_point_m_);
     return new lislam::DeviceCostFunction(1, 1, rec);
@@ -471,11 +480,14 @@ struct LidarEdgeFactor {  // lidarFeaturePointsFunction.hpp:243-293
 
   static lislam::CostFunction* Create(const lislam::Vector3d curr_point_, const lislam::Vector3d last_point_a_,
                                       const lislam::Vector3d last_point_b_, const double s_) {
-    if (s_ != 1.0) return nullptr;  // DISTORTION 0 only (see the header comment)
     double rec[12] = {0};
     lislam::detail::put3(rec, curr_point_);
     lislam::detail::put3(rec + 3, last_point_a_);
     lislam::detail::put3(rec + 6, last_point_b_);
+    if (s_ != 1.0) {  // DISTORTION 1: (curr, a, b, s), kind 5
+      rec[9] = s_;
+      return new lislam::DeviceCostFunction(5, 3, rec);
+    }
     return new lislam::DeviceCostFunction(0, 3, rec);
   }
 

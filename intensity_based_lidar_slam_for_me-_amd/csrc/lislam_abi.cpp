@@ -889,7 +889,7 @@ int lislam_eval_factors_raw(lislam_ctx* c, int32_t n, const int32_t* kind, const
                             const double* t, double* residuals, double* jac_q, double* jac_t) {
   if (!c || n < 0 || (n > 0 && (!kind || !pts)) || !q || !t) return LISLAM_ERR_ARG;
   for (int32_t i = 0; i < n; i++)
-    if (kind[i] < 0 || kind[i] > 4) return fail(c, LISLAM_ERR_ARG, "lislam_eval_factors_raw: block %d has kind %d", i, kind[i]);
+    if (kind[i] < 0 || kind[i] > 6) return fail(c, LISLAM_ERR_ARG, "lislam_eval_factors_raw: block %d has kind %d", i, kind[i]);
   if (n == 0) return LISLAM_OK;
   hipSetDevice(c->device);
   std::lock_guard<std::mutex> lock(c->factor_mu);

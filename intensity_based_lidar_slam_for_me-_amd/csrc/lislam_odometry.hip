@@ -1501,6 +1501,21 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
   const double* p = a.pts + (size_t)i * 12;
   const D3 c{p[0], p[1], p[2]};
   const int kd = a.kind[i];
+  if (kd == 5 || kd == 6) {  // DISTORTION 1: the slerp-interpolated functors, by dual numbers
+    const double qa[4] = {q.x, q.y, q.z, q.w}, ta[3] = {t.x, t.y, t.z};
+    DJet rj[3];
+    const int R = kd == 5 ? 3 : 1;
+    if (kd == 5) edge_factor_s(qa, ta, p, rj);
+    else plane_factor_s(qa, ta, p, rj);
+    for (int k = 0; k < 3; k++) {
+      if (a.res) a.res[(size_t)i * 3 + k] = k < R ? rj[k].a : 0.0;
+      if (a.jq)
+        for (int cc = 0; cc < 4; cc++) a.jq[((size_t)i * 3 + k) * 4 + cc] = k < R ? rj[k].v[cc] : 0.0;
+      if (a.jt)
+        for (int cc = 0; cc < 3; cc++) a.jt[((size_t)i * 3 + k) * 3 + cc] = k < R ? rj[k].v[4 + cc] : 0.0;
+    }
+    return;
+  }
   double r[3] = {0, 0, 0}, G[3][3] = {{0}};  // G = dr/dlp (rows = residuals)
   int R = 1;
   if (kd == 0) {

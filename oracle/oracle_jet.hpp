@@ -50,6 +50,20 @@ template <int N> inline Jet<N> sqrt(const Jet<N>& f) {
   Jet<N> r; r.a = t; for (int k = 0; k < N; k++) r.v[k] = f.v[k] / two_t; return r;
 }
 template <int N> inline bool operator<(const Jet<N>& f, double c) { return f.a < c; }
+template <int N> inline bool operator>=(const Jet<N>& f, const Jet<N>& g) { return f.a >= g.a; }
+// ceres jet.h: abs(f) = f < 0 ? -f : f; acos(f) = [acos a, -1 / sqrt(1 - a^2) v]; sin(f) = [sin a, cos a v]
+template <int N> inline Jet<N> abs(const Jet<N>& f) { return f.a < 0 ? -f : f; }
+template <int N> inline Jet<N> acos(const Jet<N>& f) {
+  const double tmp = -1.0 / std::sqrt(1.0 - f.a * f.a);
+  Jet<N> r; r.a = std::acos(f.a); for (int k = 0; k < N; k++) r.v[k] = tmp * f.v[k]; return r;
+}
+template <int N> inline Jet<N> sin(const Jet<N>& f) {
+  const double c = std::cos(f.a);
+  Jet<N> r; r.a = std::sin(f.a); for (int k = 0; k < N; k++) r.v[k] = c * f.v[k]; return r;
+}
+inline double abs(double x) { return std::fabs(x); }
+inline double acos(double x) { return std::acos(x); }
+inline double sin(double x) { return std::sin(x); }
 
 inline double sqrt(double x) { return std::sqrt(x); }
 inline bool lt0(double x) { return x < 0; }
@@ -89,6 +103,27 @@ template <typename T> inline V3<T> rotate(const Q4<T>& q, const V3<T>& v) {
 template <typename T> inline Q4<T> slerp_identity_s1(const Q4<T>& q) {
   if (lt0(q.w)) return Q4<T>{-q.x, -q.y, -q.z, -q.w};
   return q;
+}
+
+// Identity.slerp(s, q) for any s (DISTORTION 1: laserOdometry.cpp:82 with s = the point's relative
+// time): Eigen 3.3's QuaternionBase::slerp, this = (0, 0, 0, 1), so this . q = w and the result is
+// scale0 (0, 0, 0, 1) + scale1 q.
+template <typename T> inline Q4<T> slerp_identity(double s, const Q4<T>& q) {
+  const T one = T(1.0 - 2.220446049250313e-16);
+  const T d = q.w;
+  const T absD = abs(d);
+  T scale0, scale1;
+  if (absD >= one) {
+    scale0 = T(1.0 - s);
+    scale1 = T(s);
+  } else {
+    const T theta = acos(absD);
+    const T sinTheta = sin(theta);
+    scale0 = sin(T(1.0 - s) * theta) / sinTheta;
+    scale1 = sin(T(s) * theta) / sinTheta;
+  }
+  if (lt0(d)) scale1 = -scale1;
+  return Q4<T>{scale1 * q.x, scale1 * q.y, scale1 * q.z, scale0 + scale1 * q.w};
 }
 
 // Quaternion product a*b in the term grouping of Eigen 3.3's SSE2 quat_product<double>.

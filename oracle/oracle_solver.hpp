@@ -26,7 +26,8 @@ struct EdgeFactor {  // LidarEdgeFactor, lidarFeaturePointsFunction.hpp:243-293
     V3<T> c{T(cp[0]), T(cp[1]), T(cp[2])};
     V3<T> a{T(pa[0]), T(pa[1]), T(pa[2])};
     V3<T> b{T(pb[0]), T(pb[1]), T(pb[2])};
-    Q4<T> qq = slerp_identity_s1(Q4<T>{q[0], q[1], q[2], q[3]});
+    const Q4<T> q0{q[0], q[1], q[2], q[3]};
+    Q4<T> qq = s == 1.0 ? slerp_identity_s1(q0) : slerp_identity(s, q0);
     V3<T> tt{T(s) * t[0], T(s) * t[1], T(s) * t[2]};
     V3<T> lp = rotate(qq, c) + tt;
     V3<T> nu = cross(lp - a, lp - b);
@@ -56,7 +57,8 @@ struct PlaneFactor {  // LidarPlaneFactor, lidarFeaturePointsFunction.hpp:143-19
     V3<T> c{T(cp[0]), T(cp[1]), T(cp[2])};
     V3<T> j{T(pj[0]), T(pj[1]), T(pj[2])};
     V3<T> nn{T(n[0]), T(n[1]), T(n[2])};
-    Q4<T> qq = slerp_identity_s1(Q4<T>{q[0], q[1], q[2], q[3]});
+    const Q4<T> q0{q[0], q[1], q[2], q[3]};
+    Q4<T> qq = s == 1.0 ? slerp_identity_s1(q0) : slerp_identity(s, q0);
     V3<T> tt{T(s) * t[0], T(s) * t[1], T(s) * t[2]};
     V3<T> lp = rotate(qq, c) + tt;
     residual[0] = dot(lp - j, nn);

@@ -204,10 +204,59 @@ int main() {
     }
     std::printf("batched: 2304 blocks, %d parameter points, 1 launch each\n", points);
   }
-  // s != 1 is refused (DISTORTION 0 only)
-  if (LidarEdgeFactor::Create(v3(), v3(), v3(), 0.5) != nullptr) {
-    std::fprintf(stderr, "Create with s != 1 should return nullptr\n");
-    return 6;
+  // DISTORTION 1 (s != 1: Identity.slerp(s, q), s t; lidarFeaturePointsFunction.hpp:155-162,255-262):
+  // kind 5 / 6 blocks, differentiated on the device with dual numbers, against the oracle's Jet
+  // autodiff of the same functors and the header's operator()<double>; a quaternion near the
+  // identity too (|w| >= 1 - eps: Eigen's linear branch) and one with w < 0.
+  {
+    const double qs[3][4] = {{q[0], q[1], q[2], q[3]}, {0.0, 0.0, 1e-9, 1.0}, {-q[0], -q[1], -q[2], -q[3]}};
+    const double ss[3] = {0.0, 0.37, 0.85};
+    int idx = 0;
+    for (int iq = 0; iq < 3; iq++) {
+      for (int is = 0; is < 3; is++) {
+        for (int i = 0; i < 8; i++, idx++) {
+          const bool edge = i & 1;
+          lislam::Vector3d c = v3(), a = v3(), b = v3(), m = v3();
+          const double s = ss[is];
+          std::unique_ptr<lislam::CostFunction> f(edge ? LidarEdgeFactor::Create(c, a, b, s)
+                                                       : LidarPlaneFactor::Create(c, a, b, m, s));
+          if (!f) {
+            std::fprintf(stderr, "Create with s = %g failed\n", s);
+            return 6;
+          }
+          double res[3], jq[12], jt[9], host_r[3] = {0, 0, 0}, orr[3] = {0, 0, 0}, oJ[21] = {0};
+          const double* params[2] = {qs[iq], t};
+          double* jacs[2] = {jq, jt};
+          if (!f->Evaluate(params, res, jacs)) {
+            std::fprintf(stderr, "Evaluate (s = %g) failed: %s\n", s, lislam_last_error(ctx));
+            return 6;
+          }
+          const int R = edge ? 3 : 1;
+          if (edge) {
+            LidarEdgeFactor(c, a, b, s)(qs[iq], t, host_r);
+            oracle::EdgeFactor F{{c.x(), c.y(), c.z()}, {a.x(), a.y(), a.z()}, {b.x(), b.y(), b.z()}, s};
+            oracle::autodiff_eval(F, qs[iq], t, orr, oJ);
+          } else {
+            LidarPlaneFactor(c, a, b, m, s)(qs[iq], t, host_r);
+            const double cv[3] = {c.x(), c.y(), c.z()}, jv[3] = {a.x(), a.y(), a.z()}, lv[3] = {b.x(), b.y(), b.z()},
+                         mv[3] = {m.x(), m.y(), m.z()};
+            oracle::PlaneFactor F(cv, jv, lv, mv, s);
+            oracle::autodiff_eval(F, qs[iq], t, orr, oJ);
+          }
+          for (int k = 0; k < R; k++) {
+            check(close(res[k], orr[k], 1e-12, 1e-12), "distortion residual vs oracle", idx, res[k], orr[k]);
+            check(close(res[k], host_r[k], 1e-12, 1e-12), "distortion residual vs header operator()", idx, res[k], host_r[k]);
+            for (int cc = 0; cc < 4; cc++)
+              check(close(jq[k * 4 + cc], oJ[k * 7 + cc], 1e-9, 1e-10), "distortion d r / d q vs oracle autodiff", idx,
+                    jq[k * 4 + cc], oJ[k * 7 + cc]);
+            for (int cc = 0; cc < 3; cc++)
+              check(close(jt[k * 3 + cc], oJ[k * 7 + 4 + cc], 1e-9, 1e-10), "distortion d r / d t vs oracle autodiff",
+                    idx, jt[k * 3 + cc], oJ[k * 7 + 4 + cc]);
+          }
+        }
+      }
+    }
+    std::printf("distortion blocks ok (%d)\n", idx);
   }
   lislam_ctx_destroy(ctx);
   if (g_fail) {
