@@ -470,13 +470,15 @@ __device__ __forceinline__ int nn_wave(const P4* sorted, int n, const float4* ch
   int spec = -1;           // this lane group's speculative super-chunk
   bool spec_lane = false;  // this lane's super-chunk (window 0) was fetched speculatively
   {  // (ranking by bound beat taking u0's Morton neighbours u0 -+1, -+2 in an A/B: 4.15 vs 4.18 ms)
-    dkey v = (lane < nsu && lane != u0) ? dk(lb0, lane) : kIdent;
+    // A heuristic order only (any choice is exact), so 32-bit keys: the bound's bits with the
+    // lane in the low 6 (ties within 64 ulps by lane), one 32-bit wave minimum per pick.
+    uint32_t v = (lane < nsu && lane != u0 && lb0 < 25.f) ? ((__float_as_uint(lb0) & ~63u) | (uint32_t)lane) : 0xffffffffu;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
-      const dkey m = wave_min(v);
-      const int sg = dk_d(m) < 25.f ? dk_key(m) : -1;
+      const uint32_t m = wave_umin(v);
+      const int sg = m != 0xffffffffu ? (int)(m & 63u) : -1;
       if ((lane >> 4) == g) spec = sg;
-      if (sg >= 0 && lane == sg) { v = kIdent; spec_lane = true; }
+      if (sg >= 0 && lane == sg) { v = 0xffffffffu; spec_lane = true; }
     }
   }
   int c[2] = {spec >= 0 ? spec * kChunk + (lane & 15) : -1, -1};
@@ -662,10 +664,11 @@ __device__ __forceinline__ void line_search(LineSearch& s) {
     if (w == 0) {
       // first batch: around the up and the down chunk with the smallest bound among those that
       // can still improve a best (chunks i-1 .. i+2 of each), which sets tight bests at once
-      dkey mu = upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? dk(ulb, lane) : kIdent;
-      dkey md = dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? dk(dlb, lane) : kIdent;
-      wave_min2(mu, md);
-      const int iu = dk_key(mu), id = dk_key(md);
+      // (a heuristic start: 32-bit keys, the bound's bits with the lane in the low 6)
+      uint32_t mu = upend && ls_need<kCorner>(s, true, ulo, uhi, ulb) ? ((__float_as_uint(ulb) & ~63u) | (uint32_t)lane) : 0xffffffffu;
+      uint32_t md = dpend && ls_need<kCorner>(s, false, dlo, dhi, dlb) ? ((__float_as_uint(dlb) & ~63u) | (uint32_t)lane) : 0xffffffffu;
+      wave_umin2(mu, md);
+      const int iu = mu != 0xffffffffu ? (int)(mu & 63u) : kNone, id = md != 0xffffffffu ? (int)(md & 63u) : kNone;
       // lane group g: up chunk iu - 1 + g (slot 0), down chunk id - 1 + g (slot 1)
       const int g = lane >> 4;
       const int lu = (iu != kNone ? iu : 0) - 1 + g, ld = (id != kNone ? id : 0) - 1 + g;
