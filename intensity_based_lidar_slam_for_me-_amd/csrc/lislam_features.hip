@@ -1540,11 +1540,13 @@ struct LineLds {
   };
 };
 
-// Waves per SIMD asked of the 1024-point lines (kS = 16): 5 caps them at 96 VGPRs (44 B of
-// scratch per lane) for one more resident wave than the 113-VGPR build: 2.02 -> 1.96 ms per 300
-// scans isolated (profiles/r02v_experiments.txt).  Other line lengths keep the default.
+// Waves per SIMD asked of the 1024-point lines (kS = 16): 4 (113 VGPRs, no scratch).  5 caps
+// them at 96 VGPRs with 44 B of scratch per lane for one more resident wave: 2.02 -> 1.96 ms per
+// 300 scans isolated in round 2 (profiles/r02v_experiments.txt), within noise on the round-3 tree
+// (2.11 / 2.20 vs 2.17 / 2.18 ms, bench 8.59k / 8.56k vs 8.55k / 8.56k scans/s,
+// profiles/r03s_lines_wpe_ab.txt), so the spill-free build.  Other line lengths keep the default.
 #ifndef LISLAM_LINES_WPE
-#define LISLAM_LINES_WPE 5
+#define LISLAM_LINES_WPE 4
 #endif
 
 template <int kS>
