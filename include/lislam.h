@@ -161,9 +161,10 @@ int lislam_batch_set_timing(lislam_batch* b, int32_t enable);
                                 k_odom_chain (the persistent engine of few long chains: association
                                 and solve of every round in one launch) */
 /* Synchronize, then return, over the calls recorded since the previous read, the average ms
- * per call spent in each kernel (ms_per_call[6]) and the launches per call of each kernel
- * (launches_per_call[6], may be null); calls[2] (may be null) = extract / odometry calls
- * averaged.  Clears the record. */
+ * per call spent in each kernel (ms_per_call[LISLAM_NUM_KERNELS]) and the launches per call of
+ * each kernel (launches_per_call[LISLAM_NUM_KERNELS], may be null); calls[2] (may be null) =
+ * extract / odometry calls averaged.  Clears the record.  (LISLAM_NUM_KERNELS was 6 before the
+ * chain engine: size the arrays from the macro.) */
 int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls);
 
 #define LISLAM_OUT_IMAGE_RANGE 0     /* uint8  [H*W] */
@@ -212,8 +213,11 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
 #define LISLAM_ENGINE_AUTO 1
 #define LISLAM_ENGINE_ON 2
 int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
-/* Synchronize; status = 1 if the last engine launch of the batch gave up (one of its bounded
- * device waits expired: its outputs are invalid), else 0. */
+/* Synchronize; status = 1 if an engine launch of the batch gave up since the previous status call
+ * (one of its bounded device waits expired: the outputs of that launch are invalid), else 0.  The
+ * word is sticky: later launches do not clear it, and until this call reads (and clears) it,
+ * lislam_batch_download of LISLAM_OUT_PARA / POSE / STATS (and lislam_odom_step) return
+ * LISLAM_ERR_DEVICE. */
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
 
 /* Order of equal sort keys in the two std::sort calls of the feature extraction:

@@ -75,6 +75,12 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
     return LISLAM_ERR_DEVICE;
   }
   c->stream = c->own_stream;
+  // LISLAM_ENGINE (0 off, 1 auto, 2 on) seeds the odometry schedule; lislam_set_odometry_schedule
+  // changes it per context
+  if (const char* e = getenv("LISLAM_ENGINE")) {
+    const int m = atoi(e);
+    if (m >= LISLAM_ENGINE_OFF && m <= LISLAM_ENGINE_ON) c->odom_engine = m;
+  }
   *out = c;
   return LISLAM_OK;
 }
@@ -197,10 +203,15 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
   rc |= dalloc(b, &o.eng_ctl, (size_t)8 + 6 * (size_t)S);
   rc |= dalloc(b, &o.warm, (size_t)S * (b->cap_sharp + b->cap_flat) * 4);
-  rc |= dalloc(b, &o.eng_part, (size_t)S * ((b->cap_sharp + b->cap_flat) / 8 + 2) * 32);  // >= the engine's items
+  rc |= dalloc(b, &o.eng_part, (size_t)S * lislam::engine_items(b->cap_sharp + b->cap_flat) * 32);  // [chains][items][32]
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
   rc |= dalloc(b, &b->d_gate, (size_t)S);
   if (rc != LISLAM_OK) {
+    lislam_batch_destroy(b);
+    return LISLAM_ERR_DEVICE;
+  }
+  // the engine's control words (its sticky abort word is never cleared by a launch)
+  if (hipMemset(o.eng_ctl, 0, sizeof(unsigned) * ((size_t)8 + 6 * (size_t)S)) != hipSuccess) {
     lislam_batch_destroy(b);
     return LISLAM_ERR_DEVICE;
   }
@@ -443,7 +454,6 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   o.chain_len = chain_len;
   o.n_chains = n_scans > 1 ? (n_scans - 1 + chain_len - 1) / chain_len : 0;
   o.init_state = nullptr;
-  o.dbg = getenv("LISLAM_ASSOC_DEBUG") ? atoi(getenv("LISLAM_ASSOC_DEBUG")) : 0;
   if (use_aloam || init_host) {
     // the caller's arrays -> pinned staging -> device, so they may be freed on return
     const size_t init_bytes = sizeof(double) * 14 * (size_t)b->max_scans;
@@ -526,9 +536,15 @@ int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  unsigned w[2] = {0, 0};
-  if (b->engine_ran) HIPCHK(c, hipMemcpy(w, b->oa.eng_ctl, sizeof(w), hipMemcpyDeviceToHost));
-  *status = w[1] ? 1 : 0;  // the engine's abort word (a bounded wait expired)
+  // the sticky abort word: set by any engine launch whose bounded device wait expired since the last
+  // status call (or the batch's creation); reading it clears it
+  unsigned w = 0;
+  HIPCHK(c, hipMemcpy(&w, b->oa.eng_ctl + 3, sizeof(w), hipMemcpyDeviceToHost));
+  if (w) {
+    const unsigned z = 0;
+    HIPCHK(c, hipMemcpy(b->oa.eng_ctl + 3, &z, sizeof(z), hipMemcpyHostToDevice));
+  }
+  *status = w ? 1 : 0;
   return LISLAM_OK;
 }
 
@@ -613,9 +629,19 @@ static int output_source(lislam_batch* b, int what, int scan, const void** src_o
                    : (const void*)(f.less_flat + scan * N);
       break;
     }
-    case LISLAM_OUT_PARA: src = o.para + (size_t)scan * 7; cnt = 7; esz = 8; break;
-    case LISLAM_OUT_POSE: src = o.pose + (size_t)scan * 7; cnt = 7; esz = 8; break;
-    case LISLAM_OUT_STATS: src = o.stats + (size_t)scan * 8; cnt = 8; esz = 4; break;
+    case LISLAM_OUT_PARA:
+    case LISLAM_OUT_POSE:
+    case LISLAM_OUT_STATS: {
+      // an engine launch that gave up left these unwritten: refuse them until the status is read
+      unsigned ab = 0;
+      HIPCHK(c, hipMemcpy(&ab, o.eng_ctl + 3, sizeof(ab), hipMemcpyDeviceToHost));
+      if (ab) return fail(c, LISLAM_ERR_DEVICE, "the odometry chain engine aborted (a bounded device wait expired); "
+                                                 "lislam_batch_odometry_status clears it");
+      if (what == LISLAM_OUT_PARA) { src = o.para + (size_t)scan * 7; cnt = 7; esz = 8; }
+      else if (what == LISLAM_OUT_POSE) { src = o.pose + (size_t)scan * 7; cnt = 7; esz = 8; }
+      else { src = o.stats + (size_t)scan * 8; cnt = 8; esz = 4; }
+      break;
+    }
     case LISLAM_OUT_ORB_T:
     case LISLAM_OUT_ORB_STATS:
     case LISLAM_OUT_ORB_KEYPOINTS:

@@ -99,7 +99,6 @@ struct OdomArgs {
   double* para;    // [S][7] q_last_curr (x,y,z,w), t_last_curr after this scan
   double* pose;    // [S][7] q_w_curr, t_w_curr in the chain's frame
   int* stats;      // [S][8] corners/planes for outer 0/1, LM iterations 0/1, terminations 0/1
-  int dbg;         // ablation switch for profiling (0 in production): 1 skip 1-NN, 2 skip line search
   const int* gate;  // [S] use_aloam per scan (laserOdometry.cpp:403-417), or null = every scan
   // chain engine (k_odom_chain): control words (zeroed before every launch) and the per-query
   // association of the first outer pass, the second pass's starting bounds
@@ -146,9 +145,12 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
 // the a.n_chains chains, association and solve, sequenced on the device.  Returns the grid size.
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
-// lislam_set_odometry_schedule (LISLAM_ENGINE_*); AUTO = the environment's LISLAM_ENGINE (0 off,
-// 2 on) if set, else on for at most 4 chains.
+// lislam_set_odometry_schedule (LISLAM_ENGINE_*; a context starts from the environment's
+// LISLAM_ENGINE if set); AUTO = on for at most 4 chains.
 bool use_chain_engine(const OdomArgs& a, int mode);
+// Association items per (pass, chain) of the engine for cap_queries = cap_sharp + cap_flat (the
+// size of OdomArgs::eng_part's per-chain rows).
+int engine_items(int cap_queries);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
 // AutoDiffCostFunction<F, R, 4, 3>::Evaluate of the functors of lidarFeaturePointsFunction.hpp:

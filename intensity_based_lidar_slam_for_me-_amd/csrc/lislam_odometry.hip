@@ -5,19 +5,24 @@
 // para_q/para_t from pair to pair as the initial guess (:130-135) and accumulates the pose
 // (:716-717).  The serial dependency is only along a chain, so every pair of every chain at the
 // same position r ("round") runs together, as two phases per outer pass (:417):
-//   k_odom_assoc  one thread per query of every chain: TransformToStart (:147-172), exact 1-NN
-//                 in the previous less-sharp / less-flat cloud (KdTreeFLANN :452/:574) and the
-//                 scan-line searches (:467-520, :589-646), both pruned by chunk / super-chunk
-//                 AABBs of the target cloud (k_target_index) without changing any result: the
-//                 float lower bound of a box never exceeds the float distance of a point inside
-//                 it (monotone rounding), and boxes are skipped only when that bound is >= the
-//                 current best (ties keep the reference's visit order).
-//   k_odom_lm     one workgroup per chain: ceres::Solve(DENSE_QR, max 4 it) restated as a device
-//                 trust-region Levenberg-Marquardt (Ceres 1.14 defaults); every evaluation is one
-//                 fp64 pass over the residual blocks producing cost, J^T J and J^T r of the
-//                 Huber-corrected LidarEdgeFactor / LidarPlaneFactor, reduced across the
-//                 workgroup; thread 0 runs the 6x6 step logic.
+//   association   per query: TransformToStart (:147-172), exact 1-NN in the previous less-sharp /
+//                 less-flat cloud (KdTreeFLANN :452/:574) and the scan-line searches (:467-520,
+//                 :589-646), both pruned by chunk / super-chunk AABBs of the target cloud
+//                 (k_target_index) without changing any result: the float lower bound of a box
+//                 never exceeds the float distance of a point inside it (monotone rounding), and
+//                 boxes are skipped only when that bound is >= the current best (ties keep the
+//                 reference's visit order).
+//   solve         per chain: ceres::Solve(DENSE_QR, max 4 it) restated as a device trust-region
+//                 Levenberg-Marquardt (Ceres 1.14 defaults); every evaluation is one fp64 pass
+//                 over the residual blocks producing cost, J^T J and J^T r of the Huber-corrected
+//                 LidarEdgeFactor / LidarPlaneFactor, reduced across the workgroup.
+// Two schedules run them: the persistent chain engine (k_odom_chain, few long chains: every pass
+// of every chain in one launch) and per-round launches (k_odom_assoc16 + k_odom_lm2, many short
+// chains).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 #include "lislam_device.hpp"
 #include "lislam_factors.hpp"
@@ -29,8 +34,6 @@ namespace lislam {
 // a value every lane holds alike (LDS broadcasts), as a scalar: branches on it stay uniform
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-constexpr int kLmThreads = 512;
-constexpr int kLmWaves = kLmThreads / 64;
 constexpr double kDistSq = 25.0;   // DISTANCE_SQ_THRESHOLD (laserOdometry.cpp:89)
 constexpr double kNearby = 2.5;    // NEARBY_SCAN (:90)
 
@@ -320,8 +323,6 @@ __device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, cons
 //   line search  (distance, walk rank) with rank = j - closest going up, n + closest - j going
 //                down == the first strict '<' improvement along the reference's walk (:467-520,
 //                :589-646); a chunk is skipped only if its float bound is > the current best.
-constexpr int kAssocWaves = 4;  // queries per 256-thread workgroup
-
 #ifdef LISLAM_PHASE_PROF  // developer statistics of the searches (scripts/phase_prof.py)
 __device__ unsigned long long g_assoc_stats[16];
 #ifdef LISLAM_ASSOC_COUNT  // search statistics (global atomics: they distort the timing)
@@ -329,13 +330,6 @@ __device__ unsigned long long g_assoc_stats[16];
 #else
 #define ASTAT(i)
 #endif
-// per-wave (start, end, kind, target size) of one association launch (round g_wave_round)
-__device__ unsigned long long* g_wave_log;
-__device__ int g_wave_round;
-extern "C" int lislam_debug_wave_log(unsigned long long* dev_buf, int round) {
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_log), &dev_buf, sizeof(dev_buf)) != hipSuccess) return -2;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_round), &round, sizeof(round)) == hipSuccess ? 0 : -2;
-}
 extern "C" int lislam_debug_assoc_stats(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_assoc_stats), sizeof(g_assoc_stats)) != hipSuccess) return -2;
   static const unsigned long long zero[16] = {0};
@@ -720,101 +714,9 @@ __device__ __forceinline__ bool pair_of(const OdomArgs& a, int c, int r, int* k)
   return *k <= k1;
 }
 
-// Grid: qblocks = ceil((cap_sharp + cap_flat) / 4) workgroups of 4 waves per chain of the group.  Wave w of
-// pair k takes corner query w (w < n_sharp) or surf query w - n_sharp, in Morton order.  With
-// 8 or more chains, workgroup b serves chain 8 * ((b / 8) / qblocks) + b % 8: workgroups are
-// dealt round-robin over the 8 XCDs, so each XCD's L2 holds the target clouds of only its own
-// chains (placement is a speed matter only).
-template <int kW>
-__global__ __launch_bounds__(64 * kW) void k_odom_assoc(OdomArgs a, int r, int qblocks) {
-  int c, qb;
-  if (a.cn >= 8) {
-    const int b = blockIdx.x, x = b & 7, rr = b >> 3;
-    c = 8 * (rr / qblocks) + x;
-    qb = rr % qblocks;
-  } else {
-    c = blockIdx.x / qblocks;
-    qb = blockIdx.x % qblocks;
-  }
-  if (c >= a.cn) return;
-  c += a.c0;
-  int k;
-  if (!pair_of(a, c, r, &k)) return;
-  if (a.gate && !a.gate[k]) return;  // not optimized: no association (laserOdometry.cpp:417)
-  const int lane = lane_id();
-  const int w = qb * kW + (int)(threadIdx.x >> 6);
-  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  if (w >= ns + nf) return;  // whole waves leave; nothing below synchronizes the workgroup
-#ifdef LISLAM_PHASE_PROF
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-  const bool corner = w < ns;
-  const int t = corner ? w : w - ns;
-  const P4 qp = ld4(corner ? reinterpret_cast<const P4*>(a.qpts_sharp) + (size_t)k * a.cap_sharp + t
-                           : reinterpret_cast<const P4*>(a.qpts_flat) + (size_t)k * a.cap_flat + t);
-  const int q = __float_as_int(qp.i);
-  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
-  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
-  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
-  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
-  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
-  double x[7];
-  const double* st = a.state + (size_t)c * 16;
-  for (int e = 0; e < 7; e++) x[e] = st[e];
-  const P4 cur{qp.x, qp.y, qp.z, 0.f};  // the query point (its intensity is not read)
-  const P4 sel = transform_to_start(cur, x);
-#ifdef LISLAM_PHASE_PROF  // ablations for timing only (LISLAM_ASSOC_DEBUG): 1 skip the 1-NN, 2 skip the line searches
-  int closest = (a.dbg & 1) ? (nL > 0 ? (int)((unsigned)q * 2654435761u % (unsigned)nL) : -1)
-                            : nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel);
-  if (a.dbg & 2) closest = -1;
-#else
-  const int closest = nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel);
-#endif
-  const int slot = corner ? q : a.cap_sharp + q;
-  double* rec = a.blk + ((size_t)c * (a.cap_sharp + a.cap_flat) + slot) * 9;
-  bool found = false;
-  double v = 0.0;  // this lane's record entry (lanes 0..8)
-  ASTAT(corner ? 8 : 9);
-  if (closest >= 0) {
-    ASTAT(corner ? 10 : 11);
-    const P4 pa = ld4(L + closest);
-    LineSearch s{L, ix.chunk + mo, nL, (nL + kChunk - 1) / kChunk, closest, int(pa.i), sel, dk(25.f, kNone), dk(25.f, kNone)};
-    if (corner) {  // LidarEdgeFactor(curr, a, b)
-      line_search<true>(s);
-      if (dk_key(s.b2) != kNone) {
-        const P4 pb = ld4(L + rank_to_index(s, dk_key(s.b2)));
-        const float e9[9] = {cur.x, cur.y, cur.z, pa.x, pa.y, pa.z, pb.x, pb.y, pb.z};
-        for (int e = 0; e < 9; e++) if (lane == e) v = e9[e];
-        found = true;
-      }
-    } else {        // LidarPlaneFactor(curr, j, l, m)
-      line_search<false>(s);
-      if (dk_key(s.b2) != kNone && dk_key(s.b3) != kNone) {
-        const P4 pl = ld4(L + rank_to_index(s, dk_key(s.b2))), pm = ld4(L + rank_to_index(s, dk_key(s.b3)));
-        const D3 j{pa.x, pa.y, pa.z};
-        const D3 nrm = plane_normal(j, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
-        const double e9[9] = {cur.x, cur.y, cur.z, j.x, j.y, j.z, nrm.x, nrm.y, nrm.z};
-        for (int e = 0; e < 9; e++) if (lane == e) v = e9[e];
-        found = true;
-      }
-    }
-  }
-  if (found && lane < 9) rec[lane] = v;
-  // the LM kernel counts corner_correspondence / plane_correspondence (:562/:685) from the kinds
-  if (lane == 0) a.blk_kind[(size_t)c * (a.cap_sharp + a.cap_flat) + slot] = found ? (corner ? 0 : 1) : -1;
-#ifdef LISLAM_PHASE_PROF
-  if (g_wave_log && r == g_wave_round && lane == 0) {
-    unsigned long long* o = g_wave_log + ((size_t)blockIdx.x * kW + (threadIdx.x >> 6)) * 4;
-    o[0] = t_start;
-    o[1] = __builtin_amdgcn_s_memrealtime();
-    o[2] = (unsigned long long)(corner ? 1 : 2) | ((unsigned long long)c << 8) | ((unsigned long long)q << 32);
-    o[3] = (unsigned long long)nL;
-  }
-#endif
-}
-
 // ------------------------------------------------------------------ 16-lane association
-// The same exact searches as k_odom_assoc with one query per 16-lane row, four queries per wave:
+// The same exact searches as the engine's (nn_wave / line_search) with one query per 16-lane row,
+// four queries per wave:
 // a round trip looks at one 16-point chunk per query (lane r = lane & 15 takes point r of it),
 // and the lexicographic minima are row reductions by DPP inside the row.  The four rows advance
 // in lockstep; a row with nothing left to do contributes the identity, so every lane is active at
@@ -1067,67 +969,6 @@ __global__ __launch_bounds__(64 * kW) void k_odom_assoc16(OdomArgs a, int r, int
 }
 
 // ------------------------------------------------------------------ phase 2: LM solve
-struct LmShared {
-  double red[kLmWaves * 4][kAcc];  // one partial sum per 16-lane row
-  double x[7];
-  double acc[kAcc];
-  int cnt[kLmWaves][2];
-  int nc, np;
-  int flag;
-};
-
-// corner_correspondence / plane_correspondence (:562/:685) of the current association
-__device__ __forceinline__ void count_kinds(LmShared& sh, const int* kind, int ns, int cap_sharp, int nf) {
-  int c0 = 0, c1 = 0;
-  for (int i = threadIdx.x; i < ns + nf; i += kLmThreads) {
-    const int kd = kind[i < ns ? i : cap_sharp + (i - ns)];
-    c0 += kd == 0;
-    c1 += kd == 1;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    c0 += __shfl_xor(c0, o);
-    c1 += __shfl_xor(c1, o);
-  }
-  if ((threadIdx.x & 63) == 0) { sh.cnt[threadIdx.x >> 6][0] = c0; sh.cnt[threadIdx.x >> 6][1] = c1; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int a0 = 0, a1 = 0;
-    for (int w = 0; w < kLmWaves; w++) { a0 += sh.cnt[w][0]; a1 += sh.cnt[w][1]; }
-    sh.nc = a0;
-    sh.np = a1;
-  }
-  __syncthreads();
-}
-
-// One evaluation at sh.x: cost, J^T J (upper, row-major), J^T r -> sh.acc
-__device__ __forceinline__ void evaluate(LmShared& sh, const double* blk, const int* kind, int ns, int cap_sharp, int nf) {
-  double acc[kAcc];
-#pragma unroll
-  for (int e = 0; e < kAcc; e++) acc[e] = 0;
-  const DQ q{sh.x[0], sh.x[1], sh.x[2], sh.x[3]};
-  const D3 t{sh.x[4], sh.x[5], sh.x[6]};
-  const int total = ns + nf;
-  for (int i = threadIdx.x; i < total; i += kLmThreads) {
-    const int idx = i < ns ? i : cap_sharp + (i - ns);
-    const int kd = kind[idx];
-    if (kd < 0) continue;
-    block_accum(kd, blk + (size_t)idx * 9, q, t, acc);
-  }
-  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
-#pragma unroll
-  for (int e = 0; e < kAcc; e++) {
-    const double v = row_sum(acc[e]);
-    if ((lane & 15) == 0) sh.red[row][e] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < kAcc) {
-    double v = 0;
-    for (int w = 0; w < kLmWaves * 4; w++) v += sh.red[w][threadIdx.x];
-    sh.acc[threadIdx.x] = v;
-  }
-  __syncthreads();
-}
-
 #ifdef LISLAM_PHASE_PROF
 __device__ unsigned long long g_lm_phase[8];
 extern "C" int lislam_debug_lm_phases(unsigned long long* out) {
@@ -1146,82 +987,8 @@ extern "C" int lislam_debug_lm_phases(unsigned long long* out) {
 #else
 #define LM_PHASE(i)
 #endif
-__global__ __launch_bounds__(kLmThreads) void k_odom_lm(OdomArgs a, int r, int outer) {
-  __shared__ LmShared sh;
-#ifdef LISLAM_PHASE_PROF
-  unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
-#endif
-  const int c = a.c0 + blockIdx.x;
-  int k;
-  if (!pair_of(a, c, r, &k)) return;
-  double* st = a.state + (size_t)c * 16;
-  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  const double* blk = a.blk + (size_t)c * (a.cap_sharp + a.cap_flat) * 9;
-  const int* kind = a.blk_kind + (size_t)c * (a.cap_sharp + a.cap_flat);
-  const bool gated_off = a.gate && !a.gate[k];  // use_aloam false: no solve, the pose still accumulates
-  if (gated_off) {
-    if (threadIdx.x == 0) sh.nc = sh.np = 0;
-    __syncthreads();
-  } else {
-    count_kinds(sh, kind, ns, a.cap_sharp, nf);
-  }
-  const int nc = sh.nc, np = sh.np;
-  // The solver state lives in LDS and is in registers only inside thread 0's step, so it does not
-  // stack on the evaluation's registers (which spilled to scratch when it was held across).
-  __shared__ LM lm;
-  bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
-  if (go) {
-    if (threadIdx.x == 0)
-      for (int e = 0; e < 7; e++) sh.x[e] = st[e];
-    __syncthreads();
-    evaluate(sh, blk, kind, ns, a.cap_sharp, nf);
-    if (threadIdx.x == 0) {
-      const bool cont = lm_start(lm, sh.x, sh.acc, a.max_iterations);
-      sh.flag = cont;
-      if (cont)
-        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
-    }
-    __syncthreads();
-    go = uni(sh.flag);
-  }
-  LM_PHASE(0);
-  while (go) {
-    evaluate(sh, blk, kind, ns, a.cap_sharp, nf);  // cost + J^T J + J^T r at the candidate
-    LM_PHASE(1);
-    if (threadIdx.x == 0) {
-      const bool cont = lm_next(lm, sh.acc, a.max_iterations);
-      sh.flag = cont;
-      if (cont)
-        for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
-    }
-    __syncthreads();
-    LM_PHASE(2);
-    go = sh.flag;
-  }
-  if (threadIdx.x != 0) return;
-  int* so = a.stats + (size_t)k * 8;
-  so[outer * 2 + 0] = nc;
-  so[outer * 2 + 1] = np;
-  so[4 + outer] = (nc + np) > 0 ? lm.it : 0;
-  so[6 + outer] = (nc + np) > 0 ? lm.term : 1;
-  if ((nc + np) > 0)
-    for (int e = 0; e < 7; e++) st[e] = lm.x[e];
-  if (outer == 1) {
-    // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr
-    DQ qw{st[7], st[8], st[9], st[10]};
-    D3 tw{st[11], st[12], st[13]};
-    tw = tw + qrot(qw, D3{st[4], st[5], st[6]});
-    qw = qmul(qw, DQ{st[0], st[1], st[2], st[3]});
-    st[7] = qw.x; st[8] = qw.y; st[9] = qw.z; st[10] = qw.w; st[11] = tw.x; st[12] = tw.y; st[13] = tw.z;
-    double* op = a.para + (size_t)k * 7;
-    double* ow = a.pose + (size_t)k * 7;
-    for (int e = 0; e < 7; e++) { op[e] = st[e]; ow[e] = st[7 + e]; }
-  }
-}
-
-// ---- the same solve with the chain's residual blocks held in LDS across its evaluations
-// k_odom_lm reads every block record from global memory at every evaluation; here one workgroup
-// of 16 waves per chain reads them once, into LDS, compacted to the bits the records carry: the
+// ---- the per-round solve, the chain's residual blocks held in LDS across its evaluations
+// One workgroup per chain reads the block records once, into LDS, compacted to the bits the records carry: the
 // query point and the first matched point are floats in every record (laserOdometry.cpp:554-556,
 // :677-681 take them from float clouds), the third triple is the edge's second point (float) or
 // the plane's unit normal (double).  Blocks past kLmLds (only when cap_sharp + cap_flat exceeds
@@ -1673,10 +1440,13 @@ __device__ __forceinline__ double uniform_d(double v) {
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// control words: [0] ticket, [1] abort, [2] error, [3] -, [4, 4 + C) lm_gen, then assoc_done[C][2 R]
+// control words: [0] ticket, [1] abort (this launch), [2] error, [3] sticky abort (set with [1], never
+// cleared by a launch: lislam_batch_odometry_status reads and clears it), [4, 4 + C) lm_gen, then
+// assoc_done[C][2 R]
 struct EngCtl {
   unsigned* w;
   int C, R, I;
+  unsigned long long wait_ticks;  // bound of every device wait (s_memrealtime ticks, 100 MHz)
   int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
   int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at once
   __device__ unsigned* ticket() const { return w; }
@@ -1716,16 +1486,18 @@ __device__ __forceinline__ void eng_trace(int slot, unsigned v) {
   if (t && blockIdx.x < g_eng_trace_n) __hip_atomic_store(t + (blockIdx.x * 16 + slot) * 16, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // a 64-B line each
 }
 
-// One lane: wait until *p >= target; false = aborted (2 s bound, or another workgroup's abort).
+// One lane: wait until *p >= target; false = aborted (the bound, 2 s by default, or another
+// workgroup's abort).  An expired bound raises this launch's abort word and the sticky one.
 // Arguments by value: a struct passed by reference would live in scratch, and values loaded from
 // scratch count as divergent, which would put the ticket loop's barriers in divergent control flow.
-__device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w) {
+__device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w, unsigned long long bound) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (ld_rlx(p) >= target) return true;
     if (ld_rlx(abort_w)) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {  // 100 MHz clock
       st_rlx(abort_w, 1u);
+      st_rlx(abort_w + 2, 1u);  // sticky (EngCtl word 3)
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1877,7 +1649,7 @@ __device__ __forceinline__ void eng_rt_x(const double* xs, double (&R)[9], D3& t
 }
 __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) { eng_rt_x(sh.x, R, t); }
 
-// One association item, one query per wave (the 64-lane searches of k_odom_assoc: every round
+// One association item, one query per wave (the 64-lane searches nn_wave / line_search: every round
 // trip looks at 64 candidates): query item * kEngQ + wave of pair k, at the pass's x (each wave's
 // own copy).  Faster than four 16-lane rows per wave when one chain's ~2000 queries are all the
 // GPU runs (latency bound: 16.5 vs 34.9 us per round as separate launches).  The record goes out
@@ -2614,7 +2386,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     // An item of the second outer pass first waits for the first pass's items (its seeds), long
     // done in the common case; then every wave loads what needs no x while the lead waits for x.
     if (wave0) {
-      if (lead) sh.flag0 = (live && is_item && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w()) : true;
+      if (lead) sh.flag0 = (live && is_item && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : true;
     }
     __syncthreads();
     bool ok = uni(sh.flag0) != 0;
@@ -2636,8 +2408,8 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
           // every item after the chain's previous solve; the solve after its pair's live items too
           // (which imply the first wait, except for a pair without queries: ieff == 0)
           if (is_item) eng_prof(tk, 2, rt_now());  // the item's lead starts its wait for x
-          ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w());
-          if (ok && !is_item) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w());
+          ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks);
+          if (ok && !is_item) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks);
           eng_trace(1, ok ? 2u : 99u);
           eng_prof(tk, 1, rt_now());
           if (ok && c == 0 && r == 0 && o == 0 && !is_item && !a.init_state) {  // scan 0 of the batch: first frame
@@ -2694,14 +2466,25 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
   }
 }
 
-extern "C" int lislam_debug_engine_items(int cap_queries) { return (cap_queries + kEngQ - 1) / kEngQ; }
+extern "C" int lislam_debug_engine_items(int cap_queries) { return engine_items(cap_queries); }
+int engine_items(int cap_queries) { return (cap_queries + kEngQ - 1) / kEngQ; }
 
 bool use_chain_engine(const OdomArgs& a, int mode) {
-  static const int env = getenv("LISLAM_ENGINE") ? atoi(getenv("LISLAM_ENGINE")) : 1;
-  if (mode == 1) mode = env;
   if (mode == 0 || a.n_chains < 1 || !a.eng_ctl) return false;
   if (mode == 2) return true;
   return a.n_chains <= 4;  // few long chains (the continuous chain, a rank's shard); many short: rounds
+}
+
+// Workgroups of k_odom_chain resident at once on `dev` (CUs x occupancy), per device.
+static int engine_resident(int dev) {
+  static int cache[64] = {0};
+  if (dev >= 0 && dev < 64 && cache[dev]) return cache[dev];
+  int cus = 0, per_cu = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_odom_chain, kEngThreads, 0);
+  const int r = max(1, cus * max(per_cu, 1));
+  if (dev >= 0 && dev < 64) cache[dev] = r;
+  return r;
 }
 
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
@@ -2710,25 +2493,24 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
-  ctl.I = (a.cap_sharp + a.cap_flat + kEngQ - 1) / kEngQ;
-  const char* pf = getenv("LISLAM_ENGINE_PREFETCH");
-  ctl.prefetch = pf ? atoi(pf) : 1;
+  ctl.I = engine_items(a.cap_sharp + a.cap_flat);
+  ctl.prefetch = 1;
+  // every device wait is bounded (2 s); LISLAM_ENGINE_WAIT_US shortens it (tests: a forced abort)
+  const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
+  ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
   // Items per (pass, chain): the workgroups resident at once, less the chains' solves (the running
   // one and the next, already claimed) and one spare, shared by the chains.  More queries than
   // that are dealt as second queries to the items' waves (eng_item_run).  LISLAM_ENGINE_BUDGET
   // overrides (tests).
-  static int resident = 0;
-  if (!resident) {
-    int dev = 0, cus = 0, per_cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_odom_chain, kEngThreads, 0);
-    resident = max(1, cus * max(per_cu, 1));
-  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const int resident = engine_resident(dev);
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = bud ? max(1, atoi(bud)) : max(1, (resident - 2 * ctl.C - 1) / ctl.C);
+  // zero the control words of this launch, all but word 3 (the sticky abort)
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
-  (void)hipMemsetAsync(a.eng_ctl, 0, words * sizeof(unsigned), st);
+  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
+  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
   // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
   const int cap = cap_env ? atoi(cap_env) : 0;
@@ -2764,15 +2546,7 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
     (void)hipEventRecord(fork, st);
     for (int g = 1; g < G; g++) (void)hipStreamWaitEvent(streams[g], fork, 0);
   }
-  // queries (waves) per association workgroup: LISLAM_ASSOC_WAVES = 1, 2 (default) or 4
-  static const int kw_env = getenv("LISLAM_ASSOC_WAVES") ? atoi(getenv("LISLAM_ASSOC_WAVES")) : 2;
-  const int kw = (kw_env == 1 || kw_env == 2) ? kw_env : 4;
-  const int qblocks = (a0.cap_sharp + a0.cap_flat + kw - 1) / kw;
-  // LISLAM_ASSOC16 = 0 selects the one-query-per-wave kernel; default: four queries per wave
-  static const bool rows16 = !(getenv("LISLAM_ASSOC16") && atoi(getenv("LISLAM_ASSOC16")) == 0);
   const int qblocks16 = (a0.cap_sharp + a0.cap_flat + 8 - 1) / 8;  // 2 waves x 4 rows
-  // LISLAM_LM_V1 = 1 selects the solve that re-reads the block records at every evaluation
-  static const bool lm_v1 = getenv("LISLAM_LM_V1") && atoi(getenv("LISLAM_LM_V1")) == 1;
   const int rounds = min(a0.chain_len, a0.S - 1);
   auto timed = [&](int kernel, hipStream_t s, auto&& launch) {
     hipEvent_t b = nullptr, e = nullptr;
@@ -2790,14 +2564,10 @@ void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups
         const hipStream_t s = streams[g];
         const int cb = a.cn >= 8 ? (a.cn + 7) / 8 * 8 : a.cn;
         timed(4, s, [&] {
-          if (rows16) hipLaunchKernelGGL(k_odom_assoc16<2>, dim3(qblocks16 * cb), dim3(128), 0, s, a, r, qblocks16);
-          else if (kw == 1) hipLaunchKernelGGL(k_odom_assoc<1>, dim3(qblocks * cb), dim3(64), 0, s, a, r, qblocks);
-          else if (kw == 2) hipLaunchKernelGGL(k_odom_assoc<2>, dim3(qblocks * cb), dim3(128), 0, s, a, r, qblocks);
-          else hipLaunchKernelGGL(k_odom_assoc<4>, dim3(qblocks * cb), dim3(256), 0, s, a, r, qblocks);
+          hipLaunchKernelGGL(k_odom_assoc16<2>, dim3(qblocks16 * cb), dim3(128), 0, s, a, r, qblocks16);
         });
         timed(5, s, [&] {
-          if (lm_v1) hipLaunchKernelGGL(k_odom_lm, dim3(a.cn), dim3(kLmThreads), 0, s, a, r, outer);
-          else hipLaunchKernelGGL(k_odom_lm2, dim3(a.cn), dim3(kLm2Threads), 0, s, a, r, outer);
+          hipLaunchKernelGGL(k_odom_lm2, dim3(a.cn), dim3(kLm2Threads), 0, s, a, r, outer);
         });
       }
     }

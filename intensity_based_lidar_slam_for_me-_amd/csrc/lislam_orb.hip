@@ -1549,7 +1549,7 @@ __device__ __forceinline__ void orb_lm_body(const PairArgs& p, int max_it, int p
     }
     return;
   }
-  __shared__ LM lm;  // in registers only inside thread 0's step (see k_odom_lm)
+  __shared__ LM lm;  // in registers only inside thread 0's step
   if (threadIdx.x == 0) {
     const double I[7] = {0, 0, 0, 1, 0, 0, 0};
     for (int e = 0; e < 7; e++) sh.x[e] = I[e];

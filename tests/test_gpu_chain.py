@@ -27,6 +27,7 @@ def stream61(pkg, oracle, synth):
 
 
 def check_chain(pkg, b, feats, pose, rel, st, k0=0):
+    assert b.odometry_status() == 0  # no engine launch gave up (the sticky abort word)
     worst = 0.0
     for j in range(1, len(feats)):
         k = k0 + j
@@ -160,3 +161,59 @@ def test_engine_item_budget(pkg, oracle, synth, ctx, budget):
     pose, rel, st = oracle.odometry_chain(feats)
     check_chain(pkg, b, feats, pose, rel, st)
     b.close()
+
+
+def test_continuous_chain_config3_high_res_engine(pkg, oracle, synth):
+    """Config 3 (128 x 2048, the N_SCANS == 128 branch of scanRegistration.cpp:317-325) as one
+    continuous chain of 30 pairs through the persistent engine: every pair's pose and para within
+    1e-4 and its correspondence counts and LM iterations equal to the oracle's chain."""
+    S = 31
+    scans = synth.make_sequence(S, 128, 2048, start=200)
+    feats = [oracle.scan_registration(s) for s in scans]
+    c = pkg.Context(n_scans=128, width=2048)
+    try:
+        c.set_odometry_schedule(c.ENGINE_ON)
+        b = pkg.Batch(c, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, S - 1)
+        pose, rel, st = oracle.odometry_chain(feats)
+        worst = check_chain(pkg, b, feats, pose, rel, st)
+        print(f"128x2048 continuous chain of {S - 1} pairs: max |pose - oracle| = {worst:.3g}")
+        b.close()
+    finally:
+        c.close()
+
+
+def test_engine_abort_is_sticky_and_reported(pkg, synth, ctx):
+    """A launch whose bounded device wait expires (forced: a 1 us bound) raises the sticky abort
+    word: the odometry outputs are refused until lislam_batch_odometry_status reads it, later
+    launches do not clear it, and a clean launch after the read is valid again."""
+    S = 4
+    scans = synth.make_sequence(S, start=70)
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    b = pkg.Batch(ctx, S)
+    try:
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, S - 1)
+        assert b.odometry_status() == 0
+        ref = b.download(pkg.native.OUT_POSE, S - 1)
+        os.environ["LISLAM_ENGINE_WAIT_US"] = "1"
+        try:
+            b.odometry(S, S - 1)
+            ctx.synchronize()
+        finally:
+            del os.environ["LISLAM_ENGINE_WAIT_US"]
+        b.odometry(S, S - 1)  # a clean launch does not clear the word
+        ctx.synchronize()
+        with pytest.raises(RuntimeError):
+            b.download(pkg.native.OUT_POSE, S - 1)
+        assert b.odometry_status() == 1
+        assert b.odometry_status() == 0  # read and cleared
+        b.odometry(S, S - 1)
+        assert b.odometry_status() == 0
+        assert np.array_equal(b.download(pkg.native.OUT_POSE, S - 1), ref)
+    finally:
+        b.close()
+        ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
