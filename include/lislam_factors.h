@@ -158,19 +158,33 @@ class CostFunction {
 class DeviceCostFunction;
 
 namespace detail {
-/* Every live DeviceCostFunction, packed as lislam_eval_factors_raw records, and the outputs of the
- * last parameter point they were evaluated at.  One per process (the blocks evaluate on the one
- * SetFactorContext() context); the mutex serializes Ceres' evaluation threads. */
+/* One batched evaluation: the blocks that share a pair of parameter-block pointers, at the values
+ * those blocks were last evaluated at. */
+struct FactorBatch {
+  const double* pq = nullptr;  // the parameter blocks' addresses (Ceres' parameters[0], [1])
+  const double* pt = nullptr;
+  unsigned long long generation = 0;
+  double cq[4] = {0, 0, 0, 0}, ct[3] = {0, 0, 0};
+  std::vector<int32_t> index;  // registry slot -> row of this batch's outputs, -1 = not in it
+  std::vector<double> res, jq, jt;  // [rows][3], [rows][3][4], [rows][3][3]
+  unsigned long long used = 0;      // LRU stamp
+};
+/* Every live DeviceCostFunction, packed as lislam_eval_factors_raw records, and the batches of
+ * the parameter points they were last evaluated at: a batch holds the blocks whose Evaluate saw
+ * the same parameter-block pointers (one Ceres problem), plus the blocks not evaluated yet, so a
+ * problem's pass is one launch and two live problems at different poses do not evict each other.
+ * One per process (the blocks evaluate on the one SetFactorContext() context); the mutex
+ * serializes Ceres' evaluation threads. */
 struct FactorRegistry {
   std::mutex mu;
   std::vector<DeviceCostFunction*> blocks;  // slot i = blocks[i]
   std::vector<int32_t> kinds;
   std::vector<double> recs;                  // [n][12]
+  std::vector<const double*> seen_q, seen_t; // per slot: the pointers its last Evaluate saw (null: none yet)
   unsigned long long generation = 0;         // bumped by every Create() / destruction
-  bool cached = false;
-  unsigned long long cached_generation = 0;
-  double cq[4] = {0, 0, 0, 0}, ct[3] = {0, 0, 0};
-  std::vector<double> res, jq, jt;           // [n][3], [n][3][4], [n][3][3]
+  static constexpr int kBatches = 4;
+  FactorBatch batch[kBatches];
+  unsigned long long clock = 0;
   long long launches = 0;
 };
 inline FactorRegistry& factor_registry() {
@@ -199,6 +213,8 @@ class DeviceCostFunction : public CostFunction {
     g.blocks.push_back(this);
     g.kinds.push_back(kind);
     g.recs.insert(g.recs.end(), rec_, rec_ + 12);
+    g.seen_q.push_back(nullptr);
+    g.seen_t.push_back(nullptr);
     g.generation++;
   }
   ~DeviceCostFunction() override {
@@ -210,11 +226,15 @@ class DeviceCostFunction : public CostFunction {
       g.blocks[slot_] = m;
       g.kinds[slot_] = g.kinds[last];
       std::memcpy(&g.recs[slot_ * 12], &g.recs[last * 12], 12 * sizeof(double));
+      g.seen_q[slot_] = g.seen_q[last];
+      g.seen_t[slot_] = g.seen_t[last];
       m->slot_ = slot_;
     }
     g.blocks.pop_back();
     g.kinds.pop_back();
     g.recs.resize(last * 12);
+    g.seen_q.pop_back();
+    g.seen_t.pop_back();
     g.generation++;
   }
   DeviceCostFunction(const DeviceCostFunction&) = delete;
@@ -230,31 +250,57 @@ class DeviceCostFunction : public CostFunction {
     }
     static const double zero_t[3] = {0.0, 0.0, 0.0};
     const double* q = parameters[0];
+    const double* pt = kind_ == 4 ? nullptr : parameters[1];
     detail::FactorRegistry& g = detail::factor_registry();
     std::lock_guard<std::mutex> lock(g.mu);
+    g.seen_q[slot_] = q;
+    g.seen_t[slot_] = pt;
+    // the batch of this block's parameter pointers, valid at these values
+    detail::FactorBatch* b = nullptr;
+    for (detail::FactorBatch& e : g.batch)
+      if (e.pq == q && e.pt == pt && e.generation == g.generation && slot_ < e.index.size() && e.index[slot_] >= 0) b = &e;
     // the ground factor has no t block (its residual ignores t): any cached t serves it
-    const double* t = kind_ == 4 ? (g.cached ? g.ct : zero_t) : parameters[1];
-    if (!g.cached || g.cached_generation != g.generation || std::memcmp(g.cq, q, sizeof(g.cq)) != 0 ||
-        std::memcmp(g.ct, t, sizeof(g.ct)) != 0) {
-      // a new parameter point: every registered block at (q, t), one launch
+    const double* t = kind_ == 4 ? (b ? b->ct : zero_t) : pt;
+    if (!b || std::memcmp(b->cq, q, sizeof(b->cq)) != 0 || std::memcmp(b->ct, t, sizeof(b->ct)) != 0) {
+      // a new parameter point: every block of this problem (same pointers, or not evaluated yet)
+      // at (q, t), one launch, into the least recently used batch
+      if (!b) {
+        b = &g.batch[0];
+        for (detail::FactorBatch& e : g.batch)
+          if (e.used < b->used) b = &e;
+      }
       const size_t n = g.blocks.size();
-      g.res.resize(n * 3);
-      g.jq.resize(n * 12);
-      g.jt.resize(n * 9);
-      g.cached = false;
-      if (lislam_eval_factors_raw(ctx, (int32_t)n, g.kinds.data(), g.recs.data(), q, t, g.res.data(), g.jq.data(),
-                                  g.jt.data()) != LISLAM_OK)
+      b->index.assign(n, -1);
+      std::vector<int32_t> kinds;
+      std::vector<double> recs;
+      for (size_t i = 0; i < n; i++) {
+        const bool mine = (g.seen_q[i] == q && g.seen_t[i] == pt) || (g.seen_q[i] == nullptr);
+        if (!mine) continue;
+        b->index[i] = (int32_t)kinds.size();
+        kinds.push_back(g.kinds[i]);
+        recs.insert(recs.end(), &g.recs[i * 12], &g.recs[i * 12] + 12);
+      }
+      const size_t rows = kinds.size();
+      b->res.resize(rows * 3);
+      b->jq.resize(rows * 12);
+      b->jt.resize(rows * 9);
+      b->generation = 0;
+      if (lislam_eval_factors_raw(ctx, (int32_t)rows, kinds.data(), recs.data(), q, t, b->res.data(), b->jq.data(),
+                                  b->jt.data()) != LISLAM_OK)
         return false;
       g.launches++;
-      std::memcpy(g.cq, q, sizeof(g.cq));
-      if (t != g.ct) std::memcpy(g.ct, t, sizeof(g.ct));
-      g.cached_generation = g.generation;
-      g.cached = true;
+      b->pq = q;
+      b->pt = pt;
+      std::memcpy(b->cq, q, sizeof(b->cq));
+      if (t != b->ct) std::memcpy(b->ct, t, sizeof(b->ct));
+      b->generation = g.generation;
     }
+    b->used = ++g.clock;
+    const size_t row = (size_t)b->index[slot_];
     const bool want_q = jacobians && jacobians[0], want_t = jacobians && kind_ != 4 && jacobians[1];
-    const double* r = &g.res[slot_ * 3];
-    const double* jq = &g.jq[slot_ * 12];
-    const double* jt = &g.jt[slot_ * 9];
+    const double* r = &b->res[row * 3];
+    const double* jq = &b->jq[row * 12];
+    const double* jt = &b->jt[row * 9];
     for (int i = 0; i < residuals_; i++) {
       residuals[i] = r[i];
       if (want_q)

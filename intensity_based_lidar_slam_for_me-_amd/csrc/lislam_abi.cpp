@@ -231,6 +231,9 @@ int lislam_batch_destroy(lislam_batch* b) {
     if (b->odo_join[g]) hipEventDestroy(b->odo_join[g]);
   }
   if (b->odo_fork) hipEventDestroy(b->odo_fork);
+  if (b->eng_roles) { hipStreamSynchronize(b->eng_roles); hipStreamDestroy(b->eng_roles); }
+  if (b->eng_items) { hipStreamSynchronize(b->eng_items); hipStreamDestroy(b->eng_items); }
+  for (hipEvent_t e : {b->eng_fork, b->eng_join_r, b->eng_join_i}) if (e) hipEventDestroy(e);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
   if (b->ground) lislam_free_ground(b->ground);
@@ -504,8 +507,20 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   if (lislam::use_chain_engine(o, c->odom_engine)) {
     // few long chains: one persistent launch sequences every round on the device
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (b->eng_split < 0) {  // the engine's streams, once per batch
+      static const bool single = getenv("LISLAM_ENGINE_SINGLE") && atoi(getenv("LISLAM_ENGINE_SINGLE")) == 1;
+      b->eng_split = !single && lislam::engine_streams(c->device, &b->eng_roles, &b->eng_items) ? 1 : 0;
+      if (b->eng_split) {
+        HIPCHK(c, hipEventCreateWithFlags(&b->eng_fork, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_r, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_i, hipEventDisableTiming));
+      }
+    }
     if (ev) { e0 = b->get_event(); HIPCHK(c, hipEventRecord(e0, c->stream)); }
-    lislam::launch_odometry_chain(o, c->stream);
+    if (b->eng_split)
+      lislam::launch_odometry_chain_split(o, c->stream, b->eng_roles, b->eng_items, b->eng_fork, b->eng_join_r, b->eng_join_i);
+    else
+      lislam::launch_odometry_chain(o, c->stream);
     b->engine_ran = true;
     if (ev) { e1 = b->get_event(); HIPCHK(c, hipEventRecord(e1, c->stream)); ev->push_back({6, e0, e1}); }
     HIPCHK(c, hipGetLastError());

@@ -39,6 +39,11 @@ struct lislam_batch {
   std::vector<hipEvent_t> pool;
   int extracted = 0;
   bool engine_ran = false;  // the last odometry call ran the chain engine (lislam_batch_odometry_status)
+  // the engine's two CU-masked streams (roles / items) and their fork / join events; split: -1 not
+  // tried yet, 0 unavailable (single-launch engine), 1 ready
+  int eng_split = -1;
+  hipStream_t eng_roles = nullptr, eng_items = nullptr;
+  hipEvent_t eng_fork = nullptr, eng_join_r = nullptr, eng_join_i = nullptr;
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
   // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
   // queued on the context stream after it.

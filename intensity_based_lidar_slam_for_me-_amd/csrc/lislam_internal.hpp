@@ -144,6 +144,11 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
 // The same schedule as ONE persistent launch (k_odom_chain, lislam_odometry.hip): every round of
 // the a.n_chains chains, association and solve, sequenced on the device.  Returns the grid size.
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
+// The same engine as two launches (k_odom_roles on `roles`, k_odom_items on `items`, CU-masked
+// streams from engine_streams), forked from and joined back into st by the three events.
+int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t roles, hipStream_t items, hipEvent_t fork,
+                                hipEvent_t join_r, hipEvent_t join_i);
+bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
 // lislam_set_odometry_schedule (LISLAM_ENGINE_*; a context starts from the environment's
 // LISLAM_ENGINE if set); AUTO = on for at most 4 chains.

@@ -22,7 +22,6 @@
 // exact (distance, id)-ordered k-NN, i.e. ikd's Nearest_Search with ties broken by id.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cfloat>
@@ -32,6 +31,7 @@
 #include <cstring>
 #include <vector>
 
+#include "lislam_prims.hpp"
 #include "lislam_ctx.hpp"
 #include "lislam_device.hpp"
 #include "lislam_lm.hpp"
@@ -1036,19 +1036,15 @@ namespace {
 
 hipStream_t stream_of(lislam_ctx* c) { return c->stream; }
 
-// Stable radix sort of (u64 key, int) pairs.
-int sort_pairs_u64(lislam_ctx* c, DBuf& tmp, const uint64_t* ki, uint64_t* ko, const int* vi, int* vo, int n) {
-  size_t tb = 0;
-  MCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ki, ko, vi, vo, n, 0, 64, stream_of(c)));
-  MCHK(c, tmp.reserve(tb));
-  MCHK(c, hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, ki, ko, vi, vo, n, 0, 64, stream_of(c)));
+// Stable radix sort of (u64 / u32 key, int) pairs (lislam_prims.hpp); ki / vi are clobbered.
+int sort_pairs_u64(lislam_ctx* c, DBuf& tmp, uint64_t* ki, uint64_t* ko, int* vi, int* vo, int n) {
+  MCHK(c, tmp.reserve(prims::sort_temp_bytes(n)));
+  MCHK(c, prims::sort_pairs<uint64_t>(tmp.p, ki, ko, vi, vo, n, 64, stream_of(c)));
   return LISLAM_OK;
 }
-int sort_pairs_u32(lislam_ctx* c, DBuf& tmp, const uint32_t* ki, uint32_t* ko, const int* vi, int* vo, int n) {
-  size_t tb = 0;
-  MCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ki, ko, vi, vo, n, 0, 32, stream_of(c)));
-  MCHK(c, tmp.reserve(tb));
-  MCHK(c, hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, ki, ko, vi, vo, n, 0, 32, stream_of(c)));
+int sort_pairs_u32(lislam_ctx* c, DBuf& tmp, uint32_t* ki, uint32_t* ko, int* vi, int* vo, int n) {
+  MCHK(c, tmp.reserve(prims::sort_temp_bytes(n)));
+  MCHK(c, prims::sort_pairs<uint32_t>(tmp.p, ki, ko, vi, vo, n, 32, stream_of(c)));
   return LISLAM_OK;
 }
 
@@ -1146,25 +1142,15 @@ int add_packed(lislam_map* m, int64_t nin, bool downsample, int64_t* n_added) {
   MCHK(c, m->live.reserve(std::max<int64_t>(n0, 1)));
   int* nsel = m->counter.as<int>() + 1;
   int* nsel2 = m->counter.as<int>() + 2;
-  size_t tb = 0, tb2 = 0;
-  if (n0) {
-    hipLaunchKernelGGL(k_flags_inv, dim3(blocks(n0)), dim3(256), 0, st, m->dead.as<uint8_t>(), (int)n0, m->live.as<uint8_t>());
-    MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, m->pts.as<float4>(), m->live.as<uint8_t>(), m->tmp.as<float4>(),
-                                          nsel, (int)n0, st));
-  }
-  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb2, m->newp.as<float4>(), m->enter.as<uint8_t>(), m->tmp.as<float4>(),
-                                        nsel2, (int)nin, st));
-  MCHK(c, m->sort_tmp.reserve(std::max(tb, tb2)));
-  if (n0)
-    MCHK(c, hipcub::DeviceSelect::Flagged(m->sort_tmp.p, tb, m->pts.as<float4>(), m->live.as<uint8_t>(),
-                                          m->tmp.as<float4>(), nsel, (int)n0, st));
-  else
-    MCHK(c, hipMemsetAsync(nsel, 0, sizeof(int), st));
+  if (n0) hipLaunchKernelGGL(k_flags_inv, dim3(blocks(n0)), dim3(256), 0, st, m->dead.as<uint8_t>(), (int)n0, m->live.as<uint8_t>());
+  MCHK(c, m->sort_tmp.reserve(std::max(prims::select_temp_bytes((int)n0), prims::select_temp_bytes((int)nin))));
+  MCHK(c, prims::select_flagged(m->sort_tmp.p, m->pts.as<float4>(), m->live.as<uint8_t>(), m->tmp.as<float4>(), nsel,
+                                (int)n0, st));
   int h[2] = {0, 0};
   MCHK(c, hipMemcpyAsync(&h[0], nsel, sizeof(int), hipMemcpyDeviceToHost, st));
   MCHK(c, hipStreamSynchronize(st));
-  MCHK(c, hipcub::DeviceSelect::Flagged(m->sort_tmp.p, tb2, m->newp.as<float4>(), m->enter.as<uint8_t>(),
-                                        m->tmp.as<float4>() + h[0], nsel2, (int)nin, st));
+  MCHK(c, prims::select_flagged(m->sort_tmp.p, m->newp.as<float4>(), m->enter.as<uint8_t>(), m->tmp.as<float4>() + h[0],
+                                nsel2, (int)nin, st));
   MCHK(c, hipMemcpyAsync(&h[1], nsel2, sizeof(int), hipMemcpyDeviceToHost, st));
   MCHK(c, hipStreamSynchronize(st));
   if (n_added) *n_added = h[1];
@@ -1262,10 +1248,8 @@ int voxel_grid_device(lislam_ctx* c, MapScratch& sc, const float4* in, int n, fl
   MRC(sort_pairs_u32(c, sc.sort_tmp, sc.keys32a.as<uint32_t>(), sc.keys32b.as<uint32_t>(), sc.idxa.as<int>(),
                      sc.idxb.as<int>(), n));
   hipLaunchKernelGGL(k_vg_runs, dim3(blocks(n)), dim3(256), 0, st, sc.keys32b.as<uint32_t>(), n, a.overflow, sc.flag.as<int>());
-  size_t tb = 0;
-  MCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sc.flag.as<int>(), sc.pos.as<int>(), n, st));
-  MCHK(c, sc.sort_tmp.reserve(tb));
-  MCHK(c, hipcub::DeviceScan::ExclusiveSum(sc.sort_tmp.p, tb, sc.flag.as<int>(), sc.pos.as<int>(), n, st));
+  MCHK(c, sc.sort_tmp.reserve(prims::exclusive_sum_temp_bytes(n)));
+  MCHK(c, prims::exclusive_sum(sc.sort_tmp.p, sc.flag.as<int>(), sc.pos.as<int>(), n, st));
   hipLaunchKernelGGL(k_vg_centroids, dim3(blocks(n)), dim3(256), 0, st, in, sc.keys32b.as<uint32_t>(), sc.idxb.as<int>(),
                      sc.pos.as<int>(), sc.flag.as<int>(), n, a.overflow, out, n_out);
   MCHK(c, hipGetLastError());
@@ -1897,16 +1881,11 @@ int cm_shift(lislam_lmap* L, int w, int si, int sj, int sk) {
   MCHK(c, L->counts.reserve(64));
   hipLaunchKernelGGL(k_cm_shift, dim3(blocks(n)), dim3(256), 0, st, L->cube[w].as<int>(), n, si, sj, sk,
                      L->keep.as<int>(), L->tmp_cube.as<int>());
-  size_t tb = 0, tb2 = 0;
-  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, L->pts[w].as<float4>(), L->keep.as<int>(), L->tmp_pts.as<float4>(),
-                                        L->counts.as<int>(), n, st));
-  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb2, L->tmp_cube.as<int>(), L->keep.as<int>(), L->cube[w].as<int>(),
-                                        L->counts.as<int>() + 1, n, st));
-  MCHK(c, L->sort_tmp.reserve(std::max(tb, tb2)));
-  MCHK(c, hipcub::DeviceSelect::Flagged(L->sort_tmp.p, tb, L->pts[w].as<float4>(), L->keep.as<int>(),
-                                        L->tmp_pts.as<float4>(), L->counts.as<int>(), n, st));
-  MCHK(c, hipcub::DeviceSelect::Flagged(L->sort_tmp.p, tb2, L->tmp_cube.as<int>(), L->keep.as<int>(),
-                                        L->cube[w].as<int>(), L->counts.as<int>() + 1, n, st));
+  MCHK(c, L->sort_tmp.reserve(prims::select_temp_bytes(n)));
+  MCHK(c, prims::select_flagged(L->sort_tmp.p, L->pts[w].as<float4>(), L->keep.as<int>(), L->tmp_pts.as<float4>(),
+                                L->counts.as<int>(), n, st));
+  MCHK(c, prims::select_flagged(L->sort_tmp.p, L->tmp_cube.as<int>(), L->keep.as<int>(), L->cube[w].as<int>(),
+                                L->counts.as<int>() + 1, n, st));
   int kept = 0;
   MCHK(c, hipMemcpyAsync(&kept, L->counts.p, 4, hipMemcpyDeviceToHost, st));
   MCHK(c, hipStreamSynchronize(st));
@@ -1944,10 +1923,8 @@ int cm_update(lislam_lmap* L, int w, const float4* stack, const int* n_stack, in
   MRC(sort_pairs_u64(c, L->sort_tmp, L->keys.as<uint64_t>(), L->keys2.as<uint64_t>(), L->idx.as<int>(),
                      L->idx2.as<int>(), m));
   hipLaunchKernelGGL(k_cm_runs, dim3(blocks(m)), dim3(256), 0, st, L->keys2.as<uint64_t>(), n_stack, np, L->flag.as<int>());
-  size_t tb = 0;
-  MCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, L->flag.as<int>(), L->pos.as<int>(), m, st));
-  MCHK(c, L->sort_tmp.reserve(tb));
-  MCHK(c, hipcub::DeviceScan::ExclusiveSum(L->sort_tmp.p, tb, L->flag.as<int>(), L->pos.as<int>(), m, st));
+  MCHK(c, L->sort_tmp.reserve(prims::exclusive_sum_temp_bytes(m)));
+  MCHK(c, prims::exclusive_sum(L->sort_tmp.p, L->flag.as<int>(), L->pos.as<int>(), m, st));
   MCHK(c, L->tmp_pts.reserve((size_t)m * 16));
   MCHK(c, L->tmp_cube.reserve((size_t)m * 4));
   MCHK(c, L->counts.reserve(64));
@@ -2434,12 +2411,9 @@ int lc_prepare(lislam_ctx* c, LoopState& ls, int n, const lislam_icp_config* cfg
   MCHK(c, ls.cnt.reserve(16));
   hipLaunchKernelGGL(k_lc_flags, dim3(blocks(n)), dim3(256), 0, st, ls.tf.as<float4>(), n, cfg->use_crop ? 1 : 0,
                      -cfg->crop_size, cfg->crop_size, ls.flag.as<uint8_t>());
-  size_t tb = 0;
-  MCHK(c, hipcub::DeviceSelect::Flagged(nullptr, tb, ls.tf.as<float4>(), ls.flag.as<uint8_t>(), ls.sel.as<float4>(),
-                                        ls.cnt.as<int>(), n, st));
-  MCHK(c, ls.tmp.reserve(tb));
-  MCHK(c, hipcub::DeviceSelect::Flagged(ls.tmp.p, tb, ls.tf.as<float4>(), ls.flag.as<uint8_t>(), ls.sel.as<float4>(),
-                                        ls.cnt.as<int>(), n, st));
+  MCHK(c, ls.tmp.reserve(prims::select_temp_bytes(n)));
+  MCHK(c, prims::select_flagged(ls.tmp.p, ls.tf.as<float4>(), ls.flag.as<uint8_t>(), ls.sel.as<float4>(), ls.cnt.as<int>(), n,
+                                st));
   int m = 0;
   MCHK(c, hipMemcpyAsync(&m, ls.cnt.p, sizeof(int), hipMemcpyDeviceToHost, st));
   MCHK(c, hipStreamSynchronize(st));
@@ -2746,6 +2720,61 @@ int lislam_odom_fuse(lislam_odom_fuser* f, const double* aloam, const double* in
   MCHK(c, hipMemcpyAsync(fused, dout, pb, hipMemcpyDefault, st));
   MCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------ primitives check
+// Host-array entry points of the map path's primitives (lislam_prims.hpp) for the GPU tests
+// (tests/test_gpu_prims.py): each copies in, runs the primitive on the default stream, copies out.
+extern "C" {
+
+int lislam_debug_sort_pairs(const void* keys, const int32_t* vals, int32_t n, int32_t key_bits, void* keys_out,
+                            int32_t* vals_out) {
+  if (n < 0 || (key_bits != 32 && key_bits != 64)) return LISLAM_ERR_ARG;
+  const size_t kb = (size_t)std::max(n, 1) * (key_bits / 8), vb = (size_t)std::max(n, 1) * 4;
+  void *ki = nullptr, *ko = nullptr, *vi = nullptr, *vo = nullptr, *tmp = nullptr;
+  int rc = LISLAM_ERR_DEVICE;
+  if (hipMalloc(&ki, kb) == hipSuccess && hipMalloc(&ko, kb) == hipSuccess && hipMalloc(&vi, vb) == hipSuccess &&
+      hipMalloc(&vo, vb) == hipSuccess && hipMalloc(&tmp, prims::sort_temp_bytes(n)) == hipSuccess &&
+      hipMemcpy(ki, keys, kb, hipMemcpyHostToDevice) == hipSuccess &&
+      hipMemcpy(vi, vals, vb, hipMemcpyHostToDevice) == hipSuccess) {
+    const hipError_t e = key_bits == 64
+        ? prims::sort_pairs<uint64_t>(tmp, (uint64_t*)ki, (uint64_t*)ko, (int*)vi, (int*)vo, n, 64, nullptr)
+        : prims::sort_pairs<uint32_t>(tmp, (uint32_t*)ki, (uint32_t*)ko, (int*)vi, (int*)vo, n, 32, nullptr);
+    if (e == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(keys_out, ko, (size_t)n * (key_bits / 8), hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(vals_out, vo, (size_t)n * 4, hipMemcpyDeviceToHost) == hipSuccess)
+      rc = LISLAM_OK;
+  }
+  for (void* p : {ki, ko, vi, vo, tmp}) if (p) (void)hipFree(p);
+  return rc;
+}
+
+int lislam_debug_select_scan(const uint8_t* flags, const int32_t* vals, int32_t n, int32_t* selected, int32_t* count,
+                             int32_t* exclusive) {
+  if (n < 0) return LISLAM_ERR_ARG;
+  const size_t nb = (size_t)std::max(n, 1);
+  void *f = nullptr, *v = nullptr, *o = nullptr, *x = nullptr, *cnt = nullptr, *tmp = nullptr;
+  int rc = LISLAM_ERR_DEVICE;
+  if (hipMalloc(&f, nb) == hipSuccess && hipMalloc(&v, nb * 4) == hipSuccess && hipMalloc(&o, nb * 4) == hipSuccess &&
+      hipMalloc(&x, nb * 4) == hipSuccess && hipMalloc(&cnt, 16) == hipSuccess &&
+      hipMalloc(&tmp, std::max(prims::select_temp_bytes(n), prims::exclusive_sum_temp_bytes(n))) == hipSuccess &&
+      hipMemcpy(f, flags, nb, hipMemcpyHostToDevice) == hipSuccess &&
+      hipMemcpy(v, vals, nb * 4, hipMemcpyHostToDevice) == hipSuccess) {
+    hipError_t e = prims::select_flagged(tmp, (const int*)v, (const uint8_t*)f, (int*)o, (int*)cnt, n, nullptr);
+    if (e == hipSuccess) e = prims::exclusive_sum(tmp, (const int*)v, (int*)x, n, nullptr);
+    int c = 0;
+    if (e == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(&c, cnt, 4, hipMemcpyDeviceToHost) == hipSuccess && c >= 0 && c <= n &&
+        hipMemcpy(selected, o, (size_t)c * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(exclusive, x, (size_t)n * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+      *count = c;
+      rc = LISLAM_OK;
+    }
+  }
+  for (void* p : {f, v, o, x, cnt, tmp}) if (p) (void)hipFree(p);
+  return rc;
 }
 
 }  // extern "C"

@@ -20,9 +20,13 @@
 // of every chain in one launch) and per-round launches (k_odom_assoc16 + k_odom_lm2, many short
 // chains).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "lislam_device.hpp"
 #include "lislam_factors.hpp"
@@ -1350,7 +1354,7 @@ extern "C" int lislam_debug_engine_prof_read(unsigned long long* out, int n_tick
 }
 // LISLAM_ENG_PROF = 0 compiles the engine's developer timestamps out (rt_now() = 0, eng_prof a no-op).
 #ifndef LISLAM_ENG_PROF
-#define LISLAM_ENG_PROF 1
+#define LISLAM_ENG_PROF 0  // developer builds: -DLISLAM_ENG_PROF=1 (scripts/engine_prof.py); the stamps cost ~4 %
 #endif
 __device__ __forceinline__ void eng_prof(unsigned tk, int slot, unsigned long long v, bool add = false) {
 #if LISLAM_ENG_PROF
@@ -1404,15 +1408,18 @@ extern "C" int lislam_debug_engine_qlog(int* dev_buf, int pair) {
 constexpr int kEngThreads = LISLAM_ENG_THREADS;
 constexpr int kEngWaves = kEngThreads / 64;
 constexpr int kEngQ = kEngWaves;      // queries per association item: one per wave (64 lanes)
-#ifndef LISLAM_ENG_LDS
-#define LISLAM_ENG_LDS 2304           // 64 lines: 12 * 64 sharp + 24 * 64 flat queries
-#endif
-constexpr int kEngLds = LISLAM_ENG_LDS;
-constexpr int kRecWords = 8;          // u64 words per record: c.xy, c.z a.x, a.yz, kind, u/n xyz, -
-#ifndef LISLAM_REC_UNROLL
-#define LISLAM_REC_UNROLL 2           // records per solve-load round trip and thread
-#endif
-constexpr int kRecUnroll = LISLAM_REC_UNROLL;
+// A block record: 64 B = four 16-B quads, written by the association wave of its query (lanes 0..3,
+// write-through) and read by the solve with 16-B loads:
+//   q0 c.x c.y c.z a.x (float) | q1 a.y a.z (float) kind (int) - | q2 u.x u.y (double) | q3 u.z (double) -
+// (c the query point, a the first matched point, u the edge direction / plane normal).
+constexpr int kRecBytes = 64;
+constexpr int kRecWords = kRecBytes / 8;
+constexpr int kAuxSc1 = 16;  // buffer instruction cache policy: sc1 (write-through stores, L1-bypassing loads)
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, unsigned bytes) {  // base wave-uniform
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 __device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
@@ -1448,6 +1455,7 @@ struct EngCtl {
   int C, R, I;
   unsigned long long wait_ticks;  // bound of every device wait (s_memrealtime ticks, 100 MHz)
   int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
+  int roles;     // solve-role tickets ahead of the items in this launch's queue (C, or 0: roles in their own launch)
   int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at once
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
@@ -1505,15 +1513,13 @@ __device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* ab
 }
 
 struct EngShared {
-  float cf[6][kEngLds];   // query point c, first matched point a (edge) / j (plane)
-  double ud[3][kEngLds];  // edge: u = (a - b) / |a - b|; plane: unit normal
-  int8_t kd[kEngLds];     // 0 edge, 1 plane, -1 none
   double red[kEngWaves * 4][32];  // kAcc sums (+ 2 counts) per 16-lane row
   double xw[kEngWaves][8];        // each wave's copy of its item's x (the item's queries read it here)
   P4 prew[kEngWaves][4];          // each wave's ItemPre of its first query: qp, the seeds' points
   int prei[kEngWaves][4];         // ... and the seeds' indices
   double acc[kAcc];
   double x[7];
+  double cx[7], cpw[7];  // solve role: the chain's x (para_q / para_t) and pose between passes
   int cnt[kEngWaves][2];
   unsigned ticket;
   int flag, flag0, nc, np, pref;
@@ -1655,7 +1661,7 @@ __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& 
 // GPU runs (latency bound: 16.5 vs 34.9 us per round as separate launches).  The record goes out
 // write-through; the wave's share of the solve's first evaluation (its block's 28 sums at x and
 // the corner / plane counts) goes to sh.red[wave].
-__device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int k, int w, uint64_t* rec, int* warm, int outer,
+__device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int k, int w, Rsrc rec, int* warm, int outer,
                                           unsigned tk, const ItemPre& pre, const double (&x)[7]) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id();
@@ -1748,19 +1754,20 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   if (outer == 0 && lane < 3)  // seeds of the second pass (write-through: another workgroup reads them)
     __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), (unsigned)(lane == 0 ? closest : lane == 1 ? i2 : i3),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lane < 7 && (lane == 3 || kind >= 0)) {
-    auto pk = [](float lo, float hi) { return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32); };
-    uint64_t v;
-    switch (lane) {
-      case 0: v = pk(cur.x, cur.y); break;
-      case 1: v = pk(cur.z, pa.x); break;
-      case 2: v = pk(pa.y, pa.z); break;
-      case 3: v = (uint64_t)(uint32_t)kind; break;
-      case 4: v = (uint64_t)__double_as_longlong(u.x); break;
-      case 5: v = (uint64_t)__double_as_longlong(u.y); break;
-      default: v = (uint64_t)__double_as_longlong(u.z); break;
+  // the record: four 16-B write-through stores (lanes 0..3; the kind word always, the rest with a
+  // correspondence) -- layout of rec_unpack
+  if (lane < 4 && (lane == 1 || kind >= 0)) {
+    v4u q;
+    if (lane == 0) q = v4u{__float_as_uint(cur.x), __float_as_uint(cur.y), __float_as_uint(cur.z), __float_as_uint(pa.x)};
+    else if (lane == 1) q = v4u{__float_as_uint(pa.y), __float_as_uint(pa.z), (unsigned)kind, 0u};
+    else if (lane == 2) {
+      const uint64_t ux = (uint64_t)__double_as_longlong(u.x), uy = (uint64_t)__double_as_longlong(u.y);
+      q = v4u{(unsigned)ux, (unsigned)(ux >> 32), (unsigned)uy, (unsigned)(uy >> 32)};
+    } else {
+      const uint64_t uz = (uint64_t)__double_as_longlong(u.z);
+      q = v4u{(unsigned)uz, (unsigned)(uz >> 32), 0u, 0u};
     }
-    st_sc1(rec + (size_t)w * kRecWords + lane, v);
+    __builtin_amdgcn_raw_buffer_store_b128(q, rec, w * kRecBytes + lane * 16, 0, kAuxSc1);
   }
   // the share of the first evaluation, added to the wave's row sh.red[wave] (kind is wave-uniform;
   // every lane computes, lane 0 adds; a wave's LDS accesses stay in order)
@@ -1786,7 +1793,7 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
 // holds more queries than the engine keeps items in flight (EngCtl::budget), so that no item
 // waits for a workgroup to come free.  The wave's share of the first evaluation (its blocks' 28
 // sums at x, and the corner / plane counts) goes to sh.red[wave].
-__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, int ieff, uint64_t* rec,
+__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, int ieff, Rsrc rec,
                                              int* warm, int outer, unsigned tk) {
   const int ql = (int)(threadIdx.x >> 6);
   const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
@@ -1875,76 +1882,27 @@ __device__ __forceinline__ int row_reduce_scatter28(const double (&s)[kAcc], dou
 
 __device__ __forceinline__ int part_base(int part) { return 14 * (part & 1) + 7 * (part >> 1); }
 
-__device__ __forceinline__ void eng_reduce(double (&s)[kAcc], EngShared& sh) {
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  double o[7];
-  const int part = row_reduce_scatter28(s, o);
-#pragma unroll
-  for (int q = 0; q < 7; q++) o[q] = rows_sum(o[q]);  // the wave's sums of part(lane)
-  if (lane < 4) {
-    const int base = part_base(part);
-#pragma unroll
-    for (int q = 0; q < 7; q++) sh.red[wv][base + q] = o[q];
-  }
-  __syncthreads();
-  if (threadIdx.x < kAcc) {
-    double v = 0.0;
-#pragma unroll
-    for (int w = 0; w < kEngWaves; w++) v += sh.red[w][threadIdx.x];
-    double sc;
-    const int ai = acc_index(threadIdx.x, &sc);
-    sh.acc[ai] = sc * v;
-  }
-  __syncthreads();
-}
-
-// One evaluation at sh.x over `total` records (LDS for i < kEngLds, write-through records beyond).
-__device__ __forceinline__ void eng_evaluate(EngShared& sh, const uint64_t* rec, int total, unsigned tk) {
-  double s[kAcc];
-#pragma unroll
-  for (int e = 0; e < kAcc; e++) s[e] = 0.0;
-  double R[9];
-  D3 t;
-  eng_rt(sh, R, t);
-  for (int i = threadIdx.x; i < total; i += kEngThreads) {
-    int kd;
-    D3 c, pa, u;
-    if (i < kEngLds) {
-      kd = sh.kd[i];
-      if (kd < 0) continue;
-      c = D3{sh.cf[0][i], sh.cf[1][i], sh.cf[2][i]};
-      pa = D3{sh.cf[3][i], sh.cf[4][i], sh.cf[5][i]};
-      u = D3{sh.ud[0][i], sh.ud[1][i], sh.ud[2][i]};
-    } else {
-      const uint64_t* rw = rec + (size_t)i * kRecWords;
-      kd = (int)(uint32_t)ld_sc1(rw + 3);
-      if (kd < 0) continue;
-      const uint64_t w0 = ld_sc1(rw), w1 = ld_sc1(rw + 1), w2 = ld_sc1(rw + 2);
-      c = D3{__uint_as_float((uint32_t)w0), __uint_as_float((uint32_t)(w0 >> 32)), __uint_as_float((uint32_t)w1)};
-      pa = D3{__uint_as_float((uint32_t)(w1 >> 32)), __uint_as_float((uint32_t)w2), __uint_as_float((uint32_t)(w2 >> 32))};
-      u = D3{ld_sc1d((const double*)(rw + 4)), ld_sc1d((const double*)(rw + 5)), ld_sc1d((const double*)(rw + 6))};
-    }
-    eng_block(kd, c, pa, u, R, t, s);
-  }
-  const unsigned long long t_red = threadIdx.x == 0 ? rt_now() : 0ull;
-  eng_reduce(s, sh);
-  if (threadIdx.x == 0) eng_prof(tk, 7, rt_now() - t_red, true);
-}
-
-// ---- the step logic of lislam_lm.hpp (Ceres 1.14 LM, same decisions) for thread 0, lean:
-// A held packed (21), the Cholesky's column reciprocals from rsqrt (no sqrt + division per column),
-// the model cost change from the solve (m = 0.5 (y.Sg + y.(D/radius)y), the same quantity as
-// -(step.Sg + 0.5 step'SAS step) since (SAS + D/radius) y = Sg), EigenQuaternionParameterization's
-// sin|d|/|d| and cos|d| as series in |d|^2 below |d| = 0.5 (library sincos above), and the
-// gradient test's rotation part only when its translation part is not already above 1e-10.
+// ---- the step logic of lislam_lm.hpp (Ceres 1.14 LM, same decisions), on every lane of wave 0.
+// Written for a short dependent chain (fp64 on gfx950: ~32 cycles per dependent operation):
+// - the 6x6 system by its 3x3 blocks: adjugate inverse of the rotation block, Schur complement of
+//   the translation block, adjugate again (positive definiteness by the leading minors of both:
+//   Sylvester, the same test as a Cholesky's positive pivots);
+// - 1 / radius carried beside radius (scaled by the same powers of two and the same factor m);
+// - rel by the reciprocal of the model cost change, computed while the candidate is evaluated;
+// - the parameter tolerance of a candidate decided while it is evaluated;
+// - sin|d|/|d| and cos|d| of EigenQuaternionParameterization's plus by Estrin's scheme.
 struct EngLM {
   double x[7], xc[7], A[21], g[6], scale[6], iscale[6], diag[6];
-  double cost, radius, dfac, mcc;
-  int reuse, it, invalid, term;
-  int prof;                      // developer profile armed (g_eng_prof): sub-phase ticks into pacc
-  unsigned long long pacc[4];    // lm_next, factorization, propose, steps (added to g_step_acc at the end)
+  double cost, radius, ir, dfac, mcc, imcc;
+  int reuse, it, invalid, term, ptol;
 };
 
+__device__ __forceinline__ double rcp_d(double d) {  // 1 / d to ~1 ulp (d normal, nonzero)
+  double y = __builtin_amdgcn_rcp(d);
+  y = fma(fma(-d, y, 1.0), y, y);
+  y = fma(fma(-d, y, 1.0), y, y);
+  return y;
+}
 __device__ __forceinline__ double rsqrt_d(double d) {  // 1 / sqrt(d), d > 0, to ~1 ulp
   double y = __builtin_amdgcn_rsq(d);
   y = y * fma(-0.5 * d, y * y, 1.5);
@@ -1965,18 +1923,25 @@ __device__ __forceinline__ void eng_quat_plus(const double* x, const double* d, 
     return;
   }
   double sdd, cs;
-  if (n2 <= 0.25) {  // Taylor series in n2 to x^16 (truncation < 1e-19)
-    sdd = fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, 2.8114572543455206e-15, -7.6471637318198164e-13),
-          1.6059043836821613e-10), -2.5052108385441720e-08), 2.7557319223985893e-06), -1.9841269841269841e-04),
-          8.3333333333333333e-03), -1.6666666666666666e-01), 1.0);
-    cs = fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, fma(n2, 4.7794773323873853e-14, -1.1470745597729725e-11),
-         2.0876756987868099e-09), -2.7557319223985888e-07), 2.4801587301587302e-05), -1.3888888888888889e-03),
-         4.1666666666666664e-02), -0.5), 1.0);
+  if (n2 <= 0.25) {  // Taylor series in n2 to x^16 (truncation < 1e-19), Estrin's scheme
+    const double z2 = n2 * n2, z4 = z2 * z2, z8 = z4 * z4;
+    sdd = fma(z8, 2.8114572543455206e-15,
+              fma(z4, fma(z2, fma(n2, -7.6471637318198164e-13, 1.6059043836821613e-10),
+                          fma(n2, -2.5052108385441720e-08, 2.7557319223985893e-06)),
+                  fma(z2, fma(n2, -1.9841269841269841e-04, 8.3333333333333333e-03), fma(n2, -1.6666666666666666e-01, 1.0))));
+    cs = fma(z8, 4.7794773323873853e-14,
+             fma(z4, fma(z2, fma(n2, -1.1470745597729725e-11, 2.0876756987868099e-09),
+                         fma(n2, -2.7557319223985888e-07, 2.4801587301587302e-05)),
+                 fma(z2, fma(n2, -1.3888888888888889e-03, 4.1666666666666664e-02), fma(n2, -0.5, 1.0))));
   } else {
     sincos_slow(n2, &sdd, &cs);
   }
-  const DQ r = qmul(DQ{sdd * d[0], sdd * d[1], sdd * d[2], cs}, DQ{x[0], x[1], x[2], x[3]});
-  xp[0] = r.x; xp[1] = r.y; xp[2] = r.z; xp[3] = r.w;
+  const double ax = sdd * d[0], ay = sdd * d[1], az = sdd * d[2];
+  // (a, cs) (x) (x0..x3): pairwise sums (depth 3)
+  xp[0] = fma(cs, x[0], ax * x[3]) + fma(ay, x[2], -az * x[1]);
+  xp[1] = fma(cs, x[1], ay * x[3]) + fma(az, x[0], -ax * x[2]);
+  xp[2] = fma(cs, x[2], az * x[3]) + fma(ax, x[1], -ay * x[0]);
+  xp[3] = fma(cs, x[3], -ax * x[0]) - fma(ay, x[1], az * x[2]);
 }
 // grad_max_norm(x, g) <= 1e-10: max_k |x_k - (x (+) -g)_k|
 __device__ __forceinline__ bool eng_grad_small(const double* x, const double* g) {
@@ -1992,85 +1957,103 @@ __device__ __forceinline__ bool eng_grad_small(const double* x, const double* g)
 // packed upper index of (i, j), i <= j
 __device__ __forceinline__ constexpr int pu(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
 
-// Developer sub-phase profile of the step (lane 0 of the solve): accumulated ticks of the lm_next
-// logic, the factorization and the rest of propose; read and cleared by lislam_debug_step_prof.
-__device__ unsigned long long g_step_acc[4];
-extern "C" int lislam_debug_step_prof(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_acc), sizeof(g_step_acc)) != hipSuccess) return -2;
-  static const unsigned long long z[4] = {0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_step_acc), z, sizeof(z)) == hipSuccess ? 0 : -2;
+// Adjugate of a symmetric 3x3 [[a, b, c], [b, d, e], [c, e, f]]: cofactors (symmetric) and det.
+struct Sym3Inv {
+  double c00, c01, c02, c11, c12, c22, det;
+};
+__device__ __forceinline__ Sym3Inv sym3_adj(double a, double b, double c, double d, double e, double f) {
+  Sym3Inv r;
+  r.c00 = fma(d, f, -e * e);
+  r.c01 = fma(c, e, -b * f);
+  r.c02 = fma(b, e, -c * d);
+  r.c11 = fma(a, f, -c * c);
+  r.c12 = fma(b, c, -a * e);
+  r.c22 = fma(a, d, -b * b);
+  r.det = fma(a, r.c00, fma(b, r.c01, c * r.c02));
+  return r;
 }
 
-// Propose the next candidate into s.xc; false = stop (s.term set).  The scaled, regularized matrix
-// is factored in place (21 doubles) and rebuilt from s.A only for another try at a smaller radius.
-__device__ __forceinline__ bool eng_propose(__attribute__((address_space(3))) EngLM& s, int max_it) {
-  // Ceres solves (S A S + D / radius) y = S g and steps -S y (S the Jacobi scaling, D its clamped
-  // diagonal).  With z = S y that is (A + S^-1 D S^-1 / radius) z = g, step -z, and the model cost
-  // change 0.5 (y.Sg + y.(D / radius) y) = 0.5 (z.g + z.(D' / radius) z), D' = S^-1 D S^-1: the same
-  // system without scaling the matrix (s.diag holds D'; s.scale / s.iscale hold S^2 / S^-2).
-  double b[6];
+// Solve M y = b, M = A (packed upper, 6x6) + diag(Dr); false = not positive definite.
+__device__ __forceinline__ bool solve6(const double* A, const double* Dr, const double* b, double* y) {
+  // P (rotation block 0..2), Q (0..2 x 3..5), S (translation block 3..5)
+  const double p00 = A[pu(0, 0)] + Dr[0], p01 = A[pu(0, 1)], p02 = A[pu(0, 2)];
+  const double p11 = A[pu(1, 1)] + Dr[1], p12 = A[pu(1, 2)], p22 = A[pu(2, 2)] + Dr[2];
+  double Q[3][3];
 #pragma unroll
-  for (int e = 0; e < 6; e++) b[e] = s.g[e];
-  while (s.it < max_it) {
-    s.it++;
-    if (!s.reuse)
+  for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int e = 0; e < 6; e++) s.diag[e] = fmin(fmax(s.scale[e] * s.A[pu(e, e)], 1e-6), 1e32) * s.iscale[e];
-    s.reuse = 1;
-    const double ir = 1.0 / s.radius;
-    double Dr[6];
+    for (int j = 0; j < 3; j++) Q[i][j] = A[pu(i, 3 + j)];
+  const Sym3Inv P = sym3_adj(p00, p01, p02, p11, p12, p22);
+  const double ip = rcp_d(P.det);
+  const double adjP[3][3] = {{P.c00, P.c01, P.c02}, {P.c01, P.c11, P.c12}, {P.c02, P.c12, P.c22}};
+  // W = P^-1 Q, u1 = P^-1 b1
+  double W[3][3], u1[3];
 #pragma unroll
-    for (int e = 0; e < 6; e++) Dr[e] = s.diag[e] * ir;
-    // L (lower factor, L[i][j] at pu(j, i)) overwrites A + D' / radius; inv = 1 / L[j][j]
-    double L[21], inv[6];
+  for (int i = 0; i < 3; i++) {
 #pragma unroll
-    for (int j = 0; j < 6; j++)
+    for (int j = 0; j < 3; j++) W[i][j] = fma(adjP[i][0], Q[0][j], fma(adjP[i][1], Q[1][j], adjP[i][2] * Q[2][j])) * ip;
+    u1[i] = fma(adjP[i][0], b[0], fma(adjP[i][1], b[1], adjP[i][2] * b[2])) * ip;
+  }
+  // Schur complement S' = S - Q^T W, h = b2 - Q^T u1
+  double Sp[3][3], h[3];
 #pragma unroll
-      for (int i = j; i < 6; i++) L[pu(j, i)] = s.A[pu(j, i)];
-    bool ok = true;
-    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < 3; i++) {
 #pragma unroll
-    for (int j = 0; j < 6; j++) {
-      double d = L[pu(j, j)] + Dr[j];
-#pragma unroll
-      for (int k = 0; k < j; k++) d = fma(-L[pu(k, j)], L[pu(k, j)], d);
-      ok = ok && d > 0.0;
-      inv[j] = rsqrt_d(d > 0.0 ? d : 1.0);
-#pragma unroll
-      for (int i = j + 1; i < 6; i++) {
-        double v = L[pu(j, i)];
-#pragma unroll
-        for (int k = 0; k < j; k++) v = fma(-L[pu(k, i)], L[pu(k, j)], v);
-        L[pu(j, i)] = v * inv[j];
-      }
+    for (int j = i; j < 3; j++) {
+      const double sij = A[pu(3 + i, 3 + j)] + (i == j ? Dr[3 + i] : 0.0);
+      Sp[i][j] = sij - fma(Q[0][i], W[0][j], fma(Q[1][i], W[1][j], Q[2][i] * W[2][j]));
     }
-    double y[6];
-    if (s.prof) s.pacc[1] += __builtin_amdgcn_s_memrealtime() - tf0;
+    h[i] = b[3 + i] - fma(Q[0][i], u1[0], fma(Q[1][i], u1[1], Q[2][i] * u1[2]));
+  }
+  const Sym3Inv S = sym3_adj(Sp[0][0], Sp[0][1], Sp[0][2], Sp[1][1], Sp[1][2], Sp[2][2]);
+  const double is = rcp_d(S.det);
+  const double adjS[3][3] = {{S.c00, S.c01, S.c02}, {S.c01, S.c11, S.c12}, {S.c02, S.c12, S.c22}};
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-      double v = b[i];
+  for (int i = 0; i < 3; i++) y[3 + i] = fma(adjS[i][0], h[0], fma(adjS[i][1], h[1], adjS[i][2] * h[2])) * is;
+  // y1 = u1 - W y2
 #pragma unroll
-      for (int k = 0; k < i; k++) v = fma(-L[pu(k, i)], y[k], v);
-      y[i] = v * inv[i];
-    }
+  for (int i = 0; i < 3; i++) y[i] = u1[i] - fma(W[i][0], y[3], fma(W[i][1], y[4], W[i][2] * y[5]));
+  // Sylvester: leading minors of P and of S' positive <=> M positive definite
+  return p00 > 0.0 && P.c22 > 0.0 && P.det > 0.0 && Sp[0][0] > 0.0 && S.c22 > 0.0 && S.det > 0.0;
+}
+
+typedef __attribute__((address_space(3))) EngLM LdsLM;
+
+// Propose the next candidate into s.xc; false = stop (s.term set).  Ceres solves (S A S + D /
+// radius) y = S g and steps -S y (S the Jacobi scaling, D its clamped diagonal).  With z = S y that
+// is (A + S^-1 D S^-1 / radius) z = g, step -z, and the model cost change 0.5 (z.g + z.(D' /
+// radius) z), D' = S^-1 D S^-1 (s.diag): the same system without scaling the matrix.
+// A / g: the current evaluation (registers) -- s.A / s.g hold the same values.
+__device__ __forceinline__ bool eng_propose(LdsLM& s, const double* A, const double* g, int max_it) {
+  int it = s.it, invalid = s.invalid, reuse = s.reuse;
+  double radius = s.radius, ir = s.ir, dfac = s.dfac;
+  double diag[6];
 #pragma unroll
-    for (int i = 5; i >= 0; i--) {
-      double v = y[i];
+  for (int e = 0; e < 6; e++) diag[e] = s.diag[e];
+  bool out = false;
+  int term = 0;
+  while (it < max_it) {
+    it++;
+    if (!reuse)
 #pragma unroll
-      for (int k = i + 1; k < 6; k++) v = fma(-L[pu(i, k)], y[k], v);
-      y[i] = v * inv[i];
-    }
-    double mcc = 0.0, yb = 0.0, yd = 0.0;
+      for (int e = 0; e < 6; e++) diag[e] = fmin(fmax(s.scale[e] * A[pu(e, e)], 1e-6), 1e32) * s.iscale[e];
+    reuse = 1;
+    double Dr[6], y[6];
 #pragma unroll
-    for (int i = 0; i < 6; i++) { ok = ok && isfinite(y[i]); yb = fma(y[i], b[i], yb); yd = fma(y[i] * Dr[i], y[i], yd); }
-    if (ok) mcc = 0.5 * (yb + yd);
+    for (int e = 0; e < 6; e++) Dr[e] = diag[e] * ir;
+    bool ok = solve6(A, Dr, g, y);
+    double yb = 0.0, yd = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) { ok = ok && isfinite(y[i]); yb = fma(y[i], g[i], yb); yd = fma(y[i] * Dr[i], y[i], yd); }
+    const double mcc = ok ? 0.5 * (yb + yd) : 0.0;
     if (!ok || !(mcc > 0.0)) {  // invalid step: rejected-step radius update, solve again
-      if (++s.invalid >= 5) { s.term = 2; return false; }
-      s.radius /= s.dfac;
-      s.dfac *= 2.0;
+      if (++invalid >= 5) { term = 2; break; }
+      radius /= dfac;
+      ir *= dfac;  // dfac: a power of two, exact
+      dfac *= 2.0;
       continue;
     }
-    s.invalid = 0;
+    invalid = 0;
     double delta[6], x[7], xc[7];
 #pragma unroll
     for (int k = 0; k < 6; k++) delta[k] = -y[k];
@@ -2082,225 +2065,288 @@ __device__ __forceinline__ bool eng_propose(__attribute__((address_space(3))) En
 #pragma unroll
     for (int k = 0; k < 7; k++) s.xc[k] = xc[k];
     s.mcc = mcc;
-    return true;
+    out = true;
+    break;
   }
-  s.term = 0;  // NO_CONVERGENCE: max_num_iterations
-  return false;
+  s.it = it; s.invalid = invalid; s.reuse = reuse;
+  s.radius = radius; s.ir = ir; s.dfac = dfac;
+#pragma unroll
+  for (int e = 0; e < 6; e++) s.diag[e] = diag[e];
+  if (!out) s.term = term;  // 0 NO_CONVERGENCE (max_num_iterations) or 2 FAILURE
+  return out;
 }
 
 // After the evaluation at x0 (first) or at the candidate s.xc (acc, lislam_lm.hpp layout):
 // lm_start / lm_next, then one propose.  Returns whether a candidate (s.xc) must be evaluated.
-typedef __attribute__((address_space(3))) EngLM LdsLM;
-typedef const __attribute__((address_space(3))) double LdsD;
-// The state and the evaluation stay in LDS, addressed as LDS (ds_read / ds_write): through the
-// generic pointers a call receives they would be flat accesses, each waiting on both counters.
-#ifdef LISLAM_STEP_NOINLINE
-#define LISLAM_STEP_ATTR __noinline__
-#else
-#define LISLAM_STEP_ATTR __forceinline__  // a call saves / restores 24 callee-saved VGPRs through scratch per step
-#endif
-__device__ LISLAM_STEP_ATTR bool eng_step(LdsLM& s, LdsD* x0, LdsD* acc, bool first, int max_it) {
-  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-  bool cont = true;
+__device__ __forceinline__ bool eng_step(LdsLM& s, const double* x0, const double (&acc)[kAcc], bool first, int max_it) {
+  const double* Aa = acc + 1;
+  const double* ga = acc + 22;
   if (first) {
-    double x[7], g[6];
+    double x[7];
+#pragma unroll
     for (int e = 0; e < 7; e++) { x[e] = x0[e]; s.x[e] = x[e]; }
     s.cost = acc[0];
-    for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
-    for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
+#pragma unroll
+    for (int e = 0; e < 21; e++) s.A[e] = Aa[e];
+#pragma unroll
+    for (int e = 0; e < 6; e++) s.g[e] = ga[e];
+#pragma unroll
     for (int e = 0; e < 6; e++) {  // jacobi scaling S = 1 / (1 + sqrt(A_ee)), kept as S^2 and 1 / S^2
-      const double r = 1.0 + sqrt(acc[1 + pu(e, e)]);
+      const double r = 1.0 + sqrt(Aa[pu(e, e)]);
       const double sc = 1.0 / r;
       s.scale[e] = sc * sc;
       s.iscale[e] = r * r;
     }
-    s.radius = 1e4; s.dfac = 2.0; s.reuse = 0; s.mcc = 0;
-    s.it = 0; s.invalid = 0; s.term = 0;
-    if (!isfinite(s.cost)) { s.term = 2; cont = false; }
-    else if (eng_grad_small(x, g)) { s.term = 1; cont = false; }
-  } else {
-    double ccost = acc[0];
-    if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
-    double xc[7], xn = 0, sn = 0;
-    for (int e = 0; e < 7; e++) {
-      const double xe = s.x[e];
-      xc[e] = s.xc[e];
-      xn = fma(xe, xe, xn);
-      sn = fma(xe - xc[e], xe - xc[e], sn);
-    }
-    xn = sqrt(xn); sn = sqrt(sn);
-    const double cost = s.cost;
-    if (sn <= 1e-8 * (xn + 1e-8)) { s.term = 1; cont = false; }                  // parameter_tolerance
-    else if (fabs(cost - ccost) <= 1e-6 * cost) { s.term = 1; cont = false; }    // function_tolerance
-    else {
-      const double rel = (cost - ccost) / s.mcc;
-      if (rel > 1e-3) {  // min_relative_decrease: accept
-        double g[6];
-        for (int e = 0; e < 7; e++) s.x[e] = xc[e];
-        for (int e = 0; e < 21; e++) s.A[e] = acc[1 + e];
-        for (int e = 0; e < 6; e++) { g[e] = acc[22 + e]; s.g[e] = g[e]; }
-        s.cost = ccost;
-        const double t3 = 2.0 * rel - 1.0;
-        s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
-        s.dfac = 2.0;
-        s.reuse = 0;
-        if (eng_grad_small(xc, g)) { s.term = 1; cont = false; }                 // gradient_tolerance
-      } else {  // reject
-        s.radius /= s.dfac;
-        s.dfac *= 2.0;
-        s.reuse = 1;
-      }
-      if (cont && s.radius <= 1e-32) { s.term = 1; cont = false; }
-    }
+    s.radius = 1e4; s.ir = 1.0 / 1e4; s.dfac = 2.0; s.reuse = 0; s.mcc = 0; s.imcc = 0;
+    s.it = 0; s.invalid = 0; s.term = 0; s.ptol = 0;
+    if (!isfinite(acc[0])) { s.term = 2; return false; }
+    if (eng_grad_small(x, ga)) { s.term = 1; return false; }
+    return eng_propose(s, Aa, ga, max_it);
   }
-  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
-  const bool r = cont && eng_propose(s, max_it);
-  if (s.prof) {  // LDS counters: a global read-modify-write here would sit inside the timed window
-    s.pacc[0] += ts1 - ts0;
-    s.pacc[2] += __builtin_amdgcn_s_memrealtime() - ts1;
-    s.pacc[3] += 1;
+  double ccost = acc[0];
+  if (!isfinite(ccost)) ccost = 1.7976931348623157e308;
+  const double cost = s.cost;
+  if (s.ptol) { s.term = 1; return false; }                                   // parameter_tolerance
+  if (fabs(cost - ccost) <= 1e-6 * cost) { s.term = 1; return false; }        // function_tolerance
+  const double rel = (cost - ccost) * s.imcc;
+  if (rel > 1e-3) {  // min_relative_decrease: accept
+    double xc[7];
+#pragma unroll
+    for (int e = 0; e < 7; e++) { xc[e] = s.xc[e]; s.x[e] = xc[e]; }
+#pragma unroll
+    for (int e = 0; e < 21; e++) s.A[e] = Aa[e];
+#pragma unroll
+    for (int e = 0; e < 6; e++) s.g[e] = ga[e];
+    s.cost = ccost;
+    const double t3 = fma(2.0, rel, -1.0);
+    const double m = fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3);
+    const double radius = fmin(1e16, s.radius / m);
+    s.radius = radius;
+    s.ir = fmax(1e-16, s.ir * m);
+    s.dfac = 2.0;
+    s.reuse = 0;
+    if (eng_grad_small(xc, ga)) { s.term = 1; return false; }                 // gradient_tolerance
+    if (radius <= 1e-32) { s.term = 1; return false; }
+    return eng_propose(s, Aa, ga, max_it);
   }
-  return r;
+  // reject: the current point's matrix (s.A, s.g) with a smaller radius
+  const double dfac = s.dfac;
+  s.radius = s.radius / dfac;
+  s.ir = s.ir * dfac;
+  s.dfac = dfac * 2.0;
+  s.reuse = 1;
+  if (s.radius <= 1e-32) { s.term = 1; return false; }
+  double A[21], g[6];
+#pragma unroll
+  for (int e = 0; e < 21; e++) A[e] = s.A[e];
+#pragma unroll
+  for (int e = 0; e < 6; e++) g[e] = s.g[e];
+  return eng_propose(s, A, g, max_it);
 }
 
-// The solve item of (c, r, o) on pair k: records -> LDS, LM, outputs; publishes lm_gen[c].
-__device__ __forceinline__ void eng_solve(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
-                                          int r, int outer, const uint64_t* rec, bool wave0, unsigned tk, int ieff) {
-  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
-  const bool gated_off = a.gate && !a.gate[k];
-  const int total = gated_off ? 0 : ns + nf;
+// While the candidate is evaluated (wave 0): 1 / mcc and the parameter tolerance of the step.
+__device__ __forceinline__ void eng_step_post(LdsLM& s) {
+  double xn = 0.0, sn = 0.0;
+#pragma unroll
+  for (int e = 0; e < 7; e++) {
+    const double xe = s.x[e], d = xe - s.xc[e];
+    xn = fma(xe, xe, xn);
+    sn = fma(d, d, sn);
+  }
+  s.ptol = sqrt(sn) <= 1e-8 * (sqrt(xn) + 1e-8);
+  s.imcc = 1.0 / s.mcc;
+}
+
+// ---- the evaluation: blocks in the evaluating waves' registers, typed slots
+// Waves 1.. of the solve hold the pass's residual blocks in registers, loaded once per pass, in
+// slots of a fixed kind: thread tp's edge slots are corner queries tp + kEvalThreads s, its plane
+// slots surf queries ns + tp + kEvalThreads s.  The block formulas are branch-free (the Huber
+// weight by selects; a missing correspondence weighs 0), so the slots' dependent chains
+// interleave.  Queries beyond the slots (H > 64 lines) are read from the records at each
+// evaluation.
+constexpr int kEvalThreads = kEngThreads - 64;
+constexpr int kEdgeSlots = 2;   // 896 >= 12 * 64 corner queries
+constexpr int kPlaneSlots = 4;  // 1792 >= 24 * 64 surf queries
+
+struct BlkReg {
+  float c[3], a[3];  // query point, first matched point a (edge) / j (plane)
+  double u[3];       // edge: u = (a - b) / |a - b|; plane: unit normal
+  int kd;            // 0 edge, 1 plane, -1 none
+};
+
+__device__ __forceinline__ void rec_unpack(const v4u& q0, const v4u& q1, const v4u& q2, const v4u& q3, BlkReg& b) {
+  b.c[0] = __uint_as_float(q0.x); b.c[1] = __uint_as_float(q0.y); b.c[2] = __uint_as_float(q0.z);
+  b.a[0] = __uint_as_float(q0.w); b.a[1] = __uint_as_float(q1.x); b.a[2] = __uint_as_float(q1.y);
+  b.kd = (int)q1.z;
+  b.u[0] = __longlong_as_double((long long)(((uint64_t)q2.y << 32) | q2.x));
+  b.u[1] = __longlong_as_double((long long)(((uint64_t)q2.w << 32) | q2.z));
+  b.u[2] = __longlong_as_double((long long)(((uint64_t)q3.y << 32) | q3.x));
+}
+// Record w (ok) or a copy of record 0 marked absent: unconditional 16-B loads, no branches.
+__device__ __forceinline__ void rec_load(Rsrc rec, int w, bool ok, BlkReg& b) {
+  const int off = (ok ? w : 0) * kRecBytes;
+  const v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rec, off, 0, kAuxSc1);
+  const v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rec, off + 16, 0, kAuxSc1);
+  const v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rec, off + 32, 0, kAuxSc1);
+  const v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rec, off + 48, 0, kAuxSc1);
+  rec_unpack(q0, q1, q2, q3, b);
+  if (!ok) b.kd = -1;
+}
+
+// HuberLoss(0.1) of s2 = |r|^2: the cost term 0.5 rho and the corrector weight rho' (rho = 2 a
+// sqrt(s) - a^2, rho' = a / sqrt(s) above a^2), both 0 for an absent block; selects, no branches.
+__device__ __forceinline__ void huber_sel(double s2, bool live, double& w, double& cterm) {
+  const bool big = s2 > 0.01;
+  const double rs = rsqrt_d(big ? s2 : 1.0);
+  cterm = live ? (big ? 0.5 * fma(0.2 * s2, rs, -0.01) : 0.5 * s2) : 0.0;
+  w = live ? (big ? fmax(2.2250738585072014e-308, 0.1 * rs) : 1.0) : 0.0;
+}
+
+__device__ __forceinline__ D3 rot_rc(const double* R, const float* c) {
+  const double cx = c[0], cy = c[1], cz = c[2];
+  return D3{fma(R[0], cx, fma(R[1], cy, R[2] * cz)), fma(R[3], cx, fma(R[4], cy, R[5] * cz)),
+            fma(R[6], cx, fma(R[7], cy, R[8] * cz))};
+}
+
+// LidarEdgeFactor block (eng_block's edge form, branch-free).
+__device__ __forceinline__ void eng_edge_sel(const BlkReg& b, const double* R, const D3& t, double (&s)[kAcc]) {
+  const D3 p = rot_rc(R, b.c);
+  const D3 u{b.u[0], b.u[1], b.u[2]};
+  const D3 e{(p.x + t.x) - (double)b.a[0], (p.y + t.y) - (double)b.a[1], (p.z + t.z) - (double)b.a[2]};
+  const double r0 = fma(e.y, u.z, -e.z * u.y), r1 = fma(e.z, u.x, -e.x * u.z), r2 = fma(e.x, u.y, -e.y * u.x);
+  double w, ct;
+  huber_sel(fma(r0, r0, fma(r1, r1, r2 * r2)), b.kd >= 0, w, ct);
+  s[0] += ct;
+  const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
+  const double wuu = w * fma(u.x, u.x, fma(u.y, u.y, u.z * u.z));
+  const double m00 = fma(-wx, u.x, wuu), m01 = -wx * u.y, m02 = -wx * u.z;
+  const double m11 = fma(-wy, u.y, wuu), m12 = -wy * u.z, m22 = fma(-wz, u.z, wuu);
+  const double v0 = w * fma(u.y, r2, -u.z * r1), v1 = w * fma(u.z, r0, -u.x * r2), v2 = w * fma(u.x, r1, -u.y * r0);
+  s[1] += m00; s[2] += m01; s[3] += m02; s[4] += m11; s[5] += m12; s[6] += m22;
+  s[22] += v0; s[23] += v1; s[24] += v2;
+  s[25] += fma(p.y, v2, -p.z * v1); s[26] += fma(p.z, v0, -p.x * v2); s[27] += fma(p.x, v1, -p.y * v0);
+  {
+    const double t0 = fma(-p.z, m01, p.y * m02), t1 = fma(-p.z, m11, p.y * m12), t2 = fma(-p.z, m12, p.y * m22);
+    s[7] += t0; s[8] += t1; s[9] += t2;
+    s[16] += fma(t1, p.z, -t2 * p.y);
+    s[17] += fma(t2, p.x, -t0 * p.z);
+    s[18] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(p.z, m00, -p.x * m02), t1 = fma(p.z, m01, -p.x * m12), t2 = fma(p.z, m02, -p.x * m22);
+    s[10] += t0; s[11] += t1; s[12] += t2;
+    s[19] += fma(t2, p.x, -t0 * p.z);
+    s[20] += fma(t0, p.y, -t1 * p.x);
+  }
+  {
+    const double t0 = fma(-p.y, m00, p.x * m01), t1 = fma(-p.y, m01, p.x * m11), t2 = fma(-p.y, m02, p.x * m12);
+    s[13] += t0; s[14] += t1; s[15] += t2;
+    s[21] += fma(t0, p.y, -t1 * p.x);
+  }
+}
+
+// LidarPlaneFactor block (eng_block's plane form, branch-free).
+__device__ __forceinline__ void eng_plane_sel(const BlkReg& b, const double* R, const D3& t, double (&s)[kAcc]) {
+  const D3 p = rot_rc(R, b.c);
+  const D3 u{b.u[0], b.u[1], b.u[2]};
+  const D3 e{(p.x + t.x) - (double)b.a[0], (p.y + t.y) - (double)b.a[1], (p.z + t.z) - (double)b.a[2]};
+  const double rp = fma(e.x, u.x, fma(e.y, u.y, e.z * u.z));
+  double w, ct;
+  huber_sel(rp * rp, b.kd >= 0, w, ct);
+  s[0] += ct;
+  const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
+  const D3 av{fma(p.y, u.z, -p.z * u.y), fma(p.z, u.x, -p.x * u.z), fma(p.x, u.y, -p.y * u.x)};
+  const double ax = w * av.x, ay = w * av.y, az = w * av.z;
+  s[1] = fma(wx, u.x, s[1]); s[2] = fma(wx, u.y, s[2]); s[3] = fma(wx, u.z, s[3]);
+  s[4] = fma(wy, u.y, s[4]); s[5] = fma(wy, u.z, s[5]); s[6] = fma(wz, u.z, s[6]);
+  s[7] = fma(ax, u.x, s[7]); s[8] = fma(ax, u.y, s[8]); s[9] = fma(ax, u.z, s[9]);
+  s[10] = fma(ay, u.x, s[10]); s[11] = fma(ay, u.y, s[11]); s[12] = fma(ay, u.z, s[12]);
+  s[13] = fma(az, u.x, s[13]); s[14] = fma(az, u.y, s[14]); s[15] = fma(az, u.z, s[15]);
+  s[16] = fma(-ax, av.x, s[16]); s[17] = fma(-ax, av.y, s[17]); s[18] = fma(-ax, av.z, s[18]);
+  s[19] = fma(-ay, av.y, s[19]); s[20] = fma(-ay, av.z, s[20]); s[21] = fma(-az, av.z, s[21]);
+  s[22] = fma(rp, wx, s[22]); s[23] = fma(rp, wy, s[23]); s[24] = fma(rp, wz, s[24]);
+  s[25] = fma(rp, ax, s[25]); s[26] = fma(rp, ay, s[26]); s[27] = fma(rp, az, s[27]);
+}
+
+struct EvalSlots {
+  BlkReg e[kEdgeSlots], p[kPlaneSlots];
+  bool tail;  // wave-uniform: a lane of this wave holds a block in edge slot 1 or plane slot 3
+};
+
+__device__ __forceinline__ void eval_slots_load(Rsrc rec, int ns, int nf, int tp, EvalSlots& S) {
+#pragma unroll
+  for (int k = 0; k < kEdgeSlots; k++) {
+    const int w = tp + k * kEvalThreads;
+    rec_load(rec, w, w < ns, S.e[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kPlaneSlots; k++) {
+    const int q = tp + k * kEvalThreads;
+    rec_load(rec, ns + q, q < nf, S.p[k]);
+  }
+  S.tail = __ballot(tp + kEvalThreads < ns || tp + 3 * kEvalThreads < nf) != 0ull;
+}
+
+// One evaluation at sh.x by the evaluating waves; each wave's 28 sums go to its row sh.red[wave]
+// (lanes 0..3 write 7 each: the reduce-scatter of row_reduce_scatter28, then rows_sum).
+__device__ __forceinline__ void eng_eval_slots(EngShared& sh, const EvalSlots& S, Rsrc rec, int ns, int nf, int tp) {
+  double s[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) s[e] = 0.0;
+  double R[9];
+  D3 t;
+  eng_rt(sh, R, t);
+  eng_edge_sel(S.e[0], R, t, s);
+  eng_plane_sel(S.p[0], R, t, s);
+  eng_plane_sel(S.p[1], R, t, s);
+  eng_plane_sel(S.p[2], R, t, s);
+  if (S.tail) {
+    eng_edge_sel(S.e[1], R, t, s);
+    eng_plane_sel(S.p[3], R, t, s);
+  }
+  // beyond the slots (H > 64 lines): from the records
+  for (int w = tp + kEdgeSlots * kEvalThreads; w < ns; w += kEvalThreads) {
+    BlkReg b;
+    rec_load(rec, w, true, b);
+    eng_edge_sel(b, R, t, s);
+  }
+  for (int q = tp + kPlaneSlots * kEvalThreads; q < nf; q += kEvalThreads) {
+    BlkReg b;
+    rec_load(rec, ns + q, true, b);
+    eng_plane_sel(b, R, t, s);
+  }
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  double o[7];
+  const int part = row_reduce_scatter28(s, o);
+#pragma unroll
+  for (int q = 0; q < 7; q++) o[q] = rows_sum(o[q]);  // the wave's sums of part(lane)
+  if (lane < 4) {
+    const int base = part_base(part);
+#pragma unroll
+    for (int q = 0; q < 7; q++) sh.red[wv][base + q] = o[q];
+  }
+}
+
+// Wave 0, after the evaluating waves' rows are in: acc (lislam_lm.hpp layout) in every lane.
+__device__ __forceinline__ void eng_gather_rows(EngShared& sh, double (&acc)[kAcc]) {
   const int lane = lane_id();
-  // the first evaluation at x (sh.x, the items' x): the sum of the items' shares
-  {  // entry e = tid % 32 of items tid / 32, tid / 32 + 16, ...: all loads in flight, then 16 rows in LDS
-    const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const double* part = a.eng_part + (size_t)c * ctl.I * 32 + e;
-    double t = 0.0;
-    for (int it0 = g; it0 < ieff; it0 += 16 * 24) {  // 24 loads in flight per thread (384 items per pass)
-      double v[24];
+  if (lane < kAcc) {
+    double r[kEngWaves - 1];
 #pragma unroll
-      for (int j = 0; j < 24; j++) {
-        const int it = it0 + 16 * j;
-        v[j] = (e < 30 && it < ieff) ? ld_sc1d(part + (size_t)it * 32) : 0.0;
-      }
+    for (int w = 1; w < kEngWaves; w++) r[w - 1] = sh.red[w][lane];
+    // pairwise tree over the rows (independent adds, not a serial chain)
 #pragma unroll
-      for (int j = 0; j < 24; j++) t += v[j];
-    }
-    if (e < 30) sh.red[g][e] = t;
-    if (e == 30 && g < 7) sh.x[g] = eng_x_word(a, c, r, outer, g);  // in flight with the shares
-    __syncthreads();
-    if (threadIdx.x < 30) {
-      double sum = 0.0;
-      for (int r2 = 0; r2 < 16; r2++) sum += sh.red[r2][threadIdx.x];
-      if (threadIdx.x < kAcc) {
-        double sc;
-        const int ai = acc_index(threadIdx.x, &sc);
-        sh.acc[ai] = sc * sum;
-      } else {
-        sh.cnt[0][threadIdx.x - kAcc] = (int)sum;
-      }
-    }
-    __syncthreads();
+    for (int h = 1; h < kEngWaves - 1; h <<= 1)
+#pragma unroll
+      for (int w = 0; w + h < kEngWaves - 1; w += 2 * h) r[w] += r[w + h];
+    double sc;
+    const int ai = acc_index(lane, &sc);
+    sh.acc[ai] = sc * r[0];
   }
-  const int nc = uni(sh.cnt[0][0]), np = uni(sh.cnt[0][1]);
-  bool go = (nc + np) > 0;  // no residual blocks: Ceres leaves the parameters untouched
-  unsigned long long t_ev = 0;
-  if (threadIdx.x == 0) { t_ev = rt_now(); eng_prof(tk, 2, t_ev); }
-  // One loop, one (inlined) step site: pass 0 is the first step on lane 0 while the other waves
-  // bring the blocks into LDS; every later pass evaluates at the candidate, then steps.
-  for (int pass = 0; go; pass++) {
-    if (pass > 0) {
-      eng_evaluate(sh, rec, total, tk);  // cost + J^T J + J^T r at each candidate
-    } else if (!wave0) {
-      // records -> LDS: every record's seven words in flight before any is stored (the loads
-      // are agent-scope atomics, which the compiler does not batch across loop iterations)
-      constexpr int kStride = kEngThreads - 64;
-      const int n = min(total, kEngLds);
-      for (int i0 = threadIdx.x - 64; i0 < n; i0 += kRecUnroll * kStride) {
-        uint64_t w[kRecUnroll][7];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int u = 0; u < kRecUnroll; u++) {
-          const int i = i0 + u * kStride;
-          const uint64_t* rw = rec + (size_t)(i < n ? i : 0) * kRecWords;
-#pragma unroll
-          for (int e = 0; e < 7; e++) w[u][e] = i < n ? ld_sc1(rw + e) : 0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < kRecUnroll; u++) {
-          const int i = i0 + u * kStride;
-          if (i < n) {
-            sh.kd[i] = (int8_t)(int)(uint32_t)w[u][3];
-            sh.cf[0][i] = __uint_as_float((uint32_t)w[u][0]); sh.cf[1][i] = __uint_as_float((uint32_t)(w[u][0] >> 32));
-            sh.cf[2][i] = __uint_as_float((uint32_t)w[u][1]); sh.cf[3][i] = __uint_as_float((uint32_t)(w[u][1] >> 32));
-            sh.cf[4][i] = __uint_as_float((uint32_t)w[u][2]); sh.cf[5][i] = __uint_as_float((uint32_t)(w[u][2] >> 32));
-            sh.ud[0][i] = __longlong_as_double((long long)w[u][4]);
-            sh.ud[1][i] = __longlong_as_double((long long)w[u][5]);
-            sh.ud[2][i] = __longlong_as_double((long long)w[u][6]);
-          }
-        }
-      }
-    }
-    if (wave0) {
-      if (lane == 0) {
-        const unsigned long long t_st = rt_now();
-        if (pass == 0) {
-          lm.prof = g_eng_prof != nullptr;
-          for (int e = 0; e < 4; e++) lm.pacc[e] = 0;
-        } else {
-          eng_prof(tk, 4, t_st - t_ev, true);
-          eng_prof(tk, 6, 1ull, true);
-        }
-        const bool cont = eng_step(*(LdsLM*)&lm, (LdsD*)sh.x, (LdsD*)sh.acc, pass == 0, a.max_iterations);
-        t_ev = rt_now();
-        eng_prof(tk, 5, t_ev - t_st, true);
-        sh.flag = cont;
-        if (cont)
-          for (int e = 0; e < 7; e++) sh.x[e] = lm.xc[e];
-      }
-    }
-    __syncthreads();
-    go = uni(sh.flag);
-    if (pass == 0 && threadIdx.x == 0) t_ev = rt_now();
-  }
-  if (!wave0) return;
-  if (lane != 0) return;
-  int* so = a.stats + (size_t)k * 8;
-  so[outer * 2 + 0] = nc;
-  so[outer * 2 + 1] = np;
-  so[4 + outer] = (nc + np) > 0 ? lm.it : 0;
-  so[6 + outer] = (nc + np) > 0 ? lm.term : 1;
-  double xs[7], pw[7];
-  double* st = a.state + (size_t)c * 16;
-  if (r == 0 && outer == 0) {  // the chain's pose at its first scan
-    if (a.init_state) {
-      for (int e = 0; e < 7; e++) pw[e] = a.init_state[(size_t)c * 14 + 7 + e];
-    } else {
-      for (int e = 0; e < 7; e++) pw[e] = e == 3 ? 1.0 : 0.0;
-    }
-  } else {
-    for (int e = 0; e < 7; e++) pw[e] = ld_sc1d(st + 7 + e);
-  }
-  eng_load_x(a, c, r, outer, xs);  // the pass's starting point (unchanged without blocks)
-  if ((nc + np) > 0)
-    for (int e = 0; e < 7; e++) xs[e] = lm.x[e];
-  if (outer == 1) {
-    // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr (:716-717)
-    DQ qw{pw[0], pw[1], pw[2], pw[3]};
-    D3 tw{pw[4], pw[5], pw[6]};
-    tw = tw + qrot(qw, D3{xs[4], xs[5], xs[6]});
-    qw = qmul(qw, DQ{xs[0], xs[1], xs[2], xs[3]});
-    pw[0] = qw.x; pw[1] = qw.y; pw[2] = qw.z; pw[3] = qw.w; pw[4] = tw.x; pw[5] = tw.y; pw[6] = tw.z;
-    double* op = a.para + (size_t)k * 7;
-    double* ow = a.pose + (size_t)k * 7;
-    for (int e = 0; e < 7; e++) { op[e] = xs[e]; ow[e] = pw[e]; }
-  }
-  for (int e = 0; e < 7; e++) { st_sc1d(st + e, xs[e]); st_sc1d(st + 7 + e, pw[e]); }
-  drain_stores();
-  st_rlx(ctl.lm_gen(c), (unsigned)(2 * r + outer + 1));
-  eng_trace(1, 5u);
-  eng_prof(tk, 3, rt_now());
-  if ((nc + np) > 0 && lm.prof)
-    for (int e = 0; e < 4; e++)
-      __hip_atomic_fetch_add(&g_step_acc[e], lm.pacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int e = 0; e < kAcc; e++) acc[e] = sh.acc[e];
 }
 
 // Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
@@ -2308,6 +2354,190 @@ __device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& c
   if (a.gate && !a.gate[k]) return 0;
   return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + kEngQ - 1) / kEngQ, ctl.budget));
 }
+
+// ---- the solve role: one workgroup per chain, for the whole chain
+// Pass ro = 2 r + o of chain c (pair k): wait for its association items, sum their shares of the
+// first evaluation (16-B loads) while the evaluating waves load the records into their slots, then
+// the LM loop (wave 0 steps, waves 1.. evaluate; 1 + 2 barriers per iteration), then publish x
+// (para_q / para_t, write-through) and lm_gen[c] = ro + 1.  The chain's x and pose stay in LDS.
+__device__ __forceinline__ void eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
+                                               int ieff, Rsrc rec, bool wave0, unsigned tk) {
+  const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
+  const int lane = lane_id();
+  const int tp = (int)threadIdx.x - 64;
+  EvalSlots S;
+  if (!wave0 && ieff > 0) eval_slots_load(rec, ns, nf, tp, S);  // in flight with the shares
+  {  // the items' shares: quad q = tid % 16 (doubles 2q, 2q + 1) of items tid / 16, + 32, + 64, ...
+    const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
+    double t0 = 0.0, t1 = 0.0;
+    for (int it0 = g; it0 < ieff; it0 += 32 * 8) {
+      v4u v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int it = it0 + 32 * j;
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(parts, (it < ieff ? it : 0) * 256 + q * 16, 0, kAuxSc1);
+        if (!(it < ieff && q < 15)) v[j] = v4u{0u, 0u, 0u, 0u};
+      }
+      double d0[8], d1[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        d0[j] = __longlong_as_double((long long)(((uint64_t)v[j].y << 32) | v[j].x));
+        d1[j] = __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z));
+      }
+#pragma unroll
+      for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+        for (int j = 0; j + h < 8; j += 2 * h) { d0[j] += d0[j + h]; d1[j] += d1[j + h]; }
+      t0 += d0[0];
+      t1 += d1[0];
+    }
+    if (q < 15) { sh.red[g][2 * q] = t0; sh.red[g][2 * q + 1] = t1; }
+  }
+  __syncthreads();
+  LdsLM& s = *(LdsLM*)&lm;
+  // Two loops, one per role, each with the same barriers (1 + 2 per LM iteration): the slots exist
+  // only in the evaluating waves' loop and the step's working set only in wave 0's, so neither is
+  // live across the other (the branch is wave-uniform; s_barrier counts waves).
+  if (wave0) {
+    const unsigned long long tf0 = rt_now();
+    if (lane < 30) {  // the 32 rows of shares: pairwise tree
+      double r[32];
+#pragma unroll
+      for (int w = 0; w < 32; w++) r[w] = sh.red[w][lane];
+#pragma unroll
+      for (int h = 1; h < 32; h <<= 1)
+#pragma unroll
+        for (int w = 0; w + h < 32; w += 2 * h) r[w] += r[w + h];
+      if (lane < kAcc) {
+        double sc;
+        const int ai = acc_index(lane, &sc);
+        sh.acc[ai] = sc * r[0];
+      } else {
+        sh.cnt[0][lane - kAcc] = (int)r[0];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int nc = uni(sh.cnt[0][0]), np = uni(sh.cnt[0][1]);
+    bool cont = false;
+    if (nc + np > 0) {  // no residual blocks: Ceres leaves the parameters untouched
+      double acc[kAcc], x0[7];
+#pragma unroll
+      for (int e = 0; e < kAcc; e++) acc[e] = sh.acc[e];
+#pragma unroll
+      for (int e = 0; e < 7; e++) { x0[e] = sh.cx[e]; sh.x[e] = x0[e]; }
+      cont = eng_step(s, x0, acc, true, a.max_iterations);  // step 0 while the records land
+      if (cont)
+#pragma unroll
+        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+    }
+    if (lane == 0) { sh.flag = cont; sh.nc = nc; sh.np = np; }
+    const unsigned long long tf1 = rt_now();
+    __syncthreads();
+    if (lane == 0) {
+      eng_prof(tk, 0, tf1 - tf0);          // step 0 (wave 0)
+      eng_prof(tk, 7, rt_now() - tf0);     // step 0 and the blocks' load (to the first barrier)
+      eng_prof(tk, 2, tf0);                // shares summed
+    }
+    bool more = uni(sh.flag) != 0;
+    while (more) {
+      const unsigned long long t0 = rt_now();
+      eng_step_post(s);  // while the candidate is evaluated
+      __syncthreads();
+      double acc[kAcc];
+      eng_gather_rows(sh, acc);
+      const unsigned long long t2 = rt_now();
+      const bool c2 = eng_step(s, nullptr, acc, false, a.max_iterations);
+      if (c2)
+#pragma unroll
+        for (int e = 0; e < 7; e++) sh.x[e] = s.xc[e];
+      if (lane == 0) {
+        sh.flag = c2;
+        eng_prof(tk, 4, t2 - t0, true);  // evaluation (wave 0's view: barrier to barrier) + the rows' sums
+        eng_prof(tk, 5, rt_now() - t2, true);  // step
+        eng_prof(tk, 6, 1ull, true);
+      }
+      __syncthreads();
+      more = uni(sh.flag) != 0;
+    }
+  } else {
+    __syncthreads();
+    bool more = uni(sh.flag) != 0;
+    while (more) {
+      eng_eval_slots(sh, S, rec, ns, nf, tp);  // cost + J^T J + J^T r at the candidate
+      __syncthreads();
+      __syncthreads();  // wave 0's step
+      more = uni(sh.flag) != 0;
+    }
+  }
+}
+
+// The solve role of chain c (ticket c): every pass of the chain, in order.  false = aborted.
+__device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c,
+                                               bool wave0, unsigned tk) {
+  const int lane = lane_id();
+  const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
+  const Rsrc rec = make_rsrc(a.blk + (size_t)c * rec_stride, (unsigned)((a.cap_sharp + a.cap_flat) * kRecBytes));
+  double* st = a.state + (size_t)c * 16;
+  if (wave0 && lane < 7) {  // the chain's x (para) and pose at its first scan
+    sh.cx[lane] = a.init_state ? a.init_state[(size_t)c * 14 + lane] : (lane == 3 ? 1.0 : 0.0);
+    sh.cpw[lane] = a.init_state ? a.init_state[(size_t)c * 14 + 7 + lane] : (lane == 3 ? 1.0 : 0.0);
+  }
+  if (wave0 && lane == 0 && c == 0 && !a.init_state) {  // scan 0 of the batch: first frame
+    for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
+    for (int e = 0; e < 8; e++) a.stats[e] = 0;
+  }
+  for (int ro = 0; ro < 2 * ctl.R; ro++) {
+    const int r = ro >> 1, o = ro & 1;
+    int k;
+    if (!pair_of(a, c, r, &k)) break;  // uniform: this chain is shorter
+    const int ieff = eng_live_items(a, ctl, k);
+    const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1)) + tk;  // profile slot of the pass (developer builds)
+    if (wave0 && lane == 0) {
+      eng_prof(ptk, 1, rt_now());
+      sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : 1;
+      eng_prof(ptk, 1, rt_now());
+    }
+    __syncthreads();
+    if (!uni(sh.flag0)) return false;
+    eng_solve_pass(a, ctl, sh, lm, c, k, ieff, rec, wave0, ptk);
+    if (wave0 && lane == 0) {
+      const int nc = sh.nc, np = sh.np;
+      int* so = a.stats + (size_t)k * 8;
+      so[o * 2 + 0] = nc;
+      so[o * 2 + 1] = np;
+      so[4 + o] = (nc + np) > 0 ? lm.it : 0;
+      so[6 + o] = (nc + np) > 0 ? lm.term : 1;
+      double xs[7];
+#pragma unroll
+      for (int e = 0; e < 7; e++) xs[e] = (nc + np) > 0 ? lm.x[e] : sh.cx[e];  // unchanged without blocks
+#pragma unroll
+      for (int e = 0; e < 7; e++) st_sc1d(st + e, xs[e]);  // the next pass's items start from it
+      drain_stores();
+      st_rlx(ctl.lm_gen(c), (unsigned)(ro + 1));
+#pragma unroll
+      for (int e = 0; e < 7; e++) sh.cx[e] = xs[e];
+      if (o == 1) {
+        // t_w_curr = t_w_curr + q_w_curr * t_last_curr; q_w_curr = q_w_curr * q_last_curr (:716-717)
+        DQ qw{sh.cpw[0], sh.cpw[1], sh.cpw[2], sh.cpw[3]};
+        D3 tw{sh.cpw[4], sh.cpw[5], sh.cpw[6]};
+        tw = tw + qrot(qw, D3{xs[4], xs[5], xs[6]});
+        qw = qmul(qw, DQ{xs[0], xs[1], xs[2], xs[3]});
+        const double pw[7] = {qw.x, qw.y, qw.z, qw.w, tw.x, tw.y, tw.z};
+        double* op = a.para + (size_t)k * 7;
+        double* ow = a.pose + (size_t)k * 7;
+        for (int e = 0; e < 7; e++) { op[e] = xs[e]; ow[e] = pw[e]; sh.cpw[e] = pw[e]; }
+      }
+      eng_trace(1, 5u);
+      eng_prof(ptk, 3, rt_now());
+    }
+    __syncthreads();
+  }
+  if (wave0 && lane < 7) { st[lane] = sh.cx[lane]; st[7 + lane] = sh.cpw[lane]; }  // the chain's final state
+  return true;
+}
+
 
 // Touch (one dword per 128-B line, plain loads: they allocate in this XCD's L2) every structure the
 // association of pair k reads: the Morton copies, the chunk / super-chunk boxes and the clouds of
@@ -2336,15 +2566,103 @@ __device__ __forceinline__ void eng_prefetch(const OdomArgs& a, EngShared& sh, i
   if (acc == 0x9e3779b9u) sh.sink = acc;  // keeps the loads
 }
 
-// An association ticket whose solve has not finished yet: its waves 1.. prefetch meanwhile.
-__device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCtl& ctl, unsigned t, unsigned per_ro) {
-  if (!ctl.prefetch) return 0;
-  const int ro = (int)(t / per_ro), rem = (int)(t % per_ro);
-  const int c = rem / (ctl.I + 1), item = rem % (ctl.I + 1);
-  if (item >= ctl.I || ro >= 2 * ctl.R || ro == 0) return 0;
+// Tickets: [0, C) the chains' solve roles, then the association items in (pass, chain, item)
+// order.  Item ticket t -> pass ro, chain c, item; pidx = its slot in the developer profile
+// (ro * C * (I + 1) + c * (I + 1) + item; the solve of a pass at item = I).
+struct ItemTicket {
+  int ro, c, item;
+};
+__device__ __forceinline__ ItemTicket item_ticket(const EngCtl& ctl, unsigned t) {
+  const unsigned tt = t - (unsigned)ctl.roles, per_ro = (unsigned)ctl.C * ctl.I;
+  const int ro = (int)(tt / per_ro), rem = (int)(tt % per_ro);
+  return ItemTicket{ro, rem / ctl.I, rem % ctl.I};
+}
+
+// An association ticket whose pass's x does not exist yet: its waves 1.. prefetch meanwhile.
+__device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCtl& ctl, unsigned t, unsigned total) {
+  if (!ctl.prefetch || t < (unsigned)ctl.roles || t >= total) return 0;
+  const ItemTicket it = item_ticket(ctl, t);
+  if (it.ro == 0) return 0;
   int k;
-  if (!pair_of(a, c, ro >> 1, &k) || item >= eng_live_items(a, ctl, k)) return 0;
-  return ld_rlx(ctl.lm_gen(c)) < (unsigned)ro ? 1 : 0;
+  if (!pair_of(a, it.c, it.ro >> 1, &k) || it.item >= eng_live_items(a, ctl, k)) return 0;
+  return ld_rlx(ctl.lm_gen(it.c)) < (unsigned)it.ro ? 1 : 0;
+}
+
+// One association item ticket (pass ro, chain c, item): wait for the pass's x, run the item's
+// queries, publish its records and share.  false = aborted.
+__device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, bool wave0, bool lead,
+                                                const ItemTicket& it) {
+  bool ok = true;
+  const int ro = uni(it.ro), c = uni(it.c), item = uni(it.item);
+  const int r = ro >> 1, o = ro & 1;
+  const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1) + c * (ctl.I + 1) + item);
+  if (wave0 && lead) eng_prof(ptk, 0, rt_now());
+  int k;
+  bool live = pair_of(a, c, r, &k);
+  // items holding queries of pair k: ceil((sharp + flat) / kEngQ), none for a gated-off scan
+  const int ieff = live ? eng_live_items(a, ctl, k) : 0;
+  if (item >= ieff) live = false;  // an empty item: nothing to wait for or signal
+  const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
+  const Rsrc rec = make_rsrc(a.blk + (size_t)c * rec_stride, (unsigned)((a.cap_sharp + a.cap_flat) * kRecBytes));
+  int* warm = a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4;
+  // An item of the second outer pass first waits for the first pass's items (its seeds), long
+  // done in the common case; then every wave loads what needs no x while the lead waits for x.
+  if (wave0) {
+    if (lead) sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : true;
+  }
+  __syncthreads();
+  ok = uni(sh.flag0) != 0;
+  if (ok && live) {  // each wave parks its first query's loads in its LDS slots
+    const ItemPre pre = eng_item_pre(a, k, item * kEngQ + (int)(threadIdx.x >> 6), warm, o);
+    const int wv = (int)(threadIdx.x >> 6), l = lane_id();
+    P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
+    int wi = pre.wi[0];
+    if (l == 1) { v = pre.wp[0]; wi = pre.wi[1]; }
+    if (l == 2) { v = pre.wp[1]; wi = pre.wi[2]; }
+    if (l == 3) v = pre.wp[2];
+    if (l < 4) sh.prew[wv][l] = v;
+    if (l < 3) sh.prei[wv][l] = wi;
+  }
+  if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
+  if (wave0) {
+    if (lead) {
+      if (ok && live) {
+        eng_prof(ptk, 2, rt_now());  // the item's lead starts its wait for x
+        ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks);
+        eng_trace(1, ok ? 2u : 99u);
+        eng_prof(ptk, 1, rt_now());
+      }
+      sh.flag = ok;
+    }
+  }
+  __syncthreads();
+  ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
+  if (ok && live) {
+    {  // each wave its own copy of x (its lanes 0..6 load it): no barrier
+      const int l = lane_id();
+      if (l < 7) sh.xw[threadIdx.x >> 6][l] = eng_x_word(a, c, r, o, l);
+    }
+    eng_item_run(a, sh, k, item, ieff, rec, warm, o, ptk);
+    drain_stores();  // this wave's record (and seed) stores
+    __syncthreads();
+    if (wave0) {
+      const unsigned long long tp0 = lead ? rt_now() : 0ull;
+      if (lane_id() < 30) {  // the item's share: the sum of its waves' shares
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < kEngWaves; w++) v += sh.red[w][lane_id()];
+        st_sc1d(a.eng_part + ((size_t)c * ctl.I + item) * 32 + lane_id(), v);
+      }
+      drain_stores();
+      if (lead) {
+        eng_prof(ptk, 7, rt_now() - tp0);
+        add_rlx(ctl.assoc_done(c, ro), 1u);
+        eng_trace(1, 4u);
+        eng_prof(ptk, 3, rt_now());
+      }
+    }
+  }
+  return ok;
 }
 
 // Control flow around the workgroup barriers.  Every branch tests a wave-uniform scalar: LDS
@@ -2353,112 +2671,82 @@ __device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCt
 // loop takes its next ticket at the bottom and tests it at the top.  (A `for (;;)` opening with
 // `if (threadIdx.x == 0)` let the compiler rotate the divergent block into the latch, so wave 0's
 // other lanes reached the next barrier ahead of lane 0 and the waves' barrier counts diverged.)
+// The first C tickets are the solve roles: they are claimed before any item, by running workgroups,
+// so every item a role waits for is claimed by a running workgroup too; the queue drains on any
+// grid of at least C + 1 workgroups (launch_odometry_chain enforces it).
 __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   __shared__ EngLM lm;
-  const unsigned per_ro = (unsigned)ctl.C * (ctl.I + 1);
-  const unsigned total = per_ro * 2u * ctl.R;
-  const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
+  const unsigned per_ro = (unsigned)ctl.C * ctl.I;
+  const unsigned total = (unsigned)ctl.roles + per_ro * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
   const bool lead = lane_id() == 0;
   if (wave0) {
     if (lead) {
       const unsigned t = add_rlx(ctl.ticket(), 1u);
       sh.ticket = t;
-      sh.pref = eng_wants_prefetch(a, ctl, t, per_ro);
+      sh.pref = eng_wants_prefetch(a, ctl, t, total);
       eng_trace(0, t);
-      if (t < total) eng_prof(t, 0, rt_now());
     }
   }
   __syncthreads();
   unsigned tk = (unsigned)uni((int)sh.ticket);
   while (tk < total) {
-    const int ro = uni((int)(tk / per_ro)), rem = (int)(tk % per_ro);
-    const int r = ro >> 1, o = ro & 1, c = uni(rem / (ctl.I + 1)), item = uni(rem % (ctl.I + 1));
-    int k;
-    bool live = pair_of(a, c, r, &k);
-    // items holding queries of pair k: ceil((sharp + flat) / kEngQ), none for a gated-off scan
-    const int ieff = live ? eng_live_items(a, ctl, k) : 0;
-    if (item < ctl.I && item >= ieff) live = false;  // an empty item: nothing to wait for or signal
-    uint64_t* rec = reinterpret_cast<uint64_t*>(a.blk + (size_t)c * rec_stride);
-    int* warm = a.warm + (size_t)c * (a.cap_sharp + a.cap_flat) * 4;
-    const bool is_item = item < ctl.I;
-    // An item of the second outer pass first waits for the first pass's items (its seeds), long
-    // done in the common case; then every wave loads what needs no x while the lead waits for x.
-    if (wave0) {
-      if (lead) sh.flag0 = (live && is_item && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : true;
-    }
-    __syncthreads();
-    bool ok = uni(sh.flag0) != 0;
-    if (ok && live && is_item) {  // each wave parks its first query's loads in its LDS slots
-      const ItemPre pre = eng_item_pre(a, k, item * kEngQ + (int)(threadIdx.x >> 6), warm, o);
-      const int wv = (int)(threadIdx.x >> 6), l = lane_id();
-      P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
-      int wi = pre.wi[0];
-      if (l == 1) { v = pre.wp[0]; wi = pre.wi[1]; }
-      if (l == 2) { v = pre.wp[1]; wi = pre.wi[2]; }
-      if (l == 3) v = pre.wp[2];
-      if (l < 4) sh.prew[wv][l] = v;
-      if (l < 3) sh.prei[wv][l] = wi;
-    }
-    if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
-    if (wave0) {
-      if (lead) {
-        if (ok && live) {
-          // every item after the chain's previous solve; the solve after its pair's live items too
-          // (which imply the first wait, except for a pair without queries: ieff == 0)
-          if (is_item) eng_prof(tk, 2, rt_now());  // the item's lead starts its wait for x
-          ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks);
-          if (ok && !is_item) ok = eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks);
-          eng_trace(1, ok ? 2u : 99u);
-          eng_prof(tk, 1, rt_now());
-          if (ok && c == 0 && r == 0 && o == 0 && !is_item && !a.init_state) {  // scan 0 of the batch: first frame
-            for (int e = 0; e < 7; e++) { a.para[e] = e == 3 ? 1.0 : 0.0; a.pose[e] = e == 3 ? 1.0 : 0.0; }
-            for (int e = 0; e < 8; e++) a.stats[e] = 0;
-          }
-        }
-        sh.flag = ok;
-      }
-    }
-    __syncthreads();
-    ok = uni(sh.flag) != 0;  // false: aborted, leave (the host reads the abort word)
-    if (ok && live) {
-      if (is_item) {
-        {  // each wave its own copy of x (its lanes 0..6 load it): no barrier
-          const int l = lane_id();
-          if (l < 7) sh.xw[threadIdx.x >> 6][l] = eng_x_word(a, c, r, o, l);
-        }
-        eng_item_run(a, sh, k, item, ieff, rec, warm, o, tk);
-        drain_stores();  // this wave's record (and seed) stores
-        __syncthreads();
-        if (wave0) {
-          const unsigned long long tp0 = lead ? rt_now() : 0ull;
-          if (lane_id() < 30) {  // the item's share: the sum of its waves' shares
-            double v = 0.0;
-#pragma unroll
-            for (int w = 0; w < kEngWaves; w++) v += sh.red[w][lane_id()];
-            st_sc1d(a.eng_part + ((size_t)c * ctl.I + item) * 32 + lane_id(), v);
-          }
-          drain_stores();
-          if (lead) {
-            eng_prof(tk, 7, rt_now() - tp0);
-            add_rlx(ctl.assoc_done(c, ro), 1u);
-            eng_trace(1, 4u);
-            eng_prof(tk, 3, rt_now());
-          }
-        }
-      } else {
-        eng_solve(a, ctl, sh, lm, c, k, r, o, rec, wave0, tk, ieff);
-        __syncthreads();
-      }
+    bool ok = true;
+    if (tk < (unsigned)ctl.roles) {
+      const int c = uni((int)tk);
+      ok = eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+    } else {
+      ok = eng_item_ticket(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
     }
     if (wave0) {
       if (lead) {
         const unsigned t = add_rlx(ctl.ticket(), 1u);
         sh.ticket = t;
-        sh.pref = eng_wants_prefetch(a, ctl, t, per_ro);
+        sh.pref = eng_wants_prefetch(a, ctl, t, total);
         eng_trace(0, t);
-        if (t < total) eng_prof(t, 0, rt_now());
+      }
+    }
+    __syncthreads();
+    tk = ok ? (unsigned)uni((int)sh.ticket) : total;
+  }
+}
+
+// ---- the engine as two launches (the production schedule): the chains' solve roles, one
+// workgroup per chain (256 VGPRs: the evaluation's register slots and the step), and the
+// association items (at most 128 VGPRs, a small LDS footprint), on two CU-masked streams: the
+// roles on one reserved CU per XCD, the items on the others.  An item workgroup then leaves half
+// of its CU's registers and most of its LDS to whatever else runs (the next batch's extraction,
+// the ORB front end), and the roles always find a CU (launch_odometry_chain).
+__global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
+  __shared__ EngShared sh;
+  __shared__ EngLM lm;
+  const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
+  const int c = (int)blockIdx.x;
+  (void)eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+}
+
+__global__ __launch_bounds__(kEngThreads, 4) void k_odom_items(OdomArgs a, EngCtl ctl) {
+  __shared__ EngShared sh;
+  const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
+  const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
+  const bool lead = lane_id() == 0;
+  if (wave0) {
+    if (lead) {
+      const unsigned t = add_rlx(ctl.ticket(), 1u);
+      sh.ticket = t;
+      sh.pref = eng_wants_prefetch(a, ctl, t, total);
+    }
+  }
+  __syncthreads();
+  unsigned tk = (unsigned)uni((int)sh.ticket);
+  while (tk < total) {
+    const bool ok = eng_item_ticket(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
+    if (wave0) {
+      if (lead) {
+        const unsigned t = add_rlx(ctl.ticket(), 1u);
+        sh.ticket = t;
+        sh.pref = eng_wants_prefetch(a, ctl, t, total);
       }
     }
     __syncthreads();
@@ -2495,18 +2783,19 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   ctl.R = min(a.chain_len, a.S - 1);
   ctl.I = engine_items(a.cap_sharp + a.cap_flat);
   ctl.prefetch = 1;
+  ctl.roles = ctl.C;
   // every device wait is bounded (2 s); LISLAM_ENGINE_WAIT_US shortens it (tests: a forced abort)
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
-  // Items per (pass, chain): the workgroups resident at once, less the chains' solves (the running
-  // one and the next, already claimed) and one spare, shared by the chains.  More queries than
+  // Items per (pass, chain): the workgroups resident at once, less the chains' solve roles and one
+  // spare, shared by the chains.  More queries than
   // that are dealt as second queries to the items' waves (eng_item_run).  LISLAM_ENGINE_BUDGET
   // overrides (tests).
   int dev = 0;
   (void)hipGetDevice(&dev);
   const int resident = engine_resident(dev);
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
-  ctl.budget = bud ? max(1, atoi(bud)) : max(1, (resident - 2 * ctl.C - 1) / ctl.C);
+  ctl.budget = bud ? max(1, atoi(bud)) : max(1, (resident - ctl.C - 1) / ctl.C);
   // zero the control words of this launch, all but word 3 (the sticky abort)
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
@@ -2515,8 +2804,80 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
   const int cap = cap_env ? atoi(cap_env) : 0;
   int grid = ctl.C * (ctl.I + 1);
-  if (cap > 0) grid = min(grid, cap);
+  if (cap > 0) grid = min(grid, max(cap, ctl.C + 1));  // the roles and one item worker at least
   hipLaunchKernelGGL(k_odom_chain, dim3(grid), dim3(kEngThreads), 0, st, a, ctl);
+  return grid;
+}
+
+// The engine as two launches on CU-masked streams (k_odom_roles / k_odom_items): the streams of
+// one batch are made once (engine_streams); false = unavailable on this device (the caller runs
+// the single-launch engine instead).  A mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950,
+// measured: scripts/micro/cumask.hip); a mask with no bit of some XCD leaves that XCD unmasked, so
+// the roles get one bit in every XCD and the items every other bit.
+bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
+  hipDeviceProp_t prop{};
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+  const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
+  const int cus = prop.multiProcessorCount, nx = 8;
+  if (!multi_xcd || cus < 4 * nx || cus % nx) return false;
+  const int words = (cus + 31) / 32;
+  std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
+  for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);
+  if (hipExtStreamCreateWithCUMask(roles, words, mr.data()) != hipSuccess) return false;
+  if (hipExtStreamCreateWithCUMask(items, words, mi.data()) != hipSuccess) {
+    (void)hipStreamDestroy(*roles);
+    *roles = nullptr;
+    return false;
+  }
+  return true;
+}
+
+// One engine at a time per device (contexts included): each split launch waits for the previous
+// one, so two pipelined batches' chains do not split the CUs the extraction beside them needs.
+static hipEvent_t engine_done_event(int dev) {
+  static std::mutex mu;
+  static hipEvent_t ev[64] = {};
+  std::lock_guard<std::mutex> lock(mu);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!ev[dev]) (void)hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming);
+  return ev[dev];
+}
+
+int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t roles, hipStream_t items, hipEvent_t fork,
+                                hipEvent_t join_r, hipEvent_t join_i) {
+  if (a.n_chains <= 0) return 0;
+  EngCtl ctl;
+  ctl.w = a.eng_ctl;
+  ctl.C = a.n_chains;
+  ctl.R = min(a.chain_len, a.S - 1);
+  ctl.I = engine_items(a.cap_sharp + a.cap_flat);
+  ctl.prefetch = 1;
+  ctl.roles = 0;
+  const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
+  ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
+  const char* cap_env = getenv("LISLAM_ENGINE_WGS");
+  const int cap = cap_env ? atoi(cap_env) : 0;
+  int grid = ctl.C * ctl.I;
+  if (cap > 0) grid = min(grid, max(cap, 1));  // one item workgroup drains the queue
+  const char* bud = getenv("LISLAM_ENGINE_BUDGET");
+  ctl.budget = bud ? max(1, atoi(bud)) : max(1, grid / ctl.C);
+  const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
+  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
+  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const hipEvent_t prev = engine_done_event(dev);
+  if (prev) (void)hipStreamWaitEvent(st, prev, 0);
+  (void)hipEventRecord(fork, st);
+  (void)hipStreamWaitEvent(roles, fork, 0);
+  (void)hipStreamWaitEvent(items, fork, 0);
+  hipLaunchKernelGGL(k_odom_roles, dim3(ctl.C), dim3(kEngThreads), 0, roles, a, ctl);
+  hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(kEngThreads), 0, items, a, ctl);
+  (void)hipEventRecord(join_r, roles);
+  (void)hipEventRecord(join_i, items);
+  (void)hipStreamWaitEvent(st, join_r, 0);
+  (void)hipStreamWaitEvent(st, join_i, 0);
+  if (prev) (void)hipEventRecord(prev, st);
   return grid;
 }
 

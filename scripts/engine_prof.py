@@ -1,7 +1,10 @@
 """Developer tool (GPU box): phase profile of the chain engine on one continuous chain — per round
 and outer pass, from the device's own clock (s_memrealtime, 10 ns ticks): association span,
 association -> solve hand-off, record load, evaluations, steps, solve -> association hand-off.
-usage: python scripts/engine_prof.py [S]"""
+usage: python scripts/engine_prof.py [S]
+The stamps are compiled out of the production library: build a variant first,
+  bash scripts/build_variant.sh prof lislam_odometry.hip -DLISLAM_ENG_PROF=1
+and run with LISLAM_ALT_LIB=scripts/_ab/liblislam_prof.so."""
 import ctypes
 import os
 import sys
@@ -41,10 +44,8 @@ with pkg.Context() as ctx:
     b.odometry(S, S - 1)
     ctx.synchronize()
     sp = np.zeros(4, np.uint64)
-    lib.lislam_debug_step_prof.argtypes = [ctypes.c_void_p]
     buf = np.zeros((T, 8), np.uint64)
     assert lib.lislam_debug_engine_prof_read(buf.ctypes.data, T) == 0
-    assert lib.lislam_debug_step_prof(sp.ctypes.data) == 0
     lib.lislam_debug_engine_prof(0)
     p = buf.reshape(2 * R, I + 1, 8).astype(np.int64)
     us = 0.01
@@ -65,7 +66,8 @@ with pkg.Context() as ctx:
         "last item done -> solve has every share (gather tail)": (lm_loaded - a_end) * us,
         "solve evaluations (sum)": ev * us,
         "solve steps (sum)": st * us,
-        "solve evaluations: reductions (sum)": lm[:, 7] * us,
+        "solve: step 0 beside the blocks' load (to the first barrier)": lm[:, 7] * us,
+        "solve: step 0 alone (wave 0)": lm[:, 0] * us,
         "solve total (ready -> done)": (lm_done - lm_ready) * us,
         "hand-off solve -> assoc (solve done -> next first item ready)": (a_start[1:] - lm_done[:-1]) * us,
     }
@@ -107,7 +109,5 @@ with pkg.Context() as ctx:
     for k, v in rows.items():
         print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")
     print(f"  evaluations per solve: mean {np.mean(npass):.2f}")
-    n = max(int(sp[3]), 1)
-    print(f"  step sub-phases per step: lm_next logic {sp[0] * us / n:.2f} us, factorization {sp[1] * us / n:.2f} us, "
-          f"propose total {sp[2] * us / n:.2f} us ({n} steps)")
+
     b.close()

@@ -204,6 +204,54 @@ int main() {
     }
     std::printf("batched: 2304 blocks, %d parameter points, 1 launch each\n", points);
   }
+  // Two problems alive at once, each over its own parameter blocks at its own pose (two Ceres
+  // problems, evaluated in turn): each problem's pass is one launch of ITS blocks, the other's
+  // batch survives it, and the values equal a per-problem EvaluateBlocks.
+  {
+    std::vector<std::unique_ptr<lislam::CostFunction>> own[2];
+    std::vector<const lislam::CostFunction*> lists[2];
+    for (int p = 0; p < 2; p++)
+      for (int i = 0; i < 600; i++) {
+        lislam::CostFunction* f = i % 3 == 0 ? LidarEdgeFactor::Create(v3(), v3(), v3(), 1.0)
+                                             : LidarPlaneFactor::Create(v3(), v3(), v3(), v3(), 1.0);
+        own[p].emplace_back(f);
+        lists[p].push_back(f);
+      }
+    double xq[2][4], xt[2][3];
+    const long long before = lislam::FactorLaunches();
+    const int rounds = 3;
+    for (int round = 0; round < rounds; round++) {
+      for (int p = 0; p < 2; p++) {
+        xq[p][0] = A(rng); xq[p][1] = A(rng); xq[p][2] = A(rng);
+        xq[p][3] = std::sqrt(1.0 - xq[p][0] * xq[p][0] - xq[p][1] * xq[p][1] - xq[p][2] * xq[p][2]);
+        for (int k = 0; k < 3; k++) xt[p][k] = U(rng);
+      }
+      std::vector<double> ref[2];
+      for (int p = 0; p < 2; p++) {
+        ref[p].resize(lists[p].size() * 3);
+        std::vector<double> jq(lists[p].size() * 12), jt(lists[p].size() * 9);
+        if (lislam::EvaluateBlocks(lists[p], xq[p], xt[p], ref[p].data(), jq.data(), jt.data()) != LISLAM_OK) return 9;
+      }
+      for (int pass = 0; pass < 2; pass++)
+        for (int p = 0; p < 2; p++) {
+          const double* params[2] = {xq[p], xt[p]};
+          for (size_t i = 0; i < lists[p].size(); i++) {
+            double res[3];
+            if (!lists[p][i]->Evaluate(params, res, nullptr)) return 10;
+            for (int k = 0; k < lists[p][i]->num_residuals(); k++)
+              check(res[k] == ref[p][i * 3 + k], "two-problem residual", (int)i, res[k], ref[p][i * 3 + k]);
+          }
+        }
+    }
+    const long long used = lislam::FactorLaunches() - before;  // (EvaluateBlocks is not counted)
+    // the first pass of the first round: problem 0's launch holds every block not evaluated yet
+    // (problem 1's too), problem 1's first call then launches its own; after that, one per point
+    if (used > 2 * rounds) {
+      std::fprintf(stderr, "two problems: %lld launches for %d rounds (want <= %d)\n", used, rounds, 2 * rounds);
+      g_fail++;
+    }
+    std::printf("two live problems: %lld launches over %d rounds of 2 x 600 blocks\n", used, rounds);
+  }
   // DISTORTION 1 (s != 1: Identity.slerp(s, q), s t; lidarFeaturePointsFunction.hpp:155-162,255-262):
   // kind 5 / 6 blocks, differentiated on the device with dual numbers, against the oracle's Jet
   // autodiff of the same functors and the header's operator()<double>; a quaternion near the

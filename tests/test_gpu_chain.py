@@ -96,10 +96,11 @@ def test_schedules_agree(pkg, synth, ctx, chain_len):
         assert np.array_equal(s0, s1), (k, s0, s1)
 
 
-@pytest.mark.parametrize("wgs", [1, 5])
+@pytest.mark.parametrize("wgs", [1, 2, 5])
 def test_engine_drains_with_few_workgroups(pkg, oracle, synth, ctx, wgs):
-    """The ticket queue needs no co-residency: a grid of 1 (every ticket in turn) or 5 workgroups
-    computes the same chain."""
+    """The ticket queue needs no co-residency beyond the chain's solve role and one item worker: a
+    grid capped at 1 (raised to that minimum of 2 by the launcher), 2 or 5 workgroups computes the
+    same chain."""
     S = 5
     scans = synth.make_sequence(S, start=40)
     feats = [oracle.scan_registration(s) for s in scans]
