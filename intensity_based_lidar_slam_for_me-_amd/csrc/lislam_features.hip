@@ -1055,6 +1055,8 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   // line (and the 64 before / after it) is loaded once: slot t's neighbours come from an LDS ring
   // of three 64-point slots (t - 1, t, t + 1), the next slot's load in flight meanwhile.
   uint32_t linkb = 0;
+  // the box of the points inside the six segments ([sI, eI), a superset of the VoxelGrid's input)
+  float bmn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, bmx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   auto ld_slot = [&](int t) -> P4 {  // cloud point off + 64 t + lane (zero outside the cloud)
     const int i = off + 64 * t + lane;
     return (i >= 0 && i < total) ? ld4(cloud + i) : P4{0.f, 0.f, 0.f, 0.f};
@@ -1089,6 +1091,11 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       }
       curv[i] = c;
       curvl[k] = c;
+      if (k >= 5 && k < len - 6) {
+        const P4 p = nb(0);
+        bmn[0] = fminf(bmn[0], p.x); bmn[1] = fminf(bmn[1], p.y); bmn[2] = fminf(bmn[2], p.z);
+        bmx[0] = fmaxf(bmx[0], p.x); bmx[1] = fmaxf(bmx[1], p.y); bmx[2] = fmaxf(bmx[2], p.z);
+      }
       if (k + 1 < len) {
         const P4 p0 = nb(0), p1 = nb(1);
         const float dx = p1.x - p0.x, dy = p1.y - p0.y, dz = p1.z - p0.z;
@@ -1104,6 +1111,15 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
     if (lane == 0) lmask[1 + t] = m;
   }
   if (lane == 0) { lmask[0] = 0; lmask[kS + 1] = 0; }
+#pragma unroll
+  for (int d = 0; d < 3; d++) {  // wave-uniform from here on
+    for (int o = 32; o > 0; o >>= 1) {
+      bmn[d] = fminf(bmn[d], __shfl_xor(bmn[d], o));
+      bmx[d] = fmaxf(bmx[d], __shfl_xor(bmx[d], o));
+    }
+    bmn[d] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, bmn[d])));
+    bmx[d] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, bmx[d])));
+  }
   wave_sync<true>();
   PHASE(0);
 
@@ -1260,9 +1276,18 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   P4* o_lsharp = a.stg_less_sharp + ((size_t)s * H + line) * kCapLessSharpPerLine;
   P4* o_flat = a.stg_flat + ((size_t)s * H + line) * kCapFlatPerLine;
   P4* o_lflat = a.stg_less_flat + (size_t)s * N + off;
-  for (int k = lane; k < n_sharp; k += 64) st4(o_sharp + k, ld4(cloud + off + ll.sharp[k]));
-  for (int k = lane; k < n_lsharp; k += 64) st4(o_lsharp + k, ld4(cloud + off + ll.less_sharp[k]));
-  for (int k = lane; k < n_flat; k += 64) st4(o_flat + k, ld4(cloud + off + ll.flat[k]));
+  {  // every pick's load in flight before the first store (<= 12 / 120 / 24 picks per line)
+    static_assert(kCapSharpPerLine <= 64 && kCapLessSharpPerLine <= 128 && kCapFlatPerLine <= 64, "pick lanes");
+    const P4 z{0.f, 0.f, 0.f, 0.f};
+    const P4 ps = lane < n_sharp ? ld4(cloud + off + ll.sharp[lane]) : z;
+    const P4 pl0 = lane < n_lsharp ? ld4(cloud + off + ll.less_sharp[lane]) : z;
+    const P4 pl1 = lane + 64 < n_lsharp ? ld4(cloud + off + ll.less_sharp[lane + 64]) : z;
+    const P4 pf = lane < n_flat ? ld4(cloud + off + ll.flat[lane]) : z;
+    if (lane < n_sharp) st4(o_sharp + lane, ps);
+    if (lane < n_lsharp) st4(o_lsharp + lane, pl0);
+    if (lane + 64 < n_lsharp) st4(o_lsharp + lane + 64, pl1);
+    if (lane < n_flat) st4(o_flat + lane, pf);
+  }
   wave_sync<true>();  // the pick lists are dead: their LDS becomes the voxel phase's (LineLds)
   // less-flat points (:570-577): label <= 0 inside the six segments, in index order
   uint32_t lfl = 0;
@@ -1277,21 +1302,40 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
   PHASE(5);
 
   // ---- VoxelGrid(0.2) of the line's less-flat points (PCL VoxelGrid::applyFilter semantics)
+  // The voxel index is a mixed-radix number (z, y, x) over the box's leaf coordinates; over any box
+  // that encloses the points it orders them the same way (lexicographically in z, y, x) and is equal
+  // exactly for points of one leaf, so the sort, std::sort's order of equal voxels and the centroids
+  // do not depend on which enclosing box is used.  The segments' box from the curvature pass serves
+  // unless its index range overflows; then the exact box of the less-flat points (PCL's own leaf-size
+  // check is on that box, and it cannot fail when the larger box passes).
   int n_lflat = 0;
   if (nlist > 0) {
     const float inv = 1.0f / 0.2f;
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    float mn[3] = {bmn[0], bmn[1], bmn[2]}, mx[3] = {bmx[0], bmx[1], bmx[2]};
+    auto box_size = [&]() {
+      const int64_t ex = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+      const int64_t ey = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+      const int64_t ez = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+      int64_t nv = 1;  // the index range: the leaves spanned per axis
 #pragma unroll
-    for (int t = 0; t < kS; t++) {
-      if (!((lfl >> t) & 1u)) continue;
-      const P4 p = ld4(cloud + off + lane + 64 * t);
-      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-    }
-    for (int d = 0; d < 3; d++) {
-      for (int o = 32; o > 0; o >>= 1) {
-        mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
-        mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+      for (int d = 0; d < 3; d++) nv *= (int64_t)((int)floorf(mx[d] * inv) - (int)floorf(mn[d] * inv) + 1);
+      return max(ex * ey * ez, nv);
+    };
+    if (box_size() > (int64_t)2147483647) {
+#pragma unroll
+      for (int d = 0; d < 3; d++) { mn[d] = 3.4e38f; mx[d] = -3.4e38f; }
+#pragma unroll
+      for (int t = 0; t < kS; t++) {
+        if (!((lfl >> t) & 1u)) continue;
+        const P4 p = ld4(cloud + off + lane + 64 * t);
+        mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+        mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+      }
+      for (int d = 0; d < 3; d++) {
+        for (int o = 32; o > 0; o >>= 1) {
+          mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+          mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+        }
       }
     }
     const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;

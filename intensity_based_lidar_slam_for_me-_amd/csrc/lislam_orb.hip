@@ -17,9 +17,10 @@
 //   k_orb_blur      1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2 separable float
 //                   Gaussian (row sums then the symmetric column sum, the FilterEngine order) on
 //                   the ROI, border copy
-//   k_orb_fastnms   1 WG per band of 4 level rows, staged in LDS: FAST-9/16 segment test +
-//                   cornerScore<16> into an LDS score tile, then 3x3 non-max suppression, mask,
-//                   border
+//   k_orb_fastnms   1 WG per band of LISLAM_FAST_BAND level rows, staged in LDS: cheap test of
+//                   every pixel of the band into one candidate list, FAST-9/16 segment test +
+//                   cornerScore<16> of the list into an LDS score tile, then 3x3 non-max
+//                   suppression, mask, border
 //   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
 //                   thread), retainBest(2n) on the FAST score (256-bin histogram), Harris responses
 //                   (a wavefront per 4 candidates, all their loads in flight), retainBest(n) on
@@ -231,11 +232,35 @@ __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
 // fixed-point resize (hval) of level l-1.  A thread owns a column of the level (its horizontal
 // taps in registers) and walks the rows; the row taps (levels >= 1 have <= 64 rows) sit one per
 // lane and are read with readlane.
+#ifdef LISLAM_PHASE_PROF
+// k_orb_pyramid phase split (profiling builds): slot 0 the image load, 8 p + l phase p (1 resize,
+// 2 padded copy, 3 blur) of level l, summed over workgroups in s_memrealtime ticks (100 MHz)
+__device__ unsigned long long g_pyr_phase[32];
+extern "C" int lislam_debug_pyr_phases(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_phase), sizeof(g_pyr_phase)) != hipSuccess) return -2;
+  static const unsigned long long zero[32] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pyr_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+#define PYR_PHASE(i)                                                          \
+  do {                                                                        \
+    __syncthreads();                                                          \
+    if (threadIdx.x == 0) {                                                   \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();      \
+      atomicAdd(&g_pyr_phase[i], now_ - t_ph);                                \
+      t_ph = now_;                                                            \
+    }                                                                         \
+  } while (0)
+#else
+#define PYR_PHASE(i)
+#endif
 constexpr int kPyrThreads = 1024;
 constexpr int kPyrLds = 112 * 1024;
 __host__ __device__ __forceinline__ int pyr_split(const Geom& g) { return (g.w[0] * g.h[0] + 15) & ~15; }
 __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kPyrLds];
+#ifdef LISLAM_PHASE_PROF
+  unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
+#endif
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[blockIdx.x] : blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -249,6 +274,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
     for (int d = threadIdx.x; d < nd; d += kPyrThreads) e32[d] = __builtin_nontemporal_load(img + d);
   }
   __syncthreads();
+  PYR_PHASE(0);
   for (int l = 0; l < kL; l++) {
     uint8_t* const cur = (l & 1) ? odd : even;
     const uint8_t* const prev = (l & 1) ? even : odd;
@@ -257,9 +283,20 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
       const int wp = g.w[l - 1], hl = g.h[l - 1] - 1;
       const int* lim = a.t.lim + l * 4;
       const int lx0 = lim[0], lx1 = lim[1], ly0 = lim[2], ly1 = lim[3];
-      // row taps of this level: lane y holds yo[y], yc[y] (rows outside [ly0, ly1) clamp)
-      const int yo_l = lane < h && lane >= ly0 && lane < ly1 ? a.t.yo[l * a.t.ys + lane] : 0;
-      const int yc_l = lane < h && lane >= ly0 && lane < ly1 ? (int)a.t.yc[l * a.t.ys + lane] : 0;
+      // row taps of this level, lane y: byte offsets of source rows ya, yb and the weight cy; a
+      // row outside [ly0, ly1) clamps to row 0 / hl with cy = 0, where the two-row formula is the
+      // one-row one: (256 ha + 32768) >> 16 = (ha + 128) >> 8
+      int ra_l = 0, rb_l = 0, cy_l = 0;
+      if (lane < h) {
+        if (lane >= ly0 && lane < ly1) {
+          const int ya = a.t.yo[l * a.t.ys + lane];
+          ra_l = ya * wp;
+          rb_l = ra_l + wp;
+          cy_l = (int)a.t.yc[l * a.t.ys + lane];
+        } else {
+          ra_l = rb_l = (lane < ly0 ? 0 : hl) * wp;
+        }
+      }
       const int xlast = a.t.xo[l * a.t.xs + w - 1];
       for (int x = threadIdx.x; x < w; x += kPyrThreads) {
         int o0 = 0, o1 = 0;
@@ -272,50 +309,67 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
         } else if (x >= lx1) {
           o0 = o1 = xlast;
         }
-        for (int y = 0; y < h; y++) {
-          uint32_t v;
-          if (y < ly0 || y >= ly1) {
-            const uint8_t* pr = prev + (y < ly0 ? 0 : hl) * wp;
-            v = min(255u, (w0 * pr[o0] + w1 * pr[o1] + 128u) >> 8);
-          } else {
-            const int ya = __builtin_amdgcn_readlane(yo_l, y);
-            const uint32_t cy = (uint32_t)__builtin_amdgcn_readlane(yc_l, y);
-            const uint8_t* pa = prev + ya * wp;
-            const uint8_t* pb = pa + wp;
+        // four rows per step, their eight source bytes' loads in flight together
+        for (int y0 = 0; y0 < h; y0 += 4) {
+          uint32_t v[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const int y = min(y0 + u, h - 1);
+            const uint8_t* pa = prev + __builtin_amdgcn_readlane(ra_l, y);
+            const uint8_t* pb = prev + __builtin_amdgcn_readlane(rb_l, y);
+            const uint32_t cy = (uint32_t)__builtin_amdgcn_readlane(cy_l, y);
             const uint32_t ha = w0 * pa[o0] + w1 * pa[o1], hb = w0 * pb[o0] + w1 * pb[o1];
-            v = min(255u, (ha * (256u - cy) + hb * cy + 32768u) >> 16);
+            v[u] = min(255u, (ha * (256u - cy) + hb * cy + 32768u) >> 16);
           }
-          cur[y * w + x] = (uint8_t)v;
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            if (y0 + u < h) cur[(y0 + u) * w + x] = (uint8_t)v[u];
         }
       }
       __syncthreads();  // level l complete; the next level writes the buffer read above
+      PYR_PHASE(8 + l);
     }
-    // the padded level: 256 dword columns x 4 row phases per pass, columns' reflections hoisted.
-    // The blurred copy (k_orb_blur's output) takes the same bytes except where a dword holds ROI
-    // columns of a ROI row: those come from the blur pass below.
+    // the padded level: ndr dword columns x P row phases (P = threads / ndr), a thread's column
+    // and its reflections fixed per level.  A dword of 4 ROI columns is the two aligned LDS dwords
+    // around it shifted (alignbyte); a border dword gathers its 4 reflected bytes.  The blurred copy
+    // (k_orb_blur's output) takes the same bytes except where a dword holds ROI columns of a ROI
+    // row: those come from the blur pass below.
     const int ndr = g.stride[l] / 4, rows = h + 2 * kB;
     uint32_t* dst = reinterpret_cast<uint32_t*>(base + g.off[l]);
     uint32_t* bdst = a.blur ? reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]) : nullptr;
-    for (int dc = threadIdx.x & 255; dc < ndr; dc += 256) {
-      int cx[4];
+    {
+      const int P = kPyrThreads / ndr, dc = (int)threadIdx.x % ndr, ph = (int)threadIdx.x / ndr;
+      if (ph < P) {
+        int cx[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) cx[k] = reflect101(4 * dc + k - kB, w);
-      const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
-      for (int rr = threadIdx.x >> 8; rr < rows; rr += kPyrThreads / 256) {
-        const uint8_t* src = cur + reflect101(rr - kB, h) * w;
-        const uint32_t v = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 |
-                           (uint32_t)src[cx[3]] << 24;
-        dst[rr * ndr + dc] = v;
-        if (bdst && !(roi_dw && rr >= kB && rr < kB + h)) bdst[rr * ndr + dc] = v;
+        for (int k = 0; k < 4; k++) cx[k] = reflect101(4 * dc + k - kB, w);
+        const bool inner = 4 * dc - kB >= 0 && 4 * dc + 3 - kB < w;
+        const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
+        for (int rr = ph; rr < rows; rr += P) {
+          const int ro = reflect101(rr - kB, h) * w;
+          uint32_t v;
+          if (inner) {
+            const int A = ro + 4 * dc - kB;
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(cur + (A & ~3));
+            v = __builtin_amdgcn_alignbyte(d[1], d[0], (uint32_t)(A & 3));
+          } else {
+            const uint8_t* src = cur + ro;
+            v = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 | (uint32_t)src[cx[3]] << 24;
+          }
+          dst[rr * ndr + dc] = v;
+          if (bdst && !(roi_dw && rr >= kB && rr < kB + h)) bdst[rr * ndr + dc] = v;
+        }
       }
     }
+    PYR_PHASE(16 + l);
     if (bdst) {
       // GaussianBlur(ROI, 7x7, sigma 2, BORDER_REFLECT_101) of the dwords holding ROI columns, in
       // k_orb_blur's float order: per row, 4 row sums of 7 taps (a sliding window of 7 rows in
       // registers), then the symmetric column sum.  A thread owns a dword column holding ROI
-      // columns and one of nseg row segments, nseg as large as one pass of the workgroup allows.
+      // columns and one of nseg row segments of >= 16 rows (each segment re-sums 6 rows; more
+      // segments than one pass of the workgroup holds would only add passes).
       const int dlo = kB / 4, ndw = (kB + w - 1) / 4 - dlo + 1;
-      const int nseg = max(1, min(h, kPyrThreads / ndw));
+      const int nseg = max(1, min(h / 16, kPyrThreads / ndw));
       for (int item = threadIdx.x; item < ndw * nseg; item += kPyrThreads) {
         const int dc = dlo + item % ndw, seg = item / ndw;
         const int ra = seg * h / nseg, rb = (seg + 1) * h / nseg;
@@ -324,12 +378,30 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
         int cs[10];  // ROI columns of padded columns c4 - 3 .. c4 + 6
 #pragma unroll
         for (int i = 0; i < 10; i++) cs[i] = reflect101(c4 - 3 + i - kB, w);
+        // columns c4 - 3 .. c4 + 6 all inside the ROI: the 10 bytes from 3 aligned LDS dwords
+        const bool inner = c4 - 3 - kB >= 0 && c4 + 6 - kB < w;
         float rs[7][4];
         auto rowsum = [&](int r, float* out) {
           const uint8_t* src = cur + reflect101(r, h) * w;
           float b[10];
+          if (inner) {
+            const int A = (int)(src - cur) + c4 - 3 - kB;
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(cur + (A & ~3));
+            const uint32_t sh = (uint32_t)(A & 3), d3 = d[3];
+            const uint32_t u0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+            const uint32_t u1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+            const uint32_t u2 = __builtin_amdgcn_alignbyte(d3, d[2], sh);
 #pragma unroll
-          for (int i = 0; i < 10; i++) b[i] = (float)src[cs[i]];
+            for (int e = 0; e < 4; e++) {
+              b[e] = (float)((u0 >> (8 * e)) & 255u);
+              b[4 + e] = (float)((u1 >> (8 * e)) & 255u);
+            }
+            b[8] = (float)(u2 & 255u);
+            b[9] = (float)((u2 >> 8) & 255u);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 10; i++) b[i] = (float)src[cs[i]];
+          }
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             float v = g.gk[0] * b[j];
@@ -366,6 +438,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
         }
       }
     }
+    PYR_PHASE(24 + l);
   }
 }
 
@@ -539,12 +612,27 @@ __device__ __forceinline__ int fast_full(const uint8_t* p, int ts) {
   return corner_score(dd, kFastT);
 }
 
+// LDS of a k_orb_fastnms workgroup for a level of width w: the image tile ((kFastBand + 8) rows of
+// fast_tile_stride bytes), the score tile ((kFastBand + 2) rows of w + 2 bytes, dword-padded) and
+// the candidate list (u16 score-tile positions: (kFastBand + 2) (w + 2) <= 65536, host-checked)
+__host__ __device__ __forceinline__ int fast_tile_stride(int w) { return 4 * ((w + 12 + 3) >> 2); }
+__host__ __device__ __forceinline__ int fast_score_bytes(int w) { return ((kFastBand + 2) * (w + 2) + 3) & ~3; }
+__host__ __device__ __forceinline__ size_t fast_lds_bytes(int w) {
+  return (size_t)(kFastBand + 8) * fast_tile_stride(w) + fast_score_bytes(w) + (size_t)2 * (kFastBand + 2) * (w + 2);
+}
+
 // FAST keypoints of a band of kFastBand ROI rows of a level: the band's pixels +-4 rows / columns
 // staged in LDS, FAST scores of the band +-1 (border pixels 0) into a second LDS tile, then
 // 3x3 non-max suppression of FAST_t, the pixel mask (runByPixelsMask) and the image border
-// (edgeThreshold 1): nms = the FAST score of a keypoint, else 0.
+// (edgeThreshold 1): nms = the FAST score of a keypoint, else 0.  The scores take two passes over
+// the whole band, one barrier apart: every pixel takes the cheap necessary test (an opposite pair
+// on each axis has a pixel beyond the threshold on the same side) and the survivors are compacted
+// into one LDS list (wave ballot + one LDS atomic per wave), then the full segment test and
+// cornerScore run on the list with every lane busy.  The list's order is the atomics' order; each
+// entry writes only its own score, so the result does not depend on it.
 __global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
-  extern __shared__ uint8_t ftile[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t ftile[];
+  __shared__ int lcnt;
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
   int l = 0;
@@ -553,51 +641,54 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
   const int r0 = ((int)blockIdx.x - g.fband[l]) * kFastBand;
   const int nr = min(kFastBand, h - r0);
   // image tile: rows r0-4 .. r0+nr+3, padded columns 16 .. (level columns -7 ..), dword rows
-  const int nd = (w + 12 + 3) >> 2, ts = 4 * nd;
-  constexpr int kC0 = kB - 16;                  // tile column of level column 0
+  const int ts = fast_tile_stride(w), nd = ts >> 2;
+  constexpr int kC0 = kB - 16;  // tile column of level column 0
   uint8_t* img = ftile;
   uint8_t* sct = ftile + (kFastBand + 8) * ts;  // scores: rows r0-1 .., columns -1 .. w
   const int ss = w + 2;
-  uint16_t* lst = reinterpret_cast<uint16_t*>(ftile + (((kFastBand + 8) * ts + (kFastBand + 2) * ss + 1) & ~1));
+  uint16_t* list = reinterpret_cast<uint16_t*>(sct + fast_score_bytes(w));
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
   stage_rows<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), base + g.off[l] + (r0 - 4 + kB) * g.stride[l] + 16,
                             g.stride[l], nr + 8, nd);
+  {
+    uint32_t* z = reinterpret_cast<uint32_t*>(sct);
+    for (int i = threadIdx.x; i < fast_score_bytes(w) / 4; i += blockDim.x) z[i] = 0u;
+  }
+  if (threadIdx.x == 0) lcnt = 0;
   __syncthreads();
-  // Scores of rows r0-1 .. r0+nr (0 off the FAST area).  Per row: every pixel takes the cheap
-  // necessary test (an opposite pair on each axis has a pixel beyond the threshold on the same
-  // side), the survivors are compacted into an LDS list (double-buffered: one barrier per row),
-  // and the full test runs on the list with every lane busy.
-  for (int i = threadIdx.x; i < (nr + 2) * ss; i += blockDim.x) sct[i] = 0;
-  __shared__ int lcnt[kFastBand + 2];
-  if (threadIdx.x < kFastBand + 2) lcnt[threadIdx.x] = 0;
-  __syncthreads();
+  // 1. cheap test of the score rows r0-1 .. r0+nr inside the FAST area (3 <= r < h-3, 3 <= c < w-3)
   const int lane = threadIdx.x & 63;
-  for (int rr = 0; rr < nr + 2; rr++) {
-    const int r = r0 - 1 + rr;
-    uint16_t* list = lst + (rr & 1) * w;
-    if (r >= 3 && r < h - 3) {
-      for (int c0 = 3; c0 < w - 3; c0 += blockDim.x) {
-        const int c = c0 + (int)threadIdx.x;
-        bool cand = false;
-        if (c < w - 3) {
-          const uint8_t* p = img + (rr + 3) * ts + c + kC0;
-          const int v = p[0];
-          auto tab = [&](int x) { const int dd = x - v; return dd < -kFastT ? 1 : dd > kFastT ? 2 : 0; };
-          cand = ((tab(p[3 * ts]) | tab(p[-3 * ts])) & (tab(p[3]) | tab(p[-3]))) != 0;
-        }
-        const uint64_t m = __ballot(cand);
-        int base = 0;
-        if (lane == 0 && m) base = atomicAdd(&lcnt[rr], __popcll(m));
-        base = __shfl(base, 0);
-        if (cand) list[base + __popcll(m & lanemask_lt())] = (uint16_t)c;
+  const int rlo = max(0, 4 - r0), rhi = min(nr + 2, h - 2 - r0);
+  for (int rr = rlo; rr < rhi; rr++) {
+    const uint8_t* prow = img + (rr + 3) * ts + kC0;
+    for (int c0 = 3; c0 < w - 3; c0 += blockDim.x) {
+      const int c = c0 + (int)threadIdx.x;
+      bool cand = false;
+      if (c < w - 3) {
+        const uint8_t* p = prow + c;
+        const int v = p[0];
+        auto tab = [&](int x) { const int dd = x - v; return dd < -kFastT ? 1 : dd > kFastT ? 2 : 0; };
+        cand = ((tab(p[3 * ts]) | tab(p[-3 * ts])) & (tab(p[3]) | tab(p[-3]))) != 0;
+      }
+      const uint64_t m = __ballot(cand);
+      if (m) {
+        int at = 0;
+        if (lane == 0) at = atomicAdd(&lcnt, __popcll(m));
+        at = __shfl(at, 0);
+        if (cand) list[at + __popcll(m & lanemask_lt())] = (uint16_t)(rr * ss + c + 1);
       }
     }
-    __syncthreads();
-    const int n = lcnt[rr];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const int c = list[i];
-      sct[rr * ss + c + 1] = (uint8_t)fast_full(img + (rr + 3) * ts + c + kC0, ts);
-    }
+  }
+  __syncthreads();
+  // 2. full test + score of the candidates (row = position / ss: exact in float, the quotient's
+  //    fractional part is >= 0.5 / ss away from an integer and the product errs by < 2^-8 / ss)
+  const int n = lcnt;
+  const float iss = 1.f / (float)ss;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int idx = list[i];
+    const int rr = (int)(((float)idx + 0.5f) * iss);
+    const int c = idx - rr * ss - 1;
+    sct[idx] = (uint8_t)fast_full(img + (rr + 3) * ts + c + kC0, ts);
   }
   __syncthreads();
   uint8_t* out = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
@@ -1083,22 +1174,53 @@ __global__ __launch_bounds__(256) void k_orb_finish(Args a) {
   }
 }
 
-// steered rBRIEF: 32 threads per keypoint, one descriptor byte each (keypoints grid-strided over
-// gridDim.x blocks of 8)
+// steered rBRIEF: 32 lanes per keypoint, one descriptor byte each (keypoints grid-strided over
+// gridDim.x blocks of 8).  The pattern's points lie in [-13, 13]^2, so rotated and rounded they
+// stay within kDescR = 18 of the keypoint: its 37 x 37 blurred patch is staged in LDS by the 32
+// lanes (10 aligned dwords per row, all loads in flight), then the 512 tests read LDS.  A patch
+// is written and read by one wavefront only (two keypoints per wavefront, one LDS slot each).
+constexpr int kDescR = 18;
+constexpr int kDescRow = 40;  // staged bytes per patch row: 37 + the dword misalignment (<= 3)
+constexpr int kDescDw = (2 * kDescR + 1) * (kDescRow / 4);  // 370 dwords per patch
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
+  __shared__ uint32_t patch[8][kDescDw];
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[gi] : gi;
-  const int byte = threadIdx.x & 31;
+  const int byte = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const int nk = a.nkp[s];
   const uint8_t* base = a.blur + (size_t)s * g.bytes;
-  for (int k = blockIdx.x * 8 + (threadIdx.x >> 5); k < nk; k += gridDim.x * 8) {
+  const uint8_t* P = reinterpret_cast<const uint8_t*>(patch[slot]);
+  for (int k = blockIdx.x * 8 + slot; k < nk; k += gridDim.x * 8) {
     const float* kp = a.kp + ((size_t)s * g.cap + k) * 6;
     const int l = (int)kp[5];
     const float scale = 1.f / g.scale[l];
     const float ang = kp[3] * (float)(kPi / 180.f);
     const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
     const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
-    int v = 0;
+    // padded rows cy - 18 .. cy + 18, padded columns pc0 .. pc0 + 39 (pc0 = cx - 18 + kB rounded
+    // down to a dword; the row has >= 44 bytes right of cx, kB = 23 > 18 above and below)
+    const int pc = cx - kDescR + kB, pc0 = pc & ~3, sh = pc - pc0;
+    const uint8_t* src = base + g.off[l] + (size_t)(cy - kDescR + kB) * g.stride[l] + pc0;
+    uint32_t v[(kDescDw + 31) / 32];
+#pragma unroll
+    for (int i = 0; i < (kDescDw + 31) / 32; i++) {
+      const int e = byte + 32 * i, row = e / 10, d = e - 10 * row;
+      if (e < kDescDw) v[i] = *(const __attribute__((address_space(1))) uint32_t*)(src + (size_t)row * g.stride[l] + 4 * d);
+    }
+    wave_lds_sync();  // the previous keypoint's tests have read the slot
+#pragma unroll
+    for (int i = 0; i < (kDescDw + 31) / 32; i++) {
+      const int e = byte + 32 * i;
+      if (e < kDescDw) patch[slot][e] = v[i];
+    }
+    wave_lds_sync();
+    const uint8_t* c0 = P + kDescR * kDescRow + kDescR + sh;  // the keypoint's byte
+    int bits = 0;
 #pragma unroll
     for (int bit = 0; bit < 8; bit++) {
       const int p = (byte * 8 + bit) * 2;
@@ -1107,11 +1229,11 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
       for (int e = 0; e < 2; e++) {
         const float qx = (float)c_pattern[(p + e) * 2], qy = (float)c_pattern[(p + e) * 2 + 1];
         const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
-        t[e] = pxc(base, g, l, cy + (int)rintf(y), cx + (int)rintf(x));
+        t[e] = c0[(int)rintf(y) * kDescRow + (int)rintf(x)];
       }
-      v |= (t[0] < t[1]) << bit;
+      bits |= (t[0] < t[1]) << bit;
     }
-    a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)v;
+    a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)bits;
   }
 }
 
@@ -1323,20 +1445,42 @@ __device__ __forceinline__ void orb_match_body(const PairArgs& p, int pi) {
   for (int j = threadIdx.x; j < nq; j += blockDim.x)
     if (best[j] != kNoMatch) atomicAdd(&hist[best[j] >> 16], 1);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int M = 0;
-    for (int b = 0; b < 257; b++) M += hist[b];
-    int G = 0;
-    while ((double)G < (double)M * p.frac) G++;
-    int cum = 0, dstar = 257, before = 0;
-    for (int b = 0; b < 257 && G > 0; b++) {
-      if (cum + hist[b] >= G) { dstar = b; before = cum; break; }
-      cum += hist[b];
+  if (threadIdx.x < 64) {
+    // wave 0: lane i holds bins 5i .. 5i+4; M = all matches, G = ceil(frac M) (the first G with
+    // G >= M frac, in double), d* = the first bin whose inclusive prefix reaches G
+    const int lane = threadIdx.x;
+    int hb[5], loc = 0;
+#pragma unroll
+    for (int e = 0; e < 5; e++) {
+      const int b = 5 * lane + e;
+      hb[e] = b < 257 ? hist[b] : 0;
+      loc += hb[e];
     }
-    sM = M;
-    sG = G;
-    sh.total = dstar;
-    sh.want = G - before;  // matches of distance d* to take, in query order
+    int inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    const int M = __shfl(inc, 63);
+    const int G = (int)ceil((double)M * p.frac);
+    int cum = inc - loc, hit = -1, before = 0;
+#pragma unroll
+    for (int e = 0; e < 5; e++) {
+      if (hit < 0 && G > 0 && cum + hb[e] >= G) { hit = 5 * lane + e; before = cum; }
+      cum += hb[e];
+    }
+    const uint64_t m = __ballot(hit >= 0);
+    if (lane == 0) {
+      sM = M;
+      sG = G;
+      sh.total = 257;
+      sh.want = G;
+    }
+    if (m && lane == __ffsll((long long)m) - 1) {
+      sh.total = hit;
+      sh.want = G - before;  // matches of distance d* to take, in query order
+    }
   }
   __syncthreads();
   const int M = sM, G = sG, dstar = sh.total, take = sh.want;
@@ -1707,6 +1851,8 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
     g.lcap[l] = 2 * g.nper[l] + 64;
     g.lofs[l + 1] = g.lofs[l] + g.lcap[l];
   }
+  if ((kFastBand + 2) * (g.w[0] + 2) > 65536)  // k_orb_fastnms' u16 candidate list
+    return ofail(c, LISLAM_ERR_ARG, "image width %d too large for the FAST band", W);
   g.fband[0] = 0;
   g.bband[0] = 0;
   for (int l = 0; l < kL; l++) {
@@ -1855,7 +2001,8 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   const Geom& g = e->g;
   // LISLAM_ORB_PYR_LEVELS=1 forces the level-by-level pyramid and the separate blur (A/B)
   static const bool by_level = getenv("LISLAM_ORB_PYR_LEVELS") && atoi(getenv("LISLAM_ORB_PYR_LEVELS")) == 1;
-  const bool fused = !by_level && g.W % 4 == 0 && g.h[1] <= 64 && pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
+  const bool fused = !by_level && g.W % 4 == 0 && g.h[1] <= 64 && g.stride[0] / 4 <= kPyrThreads &&
+                     pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
   {
     TimedScope t(c, kT_orb_pyramid);
     // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB), which
@@ -1870,8 +2017,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   }
   {
     TimedScope t(c, kT_orb_fast);
-    const size_t lds = (size_t)(kFastBand + 8) * 4 * ((g.w[0] + 15) >> 2) + (size_t)(kFastBand + 2) * (g.w[0] + 2) +
-                       1 + 2 * 2 * (size_t)g.w[0];  // image, scores, two candidate lists
+    const size_t lds = fast_lds_bytes(g.w[0]);
     hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }

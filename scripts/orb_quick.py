@@ -41,3 +41,15 @@ if hasattr(L, 'lislam_debug_sel_phases'):  # profiling build: k_orb_select phase
     tot = sum(buf[i] for i in range(5))
     for i, nm in enumerate(names):
         print(f'  select {nm:9s} {buf[i] / 100.0:12.0f} WG-us  {100 * buf[i] / max(1, tot):5.1f}%')
+if hasattr(L, 'lislam_debug_pyr_phases'):  # profiling build: k_orb_pyramid phase split (per-WG us)
+    import ctypes
+    buf = (ctypes.c_ulonglong * 32)()
+    L.lislam_debug_pyr_phases(buf)
+    b.intensity_odometry(S, 1000, mask)
+    ctx.synchronize()
+    L.lislam_debug_pyr_phases(buf)
+    print(f'  pyramid load        {buf[0] / 100.0 / S:8.2f} us per WG')
+    for p, nm in ((1, 'resize'), (2, 'padded'), (3, 'blur')):
+        row = ' '.join(f'{buf[8 * p + l] / 100.0 / S:6.2f}' for l in range(8))
+        tot = sum(buf[8 * p + l] for l in range(8)) / 100.0 / S
+        print(f'  pyramid {nm:8s} {tot:8.2f} us per WG  (levels: {row})')

@@ -18,7 +18,10 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def pkg():
-    return importlib.import_module(PKG)
+    m = importlib.import_module(PKG)
+    if os.environ.get("LISLAM_ALT_LIB"):  # developer A/B: a variant build of the library
+        m.native.load(os.environ["LISLAM_ALT_LIB"])
+    return m
 
 
 @pytest.fixture(scope="session")
