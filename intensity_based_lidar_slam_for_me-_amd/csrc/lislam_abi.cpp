@@ -487,10 +487,9 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     HIPCHK(c, hipEventRecord(b->stage_ev, c->stream));
     b->stage_busy = true;
   }
-  // chain groups: LISLAM_ODOM_GROUPS (default 2) streams, so one group's solves overlap another's
+  // chain groups: 2 streams, so one group's solves overlap another's
   // association (a solve occupies one workgroup per chain, far from filling the device)
-  static const int groups_env = getenv("LISLAM_ODOM_GROUPS") ? atoi(getenv("LISLAM_ODOM_GROUPS")) : 2;
-  const int G = std::max(1, std::min(groups_env, (int)lislam_batch::kMaxGroups));
+  const int G = std::min(2, (int)lislam_batch::kMaxGroups);
   b->odo_stream[0] = c->stream;
   for (int g = 1; g < G; g++) {
     if (!b->odo_stream[g]) HIPCHK(c, hipStreamCreateWithFlags(&b->odo_stream[g], hipStreamNonBlocking));

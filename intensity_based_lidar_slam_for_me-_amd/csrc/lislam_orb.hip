@@ -62,7 +62,6 @@ constexpr int kFastT = 20;
 constexpr int kSelThreads = LISLAM_SEL_THREADS;  // k_orb_select workgroup
 constexpr int kPairThreads = 1024;
 constexpr int kLmThreads = 256;
-constexpr int kQTile = 1024;  // queries per LDS tile in k_orb_xdist (32 KiB)
 constexpr int kNoMatch = 0x7f7f7f7f;
 #ifndef LISLAM_FAST_BAND
 #define LISLAM_FAST_BAND 4
@@ -375,13 +374,13 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
         const int ra = seg * h / nseg, rb = (seg + 1) * h / nseg;
         const int c4 = 4 * dc;  // padded column of byte 0
         if (ra >= rb) continue;
-        int cs[10];  // ROI columns of padded columns c4 - 3 .. c4 + 6
-#pragma unroll
-        for (int i = 0; i < 10; i++) cs[i] = reflect101(c4 - 3 + i - kB, w);
         // columns c4 - 3 .. c4 + 6 all inside the ROI: the 10 bytes from 3 aligned LDS dwords
         const bool inner = c4 - 3 - kB >= 0 && c4 + 6 - kB < w;
-        float rs[7][4];
-        auto rowsum = [&](int r, float* out) {
+        // float pairs (columns j, j + 1): the packed multiplies and adds round like the scalar
+        // ones, in the same order (row taps 0..6, then the symmetric column sum)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 rs[7][2];
+        auto rowsum = [&](int r, f2* out) {
           const uint8_t* src = cur + reflect101(r, h) * w;
           float b[10];
           if (inner) {
@@ -398,16 +397,16 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
             }
             b[8] = (float)(u2 & 255u);
             b[9] = (float)((u2 >> 8) & 255u);
-          } else {
+          } else {  // a dword near the ROI's edge: reflect-101 columns
 #pragma unroll
-            for (int i = 0; i < 10; i++) b[i] = (float)src[cs[i]];
+            for (int i = 0; i < 10; i++) b[i] = (float)src[reflect101(c4 - 3 + i - kB, w)];
           }
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            float v = g.gk[0] * b[j];
+          for (int jp = 0; jp < 2; jp++) {
+            f2 v = g.gk[0] * f2{b[2 * jp], b[2 * jp + 1]};
 #pragma unroll
-            for (int t = 1; t < 7; t++) v += g.gk[t] * b[j + t];
-            out[j] = v;
+            for (int t = 1; t < 7; t++) v += g.gk[t] * f2{b[2 * jp + t], b[2 * jp + 1 + t]};
+            out[jp] = v;
           }
         };
 #pragma unroll
@@ -416,22 +415,23 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
 #pragma unroll
           for (int k = 0; k < 6; k++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) rs[k][j] = rs[k + 1][j];
+            for (int jp = 0; jp < 2; jp++) rs[k][jp] = rs[k + 1][jp];
           rowsum(r + 3, rs[6]);
           const uint8_t* src = cur + r * w;
+          float cv[4];
+#pragma unroll
+          for (int jp = 0; jp < 2; jp++) {
+            f2 v = g.gk[3] * rs[3][jp];
+#pragma unroll
+            for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t][jp] + rs[3 - t][jp]);
+            cv[2 * jp] = v.x;
+            cv[2 * jp + 1] = v.y;
+          }
           uint32_t o = 0;
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const int cr = c4 + j - kB;
-            uint32_t ob;
-            if (cr >= 0 && cr < w) {
-              float v = g.gk[3] * rs[3][j];
-#pragma unroll
-              for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t][j] + rs[3 - t][j]);
-              ob = (uint32_t)min(255, max(0, (int)rintf(v)));
-            } else {
-              ob = src[cs[j + 3]];
-            }
+            const uint32_t ob = (cr >= 0 && cr < w) ? (uint32_t)min(255, max(0, (int)rintf(cv[j]))) : (uint32_t)src[reflect101(cr, w)];
             o |= ob << (8 * j);
           }
           bdst[(r + kB) * ndr + dc] = o;
@@ -1272,60 +1272,7 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 
 // batchDistance cross-check, distance part: train i -> its nearest query (first minimum); each
 // query keeps the nearest train among those that chose it (first minimum) = atomicMin of the
-// packed (distance << 16 | train) (best[] preset to 0x7f7f7f7f).  Grid (pairs, train blocks of
-// 2 x 256): each thread owns two trains; queries are staged in LDS tiles and every lane of a
-// wavefront reads the same query (broadcast).
-constexpr int kXdThreads = 256;
-constexpr int kXdTrains = 2 * kXdThreads;
-
-__device__ __forceinline__ void orb_xdist_body(const PairArgs& p, int pi) {
-  __shared__ uint4 qt[kQTile * 2];
-  const int pr = p.pslot ? p.pslot[pi] : pi;
-  const int qs = p.qscan[pi], ts = p.tscan[pi];
-  const int nq = p.qn[qs], nt = p.tn[ts];
-  const int i0 = blockIdx.y * kXdTrains;
-  if (i0 >= nt) return;
-  const uint32_t* Q = reinterpret_cast<const uint32_t*>(p.qdesc + (size_t)qs * p.qcap * 32);
-  const uint32_t* T = reinterpret_cast<const uint32_t*>(p.tdesc + (size_t)ts * p.tcap * 32);
-  int* best = p.mscratch + (size_t)pr * p.bstride;
-  const int ia = i0 + threadIdx.x, ib = ia + kXdThreads;
-  uint32_t ta[8], tb[8];
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    ta[e] = ia < nt ? T[(size_t)ia * 8 + e] : 0u;
-    tb[e] = ib < nt ? T[(size_t)ib * 8 + e] : 0u;
-  }
-  int bda = 0x7fffffff, bja = -1, bdb = 0x7fffffff, bjb = -1;
-  for (int q0 = 0; q0 < nq; q0 += kQTile) {
-    const int tn = min(kQTile, nq - q0);
-    __syncthreads();
-    const uint4* Qv = reinterpret_cast<const uint4*>(Q + (size_t)q0 * 8);
-    for (int e = threadIdx.x; e < tn * 2; e += blockDim.x) qt[e] = Qv[e];
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < tn; j++) {
-      const uint4 a0 = qt[2 * j], a1 = qt[2 * j + 1];
-      const int da = __popc(ta[0] ^ a0.x) + __popc(ta[1] ^ a0.y) + __popc(ta[2] ^ a0.z) + __popc(ta[3] ^ a0.w) +
-                     __popc(ta[4] ^ a1.x) + __popc(ta[5] ^ a1.y) + __popc(ta[6] ^ a1.z) + __popc(ta[7] ^ a1.w);
-      const int db = __popc(tb[0] ^ a0.x) + __popc(tb[1] ^ a0.y) + __popc(tb[2] ^ a0.z) + __popc(tb[3] ^ a0.w) +
-                     __popc(tb[4] ^ a1.x) + __popc(tb[5] ^ a1.y) + __popc(tb[6] ^ a1.z) + __popc(tb[7] ^ a1.w);
-      if (da < bda) { bda = da; bja = q0 + j; }
-      if (db < bdb) { bdb = db; bjb = q0 + j; }
-    }
-  }
-  if (ia < nt && bja >= 0) atomicMin(&best[bja], (bda << 16) | ia);
-  if (ib < nt && bjb >= 0) atomicMin(&best[bjb], (bdb << 16) | ib);
-}
-
-// the grid's pair indices stride over the pairs in use (*p.pcount of them when given)
-__global__ __launch_bounds__(kXdThreads) void k_orb_xdist(PairArgs p) {
-  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
-  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
-    orb_xdist_body(p, pi);
-    __syncthreads();
-  }
-}
-
+// packed (distance << 16 | train) (best[] preset to 0x7f7f7f7f).
 // The same result on the matrix cores: Hamming(q, t) = |q| + |t| - 2 <q, t> with the 256
 // descriptor bits as 0/1 int8 vectors and <q, t> from v_mfma_i32_16x16x64_i8 (four k-steps of 64
 // bits; A and B fragments use one and the same lane -> k map, so the dot product does not depend
@@ -1999,9 +1946,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     a.smap = e->smap;
   }
   const Geom& g = e->g;
-  // LISLAM_ORB_PYR_LEVELS=1 forces the level-by-level pyramid and the separate blur (A/B)
-  static const bool by_level = getenv("LISLAM_ORB_PYR_LEVELS") && atoi(getenv("LISLAM_ORB_PYR_LEVELS")) == 1;
-  const bool fused = !by_level && g.W % 4 == 0 && g.h[1] <= 64 && g.stride[0] / 4 <= kPyrThreads &&
+  const bool fused = g.W % 4 == 0 && g.h[1] <= 64 && g.stride[0] / 4 <= kPyrThreads &&
                      pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
   {
     TimedScope t(c, kT_orb_pyramid);
@@ -2139,11 +2084,7 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   {
     TimedScope t(c, kT_orb_match);
     hipLaunchKernelGGL(k_orb_mfill, dim3(gp, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
-    static const bool valu = getenv("LISLAM_XDIST_VALU") != nullptr;  // developer A/B switch
-    if (valu)
-      hipLaunchKernelGGL(k_orb_xdist, dim3(gp, cdiv(te->g.cap, kXdTrains)), dim3(kXdThreads), 0, st, p);
-    else
-      hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
+    hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
     hipLaunchKernelGGL(k_orb_match, dim3(gp), dim3(kPairThreads), 0, st, p);
   }
   if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(gp), dim3(kLmThreads), 0, st, p, 20); }
@@ -2369,11 +2310,6 @@ int batch_intensity_odometry_dev(lislam_batch* b, OrbBatch* ob, int n_scans) {
   return LISLAM_OK;
 }
 
-bool orb_host_cascade() {  // LISLAM_ORB_HOST_CASCADE = 1: decide between rounds on the host
-  static const bool v = getenv("LISLAM_ORB_HOST_CASCADE") && atoi(getenv("LISLAM_ORB_HOST_CASCADE")) == 1;
-  return v;
-}
-
 }  // namespace
 
 // Before the outputs of a device-decided cascade are read, and before lislam_batch_extract
@@ -2418,7 +2354,7 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
   ob->pending = false;  // a newer batch replaces results nobody read
   ob->info[0] = -1;
   ob->info[1] = 0;
-  const int rc = (orb_host_cascade() || n_scans < 2 || n_scans > kCascadeMax) ? batch_intensity_odometry(b, ob, n_scans)
+  const int rc = (n_scans < 2 || n_scans > kCascadeMax) ? batch_intensity_odometry(b, ob, n_scans)
                                                                                : batch_intensity_odometry_dev(b, ob, n_scans);
   c->stream = main_stream;
   OCHK(c, hipEventRecord(ob->done, ob->side));

@@ -1,17 +1,28 @@
-set -o pipefail
+# round-4 A/B + profiles: each step logs to $D; a test failure does not stop the later steps, a
+# fault / abort / time limit (exit >= 124) ends the script
 cd $GRAFT_REPO_ROOT
 D=gpurun_out/r04h
 mkdir -p $D
-LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr2.so timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py -x -v --timeout 200 --timeout-method thread > $D/orb_tests_pyr2.log 2>&1 && \
-LISLAM_ALT_LIB=scripts/_ab/liblislam_orbbase.so timeout -k 10 120 python3 -u scripts/orb_quick.py 300 > $D/orb_base.txt 2>&1 && \
-timeout -k 10 120 python3 -u scripts/orb_quick.py 300 > $D/orb_main.txt 2>&1 && \
-LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof.so timeout -k 10 120 python3 -u scripts/orb_quick.py 300 > $D/orb_prof.txt 2>&1 && \
-LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr2prof.so timeout -k 10 120 python3 -u scripts/orb_quick.py 300 > $D/orb_pyr2prof.txt 2>&1 && \
-LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so timeout -k 10 180 python3 -u scripts/engine_prof.py 300 > $D/engprof_split.txt 2>&1 && \
-LISLAM_ENGINE_WGS=248 LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so timeout -k 10 180 python3 -u scripts/engine_prof.py 300 > $D/engprof_split248.txt 2>&1 && \
-LISLAM_ENGINE_SINGLE=1 LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so timeout -k 10 180 python3 -u scripts/engine_prof.py 300 > $D/engprof_single.txt 2>&1
-test $? -eq 0 && \
-LISLAM_ALT_LIB=scripts/_ab/liblislam_lines2.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $D/parity_lines2.log 2>&1 && \
-timeout -k 10 300 python3 -u scripts/ab_lines.py scripts/_ab/liblislam_linesbase.so main > $D/ab_lines2.txt 2>&1 && \
-LISLAM_PROF_LIB=scripts/_ab/liblislam_linesbaseprof.so timeout -k 10 120 python3 -u scripts/phase_prof.py lines 300 > $D/lines_phase_base.txt 2>&1 && \
-LISLAM_PROF_LIB=scripts/_ab/liblislam_lines2prof.so timeout -k 10 120 python3 -u scripts/phase_prof.py lines 300 > $D/lines_phase_new.txt 2>&1
+step() {  # step <log> <timeout s> <command...>
+  local log=$1 to=$2; shift 2
+  timeout -k 10 $to "$@" > $D/$log 2>&1
+  local rc=$?
+  echo "$log rc=$rc" >> $D/steps.txt
+  if [ $rc -ge 124 ]; then exit $rc; fi
+  return 0
+}
+export PYTHONUNBUFFERED=1
+step orb_tests_pyr3.log 300 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3.so python -m pytest tests/test_gpu_orb.py -x -v --timeout 200 --timeout-method thread
+step orb_tests_main.log 300 python -m pytest tests/test_gpu_orb.py -x -v --timeout 200 --timeout-method thread
+step orb_pyr3.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3.so python3 scripts/orb_quick.py 300
+step orb_main.txt 120 python3 scripts/orb_quick.py 300
+step orb_base.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbbase.so python3 scripts/orb_quick.py 300
+step orb_prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof.so python3 scripts/orb_quick.py 300
+step orb_pyr3prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3prof.so python3 scripts/orb_quick.py 300
+step parity_main.log 400 python -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread
+step ab_lines.txt 300 python3 scripts/ab_lines.py scripts/_ab/liblislam_linesbase.so main
+step lines_phase_base.txt 120 env LISLAM_PROF_LIB=scripts/_ab/liblislam_linesbaseprof.so python3 scripts/phase_prof.py lines 300
+step lines_phase_new.txt 120 env LISLAM_PROF_LIB=scripts/_ab/liblislam_lines2prof.so python3 scripts/phase_prof.py lines 300
+step engprof_split.txt 180 env LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so python3 scripts/engine_prof.py 300
+step engprof_split248.txt 180 env LISLAM_ENGINE_WGS=248 LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so python3 scripts/engine_prof.py 300
+step engprof_single.txt 180 env LISLAM_ENGINE_SINGLE=1 LISLAM_ALT_LIB=scripts/_ab/liblislam_engprof.so python3 scripts/engine_prof.py 300
