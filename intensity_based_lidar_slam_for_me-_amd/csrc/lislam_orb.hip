@@ -328,14 +328,13 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
       __syncthreads();  // level l complete; the next level writes the buffer read above
       PYR_PHASE(8 + l);
     }
-    // the padded level: ndr dword columns x P row phases (P = threads / ndr), a thread's column
-    // and its reflections fixed per level.  A dword of 4 ROI columns is the two aligned LDS dwords
-    // around it shifted (alignbyte); a border dword gathers its 4 reflected bytes.  The blurred copy
-    // (k_orb_blur's output) takes the same bytes except where a dword holds ROI columns of a ROI
-    // row: those come from the blur pass below.
-    const int ndr = g.stride[l] / 4, rows = h + 2 * kB;
+    // the ROI rows of the padded level (border columns included): ndr dword columns x P row
+    // phases (P = threads / ndr), a thread's column and its reflections fixed per level.  A dword
+    // of 4 ROI columns is the two aligned LDS dwords around it shifted (alignbyte); a border dword
+    // gathers its 4 reflected bytes.  The border rows and the blurred copy are k_orb_fastnms' (its
+    // bands stage these rows anyway).
+    const int ndr = g.stride[l] / 4;
     uint32_t* dst = reinterpret_cast<uint32_t*>(base + g.off[l]);
-    uint32_t* bdst = a.blur ? reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]) : nullptr;
     {
       const int P = kPyrThreads / ndr, dc = (int)threadIdx.x % ndr, ph = (int)threadIdx.x / ndr;
       if (ph < P) {
@@ -343,102 +342,21 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
 #pragma unroll
         for (int k = 0; k < 4; k++) cx[k] = reflect101(4 * dc + k - kB, w);
         const bool inner = 4 * dc - kB >= 0 && 4 * dc + 3 - kB < w;
-        const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
-        for (int rr = ph; rr < rows; rr += P) {
-          const int ro = reflect101(rr - kB, h) * w;
+        for (int r = ph; r < h; r += P) {
           uint32_t v;
           if (inner) {
-            const int A = ro + 4 * dc - kB;
+            const int A = r * w + 4 * dc - kB;
             const uint32_t* d = reinterpret_cast<const uint32_t*>(cur + (A & ~3));
             v = __builtin_amdgcn_alignbyte(d[1], d[0], (uint32_t)(A & 3));
           } else {
-            const uint8_t* src = cur + ro;
+            const uint8_t* src = cur + r * w;
             v = (uint32_t)src[cx[0]] | (uint32_t)src[cx[1]] << 8 | (uint32_t)src[cx[2]] << 16 | (uint32_t)src[cx[3]] << 24;
           }
-          dst[rr * ndr + dc] = v;
-          if (bdst && !(roi_dw && rr >= kB && rr < kB + h)) bdst[rr * ndr + dc] = v;
+          dst[(r + kB) * ndr + dc] = v;
         }
       }
     }
     PYR_PHASE(16 + l);
-    if (bdst) {
-      // GaussianBlur(ROI, 7x7, sigma 2, BORDER_REFLECT_101) of the dwords holding ROI columns, in
-      // k_orb_blur's float order: per row, 4 row sums of 7 taps (a sliding window of 7 rows in
-      // registers), then the symmetric column sum.  A thread owns a dword column holding ROI
-      // columns and one of nseg row segments of >= 16 rows (each segment re-sums 6 rows; more
-      // segments than one pass of the workgroup holds would only add passes).
-      const int dlo = kB / 4, ndw = (kB + w - 1) / 4 - dlo + 1;
-      const int nseg = max(1, min(h / 16, kPyrThreads / ndw));
-      for (int item = threadIdx.x; item < ndw * nseg; item += kPyrThreads) {
-        const int dc = dlo + item % ndw, seg = item / ndw;
-        const int ra = seg * h / nseg, rb = (seg + 1) * h / nseg;
-        const int c4 = 4 * dc;  // padded column of byte 0
-        if (ra >= rb) continue;
-        // columns c4 - 3 .. c4 + 6 all inside the ROI: the 10 bytes from 3 aligned LDS dwords
-        const bool inner = c4 - 3 - kB >= 0 && c4 + 6 - kB < w;
-        // float pairs (columns j, j + 1): the packed multiplies and adds round like the scalar
-        // ones, in the same order (row taps 0..6, then the symmetric column sum)
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 rs[7][2];
-        auto rowsum = [&](int r, f2* out) {
-          const uint8_t* src = cur + reflect101(r, h) * w;
-          float b[10];
-          if (inner) {
-            const int A = (int)(src - cur) + c4 - 3 - kB;
-            const uint32_t* d = reinterpret_cast<const uint32_t*>(cur + (A & ~3));
-            const uint32_t sh = (uint32_t)(A & 3), d3 = d[3];
-            const uint32_t u0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
-            const uint32_t u1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
-            const uint32_t u2 = __builtin_amdgcn_alignbyte(d3, d[2], sh);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              b[e] = (float)((u0 >> (8 * e)) & 255u);
-              b[4 + e] = (float)((u1 >> (8 * e)) & 255u);
-            }
-            b[8] = (float)(u2 & 255u);
-            b[9] = (float)((u2 >> 8) & 255u);
-          } else {  // a dword near the ROI's edge: reflect-101 columns
-#pragma unroll
-            for (int i = 0; i < 10; i++) b[i] = (float)src[reflect101(c4 - 3 + i - kB, w)];
-          }
-#pragma unroll
-          for (int jp = 0; jp < 2; jp++) {
-            f2 v = g.gk[0] * f2{b[2 * jp], b[2 * jp + 1]};
-#pragma unroll
-            for (int t = 1; t < 7; t++) v += g.gk[t] * f2{b[2 * jp + t], b[2 * jp + 1 + t]};
-            out[jp] = v;
-          }
-        };
-#pragma unroll
-        for (int k = 0; k < 6; k++) rowsum(ra - 3 + k, rs[k + 1]);
-        for (int r = ra; r < rb; r++) {
-#pragma unroll
-          for (int k = 0; k < 6; k++)
-#pragma unroll
-            for (int jp = 0; jp < 2; jp++) rs[k][jp] = rs[k + 1][jp];
-          rowsum(r + 3, rs[6]);
-          const uint8_t* src = cur + r * w;
-          float cv[4];
-#pragma unroll
-          for (int jp = 0; jp < 2; jp++) {
-            f2 v = g.gk[3] * rs[3][jp];
-#pragma unroll
-            for (int t = 1; t <= 3; t++) v += g.gk[3 + t] * (rs[3 + t][jp] + rs[3 - t][jp]);
-            cv[2 * jp] = v.x;
-            cv[2 * jp + 1] = v.y;
-          }
-          uint32_t o = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int cr = c4 + j - kB;
-            const uint32_t ob = (cr >= 0 && cr < w) ? (uint32_t)min(255, max(0, (int)rintf(cv[j]))) : (uint32_t)src[reflect101(cr, w)];
-            o |= ob << (8 * j);
-          }
-          bdst[(r + kB) * ndr + dc] = o;
-        }
-      }
-    }
-    PYR_PHASE(24 + l);
   }
 }
 
@@ -612,17 +530,43 @@ __device__ __forceinline__ int fast_full(const uint8_t* p, int ts) {
   return corner_score(dd, kFastT);
 }
 
-// LDS of a k_orb_fastnms workgroup for a level of width w: the image tile ((kFastBand + 8) rows of
-// fast_tile_stride bytes), the score tile ((kFastBand + 2) rows of w + 2 bytes, dword-padded) and
-// the candidate list (u16 score-tile positions: (kFastBand + 2) (w + 2) <= 65536, host-checked)
-__host__ __device__ __forceinline__ int fast_tile_stride(int w) { return 4 * ((w + 12 + 3) >> 2); }
+// LDS of a k_orb_fastnms workgroup for a level of padded row stride ps and width w: the image tile
+// ((kFastBand + 8) padded rows), the score tile ((kFastBand + 2) rows of w + 2 bytes,
+// dword-padded) and the candidate list (u16 score-tile positions: (kFastBand + 2) (w + 2) <= 65536,
+// host-checked)
 __host__ __device__ __forceinline__ int fast_score_bytes(int w) { return ((kFastBand + 2) * (w + 2) + 3) & ~3; }
-__host__ __device__ __forceinline__ size_t fast_lds_bytes(int w) {
-  return (size_t)(kFastBand + 8) * fast_tile_stride(w) + fast_score_bytes(w) + (size_t)2 * (kFastBand + 2) * (w + 2);
+__host__ __device__ __forceinline__ size_t fast_lds_bytes(int ps, int w) {
+  return (size_t)(kFastBand + 8) * ps + fast_score_bytes(w) + (size_t)2 * (kFastBand + 2) * (w + 2);
 }
 
-// FAST keypoints of a band of kFastBand ROI rows of a level: the band's pixels +-4 rows / columns
-// staged in LDS, FAST scores of the band +-1 (border pixels 0) into a second LDS tile, then
+// Stage tile rows t = 0 .. rows-1 = level rows r0 - 4 + t, reflect-101 (so only the ROI rows of the
+// padded level are read), whole padded rows of nd dwords; every load before the first store.
+template <int kMaxRows>
+__device__ __forceinline__ void stage_rows_reflect(uint32_t* dst, const uint8_t* lvl, int ps, int r0, int h, int rows,
+                                                   int nd) {
+  for (int j0 = 0; j0 < nd; j0 += 2 * 256) {
+    uint32_t v[kMaxRows][2];
+#pragma unroll
+    for (int r = 0; r < kMaxRows; r++) {
+      const uint8_t* src = lvl + (size_t)(reflect101(r0 - 4 + r, h) + kB) * ps;
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int d = j0 + u * 256 + (int)threadIdx.x;
+        if (r < rows && d < nd) v[r][u] = *(const __attribute__((address_space(1))) uint32_t*)(src + 4 * d);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kMaxRows; r++)
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int d = j0 + u * 256 + (int)threadIdx.x;
+        if (r < rows && d < nd) dst[r * nd + d] = v[r][u];
+      }
+  }
+}
+
+// FAST keypoints of a band of kFastBand ROI rows of a level: the band's rows +-4 staged in LDS
+// (whole padded rows), FAST scores of the band +-1 (border pixels 0) into a second LDS tile, then
 // 3x3 non-max suppression of FAST_t, the pixel mask (runByPixelsMask) and the image border
 // (edgeThreshold 1): nms = the FAST score of a keypoint, else 0.  The scores take two passes over
 // the whole band, one barrier apart: every pixel takes the cheap necessary test (an opposite pair
@@ -630,7 +574,11 @@ __host__ __device__ __forceinline__ size_t fast_lds_bytes(int w) {
 // into one LDS list (wave ballot + one LDS atomic per wave), then the full segment test and
 // cornerScore run on the list with every lane busy.  The list's order is the atomics' order; each
 // entry writes only its own score, so the result does not depend on it.
-__global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
+// band_blur (the one-workgroup-per-scan pyramid, which writes only the ROI rows): the band also
+// writes its rows of the blurred copy — GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the ROI
+// from the staged rows, border columns copied — and the first / last band the level's border rows
+// (reflect-101 copies of ROI rows) of both padded pyramids.
+__global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ftile[];
   __shared__ int lcnt;
   const Geom& g = a.g;
@@ -640,16 +588,15 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
   const int w = g.w[l], h = g.h[l];
   const int r0 = ((int)blockIdx.x - g.fband[l]) * kFastBand;
   const int nr = min(kFastBand, h - r0);
-  // image tile: rows r0-4 .. r0+nr+3, padded columns 16 .. (level columns -7 ..), dword rows
-  const int ts = fast_tile_stride(w), nd = ts >> 2;
-  constexpr int kC0 = kB - 16;  // tile column of level column 0
+  // image tile: rows r0-4 .. r0+nr+3, whole padded rows (tile column = padded column)
+  const int ts = g.stride[l], nd = ts >> 2;
+  constexpr int kC0 = kB;  // tile column of level column 0
   uint8_t* img = ftile;
   uint8_t* sct = ftile + (kFastBand + 8) * ts;  // scores: rows r0-1 .., columns -1 .. w
   const int ss = w + 2;
   uint16_t* list = reinterpret_cast<uint16_t*>(sct + fast_score_bytes(w));
-  const uint8_t* base = a.pyr + (size_t)s * g.bytes;
-  stage_rows<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), base + g.off[l] + (r0 - 4 + kB) * g.stride[l] + 16,
-                            g.stride[l], nr + 8, nd);
+  uint8_t* const lvl = a.pyr + (size_t)s * g.bytes + g.off[l];
+  stage_rows_reflect<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), lvl, ts, r0, h, nr + 8, nd);
   {
     uint32_t* z = reinterpret_cast<uint32_t*>(sct);
     for (int i = threadIdx.x; i < fast_score_bytes(w) / 4; i += blockDim.x) z[i] = 0u;
@@ -705,6 +652,81 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
         if (keep && !(c >= 1 && c < w - 1 && r >= 1 && r < h - 1)) keep = false;
       }
       out[r * w + c] = keep ? (uint8_t)v : 0;
+    }
+  }
+  if (!band_blur) return;
+  // 3. the band's rows of the blurred copy: per dword column, a sliding window of 7 row sums
+  //    (float pairs: columns j, j + 1; packed multiplies and adds round like the scalar ones, in the
+  //    same order: row taps 0..6, then the symmetric column sum); bytes outside the ROI copied
+  uint32_t* const bl = reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]);
+  const uint32_t* const t32 = reinterpret_cast<const uint32_t*>(img);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  for (int dc = threadIdx.x; dc < nd; dc += blockDim.x) {
+    const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
+    if (!roi_dw) {
+      for (int k = 0; k < nr; k++) bl[(r0 + k + kB) * nd + dc] = t32[(k + 4) * nd + dc];
+      continue;
+    }
+    auto rowsum = [&](int t, f2* out2) {  // tile row t, padded columns 4 dc - 3 .. 4 dc + 6
+      const uint32_t d0 = t32[t * nd + dc - 1], d1 = t32[t * nd + dc], d2 = t32[t * nd + dc + 1];
+      float b[10];
+      b[0] = (float)((d0 >> 8) & 255u);
+      b[1] = (float)((d0 >> 16) & 255u);
+      b[2] = (float)(d0 >> 24);
+#pragma unroll
+      for (int e = 0; e < 4; e++) b[3 + e] = (float)((d1 >> (8 * e)) & 255u);
+#pragma unroll
+      for (int e = 0; e < 3; e++) b[7 + e] = (float)((d2 >> (8 * e)) & 255u);
+#pragma unroll
+      for (int jp = 0; jp < 2; jp++) {
+        f2 v = g.gk[0] * f2{b[2 * jp], b[2 * jp + 1]};
+#pragma unroll
+        for (int t2 = 1; t2 < 7; t2++) v += g.gk[t2] * f2{b[2 * jp + t2], b[2 * jp + 1 + t2]};
+        out2[jp] = v;
+      }
+    };
+    f2 rs[7][2];
+#pragma unroll
+    for (int k = 0; k < 6; k++) rowsum(1 + k, rs[k + 1]);
+    for (int k = 0; k < nr; k++) {
+#pragma unroll
+      for (int q = 0; q < 6; q++)
+#pragma unroll
+        for (int jp = 0; jp < 2; jp++) rs[q][jp] = rs[q + 1][jp];
+      rowsum(k + 7, rs[6]);
+      float cv[4];
+#pragma unroll
+      for (int jp = 0; jp < 2; jp++) {
+        f2 v = g.gk[3] * rs[3][jp];
+#pragma unroll
+        for (int t2 = 1; t2 <= 3; t2++) v += g.gk[3 + t2] * (rs[3 + t2][jp] + rs[3 - t2][jp]);
+        cv[2 * jp] = v.x;
+        cv[2 * jp + 1] = v.y;
+      }
+      const uint32_t raw = t32[(k + 4) * nd + dc];
+      uint32_t o = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int cr = 4 * dc + j - kB;
+        const uint32_t ob = (cr >= 0 && cr < w) ? (uint32_t)min(255, max(0, (int)rintf(cv[j]))) : (raw >> (8 * j)) & 255u;
+        o |= ob << (8 * j);
+      }
+      bl[(r0 + k + kB) * nd + dc] = o;
+    }
+  }
+  // 4. border rows (first / last band): padded row rr = ROI row reflect101(rr - kB), both copies
+  const bool top = r0 == 0, bottom = r0 + nr == h;
+  if (top || bottom) {
+    uint32_t* const py = reinterpret_cast<uint32_t*>(lvl);
+    for (int half = 0; half < 2; half++) {
+      if (!(half ? bottom : top)) continue;
+      for (int it = threadIdx.x; it < kB * nd; it += blockDim.x) {
+        const int q = it / nd, dc = it - q * nd;
+        const int rr = half ? kB + h + q : q;
+        const uint32_t v = py[(reflect101(rr - kB, h) + kB) * nd + dc];
+        py[rr * nd + dc] = v;
+        bl[rr * nd + dc] = v;
+      }
     }
   }
 }
@@ -1962,8 +1984,8 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   }
   {
     TimedScope t(c, kT_orb_fast);
-    const size_t lds = fast_lds_bytes(g.w[0]);
-    hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
+    const size_t lds = fast_lds_bytes(g.stride[0], g.w[0]);
+    hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a, (fused && a.blur) ? 1 : 0);
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }

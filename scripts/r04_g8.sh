@@ -17,7 +17,10 @@ step orb_tests_main.log 300 python -m pytest tests/test_gpu_orb.py -x -v --timeo
 step orb_pyr3.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3.so python3 scripts/orb_quick.py 300
 step orb_main.txt 120 python3 scripts/orb_quick.py 300
 step orb_base.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbbase.so python3 scripts/orb_quick.py 300
+step orb_fb8.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_fb8.so python3 scripts/orb_quick.py 300
+step orb_fb16.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_fb16.so python3 scripts/orb_quick.py 300
 step orb_prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof.so python3 scripts/orb_quick.py 300
+step orb_prof4.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof4.so python3 scripts/orb_quick.py 300
 step orb_pyr3prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3prof.so python3 scripts/orb_quick.py 300
 step parity_main.log 400 python -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread
 step ab_lines.txt 300 python3 scripts/ab_lines.py scripts/_ab/liblislam_linesbase.so main
