@@ -11,16 +11,20 @@
 // octave; descriptors 32 B; cloud points float4.
 //
 // Kernels (the semantics are those of oracle/oracle_orb.cpp, which restates OpenCV 4.x):
-//   k_orb_level     per level (in order), 1 thread per 4 padded pixels: level 0 copy, levels 1..7 by
-//                   the bit-exact fixed-point INTER_LINEAR_EXACT resize of the previous level;
-//                   border pixels evaluate their reflect-101 source directly
-//   k_orb_blur      1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2 separable float
-//                   Gaussian (row sums then the symmetric column sum, the FilterEngine order) on
-//                   the ROI, border copy
-//   k_orb_fastnms   1 WG per band of LISLAM_FAST_BAND level rows, staged in LDS: cheap test of
-//                   every pixel of the band into one candidate list, FAST-9/16 segment test +
+//   k_orb_pyramid   1 WG per scan (images whose levels 0 + 1 fit LDS, e.g. 64 x 1024): the level
+//                   chain in LDS — levels 1..7 by the bit-exact fixed-point INTER_LINEAR_EXACT
+//                   resize of the previous level — and each level's ROI rows (border columns
+//                   included) written once
+//   k_orb_level     (larger images) per level, in order, 1 thread per 4 padded pixels: the same
+//                   resize; border pixels evaluate their reflect-101 source directly
+//   k_orb_blur      (larger images) 1 WG per band of 8 padded rows, staged in LDS: 7x7 sigma-2
+//                   separable float Gaussian (row sums then the symmetric column sum, the
+//                   FilterEngine order) on the ROI, border copy
+//   k_orb_fastnms   1 WG per band of LISLAM_FAST_BAND level rows, reflect-staged in LDS: cheap test
+//                   of every pixel of the band into one candidate list, FAST-9/16 segment test +
 //                   cornerScore<16> of the list into an LDS score tile, then 3x3 non-max
-//                   suppression, mask, border
+//                   suppression, mask, border; after k_orb_pyramid also the band's blurred rows
+//                   (packed float pairs) and the level's border rows
 //   k_orb_select    1 WG per (scan, level): ordered compaction (a contiguous pixel segment per
 //                   thread), retainBest(2n) on the FAST score (256-bin histogram), Harris responses
 //                   (a wavefront per 4 candidates, all their loads in flight), retainBest(n) on
@@ -29,11 +33,12 @@
 //                   kept (OpenCV's set, canonical order)
 //   k_orb_finish    1 WG per scan: levels concatenated, coordinates scaled to level 0,
 //                   cloud-track lookup + |x| < 0.01 filter (extractPointsAndFilterZeroValue)
-//   k_orb_desc      32 threads per keypoint: steered rBRIEF-256 bytes
-//   k_orb_match     1 WG per scan pair: XOR-popcount distances against LDS query tiles (wave-
-//                   broadcast reads), batchDistance's cross-check,
-//                   stable counting selection of the first ceil(frac M) matches, good-frame
-//                   test, front_end_residual records
+//   k_orb_desc      32 lanes per keypoint: the keypoint's 37 x 37 blurred patch staged in LDS,
+//                   steered rBRIEF-256 bytes from it
+//   k_orb_xdist_mfma per (pair, 256 trains): Hamming distances on the int8 matrix cores over
+//                   0/1-expanded descriptors, batchDistance's cross-check (atomicMin)
+//   k_orb_match     1 WG per scan pair: stable counting selection of the first ceil(frac M)
+//                   matches, good-frame test, front_end_residual records
 //   k_orb_lm        1 WG per scan pair: Ceres-semantics LM (20 iterations) of those records
 #include <hip/hip_runtime.h>
 
@@ -73,7 +78,9 @@ constexpr int kNPatch = 749;  // pixels of the ICAngles circular patch (half siz
 constexpr int kPatchIters = (kNPatch + 63) / 64;
 __constant__ short2 c_patch[1024];  // (du, dv) of every pixel of the ICAngles patch (host-filled)
 
-__constant__ int c_pattern[256 * 4] = {
+// the rBRIEF pattern as bytes (every coordinate is in [-13, 13]): a descriptor byte's 8 point pairs
+// are 32 consecutive bytes, 8 dwords per lane
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[256 * 4] = {
 #include "lislam_orb_pattern.inc"
 };
 
@@ -223,14 +230,15 @@ __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
     *(__attribute__((address_space(1))) uint8_t*)dst = (uint8_t)word[0];
 }
 
-// The whole pyramid of a scan in one workgroup (levels 0 and 1 fit LDS together): level l-1's ROI
-// stays in LDS while level l is resized from it, ping-ponging between a level-0-sized buffer (even
-// levels) and a level-1-sized one (odd levels), and each padded level is written to HBM once, from
-// LDS, with dword stores (a dword never spans rows: strides are 16-byte multiples).  Same pixels as
-// k_orb_level: border pixels take their reflect-101 ROI pixel, ROI pixels the INTER_LINEAR_EXACT
-// fixed-point resize (hval) of level l-1.  A thread owns a column of the level (its horizontal
-// taps in registers) and walks the rows; the row taps (levels >= 1 have <= 64 rows) sit one per
-// lane and are read with readlane.
+// The pyramid of a scan in one workgroup (levels 0 and 1 fit LDS together): level l-1's ROI stays
+// in LDS while level l is resized from it, ping-ponging between a level-0-sized buffer (even levels)
+// and a level-1-sized one (odd levels); each level's ROI rows go to HBM once, from LDS, with dword
+// stores (a dword never spans rows: strides are 16-byte multiples).  Same pixels as k_orb_level:
+// ROI pixels are level 0's image or the INTER_LINEAR_EXACT fixed-point resize (hval) of level l-1,
+// border columns their reflect-101 ROI pixel.  A thread owns a column of the level (its horizontal
+// taps in registers) and walks the rows four at a time; the row taps (levels >= 1 have <= 64 rows)
+// sit one per lane and are read with readlane.  The border rows and the blurred copy are written
+// by k_orb_fastnms' bands, which stage the rows they need anyway.
 #ifdef LISLAM_PHASE_PROF
 // k_orb_pyramid phase split (profiling builds): slot 0 the image load, 8 p + l phase p (1 resize,
 // 2 padded copy, 3 blur) of level l, summed over workgroups in s_memrealtime ticks (100 MHz)
@@ -1196,14 +1204,18 @@ __global__ __launch_bounds__(256) void k_orb_finish(Args a) {
   }
 }
 
-// steered rBRIEF: 32 lanes per keypoint, one descriptor byte each (keypoints grid-strided over
-// gridDim.x blocks of 8).  The pattern's points lie in [-13, 13]^2, so rotated and rounded they
-// stay within kDescR = 18 of the keypoint: its 37 x 37 blurred patch is staged in LDS by the 32
-// lanes (10 aligned dwords per row, all loads in flight), then the 512 tests read LDS.  A patch
-// is written and read by one wavefront only (two keypoints per wavefront, one LDS slot each).
+// steered rBRIEF: 32 lanes per keypoint, one descriptor byte each.  A workgroup takes chunks of
+// kDescChunk keypoints (grid-strided): one lane per keypoint first computes its rotation (the
+// double-precision cos / sin, once per keypoint instead of once per wavefront) and patch address
+// into LDS tables, then each half-wave slot runs every 8th keypoint of the chunk.  The pattern's
+// points lie in [-13, 13]^2, so rotated and rounded they stay within kDescR = 18 of the keypoint:
+// its 37 x 37 blurred patch is staged in the slot's LDS by its 32 lanes (10 aligned dwords per row;
+// the next keypoint's loads are in flight while this one's 512 tests read LDS).  A slot is written
+// and read by one wavefront only.
 constexpr int kDescR = 18;
 constexpr int kDescRow = 40;  // staged bytes per patch row: 37 + the dword misalignment (<= 3)
 constexpr int kDescDw = (2 * kDescR + 1) * (kDescRow / 4);  // 370 dwords per patch
+constexpr int kDescChunk = 64;
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1211,51 +1223,70 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
   __shared__ uint32_t patch[8][kDescDw];
+  __shared__ float kcs[kDescChunk][2];  // cos, sin of the keypoint's angle
+  __shared__ int kpos[kDescChunk][2];   // patch byte offset in the scan's blurred pyramid, stride | shift << 16
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[gi] : gi;
   const int byte = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const int nk = a.nkp[s];
   const uint8_t* base = a.blur + (size_t)s * g.bytes;
   const uint8_t* P = reinterpret_cast<const uint8_t*>(patch[slot]);
-  for (int k = blockIdx.x * 8 + slot; k < nk; k += gridDim.x * 8) {
-    const float* kp = a.kp + ((size_t)s * g.cap + k) * 6;
-    const int l = (int)kp[5];
-    const float scale = 1.f / g.scale[l];
-    const float ang = kp[3] * (float)(kPi / 180.f);
-    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
-    const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
-    // padded rows cy - 18 .. cy + 18, padded columns pc0 .. pc0 + 39 (pc0 = cx - 18 + kB rounded
-    // down to a dword; the row has >= 44 bytes right of cx, kB = 23 > 18 above and below)
-    const int pc = cx - kDescR + kB, pc0 = pc & ~3, sh = pc - pc0;
-    const uint8_t* src = base + g.off[l] + (size_t)(cy - kDescR + kB) * g.stride[l] + pc0;
+  const int* pat = reinterpret_cast<const int*>(c_pattern) + byte * 8;  // x1 y1 x2 y2 of bits 0..7
+  for (int k0 = blockIdx.x * kDescChunk; k0 < nk; k0 += gridDim.x * kDescChunk) {
+    __syncthreads();  // the previous chunk's tables are no longer read
+    if (threadIdx.x < kDescChunk && k0 + (int)threadIdx.x < nk) {
+      const float* kp = a.kp + ((size_t)s * g.cap + k0 + threadIdx.x) * 6;
+      const int l = (int)kp[5];
+      const float scale = 1.f / g.scale[l];
+      const float ang = kp[3] * (float)(kPi / 180.f);
+      kcs[threadIdx.x][0] = (float)cos((double)ang);
+      kcs[threadIdx.x][1] = (float)sin((double)ang);
+      const int cy = (int)rintf(kp[1] * scale), cx = (int)rintf(kp[0] * scale);
+      // padded rows cy - 18 .. cy + 18, padded columns pc0 .. pc0 + 39 (pc0 = cx - 18 + kB rounded
+      // down to a dword; the row has >= 44 bytes right of cx, kB = 23 > 18 above and below)
+      const int pc = cx - kDescR + kB, pc0 = pc & ~3;
+      kpos[threadIdx.x][0] = g.off[l] + (cy - kDescR + kB) * g.stride[l] + pc0;
+      kpos[threadIdx.x][1] = g.stride[l] | (pc - pc0) << 16;
+    }
+    __syncthreads();
+    const int n = min(kDescChunk, nk - k0);
     uint32_t v[(kDescDw + 31) / 32];
+    auto load = [&](int j) {
+      const uint8_t* src = base + kpos[j][0];
+      const int ps = kpos[j][1] & 0xffff;
 #pragma unroll
-    for (int i = 0; i < (kDescDw + 31) / 32; i++) {
-      const int e = byte + 32 * i, row = e / 10, d = e - 10 * row;
-      if (e < kDescDw) v[i] = *(const __attribute__((address_space(1))) uint32_t*)(src + (size_t)row * g.stride[l] + 4 * d);
-    }
-    wave_lds_sync();  // the previous keypoint's tests have read the slot
-#pragma unroll
-    for (int i = 0; i < (kDescDw + 31) / 32; i++) {
-      const int e = byte + 32 * i;
-      if (e < kDescDw) patch[slot][e] = v[i];
-    }
-    wave_lds_sync();
-    const uint8_t* c0 = P + kDescR * kDescRow + kDescR + sh;  // the keypoint's byte
-    int bits = 0;
-#pragma unroll
-    for (int bit = 0; bit < 8; bit++) {
-      const int p = (byte * 8 + bit) * 2;
-      int t[2];
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const float qx = (float)c_pattern[(p + e) * 2], qy = (float)c_pattern[(p + e) * 2 + 1];
-        const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
-        t[e] = c0[(int)rintf(y) * kDescRow + (int)rintf(x)];
+      for (int i = 0; i < (kDescDw + 31) / 32; i++) {
+        const int e = byte + 32 * i, row = e / 10, d = e - 10 * row;
+        if (e < kDescDw) v[i] = *(const __attribute__((address_space(1))) uint32_t*)(src + row * ps + 4 * d);
       }
-      bits |= (t[0] < t[1]) << bit;
+    };
+    if (slot < n) load(slot);
+    for (int j = slot; j < n; j += 8) {
+      wave_lds_sync();  // the previous keypoint's tests have read the slot
+#pragma unroll
+      for (int i = 0; i < (kDescDw + 31) / 32; i++) {
+        const int e = byte + 32 * i;
+        if (e < kDescDw) patch[slot][e] = v[i];
+      }
+      wave_lds_sync();
+      if (j + 8 < n) load(j + 8);
+      const float ca = kcs[j][0], sa = kcs[j][1];
+      const uint8_t* c0 = P + kDescR * kDescRow + kDescR + (kpos[j][1] >> 16);  // the keypoint's byte
+      int bits = 0;
+#pragma unroll
+      for (int bit = 0; bit < 8; bit++) {
+        const int pw = pat[bit];
+        int t[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const float qx = (float)__builtin_amdgcn_sbfe(pw, 16 * e, 8), qy = (float)__builtin_amdgcn_sbfe(pw, 16 * e + 8, 8);
+          const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
+          t[e] = c0[(int)rintf(y) * kDescRow + (int)rintf(x)];
+        }
+        bits |= (t[0] < t[1]) << bit;
+      }
+      a.desc[((size_t)s * g.cap + k0 + j) * 32 + byte] = (uint8_t)bits;
     }
-    a.desc[((size_t)s * g.cap + k) * 32 + byte] = (uint8_t)bits;
   }
 }
 
@@ -1993,7 +2024,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     TimedScope t(c, kT_orb_blur);
     hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
   }
-  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), n), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), n), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -2022,7 +2053,7 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const int ns = std::min(nmax, kListSlots);
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<true>, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
-  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, 8), ns), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }

@@ -19,6 +19,7 @@ step orb_main.txt 120 python3 scripts/orb_quick.py 300
 step orb_base.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbbase.so python3 scripts/orb_quick.py 300
 step orb_fb8.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_fb8.so python3 scripts/orb_quick.py 300
 step orb_fb16.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_fb16.so python3 scripts/orb_quick.py 300
+step orb_desc4.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_desc4.so python3 scripts/orb_quick.py 300
 step orb_prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof.so python3 scripts/orb_quick.py 300
 step orb_prof4.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_orbprof4.so python3 scripts/orb_quick.py 300
 step orb_pyr3prof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_pyr3prof.so python3 scripts/orb_quick.py 300
