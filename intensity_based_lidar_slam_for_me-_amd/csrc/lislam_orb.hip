@@ -984,22 +984,35 @@ __device__ __forceinline__ void orb_select_body(const Args& a, int gi) {
   // The 9 x 16-byte patches (rows y0-4 .. y0+4 from the dword holding column x0-4) of 4
   // candidates per wave iteration are staged in LDS by 144 dword loads, then each 16-lane row
   // reads the neighbourhoods of its candidate's 49 block pixels from LDS.
+  //    Software pipelined like the angles below: the next iteration's patch dwords are loaded into
+  //    registers while this iteration's sums read LDS.
   constexpr int kPerWave = 4;
+  constexpr int kHStg = (kPerWave * 36 + 63) / 64;
   const int stride_l = g.stride[l];
   const uint8_t* lvl = base + g.off[l];
-  for (int i0 = wv * kPerWave; i0 < n; i0 += nw * kPerWave) {
-    uint32_t* hp = sh_patch + wv * kPatchDw;
+  uint32_t hbuf[kHStg];
+  auto hfetch = [&](int i0f) {
 #pragma unroll
-    for (int k = 0; k < (kPerWave * 36 + 63) / 64; k++) {
+    for (int k = 0; k < kHStg; k++) {
       const int item = lane + 64 * k;
       if (item < kPerWave * 36) {
         const int u = item / 36, rr = (item % 36) >> 2, dw = item & 3;
-        const int ci = cand[min(i0 + u, n - 1)];
+        const int ci = cand[min(i0f + u, n - 1)];
         const int x0 = ci % w, y0 = ci / w;
-        hp[item] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y0 - 4 + rr + kB) * stride_l +
-                                                                           ((x0 - 4 + kB) & ~3) + 4 * dw);
+        hbuf[k] = *(const __attribute__((address_space(1))) uint32_t*)(lvl + (y0 - 4 + rr + kB) * stride_l +
+                                                                          ((x0 - 4 + kB) & ~3) + 4 * dw);
       }
     }
+  };
+  if (wv * kPerWave < n) hfetch(wv * kPerWave);
+  for (int i0 = wv * kPerWave; i0 < n; i0 += nw * kPerWave) {
+    uint32_t* hp = sh_patch + wv * kPatchDw;
+#pragma unroll
+    for (int k = 0; k < kHStg; k++) {
+      const int item = lane + 64 * k;
+      if (item < kPerWave * 36) hp[item] = hbuf[k];
+    }
+    if (i0 + nw * kPerWave < n) hfetch(i0 + nw * kPerWave);
     wave_lds_sync();
     // lane row u = lane >> 4 takes candidate i0 + u; its 16 lanes cover the 49 block pixels
     // (pixel t, t + 16, t + 32, t + 48) and the integer sums close with one row sum each
