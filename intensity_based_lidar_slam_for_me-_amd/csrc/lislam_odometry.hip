@@ -2855,17 +2855,23 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t r
   ctl.roles = 0;
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
+  // One item workgroup per CU of the items' mask (all CUs but one per XCD): its 8 waves at <= 128
+  // VGPRs take half of each SIMD's registers, so the next batch's extraction and ORB kernels run
+  // beside the engine instead of queueing behind it.  LISLAM_ENGINE_WGS caps the grid (tests: one
+  // workgroup drains the queue).
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
-  const int cap = cap_env ? atoi(cap_env) : 0;
+  const int cap = cap_env ? atoi(cap_env) : max(1, cus - 8);
   int grid = ctl.C * ctl.I;
-  if (cap > 0) grid = min(grid, max(cap, 1));  // one item workgroup drains the queue
+  if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = bud ? max(1, atoi(bud)) : max(1, grid / ctl.C);
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
   (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
   const hipEvent_t prev = engine_done_event(dev);
   if (prev) (void)hipStreamWaitEvent(st, prev, 0);
   (void)hipEventRecord(fork, st);

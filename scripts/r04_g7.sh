@@ -10,7 +10,7 @@ LISLAM_ALT_LIB=scripts/_ab/liblislam_fb8.so timeout -k 10 120 python3 -u scripts
 LISLAM_ALT_LIB=scripts/_ab/liblislam_fb16.so timeout -k 10 120 python3 -u scripts/orb_quick.py 300 > $D/orb_fb16.txt 2>&1 && \
 LISLAM_ENGINE_SINGLE=1 CHAIN_ENGINE_ONLY=1 CHAIN_REF=$REF timeout -k 10 120 python3 -u scripts/chain_quick.py 300 5 > $D/chain_single.txt 2>&1 && \
 CHAIN_ENGINE_ONLY=1 CHAIN_REF=$REF timeout -k 10 120 python3 -u scripts/chain_quick.py 300 5 > $D/chain_split.txt 2>&1 && \
-LISLAM_ENGINE_WGS=248 CHAIN_ENGINE_ONLY=1 CHAIN_REF=$REF timeout -k 10 120 python3 -u scripts/chain_quick.py 300 5 > $D/chain_split248.txt 2>&1 && \
+LISLAM_ENGINE_WGS=600 CHAIN_ENGINE_ONLY=1 CHAIN_REF=$REF timeout -k 10 120 python3 -u scripts/chain_quick.py 300 5 > $D/chain_split600.txt 2>&1 && \
 LISLAM_ENGINE_WGS=124 CHAIN_ENGINE_ONLY=1 CHAIN_REF=$REF timeout -k 10 120 python3 -u scripts/chain_quick.py 300 5 > $D/chain_split124.txt 2>&1 && \
-LISLAM_ENGINE_WGS=248 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-budget 0 --sustain-s 0 --segmented 0 > $D/bench_split248.json 2> $D/bench_split248.err && \
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-budget 0 --sustain-s 0 --segmented 0 > $D/bench_split.json 2> $D/bench_split.err && \
 LISLAM_ENGINE_WGS=124 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-budget 0 --sustain-s 0 --segmented 0 > $D/bench_split124.json 2> $D/bench_split124.err
