@@ -2809,17 +2809,32 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   return grid;
 }
 
-// The engine as two launches on CU-masked streams (k_odom_roles / k_odom_items): the streams of
-// one batch are made once (engine_streams); false = unavailable on this device (the caller runs
-// the single-launch engine instead).  A mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950,
-// measured: scripts/micro/cumask.hip); a mask with no bit of some XCD leaves that XCD unmasked, so
-// the roles get one bit in every XCD and the items every other bit.
+// The engine as two launches (k_odom_roles / k_odom_items) on streams of their own, made once per
+// batch (engine_streams); false = unavailable on this device (the caller runs the single-launch
+// engine instead).  The streams have the device's greatest priority: when a chain starts, the next
+// batch's extraction starts beside it (it was queued behind the previous chain), and the chain's
+// workgroups must be dispatched ahead of that flood, not after it drains.  LISLAM_ENGINE_STREAMS=mask
+// (developer A/B) uses CU-masked streams instead: a mask bit i selects a CU of XCD i % 8 (gfx942 /
+// gfx950, measured: scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD
+// unmasked), the roles one CU in every XCD, the items every other CU.
 bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
   const int cus = prop.multiProcessorCount, nx = 8;
   if (!multi_xcd || cus < 4 * nx || cus % nx) return false;
+  const char* mode = getenv("LISLAM_ENGINE_STREAMS");
+  if (!(mode && std::strcmp(mode, "mask") == 0)) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return false;
+    if (hipStreamCreateWithPriority(roles, hipStreamNonBlocking, greatest) != hipSuccess) return false;
+    if (hipStreamCreateWithPriority(items, hipStreamNonBlocking, greatest) != hipSuccess) {
+      (void)hipStreamDestroy(*roles);
+      *roles = nullptr;
+      return false;
+    }
+    return true;
+  }
   const int words = (cus + 31) / 32;
   std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
   for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);

@@ -72,17 +72,28 @@ constexpr int kNoMatch = 0x7f7f7f7f;
 #define LISLAM_FAST_BAND 4
 #endif
 constexpr int kFastBand = LISLAM_FAST_BAND;  // ROI rows per k_orb_fastnms workgroup
-constexpr int kBlurBand = 8;   // padded rows per k_orb_blur workgroup  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
+constexpr int kBlurBand = 8;   // padded rows per k_orb_blur workgroup
+constexpr int kRoiBand = 16;   // ROI rows per k_orb_roiblur workgroup  // best[] sentinel (memset 0x7f): above any (distance << 16 | train)
 
 constexpr int kNPatch = 749;  // pixels of the ICAngles circular patch (half size 15; checked on the host)
 constexpr int kPatchIters = (kNPatch + 63) / 64;
 __constant__ short2 c_patch[1024];  // (du, dv) of every pixel of the ICAngles patch (host-filled)
 
-// the rBRIEF pattern as bytes (every coordinate is in [-13, 13]): a descriptor byte's 8 point pairs
-// are 32 consecutive bytes, 8 dwords per lane
-__constant__ __attribute__((aligned(16))) int8_t c_pattern[256 * 4] = {
+// the rBRIEF pattern as bytes biased by 13 (every coordinate is in [-13, 13]): a descriptor byte's 8
+// point pairs are 32 consecutive bytes, 8 dwords per lane.  (Unsigned on purpose: a sign-extended
+// byte converted to float was compiled as an unsigned conversion.)
+constexpr int kPatternInt[256 * 4] = {
 #include "lislam_orb_pattern.inc"
 };
+struct PatternU8 {
+  uint8_t v[256 * 4];
+};
+constexpr PatternU8 pattern_u8() {
+  PatternU8 p{};
+  for (int i = 0; i < 256 * 4; i++) p.v[i] = (uint8_t)(kPatternInt[i] + 13);
+  return p;
+}
+__constant__ __attribute__((aligned(16))) PatternU8 c_pattern = pattern_u8();
 
 struct Geom {
   int W, H;
@@ -101,6 +112,7 @@ struct Geom {
   int umax[kHalf + 2];
   int fband[kL + 1];  // prefix of FAST bands (kFastBand ROI rows) per level
   int bband[kL + 1];  // prefix of blur bands (kBlurBand padded rows) per level
+  int rband[kL + 1];  // prefix of ROI blur bands (kRoiBand ROI rows) per level
 };
 
 struct Tabs {  // resize coefficients of level l from level l-1 (l >= 1), per axis
@@ -547,16 +559,16 @@ __host__ __device__ __forceinline__ size_t fast_lds_bytes(int ps, int w) {
   return (size_t)(kFastBand + 8) * ps + fast_score_bytes(w) + (size_t)2 * (kFastBand + 2) * (w + 2);
 }
 
-// Stage tile rows t = 0 .. rows-1 = level rows r0 - 4 + t, reflect-101 (so only the ROI rows of the
-// padded level are read), whole padded rows of nd dwords; every load before the first store.
+// Stage tile rows t = 0 .. rows-1 = level rows r0 - halo + t, reflect-101 (so only the ROI rows of
+// the padded level are read), whole padded rows of nd dwords; every load before the first store.
 template <int kMaxRows>
-__device__ __forceinline__ void stage_rows_reflect(uint32_t* dst, const uint8_t* lvl, int ps, int r0, int h, int rows,
-                                                   int nd) {
+__device__ __forceinline__ void stage_rows_reflect(uint32_t* dst, const uint8_t* lvl, int ps, int r0, int halo, int h,
+                                                   int rows, int nd) {
   for (int j0 = 0; j0 < nd; j0 += 2 * 256) {
     uint32_t v[kMaxRows][2];
 #pragma unroll
     for (int r = 0; r < kMaxRows; r++) {
-      const uint8_t* src = lvl + (size_t)(reflect101(r0 - 4 + r, h) + kB) * ps;
+      const uint8_t* src = lvl + (size_t)(reflect101(r0 - halo + r, h) + kB) * ps;
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int d = j0 + u * 256 + (int)threadIdx.x;
@@ -582,11 +594,7 @@ __device__ __forceinline__ void stage_rows_reflect(uint32_t* dst, const uint8_t*
 // into one LDS list (wave ballot + one LDS atomic per wave), then the full segment test and
 // cornerScore run on the list with every lane busy.  The list's order is the atomics' order; each
 // entry writes only its own score, so the result does not depend on it.
-// band_blur (the one-workgroup-per-scan pyramid, which writes only the ROI rows): the band also
-// writes its rows of the blurred copy — GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the ROI
-// from the staged rows, border columns copied — and the first / last band the level's border rows
-// (reflect-101 copies of ROI rows) of both padded pyramids.
-__global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
+__global__ __launch_bounds__(256) void k_orb_fastnms(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ftile[];
   __shared__ int lcnt;
   const Geom& g = a.g;
@@ -604,7 +612,7 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
   const int ss = w + 2;
   uint16_t* list = reinterpret_cast<uint16_t*>(sct + fast_score_bytes(w));
   uint8_t* const lvl = a.pyr + (size_t)s * g.bytes + g.off[l];
-  stage_rows_reflect<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), lvl, ts, r0, h, nr + 8, nd);
+  stage_rows_reflect<kFastBand + 8>(reinterpret_cast<uint32_t*>(img), lvl, ts, r0, 4, h, nr + 8, nd);
   {
     uint32_t* z = reinterpret_cast<uint32_t*>(sct);
     for (int i = threadIdx.x; i < fast_score_bytes(w) / 4; i += blockDim.x) z[i] = 0u;
@@ -662,17 +670,35 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
       out[r * w + c] = keep ? (uint8_t)v : 0;
     }
   }
-  if (!band_blur) return;
-  // 3. the band's rows of the blurred copy: per dword column, a sliding window of 7 row sums
-  //    (float pairs: columns j, j + 1; packed multiplies and adds round like the scalar ones, in the
-  //    same order: row taps 0..6, then the symmetric column sum); bytes outside the ROI copied
-  uint32_t* const bl = reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]);
-  const uint32_t* const t32 = reinterpret_cast<const uint32_t*>(img);
+}
+
+// After k_orb_pyramid (which writes only the ROI rows): one workgroup per band of kRoiBand ROI
+// rows of a level writes the band's rows of the blurred copy — GaussianBlur(7x7, sigma 2,
+// BORDER_REFLECT_101) of the ROI from the band's rows +-3 staged in LDS (reflect-101 ROI rows, whole
+// padded rows), per dword column a sliding window of 7 row sums in float pairs (columns j, j + 1:
+// the packed multiplies and adds round like the scalar ones, in the same order: row taps 0..6,
+// then the symmetric column sum), bytes outside the ROI copied — and the first / last band the
+// level's border rows (reflect-101 copies of ROI rows) of both padded pyramids.
+__global__ __launch_bounds__(256) void k_orb_roiblur(Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rtile[];  // (kRoiBand + 6) padded rows
+  const Geom& g = a.g;
+  const int s = a.smap ? a.smap[blockIdx.y] : blockIdx.y;
+  int l = 0;
+  while ((int)blockIdx.x >= g.rband[l + 1]) l++;
+  const int w = g.w[l], h = g.h[l];
+  const int r0 = ((int)blockIdx.x - g.rband[l]) * kRoiBand;
+  const int nr = min(kRoiBand, h - r0);
+  const int nd = g.stride[l] >> 2;
+  uint8_t* const lvl = a.pyr + (size_t)s * g.bytes + g.off[l];
+  stage_rows_reflect<kRoiBand + 6>(reinterpret_cast<uint32_t*>(rtile), lvl, g.stride[l], r0, 3, h, nr + 6, nd);
+  __syncthreads();
+  uint32_t* const bl = a.blur ? reinterpret_cast<uint32_t*>(a.blur + (size_t)s * g.bytes + g.off[l]) : nullptr;
+  const uint32_t* const t32 = reinterpret_cast<const uint32_t*>(rtile);
   typedef float f2 __attribute__((ext_vector_type(2)));
-  for (int dc = threadIdx.x; dc < nd; dc += blockDim.x) {
+  for (int dc = threadIdx.x; bl && dc < nd; dc += blockDim.x) {
     const bool roi_dw = 4 * dc + 3 >= kB && 4 * dc < kB + w;
     if (!roi_dw) {
-      for (int k = 0; k < nr; k++) bl[(r0 + k + kB) * nd + dc] = t32[(k + 4) * nd + dc];
+      for (int k = 0; k < nr; k++) bl[(r0 + k + kB) * nd + dc] = t32[(k + 3) * nd + dc];
       continue;
     }
     auto rowsum = [&](int t, f2* out2) {  // tile row t, padded columns 4 dc - 3 .. 4 dc + 6
@@ -695,13 +721,13 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
     };
     f2 rs[7][2];
 #pragma unroll
-    for (int k = 0; k < 6; k++) rowsum(1 + k, rs[k + 1]);
-    for (int k = 0; k < nr; k++) {
+    for (int k = 0; k < 6; k++) rowsum(k, rs[k + 1]);
+    for (int k = 0; k < nr; k++) {  // ROI row r0 + k = tile row k + 3, from tile rows k .. k + 6
 #pragma unroll
       for (int q = 0; q < 6; q++)
 #pragma unroll
         for (int jp = 0; jp < 2; jp++) rs[q][jp] = rs[q + 1][jp];
-      rowsum(k + 7, rs[6]);
+      rowsum(k + 6, rs[6]);
       float cv[4];
 #pragma unroll
       for (int jp = 0; jp < 2; jp++) {
@@ -711,7 +737,7 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
         cv[2 * jp] = v.x;
         cv[2 * jp + 1] = v.y;
       }
-      const uint32_t raw = t32[(k + 4) * nd + dc];
+      const uint32_t raw = t32[(k + 3) * nd + dc];
       uint32_t o = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -722,7 +748,7 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
       bl[(r0 + k + kB) * nd + dc] = o;
     }
   }
-  // 4. border rows (first / last band): padded row rr = ROI row reflect101(rr - kB), both copies
+  // border rows (first / last band): padded row rr = ROI row reflect101(rr - kB), both copies
   const bool top = r0 == 0, bottom = r0 + nr == h;
   if (top || bottom) {
     uint32_t* const py = reinterpret_cast<uint32_t*>(lvl);
@@ -733,7 +759,7 @@ __global__ __launch_bounds__(256) void k_orb_fastnms(Args a, int band_blur) {
         const int rr = half ? kB + h + q : q;
         const uint32_t v = py[(reflect101(rr - kB, h) + kB) * nd + dc];
         py[rr * nd + dc] = v;
-        bl[rr * nd + dc] = v;
+        if (bl) bl[rr * nd + dc] = v;
       }
     }
   }
@@ -1244,7 +1270,7 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
   const int nk = a.nkp[s];
   const uint8_t* base = a.blur + (size_t)s * g.bytes;
   const uint8_t* P = reinterpret_cast<const uint8_t*>(patch[slot]);
-  const int* pat = reinterpret_cast<const int*>(c_pattern) + byte * 8;  // x1 y1 x2 y2 of bits 0..7
+  const uint32_t* pat = reinterpret_cast<const uint32_t*>(c_pattern.v) + byte * 8;  // x1 y1 x2 y2 of bits 0..7, + 13
   for (int k0 = blockIdx.x * kDescChunk; k0 < nk; k0 += gridDim.x * kDescChunk) {
     __syncthreads();  // the previous chunk's tables are no longer read
     if (threadIdx.x < kDescChunk && k0 + (int)threadIdx.x < nk) {
@@ -1288,11 +1314,11 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
       int bits = 0;
 #pragma unroll
       for (int bit = 0; bit < 8; bit++) {
-        const int pw = pat[bit];
+        const uint32_t pw = pat[bit];
         int t[2];
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-          const float qx = (float)__builtin_amdgcn_sbfe(pw, 16 * e, 8), qy = (float)__builtin_amdgcn_sbfe(pw, 16 * e + 8, 8);
+          const float qx = (float)((pw >> (16 * e)) & 255u) - 13.f, qy = (float)((pw >> (16 * e + 8)) & 255u) - 13.f;
           const float x = qx * ca - qy * sa, y = qx * sa + qy * ca;
           t[e] = c0[(int)rintf(y) * kDescRow + (int)rintf(x)];
         }
@@ -1868,9 +1894,11 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
     return ofail(c, LISLAM_ERR_ARG, "image width %d too large for the FAST band", W);
   g.fband[0] = 0;
   g.bband[0] = 0;
+  g.rband[0] = 0;
   for (int l = 0; l < kL; l++) {
     g.fband[l + 1] = g.fband[l] + (g.h[l] + kFastBand - 1) / kFastBand;
     g.bband[l + 1] = g.bband[l] + (g.h[l] + 2 * kB + kBlurBand - 1) / kBlurBand;
+    g.rband[l + 1] = g.rband[l] + (g.h[l] + kRoiBand - 1) / kRoiBand;
   }
   g.bytes = (off + 255) & ~255;
   g.cap = g.lofs[kL];
@@ -2016,8 +2044,9 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
                      pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
   {
     TimedScope t(c, kT_orb_pyramid);
-    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB), which
-    // also writes the blurred copy; larger images run the level-by-level kernel and k_orb_blur
+    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB; the border
+    // rows and the blurred copy follow from k_orb_roiblur); larger images run the level-by-level
+    // kernel and k_orb_blur
     if (fused) {
       hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(kPyrThreads), 0, st, a);
     } else {
@@ -2029,7 +2058,11 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
   {
     TimedScope t(c, kT_orb_fast);
     const size_t lds = fast_lds_bytes(g.stride[0], g.w[0]);
-    hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a, (fused && a.blur) ? 1 : 0);
+    hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
+  }
+  if (fused) {  // the border rows of both pyramids and the blurred copy's rows
+    TimedScope t(c, kT_orb_blur);
+    hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
