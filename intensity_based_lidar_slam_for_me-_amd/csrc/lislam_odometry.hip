@@ -2811,12 +2811,12 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
 
 // The engine as two launches (k_odom_roles / k_odom_items) on streams of their own, made once per
 // batch (engine_streams); false = unavailable on this device (the caller runs the single-launch
-// engine instead).  The streams have the device's greatest priority: when a chain starts, the next
-// batch's extraction starts beside it (it was queued behind the previous chain), and the chain's
-// workgroups must be dispatched ahead of that flood, not after it drains.  LISLAM_ENGINE_STREAMS=mask
-// (developer A/B) uses CU-masked streams instead: a mask bit i selects a CU of XCD i % 8 (gfx942 /
-// gfx950, measured: scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD
-// unmasked), the roles one CU in every XCD, the items every other CU.
+// engine instead).  CU-masked streams: a mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950,
+// measured: scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD unmasked), the
+// roles one CU in every XCD, the items every other CU, so an item workgroup never takes the CU a
+// solve role needs whole (256 VGPRs x 8 waves).  LISLAM_ENGINE_STREAMS=prio (developer A/B):
+// unmasked streams of the device's greatest priority instead — measured to starve the role of a
+// whole CU under the pipelined extraction (a 2 s engine wait expired, r04i).
 bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
@@ -2824,7 +2824,7 @@ bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   const int cus = prop.multiProcessorCount, nx = 8;
   if (!multi_xcd || cus < 4 * nx || cus % nx) return false;
   const char* mode = getenv("LISLAM_ENGINE_STREAMS");
-  if (!(mode && std::strcmp(mode, "mask") == 0)) {
+  if (mode && std::strcmp(mode, "prio") == 0) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return false;
     if (hipStreamCreateWithPriority(roles, hipStreamNonBlocking, greatest) != hipSuccess) return false;
