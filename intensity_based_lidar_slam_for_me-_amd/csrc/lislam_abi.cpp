@@ -70,7 +70,7 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
     delete c;
     return LISLAM_ERR_DEVICE;
   }
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || !lislam::work_stream(device, &c->own_stream)) {
     delete c;
     return LISLAM_ERR_DEVICE;
   }
@@ -492,7 +492,7 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   const int G = std::min(2, (int)lislam_batch::kMaxGroups);
   b->odo_stream[0] = c->stream;
   for (int g = 1; g < G; g++) {
-    if (!b->odo_stream[g]) HIPCHK(c, hipStreamCreateWithFlags(&b->odo_stream[g], hipStreamNonBlocking));
+    if (!b->odo_stream[g] && !lislam::work_stream(c->device, &b->odo_stream[g])) return fail(c, LISLAM_ERR_DEVICE, "stream");
     if (!b->odo_join[g]) HIPCHK(c, hipEventCreateWithFlags(&b->odo_join[g], hipEventDisableTiming));
   }
   if (G > 1 && !b->odo_fork) HIPCHK(c, hipEventCreateWithFlags(&b->odo_fork, hipEventDisableTiming));

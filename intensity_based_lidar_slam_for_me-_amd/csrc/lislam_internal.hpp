@@ -149,6 +149,8 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t roles, hipStream_t items, hipEvent_t fork,
                                 hipEvent_t join_r, hipEvent_t join_i);
 bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items);
+// A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).
+bool work_stream(int dev, hipStream_t* s);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
 // lislam_set_odometry_schedule (LISLAM_ENGINE_*; a context starts from the environment's
 // LISLAM_ENGINE if set); AUTO = on for at most 4 chains.

@@ -51,7 +51,6 @@ constexpr double kNearby = 2.5;    // NEARBY_SCAN (:90)
 //      scratch — and the chunk / super-chunk AABBs of the permuted cloud, which are spatially
 //      compact.  The permutation only steers the search's pruning: every association result is
 //      independent of it (exact distances, ties by original index).
-constexpr int kKeysPerLane = 16;
 
 __device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
   v &= 0x3ffu;
@@ -113,19 +112,20 @@ __device__ __forceinline__ void global_bitonic(gu64* keys, int P) {
   }
 }
 
-// Workgroup bitonic sort of the first P = 1024 nw keys (nw active waves, a power of two); the
-// other waves only join the barriers.  xch: kW * 8 * 64 keys of LDS.
-template <int kW>
-__device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kKeysPerLane], int P, uint64_t* xch) {
+// Workgroup bitonic sort of the first P = 64 kK nw keys (nw active waves, a power of two; kK keys
+// per lane, a multiple of 8); the other waves only join the barriers.  xch: kW * 8 * 64 keys of LDS.
+template <int kW, int kK>
+__device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kK], int P, uint64_t* xch) {
+  constexpr int kPer = 64 * kK;  // keys per wave
   const int w = threadIdx.x >> 6, lane = lane_id();
-  const bool active = w * 1024 < P;
-  const int base = w * 1024;
+  const bool active = w * kPer < P;
+  const int base = w * kPer;
   for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j >= 1024; j >>= 1) {  // partner wave w ^ (j / 1024), same slot and lane
-      const int pw = w ^ (j >> 10);
-      const bool up = (base & k) == 0, lower = (w & (j >> 10)) == 0;
+    for (int j = k >> 1; j >= kPer; j >>= 1) {  // partner wave w ^ (j / kPer), same slot and lane
+      const int pw = w ^ (j / kPer);
+      const bool up = (base & k) == 0, lower = (w & (j / kPer)) == 0;
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
+      for (int h = 0; h < kK / 8; h++) {
         if (active)
 #pragma unroll
           for (int t = 0; t < 8; t++) xch[(w * 8 + t) * 64 + lane] = key[h * 8 + t];
@@ -139,14 +139,16 @@ __device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kKeysPerLane], int P,
         __syncthreads();
       }
     }
-    if (active) reg_bitonic_level<kKeysPerLane>(key, k, min(k >> 1, 512), base);
+    if (active) reg_bitonic_level<kK>(key, k, min(k >> 1, kPer / 2), base);
   }
 }
 
 // which: 0 less-sharp, 1 less-flat (targets), 2 sharp, 3 flat (queries: permutation only);
-// blockIdx.x -> (scan, w0 / w1 / w2 of the launch)
-template <int kW>
-__global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+// blockIdx.x -> (scan, w0 / w1 / w2 of the launch).  kW waves of kK keys per lane (64 kK kW keys in
+// registers).
+template <int kW, int kK>
+__global__ __launch_bounds__(64 * kW, 4) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+  constexpr int kKeysPerLane = kK, kPer = 64 * kK;
   __shared__ uint64_t xch[kW * 8 * 64];
   __shared__ float red[6][kW];
   const int s = blockIdx.x / per_scan, wi = blockIdx.x % per_scan;
@@ -203,12 +205,12 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
   int P = 1024;
   while (P < n) P <<= 1;
   uint64_t key[kKeysPerLane];
-  const bool in_regs = P <= 1024 * kW;
+  const bool in_regs = P <= kPer * kW;
   gu64* gkeys = (gu64*)(ix.keys + (size_t)s * 2 * ix.cap);
   if (in_regs) {
 #pragma unroll
-    for (int t = 0; t < kKeysPerLane; t++) key[t] = key_of(wave * 1024 + t * 64 + lane);
-    wg_bitonic<kW>(key, P, xch);
+    for (int t = 0; t < kKeysPerLane; t++) key[t] = key_of(wave * kPer + t * 64 + lane);
+    wg_bitonic<kW, kK>(key, P, xch);
   } else {
     for (int j = threadIdx.x; j < P; j += 64 * kW) gkeys[j] = key_of(j);
     __syncthreads();
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     if (in_regs) {
 #pragma unroll
       for (int t = 0; t < kKeysPerLane; t++) {
-        const int i = wave * 1024 + t * 64 + lane;
+        const int i = wave * kPer + t * 64 + lane;
         if (i < n) f(i, (int)(uint32_t)key[t]);
       }
     } else {
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
     chunk_boxes(sorted, n, false, ix.nn_chunk + (size_t)s * ix.nchunk * 2, ix.nn_super + (size_t)s * ix.nsuper * 2);
     return;
   }
-  // Registers: sorted position i = 1024 wave + 64 t + lane, so a chunk (16 positions) is a 16-lane
+  // Registers: sorted position i = 64 kK wave + 64 t + lane, so a chunk (16 positions) is a 16-lane
   // row of one slot and a super-chunk (256) is the four slots t = 4 v .. 4 v + 3 of one wave:
   // both boxes are reduced from the gathered points without reading the sorted copy back.
   float4* nch_out = ix.nn_chunk + (size_t)s * ix.nchunk * 2;
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
   float slo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, shi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};  // super box (row leaders)
 #pragma unroll
   for (int t = 0; t < kKeysPerLane; t++) {
-    const int i = wave * 1024 + t * 64 + lane;
+    const int i = wave * kPer + t * 64 + lane;
     float4 p = make_float4(3.4e38f, 3.4e38f, 3.4e38f, 0.f);
     float q[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
     if (i < n) {
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(64 * kW) void k_target_index(OdomArgs a, int per_sc
         v = fminf(v, __shfl_xor(v, 32));
         r[e] = v;
       }
-      const int u = (wave * 1024 + (t - 3) * 64) >> 8;
+      const int u = (wave * kPer + (t - 3) * 64) >> 8;
       if (lane == 0 && u * kSuper < n) {
         stg4(nsu_out + 2 * u, make_float4(r[0], r[1], r[2], 0.f));
         stg4(nsu_out + 2 * u + 1, make_float4(-r[3], -r[4], -r[5], 0.f));
@@ -2847,6 +2849,28 @@ bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   return true;
 }
 
+// A stream for the library's other kernels (extraction, ORB, per-round odometry): every CU but the
+// solve roles' (one per XCD, engine_streams), so a role launched beside the next batch's extraction
+// finds a whole CU free instead of waiting for the extraction's waves on it to drain — they would
+// refill each freed slot first.  Plain non-blocking stream where CU masks do not apply.
+// LISLAM_ENGINE_STREAMS=prio / =open (developer A/B) leave it unmasked.
+bool work_stream(int dev, hipStream_t* s) {
+  hipDeviceProp_t prop{};
+  const char* mode = getenv("LISLAM_ENGINE_STREAMS");
+  const bool open = mode && (std::strcmp(mode, "prio") == 0 || std::strcmp(mode, "open") == 0);
+  if (!open && hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+    const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
+    const int cus = prop.multiProcessorCount, nx = 8;
+    if (multi_xcd && cus >= 4 * nx && cus % nx == 0) {
+      const int words = (cus + 31) / 32;
+      std::vector<uint32_t> m(words, 0u);
+      for (int i = nx; i < cus; i++) m[i / 32] |= 1u << (i % 32);
+      if (hipExtStreamCreateWithCUMask(s, words, m.data()) == hipSuccess) return true;
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
+}
+
 // One engine at a time per device (contexts included): each split launch waits for the previous
 // one, so two pipelined batches' chains do not split the CUs the extraction beside them needs.
 static hipEvent_t engine_done_event(int dev) {
@@ -2911,10 +2935,11 @@ void launch_factors(const FactorArgs& a, hipStream_t st) {
 }
 
 void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st) {
-  // less-flat clouds: 16 waves (16384 keys in registers, 64 KiB LDS exchange, two workgroups per
-  // CU); less-sharp + query clouds: 8 waves (8192 keys)
-  hipLaunchKernelGGL(k_target_index<16>, dim3(n_scans), dim3(1024), 0, st, a, 1, 1, 1, 1);
-  hipLaunchKernelGGL(k_target_index<8>, dim3(3 * n_scans), dim3(512), 0, st, a, 3, 0, 2, 3);
+  // less-flat clouds: 8 waves of 32 keys per lane (16384 keys in registers); less-sharp + query
+  // clouds: 8 waves of 16 (8192 keys).  Workgroups of 512 threads at <= 128 VGPRs and 32 KiB of LDS
+  // run beside the chain engine's item workgroups (2 waves per SIMD at 128 VGPRs).
+  hipLaunchKernelGGL((k_target_index<8, 32>), dim3(n_scans), dim3(512), 0, st, a, 1, 1, 1, 1);
+  hipLaunchKernelGGL((k_target_index<8, 16>), dim3(3 * n_scans), dim3(512), 0, st, a, 3, 0, 2, 3);
 }
 
 void launch_odometry(const OdomArgs& a0, const hipStream_t* streams, int ngroups, hipEvent_t fork,

@@ -242,9 +242,9 @@ __global__ __launch_bounds__(256) void k_orb_level(Args a, int l, int mode) {
     *(__attribute__((address_space(1))) uint8_t*)dst = (uint8_t)word[0];
 }
 
-// The pyramid of a scan in one workgroup (levels 0 and 1 fit LDS together): level l-1's ROI stays
-// in LDS while level l is resized from it, ping-ponging between a level-0-sized buffer (even levels)
-// and a level-1-sized one (odd levels); each level's ROI rows go to HBM once, from LDS, with dword
+// The pyramid of a scan in one workgroup (80 KiB of LDS: level 0 in 64, then two buffers of 48 and
+// 32): level l-1's ROI stays in LDS while level l is resized from it (level 1, which overwrites
+// level 0, through its ROI rows in HBM); each level's ROI rows go to HBM from LDS with dword
 // stores (a dword never spans rows: strides are 16-byte multiples).  Same pixels as k_orb_level:
 // ROI pixels are level 0's image or the INTER_LINEAR_EXACT fixed-point resize (hval) of level l-1,
 // border columns their reflect-101 ROI pixel.  A thread owns a column of the level (its horizontal
@@ -273,7 +273,10 @@ extern "C" int lislam_debug_pyr_phases(unsigned long long* out) {
 #define PYR_PHASE(i)
 #endif
 constexpr int kPyrThreads = 1024;
-constexpr int kPyrLds = 112 * 1024;
+// LDS: level 0 in [0, 64 KiB); levels >= 1 ping-pong between [0, 48 KiB) (odd levels) and
+// [48 KiB, 80 KiB) (even levels).  <= 80 KiB per workgroup runs beside the chain engine's items.
+constexpr int kPyrLds0 = 64 * 1024, kPyrOdd = 48 * 1024, kPyrEven = 32 * 1024;
+constexpr int kPyrLds = kPyrOdd + kPyrEven;
 __host__ __device__ __forceinline__ int pyr_split(const Geom& g) { return (g.w[0] * g.h[0] + 15) & ~15; }
 __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kPyrLds];
@@ -283,22 +286,20 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
   const Geom& g = a.g;
   const int s = a.smap ? a.smap[blockIdx.x] : blockIdx.x;
   const int lane = threadIdx.x & 63;
-  uint8_t* const even = lds;
-  uint8_t* const odd = lds + pyr_split(g);
   uint8_t* const base = a.pyr + (size_t)s * g.bytes;
   {
     const uint32_t* img = reinterpret_cast<const uint32_t*>(a.img + (size_t)s * g.W * g.H);
-    uint32_t* e32 = reinterpret_cast<uint32_t*>(even);
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(lds);
     const int nd = g.W * g.H / 4;
     for (int d = threadIdx.x; d < nd; d += kPyrThreads) e32[d] = __builtin_nontemporal_load(img + d);
   }
   __syncthreads();
   PYR_PHASE(0);
   for (int l = 0; l < kL; l++) {
-    uint8_t* const cur = (l & 1) ? odd : even;
-    const uint8_t* const prev = (l & 1) ? even : odd;
     const int w = g.w[l], h = g.h[l];
+    uint8_t* const cur = (l & 1) || l == 0 ? lds : lds + kPyrOdd;
     if (l > 0) {
+      const uint8_t* const prev = l == 1 || !(l & 1) ? lds : lds + kPyrOdd;
       const int wp = g.w[l - 1], hl = g.h[l - 1] - 1;
       const int* lim = a.t.lim + l * 4;
       const int lx0 = lim[0], lx1 = lim[1], ly0 = lim[2], ly1 = lim[3];
@@ -317,6 +318,9 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
         }
       }
       const int xlast = a.t.xo[l * a.t.xs + w - 1];
+      // level 1 overwrites level 0's LDS, so it goes to its ROI rows in HBM first and comes back
+      // after the barrier; later levels are written to the other LDS buffer directly
+      uint8_t* const roi1 = base + g.off[1] + kB * g.stride[1] + kB;
       for (int x = threadIdx.x; x < w; x += kPyrThreads) {
         int o0 = 0, o1 = 0;
         uint32_t w0 = 256u, w1 = 0u;  // hval = w0 * pr[o0] + w1 * pr[o1]
@@ -341,8 +345,21 @@ __global__ __launch_bounds__(kPyrThreads) void k_orb_pyramid(Args a) {
             v[u] = min(255u, (ha * (256u - cy) + hb * cy + 32768u) >> 16);
           }
 #pragma unroll
-          for (int u = 0; u < 4; u++)
-            if (y0 + u < h) cur[(y0 + u) * w + x] = (uint8_t)v[u];
+          for (int u = 0; u < 4; u++) {
+            if (y0 + u >= h) break;
+            if (l == 1)
+              roi1[(size_t)(y0 + u) * g.stride[1] + x] = (uint8_t)v[u];
+            else
+              cur[(y0 + u) * w + x] = (uint8_t)v[u];
+          }
+        }
+      }
+      if (l == 1) {
+        __threadfence_block();
+        __syncthreads();  // level 0 is read and level 1 is in HBM: bring it into LDS
+        for (int i = threadIdx.x; i < w * h; i += kPyrThreads) {
+          const int y = i / w, x = i - y * w;
+          cur[i] = roi1[(size_t)y * g.stride[1] + x];
         }
       }
       __syncthreads();  // level l complete; the next level writes the buffer read above
@@ -1184,20 +1201,11 @@ __device__ __forceinline__ void orb_select_body(const Args& a, int gi) {
   if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
 }
 
-// kStrided: the grid's scan indices stride over the scans in use (*a.scount of them); otherwise one
-// scan per grid scan index (the loop costs the body registers, so the common launch has none)
-template <bool kStrided>
-__global__ __launch_bounds__(kSelThreads) void k_orb_select(Args a) {
+// One scan per grid scan index; with a device list (a.scount) the indices past its count exit.
+__global__ __launch_bounds__(kSelThreads, 4) void k_orb_select(Args a) {
   const int S = gridDim.x / kL;
   const int cnt = a.scount ? *a.scount : S;
-  if (!kStrided) {
-    if ((int)(blockIdx.x % S) < cnt) orb_select_body(a, blockIdx.x % S);
-    return;
-  }
-  for (int gi = blockIdx.x % S; gi < cnt; gi += S) {
-    orb_select_body(a, gi);
-    __syncthreads();
-  }
+  if ((int)(blockIdx.x % S) < cnt) orb_select_body(a, blockIdx.x % S);
 }
 
 // levels in order, level-0 coordinates, cloud-track lookup and zero filter (a9)
@@ -1567,7 +1575,7 @@ __device__ __forceinline__ void orb_match_body(const PairArgs& p, int pi) {
 }
 
 // the grid's pair indices stride over the pairs in use (*p.pcount of them when given)
-__global__ __launch_bounds__(kPairThreads) void k_orb_match(PairArgs p) {
+__global__ __launch_bounds__(kPairThreads, 8) void k_orb_match(PairArgs p) {
   const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
   for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
     orb_match_body(p, pi);
@@ -2040,13 +2048,13 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     a.smap = e->smap;
   }
   const Geom& g = e->g;
-  const bool fused = g.W % 4 == 0 && g.h[1] <= 64 && g.stride[0] / 4 <= kPyrThreads &&
-                     pyr_split(g) + g.w[1] * g.h[1] <= kPyrLds;
+  const bool fused = g.W % 4 == 0 && g.h[1] <= 64 && g.stride[0] / 4 <= kPyrThreads && pyr_split(g) <= kPyrLds0 &&
+                     g.w[1] * g.h[1] <= kPyrOdd && g.w[2] * g.h[2] <= kPyrEven;
   {
     TimedScope t(c, kT_orb_pyramid);
-    // one workgroup per scan when levels 0 and 1 fit LDS together (64 x 1024: 108 KiB; the border
-    // rows and the blurred copy follow from k_orb_roiblur); larger images run the level-by-level
-    // kernel and k_orb_blur
+    // one workgroup per scan when level 0 fits 64 KiB of LDS (64 x 1024; the border rows and the
+    // blurred copy follow from k_orb_roiblur); larger images run the level-by-level kernel and
+    // k_orb_blur
     if (fused) {
       hipLaunchKernelGGL(k_orb_pyramid, dim3(n), dim3(kPyrThreads), 0, st, a);
     } else {
@@ -2064,7 +2072,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     TimedScope t(c, kT_orb_blur);
     hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<false>, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
   if (!fused) {
     TimedScope t(c, kT_orb_blur);
@@ -2097,7 +2105,9 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const Geom& g = e->g;
   // kListSlots grid scan indices stride over the list: the count is only known on the device
   const int ns = std::min(nmax, kListSlots);
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select<true>, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
+  // select: one grid slot per possible list entry (the strided body needed 180 VGPRs, more than a
+  // workgroup beside the chain engine's items may hold); the slots past the count exit at once
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(nmax * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
   { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
@@ -2247,7 +2257,7 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     ob->has_mask = mask != nullptr;
     ob->e1 = new OrbEngine();
     ob->e2 = new OrbEngine();
-    OCHK(c, hipStreamCreateWithFlags(&ob->side, hipStreamNonBlocking));
+    if (!work_stream(c->device, &ob->side)) return ofail(c, LISLAM_ERR_DEVICE, "ORB stream");
     OCHK(c, hipEventCreateWithFlags(&ob->done, hipEventDisableTiming));
     // the engines' tables and mask pyramids are uploaded / built on the side stream, where the
     // front end that reads them runs
