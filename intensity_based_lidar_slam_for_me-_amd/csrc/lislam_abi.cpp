@@ -107,6 +107,12 @@ const char* lislam_last_error(const lislam_ctx* c) { return c ? c->err.c_str() :
 int lislam_synchronize(lislam_ctx* c) {
   if (!c) return LISLAM_ERR_ARG;
   hipSetDevice(c->device);
+  for (lislam_batch* b : c->batches)
+    if (b->eng_pending) {
+      HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
+      b->eng_pending = false;
+    }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return LISLAM_OK;
 }
@@ -124,12 +130,30 @@ int lislam_get_stream(lislam_ctx* c, void** s) {
 }
 
 // ------------------------------------------------------------------------------ batch
+// The context stream waits for the batch's split engine launch, if one is pending (lislam_batch.hpp).
+static int engine_settle(lislam_batch* b) {
+  if (!b->eng_pending) return LISLAM_OK;
+  lislam_ctx* c = b->ctx;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
+  b->eng_pending = false;
+  return LISLAM_OK;
+}
+#define SETTLE(b)                           \
+  do {                                      \
+    const int rc_ = engine_settle(b);       \
+    if (rc_ != LISLAM_OK) return rc_;       \
+  } while (0)
+
 int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   if (!c || !out || max_scans < 1) return LISLAM_ERR_ARG;
   hipSetDevice(c->device);
   lislam_batch* b = new lislam_batch();
   b->ctx = c;
   hipEventCreateWithFlags(&b->ev_images, hipEventDisableTiming);
+  hipEventCreateWithFlags(&b->eng_ready, hipEventDisableTiming);
+  c->batches.push_back(b);
   const int S = max_scans, H = c->cfg.n_scans, W = c->cfg.width, N = H * W;
   b->max_scans = S; b->H = H; b->W = W; b->N = N;
   b->cap_sharp = kCapSharpPerLine * H;
@@ -222,7 +246,14 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
 int lislam_batch_destroy(lislam_batch* b) {
   if (!b) return LISLAM_OK;
   hipSetDevice(b->ctx->device);
+  if (b->eng_roles) hipStreamSynchronize(b->eng_roles);
+  if (b->eng_items) hipStreamSynchronize(b->eng_items);
   hipStreamSynchronize(b->ctx->stream);
+  {
+    auto& v = b->ctx->batches;
+    for (size_t i = 0; i < v.size(); i++)
+      if (v[i] == b) { v.erase(v.begin() + i); break; }
+  }
   for (void* p : b->allocs) hipFree(p);
   for (auto& v : b->ext_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (auto& v : b->odo_ev) for (auto& t : v) { hipEventDestroy(t.b); hipEventDestroy(t.e); }
@@ -239,6 +270,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (b->ground) lislam_free_ground(b->ground);
   if (b->wire) hipFree(b->wire);
   if (b->ev_images) hipEventDestroy(b->ev_images);
+  if (b->eng_ready) hipEventDestroy(b->eng_ready);
   if (b->stage_ev) hipEventDestroy(b->stage_ev);
   if (b->copy_stream) {
     hipStreamSynchronize(b->copy_stream);
@@ -268,6 +300,7 @@ static int output_source(lislam_batch* b, int what, int scan, const void** src_o
 
 int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   const size_t n = (size_t)n_scans * b->N;
@@ -294,6 +327,7 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
 
 int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   static const lislam_point_layout kPacked{16, 0, 4, 8, 12};
@@ -348,6 +382,7 @@ int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_sca
 int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
                         double* out_pose, int32_t* summary) {
   return lislam_batch_mapopt_corner(b, m, nullptr, scan, odom, state, out_pose, summary);
+  SETTLE(b);
 }
 
 // With the corner ikd-Tree: pc_corner is the scan's less-sharp cloud (/laser_cloud_less_sharp,
@@ -355,6 +390,7 @@ int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const doub
 int lislam_batch_mapopt_corner(lislam_batch* b, lislam_map* m, lislam_map* cm, int32_t scan, const double* odom,
                                double* state, double* out_pose, int32_t* summary) {
   if (!b || !m || !odom || !state || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   const void *g = nullptr, *lf = nullptr;
@@ -383,6 +419,7 @@ int lislam_batch_mapopt_corner(lislam_batch* b, lislam_map* m, lislam_map* cm, i
 int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, void* dst, const lislam_point_layout* layout,
                                 int32_t cap, int32_t* n) {
   if (!b || !dst || !layout || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   if (layout->point_step < 4 || std::max({layout->off_x, layout->off_y, layout->off_z, layout->off_intensity}) + 4 > layout->point_step)
     return fail(c, LISLAM_ERR_ARG, "bad point layout");
@@ -411,6 +448,7 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
 
 int lislam_batch_input_device_ptr(lislam_batch* b, void** dptr) {
   if (!b || !dptr) return LISLAM_ERR_ARG;
+  SETTLE(b);
   *dptr = (void*)b->fa.pts;
   return LISLAM_OK;
 }
@@ -423,6 +461,7 @@ int lislam_batch_set_timing(lislam_batch* b, int32_t enable) {
 
 int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   if (!b || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   // a pending ORB cascade may still need the current images (its host-round redo): settle it
@@ -443,6 +482,7 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
   launch_features(f, c->stream, ev, b->ev_images);
   launch_target_index(b->oa, n_scans, c->stream);  // spatial index of the clouds odometry searches
   if (ev) HIPCHK(c, hipEventRecord(ev[4], c->stream));
+  HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));  // the chain engine's inputs
   HIPCHK(c, hipGetLastError());
   b->extracted = n_scans;
   return LISLAM_OK;
@@ -450,6 +490,7 @@ int lislam_batch_extract(lislam_batch* b, int32_t n_scans) {
 
 static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const double* init_host,
                         const int32_t* use_aloam = nullptr) {
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   OdomArgs o = b->oa;
   o.gate = nullptr;
@@ -515,13 +556,20 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_i, hipEventDisableTiming));
       }
     }
-    if (ev) { e0 = b->get_event(); HIPCHK(c, hipEventRecord(e0, c->stream)); }
-    if (b->eng_split)
-      lislam::launch_odometry_chain_split(o, c->stream, b->eng_roles, b->eng_items, b->eng_fork, b->eng_join_r, b->eng_join_i);
-    else
+    if (ev) { e0 = b->get_event(); e1 = b->get_event(); }
+    if (b->eng_split) {
+      // the inputs: the last extract (its eng_ready), or the staging copies just queued
+      if (use_aloam || init_host) HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
+      lislam::launch_odometry_chain_split(o, b->eng_roles, b->eng_items, b->eng_ready, b->eng_fork, b->eng_join_r,
+                                          b->eng_join_i, e0, e1);
+      b->eng_pending = true;
+    } else {
+      if (ev) HIPCHK(c, hipEventRecord(e0, c->stream));
       lislam::launch_odometry_chain(o, c->stream);
+      if (ev) HIPCHK(c, hipEventRecord(e1, c->stream));
+    }
     b->engine_ran = true;
-    if (ev) { e1 = b->get_event(); HIPCHK(c, hipEventRecord(e1, c->stream)); ev->push_back({6, e0, e1}); }
+    if (ev) ev->push_back({6, e0, e1});
     HIPCHK(c, hipGetLastError());
     return LISLAM_OK;
   }
@@ -547,6 +595,7 @@ int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_
 
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
   if (!b || !status) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -564,6 +613,7 @@ int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
 
 int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls) {
   if (!b || !ms_per_call) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -690,6 +740,7 @@ extern "C" {
 
 int lislam_batch_download(lislam_batch* b, int32_t what, int32_t scan, void* dst, int32_t cap, int32_t* n) {
   if (!b || (!dst && !n) || scan < 0 || scan >= b->max_scans) return LISLAM_ERR_ARG;
+  SETTLE(b);
   lislam_ctx* c = b->ctx;
   int cnt = 0;
   const void* src = nullptr;

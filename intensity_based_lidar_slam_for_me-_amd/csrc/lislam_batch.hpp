@@ -44,6 +44,13 @@ struct lislam_batch {
   int eng_split = -1;
   hipStream_t eng_roles = nullptr, eng_items = nullptr;
   hipEvent_t eng_fork = nullptr, eng_join_r = nullptr, eng_join_i = nullptr;
+  // the split engine is not joined back into the context stream at launch (a join there would also
+  // hold back whatever another context queued behind it on a shared hardware queue): eng_pending
+  // until the next batch call that touches the batch's buffers, or lislam_synchronize, makes the
+  // context stream wait for it.  eng_ready: recorded on the context stream at the end of every
+  // lislam_batch_extract (and after odometry's staging copies); the engine starts from it.
+  bool eng_pending = false;
+  hipEvent_t eng_ready = nullptr;
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
   // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
   // queued on the context stream after it.

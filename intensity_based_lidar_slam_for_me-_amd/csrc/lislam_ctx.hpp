@@ -35,6 +35,7 @@ struct lislam_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   lislam_batch* single = nullptr;  // 2-scan batch behind lislam_scan_registration / odom_step
+  std::vector<lislam_batch*> batches;  // live batches (lislam_synchronize settles their engines)
   void* map_scratch = nullptr;     // device scratch of the stateless mapping entry points
   lislam_ktimer mtimer;            // mapping-kernel timing
   int ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order

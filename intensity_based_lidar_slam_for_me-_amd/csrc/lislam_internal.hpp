@@ -146,8 +146,11 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 // The same engine as two launches (k_odom_roles on `roles`, k_odom_items on `items`, CU-masked
 // streams from engine_streams), forked from and joined back into st by the three events.
-int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t roles, hipStream_t items, hipEvent_t fork,
-                                hipEvent_t join_r, hipEvent_t join_i);
+// Nothing is queued on the context stream: the roles stream waits for `ready` (the inputs) and for
+// the previous engine of the device, the items stream forks from it; join_r / join_i mark the end
+// (the caller makes its stream wait for them later); t0 / t1 (nullable): timing events.
+int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_t items, hipEvent_t ready, hipEvent_t fork,
+                                hipEvent_t join_r, hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1);
 bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items);
 // A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).
 bool work_stream(int dev, hipStream_t* s);

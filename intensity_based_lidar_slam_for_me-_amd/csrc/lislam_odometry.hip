@@ -2882,8 +2882,8 @@ static hipEvent_t engine_done_event(int dev) {
   return ev[dev];
 }
 
-int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t roles, hipStream_t items, hipEvent_t fork,
-                                hipEvent_t join_r, hipEvent_t join_i) {
+int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_t items, hipEvent_t ready, hipEvent_t fork,
+                                hipEvent_t join_r, hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1) {
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
   ctl.w = a.eng_ctl;
@@ -2909,20 +2909,22 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t st, hipStream_t r
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = bud ? max(1, atoi(bud)) : max(1, grid / ctl.C);
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
-  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
-  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
   const hipEvent_t prev = engine_done_event(dev);
-  if (prev) (void)hipStreamWaitEvent(st, prev, 0);
-  (void)hipEventRecord(fork, st);
-  (void)hipStreamWaitEvent(roles, fork, 0);
+  (void)hipStreamWaitEvent(roles, ready, 0);
+  if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
+  if (t0) (void)hipEventRecord(t0, roles);
+  // zero the control words of this launch, all but word 3 (the sticky abort)
+  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);
+  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), roles);
+  (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(ctl.C), dim3(kEngThreads), 0, roles, a, ctl);
   hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(kEngThreads), 0, items, a, ctl);
   (void)hipEventRecord(join_r, roles);
   (void)hipEventRecord(join_i, items);
-  (void)hipStreamWaitEvent(st, join_r, 0);
-  (void)hipStreamWaitEvent(st, join_i, 0);
-  if (prev) (void)hipEventRecord(prev, st);
+  (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do
+  if (t1) (void)hipEventRecord(t1, items);
+  if (prev) (void)hipEventRecord(prev, items);
   return grid;
 }
 
