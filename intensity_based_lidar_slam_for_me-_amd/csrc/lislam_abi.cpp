@@ -56,6 +56,24 @@ bool is_packed(const lislam_point_layout* L) {
 
 }  // namespace
 
+namespace lislam {
+
+static hipEvent_t g_epoch[64] = {};
+
+void timeline_epoch(int dev, hipStream_t s) {
+  if (!getenv("LISLAM_TIMELINE") || dev < 0 || dev >= 64 || g_epoch[dev]) return;
+  if (hipEventCreate(&g_epoch[dev]) == hipSuccess) (void)hipEventRecord(g_epoch[dev], s);
+}
+
+void timeline_print(int dev, const char* who, const void* obj, int kernel, hipEvent_t b, hipEvent_t e) {
+  if (dev < 0 || dev >= 64 || !g_epoch[dev]) return;
+  float t0 = 0, t1 = 0;
+  if (hipEventElapsedTime(&t0, g_epoch[dev], b) != hipSuccess || hipEventElapsedTime(&t1, g_epoch[dev], e) != hipSuccess) return;
+  fprintf(stderr, "timeline %s %p %d %.3f %.3f\n", who, obj, kernel, t0, t1);
+}
+
+}  // namespace lislam
+
 extern "C" {
 
 int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out) {
@@ -75,6 +93,7 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
     return LISLAM_ERR_DEVICE;
   }
   c->stream = c->own_stream;
+  timeline_epoch(device, c->stream);
   // LISLAM_ENGINE (0 off, 1 auto, 2 on) seeds the odometry schedule; lislam_set_odometry_schedule
   // changes it per context
   if (const char* e = getenv("LISLAM_ENGINE")) {
@@ -625,11 +644,13 @@ int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* laun
     return ms;
   };
   for (auto& v : b->ext_ev) {
+    timeline_print(c->device, "extract", b, 0, v[0], v[4]);
     for (int i = 0; i < 4; i++) { acc[i] += el(v[i], v[i + 1]); launches[i] += i == 3 ? 2 : i == 0 ? 3 : 1; }  // front: 3 launches, k_target_index: 2
     for (hipEvent_t e : v) b->pool.push_back(e);
   }
   for (auto& v : b->odo_ev) {
     for (auto& t : v) {  // every launch bracketed on its own stream
+      timeline_print(c->device, "odometry", b, t.kernel, t.b, t.e);
       acc[t.kernel] += el(t.b, t.e);
       launches[t.kernel] += 1;
       b->pool.push_back(t.b);

@@ -72,5 +72,13 @@ struct TimedScope {
   }
 };
 
+namespace lislam {
+// Developer timeline (LISLAM_TIMELINE=1): timeline_epoch records a per-device epoch event on s
+// once (at the first context's creation); timeline_print writes a timed launch's start / end in ms
+// from that epoch to stderr, so the streams of pipelined contexts line up on one clock.
+void timeline_epoch(int dev, hipStream_t s);
+void timeline_print(int dev, const char* who, const void* obj, int kernel, hipEvent_t b, hipEvent_t e);
+}  // namespace lislam
+
 // Frees lislam_ctx::map_scratch (lislam_map.hip).
 void lislam_free_map_scratch(void* p);

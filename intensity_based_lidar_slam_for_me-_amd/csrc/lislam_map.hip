@@ -1311,6 +1311,7 @@ int lislam_map_kernel_times(lislam_ctx* c, float* ms, int32_t* launches) {
   for (auto& r : c->mtimer.rec) {
     float t = 0;
     MCHK(c, hipEventElapsedTime(&t, r.second.first, r.second.second));
+    lislam::timeline_print(c->device, "ctx", c, r.first, r.second.first, r.second.second);
     ms[r.first] += t;
     if (launches) launches[r.first]++;
     c->mtimer.pool.push_back(r.second.first);

@@ -1,7 +1,7 @@
 # kernel trace of the pipelined bench (timeline of chains vs extraction / ORB); a heartbeat file
 # shows progress while the profiled bench runs
 cd $GRAFT_REPO_ROOT
-D=$GRAFT_REPO_ROOT/gpurun_out/r04o
+D=$GRAFT_REPO_ROOT/gpurun_out/r04v
 mkdir -p $D
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 ( while sleep 20; do date >> $D/heartbeat; done ) &
