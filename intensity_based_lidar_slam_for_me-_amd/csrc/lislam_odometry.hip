@@ -23,6 +23,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -1452,18 +1453,25 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // control words: [0] ticket, [1] abort (this launch), [2] error, [3] sticky abort (set with [1], never
 // cleared by a launch: lislam_batch_odometry_status reads and clears it), [4, 4 + C) lm_gen, then
 // assoc_done[C][2 R]
+constexpr int kMaxShareItems = 256;  // 16 threads x 8 loads per item row: 32 rows per round x 8
 struct EngCtl {
   unsigned* w;
   int C, R, I;
   unsigned long long wait_ticks;  // bound of every device wait (s_memrealtime ticks, 100 MHz)
   int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
   int roles;     // solve-role tickets ahead of the items in this launch's queue (C, or 0: roles in their own launch)
-  int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at once
+  int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at
+                 // once, and at most kMaxShareItems (the solve sums the shares in one round of loads)
+  unsigned gen;  // this launch's number: with the pass, the tag of a complete item row (eng_tag)
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
   __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
 };
+// Word 31 of an item's eng_part row once its records and share of pass ro are written.
+__device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
+  return ((uint64_t)ctl.gen << 32) | (uint64_t)(unsigned)(ro + 1);
+}
 
 // Developer trace of the engine (null in production): per workgroup {ticket, stage, LM passes,
 // time}, stored system-scope into host-pinned memory so the host can read it while the kernel runs.
@@ -2358,43 +2366,191 @@ __device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& c
 }
 
 // ---- the solve role: one workgroup per chain, for the whole chain
-// Pass ro = 2 r + o of chain c (pair k): wait for its association items, sum their shares of the
-// first evaluation (16-B loads) while the evaluating waves load the records into their slots, then
-// the LM loop (wave 0 steps, waves 1.. evaluate; 1 + 2 barriers per iteration), then publish x
-// (para_q / para_t, write-through) and lm_gen[c] = ro + 1.  The chain's x and pose stay in LDS.
-__device__ __forceinline__ void eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c, int k,
-                                               int ieff, Rsrc rec, bool wave0, unsigned tk) {
+// Pass ro = 2 r + o of chain c (pair k): gather its association items' records and shares of the
+// first evaluation, then the LM loop (wave 0 steps, waves 1.. evaluate; 1 + 2 barriers per
+// iteration), then publish x (para_q / para_t, write-through) and lm_gen[c] = ro + 1.  The chain's
+// x and pose stay in LDS.
+//
+// Gather, progressive (k_odom_roles, kProg): every item tags its eng_part row (eng_tag) once its
+// records and share are written; wave 0 polls the tags and marks each complete item in LDS, and
+// waves 1.. load that item's records into their slots and its share quads straight into LDS
+// (buffer_load ... lds) as it lands — so when the last item finishes only its own loads remain.
+// Bulk (k_odom_chain): wait for every item (the assoc_done count), then load everything.
+// Both sum the shares in the same fixed tree: the results are identical.
+constexpr int kShareQuads = 15;  // doubles 0..29 of an item's row: 28 sums + 2 counts
+struct EngGather {
+  v4u shr[kMaxShareItems * kShareQuads];  // the items' rows, packed: quad q of item i at i * 15 + q
+  unsigned ready[kMaxShareItems];         // ro + 1 once item i's row of pass ro is complete
+  int abort;
+};
+
+// Wave 0: poll the tags of the pass's ieff items (lane l: items l, l + 64, ...) and publish each
+// complete one in gt.ready.  false = aborted (the bound expired here, or another workgroup's abort).
+__device__ __forceinline__ bool gather_poll(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro, int ieff) {
+  const int lane = lane_id();
+  const uint64_t want = eng_tag(ctl, ro);
+  const uint64_t* tags = reinterpret_cast<const uint64_t*>(a.eng_part + (size_t)c * ctl.I * 32) + 31;
+  unsigned pend = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (lane + 64 * j < ieff) pend |= 1u << j;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    uint64_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = ((pend >> j) & 1u) ? ld_sc1(tags + (size_t)(lane + 64 * j) * 32) : 0ull;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (((pend >> j) & 1u) && v[j] == want) {
+        __hip_atomic_store(&gt.ready[lane + 64 * j], (unsigned)(ro + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pend &= ~(1u << j);
+      }
+    if (__ballot(pend != 0u) == 0ull) return true;
+    bool stop = ld_rlx(ctl.abort_w()) != 0u;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ctl.wait_ticks) {
+      if (lane == 0) {
+        st_rlx(ctl.abort_w(), 1u);
+        st_rlx(ctl.abort_w() + 2, 1u);  // sticky (EngCtl word 3)
+      }
+      stop = true;
+    }
+    if (__builtin_amdgcn_readfirstlane((int)stop)) {
+      if (lane == 0) __hip_atomic_store(&gt.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void blk_absent(BlkReg& b) {
+  b.c[0] = b.c[1] = b.c[2] = 0.f;
+  b.a[0] = b.a[1] = b.a[2] = 0.f;
+  b.u[0] = b.u[1] = b.u[2] = 0.0;
+  b.kd = -1;
+}
+
+// Waves 1..: as gather_poll marks items complete, load their records into this thread's slots and
+// their share quads (quad Q = tp + 448 i of the packed rows) into gt.shr; returns once every load
+// is issued and landed (or on abort).
+__device__ __forceinline__ void gather_fill(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro, int ieff,
+                                            Rsrc rec, int ns, int nf, int tp, EvalSlots& S) {
+  const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
+  const unsigned pass = (unsigned)(ro + 1);
+  const int nquad = ieff * kShareQuads;
+  const int wbase = uni(tp & ~63);  // this wave's first tp
+  unsigned pend = 0u;  // bits 0..1 edge slots, 2..5 plane slots, 6..14 share quads
+#pragma unroll
+  for (int k = 0; k < kEdgeSlots; k++) {
+    blk_absent(S.e[k]);
+    if (tp + k * kEvalThreads < ns) pend |= 1u << k;
+  }
+#pragma unroll
+  for (int k = 0; k < kPlaneSlots; k++) {
+    blk_absent(S.p[k]);
+    if (tp + k * kEvalThreads < nf) pend |= 1u << (kEdgeSlots + k);
+  }
+  constexpr int kQ0 = kEdgeSlots + kPlaneSlots, kQuadRounds = (kMaxShareItems * kShareQuads + kEvalThreads - 1) / kEvalThreads;
+#pragma unroll
+  for (int i = 0; i < kQuadRounds; i++)
+    if (tp + i * kEvalThreads < nquad) pend |= 1u << (kQ0 + i);
+  auto ready = [&](int item) {
+    return __hip_atomic_load(&gt.ready[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == pass;
+  };
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__ballot(pend != 0u) != 0ull) {
+#pragma unroll
+    for (int k = 0; k < kEdgeSlots; k++) {
+      const int w = tp + k * kEvalThreads;
+      if (((pend >> k) & 1u) && ready((w / kEngQ) % ieff)) {
+        rec_load(rec, w, true, S.e[k]);
+        pend &= ~(1u << k);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kPlaneSlots; k++) {
+      const int w = ns + tp + k * kEvalThreads;
+      if (((pend >> (kEdgeSlots + k)) & 1u) && ready((w / kEngQ) % ieff)) {
+        rec_load(rec, w, true, S.p[k]);
+        pend &= ~(1u << (kEdgeSlots + k));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kQuadRounds; i++) {
+      const int Q = tp + i * kEvalThreads, item = Q / kShareQuads;
+      if (((pend >> (kQ0 + i)) & 1u) && ready(item)) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(parts, (__attribute__((address_space(3))) void*)&gt.shr[wbase + i * kEvalThreads], 16,
+                                                 item * 256 + (Q - item * kShareQuads) * 16, 0, 0, kAuxSc1);
+        pend &= ~(1u << (kQ0 + i));
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&gt.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * ctl.wait_ticks) {  // never expected: wave 0's bound is half
+      if (lane_id() == 0) {
+        st_rlx(ctl.abort_w(), 1u);
+        st_rlx(ctl.abort_w() + 2, 1u);
+      }
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  S.tail = __ballot(tp + kEvalThreads < ns || tp + 3 * kEvalThreads < nf) != 0ull;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS writes have landed (and the records)
+}
+
+template <bool kProg>
+__device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, EngGather* gt,
+                                               int c, int k, int ro, int ieff, Rsrc rec, bool wave0, unsigned tk) {
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const int lane = lane_id();
   const int tp = (int)threadIdx.x - 64;
   EvalSlots S;
-  if (!wave0 && ieff > 0) eval_slots_load(rec, ns, nf, tp, S);  // in flight with the shares
-  {  // the items' shares: quad q = tid % 16 (doubles 2q, 2q + 1) of items tid / 16, + 32, + 64, ...
-    const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
-    const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
-    double t0 = 0.0, t1 = 0.0;
-    for (int it0 = g; it0 < ieff; it0 += 32 * 8) {
-      v4u v[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int it = it0 + 32 * j;
-        v[j] = __builtin_amdgcn_raw_buffer_load_b128(parts, (it < ieff ? it : 0) * 256 + q * 16, 0, kAuxSc1);
-        if (!(it < ieff && q < 15)) v[j] = v4u{0u, 0u, 0u, 0u};
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;  // share quad q of items g, g + 32, ..., g + 224
+  double d0[8], d1[8];
+  if constexpr (kProg) {
+    if (ieff > 0) {
+      if (wave0) {
+        eng_prof(tk, 1, rt_now());
+        const bool ok = gather_poll(a, ctl, *gt, c, ro, ieff);
+        if (lane == 0) sh.flag0 = ok;
+        eng_prof(tk, 1, rt_now());
+      } else {
+        gather_fill(a, ctl, *gt, c, ro, ieff, rec, ns, nf, tp, S);
       }
-      double d0[8], d1[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        d0[j] = __longlong_as_double((long long)(((uint64_t)v[j].y << 32) | v[j].x));
-        d1[j] = __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z));
-      }
-#pragma unroll
-      for (int h = 1; h < 8; h <<= 1)
-#pragma unroll
-        for (int j = 0; j + h < 8; j += 2 * h) { d0[j] += d0[j + h]; d1[j] += d1[j + h]; }
-      t0 += d0[0];
-      t1 += d1[0];
+    } else if (wave0 && lane == 0) {
+      sh.flag0 = 1;
     }
-    if (q < 15) { sh.red[g][2 * q] = t0; sh.red[g][2 * q + 1] = t1; }
+    __syncthreads();
+    if (!uni(sh.flag0)) return false;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int it = g + 32 * j;
+      const bool ok = it < ieff && q < kShareQuads;
+      const v4u v = gt->shr[ok ? it * kShareQuads + q : 0];
+      d0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x)) : 0.0;
+      d1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z)) : 0.0;
+    }
+  } else {
+    if (!wave0 && ieff > 0) eval_slots_load(rec, ns, nf, tp, S);  // in flight with the shares
+    const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
+    v4u v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int it = g + 32 * j;
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(parts, (it < ieff ? it : 0) * 256 + q * 16, 0, kAuxSc1);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const bool ok = g + 32 * j < ieff && q < kShareQuads;
+      d0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].y << 32) | v[j].x)) : 0.0;
+      d1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z)) : 0.0;
+    }
+  }
+  {  // the items' shares: pairwise tree over items g + 32 j, then (wave 0) over the 32 rows
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+      for (int j = 0; j + h < 8; j += 2 * h) { d0[j] += d0[j + h]; d1[j] += d1[j + h]; }
+    if (q < kShareQuads) { sh.red[g][2 * q] = d0[0]; sh.red[g][2 * q + 1] = d1[0]; }
   }
   __syncthreads();
   LdsLM& s = *(LdsLM*)&lm;
@@ -2473,12 +2629,20 @@ __device__ __forceinline__ void eng_solve_pass(const OdomArgs& a, const EngCtl& 
       more = uni(sh.flag) != 0;
     }
   }
+  return true;
 }
 
 // The solve role of chain c (ticket c): every pass of the chain, in order.  false = aborted.
-__device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c,
-                                               bool wave0, unsigned tk) {
+// gt: the progressive gather's LDS (kProg), else null.
+template <bool kProg>
+__device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, EngGather* gt,
+                                               int c, bool wave0, unsigned tk) {
   const int lane = lane_id();
+  if constexpr (kProg) {
+    for (int i = threadIdx.x; i < kMaxShareItems; i += kEngThreads) gt->ready[i] = 0u;
+    if (threadIdx.x == 0) gt->abort = 0;
+    __syncthreads();
+  }
   const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
   const Rsrc rec = make_rsrc(a.blk + (size_t)c * rec_stride, (unsigned)((a.cap_sharp + a.cap_flat) * kRecBytes));
   double* st = a.state + (size_t)c * 16;
@@ -2496,14 +2660,16 @@ __device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& 
     if (!pair_of(a, c, r, &k)) break;  // uniform: this chain is shorter
     const int ieff = eng_live_items(a, ctl, k);
     const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1)) + tk;  // profile slot of the pass (developer builds)
-    if (wave0 && lane == 0) {
-      eng_prof(ptk, 1, rt_now());
-      sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : 1;
-      eng_prof(ptk, 1, rt_now());
+    if constexpr (!kProg) {
+      if (wave0 && lane == 0) {
+        eng_prof(ptk, 1, rt_now());
+        sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : 1;
+        eng_prof(ptk, 1, rt_now());
+      }
+      __syncthreads();
+      if (!uni(sh.flag0)) return false;
     }
-    __syncthreads();
-    if (!uni(sh.flag0)) return false;
-    eng_solve_pass(a, ctl, sh, lm, c, k, ieff, rec, wave0, ptk);
+    if (!eng_solve_pass<kProg>(a, ctl, sh, lm, gt, c, k, ro, ieff, rec, wave0, ptk)) return false;
     if (wave0 && lane == 0) {
       const int nc = sh.nc, np = sh.np;
       int* so = a.stats + (size_t)k * 8;
@@ -2658,6 +2824,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
       drain_stores();
       if (lead) {
         eng_prof(ptk, 7, rt_now() - tp0);
+        st_sc1(reinterpret_cast<uint64_t*>(a.eng_part + ((size_t)c * ctl.I + item) * 32) + 31, eng_tag(ctl, ro));  // row complete
         add_rlx(ctl.assoc_done(c, ro), 1u);
         eng_trace(1, 4u);
         eng_prof(ptk, 3, rt_now());
@@ -2697,7 +2864,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     bool ok = true;
     if (tk < (unsigned)ctl.roles) {
       const int c = uni((int)tk);
-      ok = eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+      ok = eng_solve_role<false>(a, ctl, sh, lm, nullptr, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
     } else {
       ok = eng_item_ticket(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
     }
@@ -2723,9 +2890,10 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
 __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   __shared__ EngLM lm;
+  __shared__ EngGather gt;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
   const int c = (int)blockIdx.x;
-  (void)eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+  (void)eng_solve_role<true>(a, ctl, sh, lm, &gt, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
 }
 
 __global__ __launch_bounds__(kEngThreads, 4) void k_odom_items(OdomArgs a, EngCtl ctl) {
@@ -2757,6 +2925,12 @@ __global__ __launch_bounds__(kEngThreads, 4) void k_odom_items(OdomArgs a, EngCt
 }
 
 extern "C" int lislam_debug_engine_items(int cap_queries) { return engine_items(cap_queries); }
+// A number per engine launch (the item rows' tags tell this launch's passes from an earlier one's).
+static unsigned next_engine_gen() {
+  static std::atomic<unsigned> gen{0};
+  return ++gen;
+}
+
 int engine_items(int cap_queries) { return (cap_queries + kEngQ - 1) / kEngQ; }
 
 bool use_chain_engine(const OdomArgs& a, int mode) {
@@ -2780,6 +2954,7 @@ static int engine_resident(int dev) {
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
+  ctl.gen = next_engine_gen();
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
@@ -2797,7 +2972,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   (void)hipGetDevice(&dev);
   const int resident = engine_resident(dev);
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
-  ctl.budget = bud ? max(1, atoi(bud)) : max(1, (resident - ctl.C - 1) / ctl.C);
+  ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, (resident - ctl.C - 1) / ctl.C));
   // zero the control words of this launch, all but word 3 (the sticky abort)
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
@@ -2886,6 +3061,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
                                 hipEvent_t join_r, hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1) {
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
+  ctl.gen = next_engine_gen();
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
@@ -2907,7 +3083,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   int grid = ctl.C * ctl.I;
   if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
-  ctl.budget = bud ? max(1, atoi(bud)) : max(1, grid / ctl.C);
+  ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
   const hipEvent_t prev = engine_done_event(dev);
   (void)hipStreamWaitEvent(roles, ready, 0);
