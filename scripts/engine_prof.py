@@ -43,6 +43,7 @@ with pkg.Context() as ctx:
     assert lib.lislam_debug_engine_prof(T) == 0
     b.odometry(S, S - 1)
     ctx.synchronize()
+    nq = np.array([b.count(pkg.native.OUT_SHARP, k) + b.count(pkg.native.OUT_FLAT, k) for k in range(1, S)])
     sp = np.zeros(4, np.uint64)
     buf = np.zeros((T, 8), np.uint64)
     assert lib.lislam_debug_engine_prof_read(buf.ctypes.data, T) == 0
@@ -109,5 +110,8 @@ with pkg.Context() as ctx:
     for k, v in rows.items():
         print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")
     print(f"  evaluations per solve: mean {np.mean(npass):.2f}")
+    nrun = valid.sum(1)
+    print(f"  items run per pass: mean {nrun.mean():.1f} min {nrun.min()} max {nrun.max()} (of {I} per pass); "
+          f"queries per pass (n_sharp + n_flat): mean {np.mean(nq):.0f} max {np.max(nq)}")
 
     b.close()
