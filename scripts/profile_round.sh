@@ -9,6 +9,9 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+( while sleep 30; do date >> $OUT/heartbeat; done ) &  # progress for the box's silence watchdog
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 400 python bench.py --scan-cache /tmp/lislam_scans $EXTRA > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $ROOT/bench.py --steps 3 --warmup 1 --cpu-budget 0 --sustain-s 0 --scan-cache /tmp/lislam_scans $EXTRA > $OUT/trace_bench.json 2> $OUT/trace.err || exit 2

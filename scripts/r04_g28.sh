@@ -1,0 +1,23 @@
+# work stealing (overflow rows 256 + o, roles LDS < 80 KB): a short chain first, then chain tests,
+# phase profile, chain timing and the pipelined bench
+cd $GRAFT_REPO_ROOT
+D=gpurun_out/r04ag
+mkdir -p $D
+step() {  # step <log> <timeout s> <command...>
+  local log=$1 to=$2; shift 2
+  timeout -k 10 $to "$@" > $D/$log 2>&1
+  local rc=$?
+  echo "$log rc=$rc" >> $D/steps.txt
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  return 0
+}
+export PYTHONUNBUFFERED=1
+( while sleep 30; do date >> $D/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+step quick61.txt 60 env CHAIN_ENGINE_ONLY=1 python3 scripts/chain_quick.py 61 2
+step chain_tests.log 240 python -m pytest tests/test_gpu_chain.py -x -v --timeout 200 --timeout-method thread
+step engprof.txt 120 env LISLAM_ALT_LIB=scripts/_ab/liblislam_prof.so python3 scripts/engine_prof.py 300
+step chain_main1.txt 120 env CHAIN_ENGINE_ONLY=1 python3 scripts/chain_quick.py 300 5
+step chain_main2.txt 120 env CHAIN_ENGINE_ONLY=1 python3 scripts/chain_quick.py 300 5
+step bench.json 300 python bench.py --steps 12 --warmup 2 --cpu-budget 0 --sustain-s 0 --segmented 0
