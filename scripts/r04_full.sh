@@ -1,7 +1,10 @@
 # the round-end checks on the current tree: the whole -m gpu suite, smoke(), the default bench line
 cd $GRAFT_REPO_ROOT
-D=gpurun_out/r04full
+D=gpurun_out/${R04FULL_TAG:-r04full}
 mkdir -p $D
+( while sleep 30; do date >> $D/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1
 rc=$?
 echo "tests rc=$rc" > $D/steps.txt
