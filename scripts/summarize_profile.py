@@ -26,7 +26,7 @@ def short(name):
 # kernel (native.KERNELS / the ORB timers); kernels of one logical name are summed per step
 LOGICAL = [("k_front_", "k_scan_front"), ("k_scan_lines", "k_scan_lines"), ("k_scan_compact", "k_scan_compact"),
            ("k_target_index", "k_target_index"), ("k_odom_assoc", "k_odom_assoc"), ("k_odom_lm", "k_odom_lm"),
-           ("k_odom_chain", "k_odom_chain"),
+           ("k_odom_chain", "k_odom_chain"), ("k_odom_items", "k_odom_chain"), ("k_odom_roles", "k_odom_chain+"),
            ("k_knn", "k_knn"), ("k_fit", "k_fit"), ("k_lm_eval", "k_lm_eval"), ("k_lm_step", "k_lm_step")]
 
 
@@ -81,7 +81,9 @@ for k in fetch:
                          "traffic_bytes_per_launch": per,
                          "avg_ns": float(s.get("AverageNs", 0) or 0), "calls": int(s.get("Calls", 0) or 0)}
 # per logical kernel: traffic per launch of the logical kernel (its rocprof kernels' traffic per
-# step / its launches per step), what bench.py's roofline line looks up
+# step / its launches per step), what bench.py's roofline line looks up.  The split chain engine is
+# two concurrent launches: k_odom_items counts the launches (and sets the duration), k_odom_roles'
+# traffic is added to the same engine launch ("k_odom_chain+").
 steps_pmc = 1  # profile_round.sh's PMC passes run one step
 lg = {}
 for k in fetch:
@@ -90,9 +92,9 @@ for k in fetch:
         continue
     f, nf = fetch[k]
     w, nw = write.get(k, [0.0, 1])
-    a = lg.setdefault(name, [0.0, 0])
+    a = lg.setdefault(name.rstrip("+"), [0.0, 0])
     a[0] += (2 * f + w) * 1024
-    a[1] += nf
+    a[1] += 0 if name.endswith("+") else nf
 out["kernels_logical"] = {k: {"launches_profiled": v[1], "traffic_bytes_per_launch": v[0] / max(1, v[1])}
                           for k, v in lg.items()}
 # SQ counters per launch (summed over the dispatch's shader engines); the fractions of the wave
@@ -100,6 +102,8 @@ out["kernels_logical"] = {k: {"launches_profiled": v[1], "traffic_bytes_per_laun
 # instruction active (SQ_ACTIVE_INST_ANY) name the bound that applies to a latency-bound kernel
 for k, cs in sq.items():
     name = logical(k) or k
+    if name.endswith("+"):
+        name = k.replace("void ", "").split("::")[-1].split("<")[0]
     per = {c: v[0] / max(1, v[1]) for c, v in cs.items()}
     wc = per.get("SQ_WAVE_CYCLES", 0.0)
     if wc > 0:
