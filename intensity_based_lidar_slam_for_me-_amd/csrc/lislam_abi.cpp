@@ -567,7 +567,9 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     // few long chains: one persistent launch sequences every round on the device
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (b->eng_split < 0) {  // the engine's streams, once per batch
-      static const bool single = getenv("LISLAM_ENGINE_SINGLE") && atoi(getenv("LISLAM_ENGINE_SINGLE")) == 1;
+      // LISLAM_ENGINE_SINGLE=1: the single-launch engine (k_odom_chain) even where CU masks exist
+      // (read once per batch: the tests run both engines in one process)
+      const bool single = getenv("LISLAM_ENGINE_SINGLE") && atoi(getenv("LISLAM_ENGINE_SINGLE")) == 1;
       b->eng_split = !single && lislam::engine_streams(c->device, &b->eng_roles, &b->eng_items) ? 1 : 0;
       if (b->eng_split) {
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_fork, hipEventDisableTiming));

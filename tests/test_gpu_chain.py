@@ -57,6 +57,27 @@ def test_continuous_chain_60_pairs_engine(pkg, oracle, ctx, stream61):
     ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
 
 
+def test_continuous_chain_60_pairs_single_launch_engine(pkg, oracle, ctx, stream61):
+    """The same chain through the single-launch engine (k_odom_chain: roles and items in one grid),
+    the fallback where CU-masked streams are unavailable (LISLAM_ENGINE_SINGLE=1 forces it)."""
+    scans, feats = stream61
+    S = len(scans)
+    ctx.set_odometry_schedule(ctx.ENGINE_ON)
+    os.environ["LISLAM_ENGINE_SINGLE"] = "1"
+    try:
+        b = pkg.Batch(ctx, S)
+        b.upload(scans)
+        b.extract(S)
+        b.odometry(S, S - 1)  # the batch's first engine launch reads the variable
+        ctx.synchronize()
+    finally:
+        del os.environ["LISLAM_ENGINE_SINGLE"]
+        ctx.set_odometry_schedule(ctx.ENGINE_AUTO)
+    pose, rel, st = oracle.odometry_chain(feats)
+    check_chain(pkg, b, feats, pose, rel, st)
+    b.close()
+
+
 def test_continuous_chain_60_pairs_round_launches(pkg, oracle, ctx, stream61):
     """The same chain through the per-round launches (k_odom_assoc16 + k_odom_lm2)."""
     scans, feats = stream61
