@@ -213,11 +213,12 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
 #define LISLAM_ENGINE_AUTO 1
 #define LISLAM_ENGINE_ON 2
 int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
-/* Synchronize; status = 1 if an engine launch of the batch gave up since the previous status call
- * (one of its bounded device waits expired: the outputs of that launch are invalid), else 0.  The
- * word is sticky: later launches do not clear it, and until this call reads (and clears) it,
- * lislam_batch_download of LISLAM_OUT_PARA / POSE / STATS (and lislam_odom_step) return
- * LISLAM_ERR_DEVICE. */
+/* status = the number of engine launches of the batch that gave up since the previous status call
+ * (one of the engine's bounded device waits expired, e.g. when its two launches could not run
+ * together).  An aborted launch is recovered, not refused: the next call on the batch (any
+ * lislam_batch_* call, lislam_odom_step, lislam_synchronize) waits for the engine on the host and
+ * re-runs that launch's chains on the per-round schedule (LISLAM_ENGINE_OFF, no device waits) before
+ * it goes on, so the outputs are always those of a complete schedule.  Reading the count clears it. */
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
 
 /* Order of equal sort keys in the two std::sort calls of the feature extraction:
@@ -450,12 +451,14 @@ int lislam_odom_fuse(lislam_odom_fuser* f, const double* aloam, const double* in
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
  * clears the record. */
-#define LISLAM_MAP_NUM_KERNELS 20 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+#define LISLAM_MAP_NUM_KERNELS 21 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
                                      gather + cell table), Add_Points downsample (claim + resolve),
                                      k_orb_pyramid, k_orb_fast, k_orb_select, k_orb_finish,
-                                     k_orb_blur, k_orb_desc, k_orb_match, k_orb_lm,
+                                     k_orb_blur (the padded-level blur of images too large for
+                                     k_orb_pyramid), k_orb_desc, k_orb_match, k_orb_lm,
                                      k_ground_screen, k_ground_ransac, k_ground_extract,
-                                     k_lc_step, k_lc_apply, k_fuse */
+                                     k_lc_step, k_lc_apply, k_fuse, k_orb_roiblur (the ROI blur +
+                                     border rows after k_orb_pyramid) */
 int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
 int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 

@@ -158,30 +158,32 @@ class CostFunction {
 class DeviceCostFunction;
 
 namespace detail {
-/* One batched evaluation: the blocks that share a pair of parameter-block pointers, at the values
- * those blocks were last evaluated at. */
+/* One batched evaluation: the blocks of one group (one Ceres problem) at one parameter point. */
 struct FactorBatch {
-  const double* pq = nullptr;  // the parameter blocks' addresses (Ceres' parameters[0], [1])
-  const double* pt = nullptr;
+  unsigned long long group = 0;  // the group whose blocks the launch held (0: none yet)
   unsigned long long generation = 0;
-  double cq[4] = {0, 0, 0, 0}, ct[3] = {0, 0, 0};
+  double cq[4] = {0, 0, 0, 0}, ct[3] = {0, 0, 0};  // the parameter values it was evaluated at
   std::vector<int32_t> index;  // registry slot -> row of this batch's outputs, -1 = not in it
   std::vector<double> res, jq, jt;  // [rows][3], [rows][3][4], [rows][3][3]
   unsigned long long used = 0;      // LRU stamp
 };
-/* Every live DeviceCostFunction, packed as lislam_eval_factors_raw records, and the batches of
- * the parameter points they were last evaluated at: a batch holds the blocks whose Evaluate saw
- * the same parameter-block pointers (one Ceres problem), plus the blocks not evaluated yet, so a
- * problem's pass is one launch and two live problems at different poses do not evict each other.
- * One per process (the blocks evaluate on the one SetFactorContext() context); the mutex
- * serializes Ceres' evaluation threads. */
+/* Every live DeviceCostFunction, packed as lislam_eval_factors_raw records, and the batches of the
+ * parameter points they were last evaluated at.  Blocks are grouped by problem, not by the
+ * parameter-block pointers Evaluate sees: Ceres' evaluator points each block's state into its own
+ * x / candidate-x vectors, so those pointers change between evaluations of one problem.  A block
+ * with no group joins the group of the first batch that serves it (its values matched); a miss
+ * launches the block's whole group (plus every block with no group yet) at the new values, into the
+ * least recently used batch.  So a problem's pass is one launch, and two live problems at different
+ * poses do not evict each other.  One per process (the blocks evaluate on the one
+ * SetFactorContext() context); the mutex serializes Ceres' evaluation threads. */
 struct FactorRegistry {
   std::mutex mu;
   std::vector<DeviceCostFunction*> blocks;  // slot i = blocks[i]
   std::vector<int32_t> kinds;
   std::vector<double> recs;                  // [n][12]
-  std::vector<const double*> seen_q, seen_t; // per slot: the pointers its last Evaluate saw (null: none yet)
+  std::vector<unsigned long long> group;     // per slot: its problem's group (0: not evaluated yet)
   unsigned long long generation = 0;         // bumped by every Create() / destruction
+  unsigned long long next_group = 0;
   static constexpr int kBatches = 4;
   FactorBatch batch[kBatches];
   unsigned long long clock = 0;
@@ -213,8 +215,7 @@ class DeviceCostFunction : public CostFunction {
     g.blocks.push_back(this);
     g.kinds.push_back(kind);
     g.recs.insert(g.recs.end(), rec_, rec_ + 12);
-    g.seen_q.push_back(nullptr);
-    g.seen_t.push_back(nullptr);
+    g.group.push_back(0);
     g.generation++;
   }
   ~DeviceCostFunction() override {
@@ -226,15 +227,13 @@ class DeviceCostFunction : public CostFunction {
       g.blocks[slot_] = m;
       g.kinds[slot_] = g.kinds[last];
       std::memcpy(&g.recs[slot_ * 12], &g.recs[last * 12], 12 * sizeof(double));
-      g.seen_q[slot_] = g.seen_q[last];
-      g.seen_t[slot_] = g.seen_t[last];
+      g.group[slot_] = g.group[last];
       m->slot_ = slot_;
     }
     g.blocks.pop_back();
     g.kinds.pop_back();
     g.recs.resize(last * 12);
-    g.seen_q.pop_back();
-    g.seen_t.pop_back();
+    g.group.pop_back();
     g.generation++;
   }
   DeviceCostFunction(const DeviceCostFunction&) = delete;
@@ -253,29 +252,29 @@ class DeviceCostFunction : public CostFunction {
     const double* pt = kind_ == 4 ? nullptr : parameters[1];
     detail::FactorRegistry& g = detail::factor_registry();
     std::lock_guard<std::mutex> lock(g.mu);
-    g.seen_q[slot_] = q;
-    g.seen_t[slot_] = pt;
-    // the batch of this block's parameter pointers, valid at these values
+    // a batch that holds this block at these values (the ground factor has no t block: its
+    // residual ignores t, so any batch at its q serves it)
+    auto at = [&](const detail::FactorBatch& e) {
+      return std::memcmp(e.cq, q, sizeof(e.cq)) == 0 && (kind_ == 4 || std::memcmp(e.ct, pt, sizeof(e.ct)) == 0);
+    };
     detail::FactorBatch* b = nullptr;
     for (detail::FactorBatch& e : g.batch)
-      if (e.pq == q && e.pt == pt && e.generation == g.generation && slot_ < e.index.size() && e.index[slot_] >= 0) b = &e;
-    // the ground factor has no t block (its residual ignores t): any cached t serves it
-    const double* t = kind_ == 4 ? (b ? b->ct : zero_t) : pt;
-    if (!b || std::memcmp(b->cq, q, sizeof(b->cq)) != 0 || std::memcmp(b->ct, t, sizeof(b->ct)) != 0) {
-      // a new parameter point: every block of this problem (same pointers, or not evaluated yet)
-      // at (q, t), one launch, into the least recently used batch
-      if (!b) {
-        b = &g.batch[0];
-        for (detail::FactorBatch& e : g.batch)
-          if (e.used < b->used) b = &e;
-      }
+      if (e.generation == g.generation && slot_ < e.index.size() && e.index[slot_] >= 0 && at(e)) b = &e;
+    if (!b) {
+      // a new parameter point of this block's problem: every block of its group, and every block not
+      // evaluated yet, at (q, t) in one launch, into the least recently used batch
+      b = &g.batch[0];
+      for (detail::FactorBatch& e : g.batch)
+        if (e.used < b->used) b = &e;
+      unsigned long long grp = g.group[slot_];
+      if (grp == 0) grp = ++g.next_group;
+      const double* t = kind_ == 4 ? zero_t : pt;
       const size_t n = g.blocks.size();
       b->index.assign(n, -1);
       std::vector<int32_t> kinds;
       std::vector<double> recs;
       for (size_t i = 0; i < n; i++) {
-        const bool mine = (g.seen_q[i] == q && g.seen_t[i] == pt) || (g.seen_q[i] == nullptr);
-        if (!mine) continue;
+        if (g.group[i] != grp && g.group[i] != 0) continue;
         b->index[i] = (int32_t)kinds.size();
         kinds.push_back(g.kinds[i]);
         recs.insert(recs.end(), &g.recs[i * 12], &g.recs[i * 12] + 12);
@@ -289,12 +288,13 @@ class DeviceCostFunction : public CostFunction {
                                   b->jt.data()) != LISLAM_OK)
         return false;
       g.launches++;
-      b->pq = q;
-      b->pt = pt;
+      b->group = grp;
       std::memcpy(b->cq, q, sizeof(b->cq));
-      if (t != b->ct) std::memcpy(b->ct, t, sizeof(b->ct));
+      std::memcpy(b->ct, t, sizeof(b->ct));
       b->generation = g.generation;
     }
+    // the block belongs to the group of the first batch that serves it
+    if (g.group[slot_] == 0) g.group[slot_] = b->group;
     b->used = ++g.clock;
     const size_t row = (size_t)b->index[slot_];
     const bool want_q = jacobians && jacobians[0], want_t = jacobians && kind_ != 4 && jacobians[1];

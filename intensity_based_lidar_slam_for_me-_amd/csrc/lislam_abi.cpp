@@ -123,15 +123,15 @@ int lislam_ctx_destroy(lislam_ctx* c) {
 
 const char* lislam_last_error(const lislam_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+static int engine_settle(lislam_batch* b);
+
 int lislam_synchronize(lislam_ctx* c) {
   if (!c) return LISLAM_ERR_ARG;
   hipSetDevice(c->device);
-  for (lislam_batch* b : c->batches)
-    if (b->eng_pending) {
-      HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
-      b->eng_pending = false;
-    }
+  for (lislam_batch* b : c->batches) {
+    const int rc = engine_settle(b);
+    if (rc != LISLAM_OK) return rc;
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return LISLAM_OK;
 }
@@ -149,14 +149,30 @@ int lislam_get_stream(lislam_ctx* c, void** s) {
 }
 
 // ------------------------------------------------------------------------------ batch
-// The context stream waits for the batch's split engine launch, if one is pending (lislam_batch.hpp).
+// The context stream waits for the batch's split engine launch, if one is pending, and the outcome of
+// the last engine launch is resolved (lislam_batch.hpp): an aborted launch is re-run on the per-round
+// schedule, queued on the context stream ahead of whatever the calling batch function queues next.
 static int engine_settle(lislam_batch* b) {
-  if (!b->eng_pending) return LISLAM_OK;
+  if (!b->eng_pending && !b->eng_check) return LISLAM_OK;
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
-  HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
-  b->eng_pending = false;
+  if (b->eng_pending) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
+    b->eng_pending = false;
+  }
+  if (!b->eng_check) return LISLAM_OK;
+  b->eng_check = false;
+  // the host waits for the engine itself (not the context stream, which may hold later work)
+  HIPCHK(c, hipEventSynchronize(b->eng_done));
+  if (*b->h_abort == 0) return LISLAM_OK;
+  *b->h_abort = 0;
+  HIPCHK(c, hipMemsetAsync(b->oa.eng_ctl + 3, 0, sizeof(unsigned), c->stream));
+  b->eng_fallbacks++;
+  // the per-round schedule has no device waits: it cannot abort
+  lislam::launch_odometry(b->eng_args, b->odo_stream, lislam_batch::kGroups, b->odo_fork, b->odo_join, nullptr,
+                          &lislam_batch::event_cb, b);
+  HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
 #define SETTLE(b)                           \
@@ -290,6 +306,8 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (b->wire) hipFree(b->wire);
   if (b->ev_images) hipEventDestroy(b->ev_images);
   if (b->eng_ready) hipEventDestroy(b->eng_ready);
+  if (b->eng_done) hipEventDestroy(b->eng_done);
+  if (b->h_abort) hipHostFree(b->h_abort);
   if (b->stage_ev) hipEventDestroy(b->stage_ev);
   if (b->copy_stream) {
     hipStreamSynchronize(b->copy_stream);
@@ -401,7 +419,6 @@ int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_sca
 int lislam_batch_mapopt(lislam_batch* b, lislam_map* m, int32_t scan, const double* odom, double* state,
                         double* out_pose, int32_t* summary) {
   return lislam_batch_mapopt_corner(b, m, nullptr, scan, odom, state, out_pose, summary);
-  SETTLE(b);
 }
 
 // With the corner ikd-Tree: pc_corner is the scan's less-sharp cloud (/laser_cloud_less_sharp,
@@ -548,8 +565,9 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     b->stage_busy = true;
   }
   // chain groups: 2 streams, so one group's solves overlap another's
-  // association (a solve occupies one workgroup per chain, far from filling the device)
-  const int G = std::min(2, (int)lislam_batch::kMaxGroups);
+  // association (a solve occupies one workgroup per chain, far from filling the device); the engine's
+  // abort recovery runs the same schedule, so the streams exist before any engine launch
+  const int G = lislam_batch::kGroups;
   b->odo_stream[0] = c->stream;
   for (int g = 1; g < G; g++) {
     if (!b->odo_stream[g] && !lislam::work_stream(c->device, &b->odo_stream[g])) return fail(c, LISLAM_ERR_DEVICE, "stream");
@@ -576,19 +594,29 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_r, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_i, hipEventDisableTiming));
       }
+      HIPCHK(c, hipEventCreateWithFlags(&b->eng_done, hipEventDisableTiming));
+      HIPCHK(c, hipHostMalloc((void**)&b->h_abort, sizeof(unsigned), hipHostMallocDefault));
+      *b->h_abort = 0;
     }
     if (ev) { e0 = b->get_event(); e1 = b->get_event(); }
+    hipStream_t tail = c->stream;  // where the engine ends
     if (b->eng_split) {
-      // the inputs: the last extract (its eng_ready), or the staging copies just queued
-      if (use_aloam || init_host) HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
+      // the inputs: everything queued on the context stream so far (the last extract, any per-round
+      // odometry queued after it, the staging copies just queued)
+      HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
       lislam::launch_odometry_chain_split(o, b->eng_roles, b->eng_items, b->eng_ready, b->eng_fork, b->eng_join_r,
                                           b->eng_join_i, e0, e1);
       b->eng_pending = true;
+      tail = b->eng_items;  // joined with the roles stream
     } else {
       if (ev) HIPCHK(c, hipEventRecord(e0, c->stream));
       lislam::launch_odometry_chain(o, c->stream);
       if (ev) HIPCHK(c, hipEventRecord(e1, c->stream));
     }
+    HIPCHK(c, hipMemcpyAsync(b->h_abort, b->oa.eng_ctl + 3, sizeof(unsigned), hipMemcpyDeviceToHost, tail));
+    HIPCHK(c, hipEventRecord(b->eng_done, tail));
+    b->eng_args = o;
+    b->eng_check = true;
     b->engine_ran = true;
     if (ev) ev->push_back({6, e0, e1});
     HIPCHK(c, hipGetLastError());
@@ -616,19 +644,12 @@ int lislam_batch_odometry_gated(lislam_batch* b, int32_t n_scans, int32_t chain_
 
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
   if (!b || !status) return LISLAM_ERR_ARG;
+  // engine launches that gave up (a bounded device wait expired) since the last status call or the
+  // batch's creation; each was re-run on the per-round schedule when it settled, so the outputs are
+  // valid.  Reading the count clears it.
   SETTLE(b);
-  lislam_ctx* c = b->ctx;
-  hipSetDevice(c->device);
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  // the sticky abort word: set by any engine launch whose bounded device wait expired since the last
-  // status call (or the batch's creation); reading it clears it
-  unsigned w = 0;
-  HIPCHK(c, hipMemcpy(&w, b->oa.eng_ctl + 3, sizeof(w), hipMemcpyDeviceToHost));
-  if (w) {
-    const unsigned z = 0;
-    HIPCHK(c, hipMemcpy(b->oa.eng_ctl + 3, &z, sizeof(z), hipMemcpyHostToDevice));
-  }
-  *status = w ? 1 : 0;
+  *status = b->eng_fallbacks;
+  b->eng_fallbacks = 0;
   return LISLAM_OK;
 }
 
@@ -719,11 +740,7 @@ static int output_source(lislam_batch* b, int what, int scan, const void** src_o
     case LISLAM_OUT_PARA:
     case LISLAM_OUT_POSE:
     case LISLAM_OUT_STATS: {
-      // an engine launch that gave up left these unwritten: refuse them until the status is read
-      unsigned ab = 0;
-      HIPCHK(c, hipMemcpy(&ab, o.eng_ctl + 3, sizeof(ab), hipMemcpyDeviceToHost));
-      if (ab) return fail(c, LISLAM_ERR_DEVICE, "the odometry chain engine aborted (a bounded device wait expired); "
-                                                 "lislam_batch_odometry_status clears it");
+      // (an aborted engine launch has been re-run by the caller's SETTLE before this point)
       if (what == LISLAM_OUT_PARA) { src = o.para + (size_t)scan * 7; cnt = 7; esz = 8; }
       else if (what == LISLAM_OUT_POSE) { src = o.pose + (size_t)scan * 7; cnt = 7; esz = 8; }
       else { src = o.stats + (size_t)scan * 8; cnt = 8; esz = 4; }

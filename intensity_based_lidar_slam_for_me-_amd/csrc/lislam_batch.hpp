@@ -34,6 +34,7 @@ struct lislam_batch {
   // chain groups of the odometry schedule: group 0 on the context stream, the others on their own
   // streams (created on first use), forked / joined by events
   static constexpr int kMaxGroups = 4;
+  static constexpr int kGroups = 2;  // groups used: one group's solves overlap the other's association
   hipStream_t odo_stream[kMaxGroups] = {};
   hipEvent_t odo_fork = nullptr, odo_join[kMaxGroups] = {};
   std::vector<hipEvent_t> pool;
@@ -51,6 +52,17 @@ struct lislam_batch {
   // lislam_batch_extract (and after odometry's staging copies); the engine starts from it.
   bool eng_pending = false;
   hipEvent_t eng_ready = nullptr;
+  // Abort recovery.  Every engine launch (split or single) copies its sticky abort word into h_abort
+  // (pinned) and records eng_done behind it; eng_check stays set until the next batch call settles
+  // it: the host waits for eng_done and, if the engine gave up (a bounded device wait expired), clears
+  // the word and re-runs eng_args on the per-round schedule on the context stream before the call
+  // goes on, so a caller never sees the aborted launch's outputs.  eng_fallbacks counts those
+  // recoveries until lislam_batch_odometry_status reads (and clears) it.
+  bool eng_check = false;
+  hipEvent_t eng_done = nullptr;
+  unsigned* h_abort = nullptr;
+  OdomArgs eng_args{};
+  int eng_fallbacks = 0;
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
   // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
   // queued on the context stream after it.

@@ -2991,27 +2991,14 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
 // engine instead).  CU-masked streams: a mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950,
 // measured: scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD unmasked), the
 // roles one CU in every XCD, the items every other CU, so an item workgroup never takes the CU a
-// solve role needs whole (256 VGPRs x 8 waves).  LISLAM_ENGINE_STREAMS=prio (developer A/B):
-// unmasked streams of the device's greatest priority instead — measured to starve the role of a
-// whole CU under the pipelined extraction (a 2 s engine wait expired, r04i).
+// solve role needs whole (256 VGPRs x 8 waves).  (Unmasked priority streams were measured to starve
+// the role of a whole CU under the pipelined extraction, r04i, and are not offered.)
 bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
   const int cus = prop.multiProcessorCount, nx = 8;
   if (!multi_xcd || cus < 4 * nx || cus % nx) return false;
-  const char* mode = getenv("LISLAM_ENGINE_STREAMS");
-  if (mode && std::strcmp(mode, "prio") == 0) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return false;
-    if (hipStreamCreateWithPriority(roles, hipStreamNonBlocking, greatest) != hipSuccess) return false;
-    if (hipStreamCreateWithPriority(items, hipStreamNonBlocking, greatest) != hipSuccess) {
-      (void)hipStreamDestroy(*roles);
-      *roles = nullptr;
-      return false;
-    }
-    return true;
-  }
   const int words = (cus + 31) / 32;
   std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
   for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);
@@ -3028,12 +3015,9 @@ bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
 // solve roles' (one per XCD, engine_streams), so a role launched beside the next batch's extraction
 // finds a whole CU free instead of waiting for the extraction's waves on it to drain — they would
 // refill each freed slot first.  Plain non-blocking stream where CU masks do not apply.
-// LISLAM_ENGINE_STREAMS=prio / =open (developer A/B) leave it unmasked.
 bool work_stream(int dev, hipStream_t* s) {
   hipDeviceProp_t prop{};
-  const char* mode = getenv("LISLAM_ENGINE_STREAMS");
-  const bool open = mode && (std::strcmp(mode, "prio") == 0 || std::strcmp(mode, "open") == 0);
-  if (!open && hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
     const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
     const int cus = prop.multiProcessorCount, nx = 8;
     if (multi_xcd && cus >= 4 * nx && cus % nx == 0) {
@@ -3047,14 +3031,16 @@ bool work_stream(int dev, hipStream_t* s) {
 }
 
 // One engine at a time per device (contexts included): each split launch waits for the previous
-// one, so two pipelined batches' chains do not split the CUs the extraction beside them needs.
-static hipEvent_t engine_done_event(int dev) {
-  static std::mutex mu;
-  static hipEvent_t ev[64] = {};
-  std::lock_guard<std::mutex> lock(mu);
-  if (dev < 0 || dev >= 64) return nullptr;
-  if (!ev[dev]) (void)hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming);
-  return ev[dev];
+// one, so two pipelined batches' chains do not split the CUs the extraction beside them needs.  The
+// wait on the previous engine and the re-record of the event are one critical section (the mutex),
+// so two host threads launching on different contexts cannot both pass the gate.
+struct EngineGate {
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+};
+static EngineGate* engine_gate(int dev) {
+  static EngineGate gates[64];
+  return dev >= 0 && dev < 64 ? &gates[dev] : nullptr;
 }
 
 int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_t items, hipEvent_t ready, hipEvent_t fork,
@@ -3085,7 +3071,13 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
   const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
-  const hipEvent_t prev = engine_done_event(dev);
+  EngineGate* gate = engine_gate(dev);
+  std::unique_lock<std::mutex> lock;
+  if (gate) {
+    lock = std::unique_lock<std::mutex>(gate->mu);
+    if (!gate->ev) (void)hipEventCreateWithFlags(&gate->ev, hipEventDisableTiming);
+  }
+  const hipEvent_t prev = gate ? gate->ev : nullptr;
   (void)hipStreamWaitEvent(roles, ready, 0);
   if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
   if (t0) (void)hipEventRecord(t0, roles);

@@ -2069,7 +2069,7 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     hipLaunchKernelGGL(k_orb_fastnms, dim3(g.fband[kL], n), dim3(256), lds, st, a);
   }
   if (fused) {  // the border rows of both pyramids and the blurred copy's rows
-    TimedScope t(c, kT_orb_blur);
+    TimedScope t(c, kT_orb_roiblur);
     hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
   { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }

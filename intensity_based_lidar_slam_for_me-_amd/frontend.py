@@ -212,8 +212,8 @@ class Batch:
                   "lislam_batch_odometry_gated")
 
     def odometry_status(self) -> int:
-        """1 if an engine launch gave up since the previous call (a bounded device wait expired; the
-        word is sticky across launches and this call clears it), else 0."""
+        """Engine launches that gave up since the previous call (a bounded device wait expired); each
+        was re-run on the per-round schedule before its outputs could be read.  The call clears it."""
         st = ctypes.c_int32(0)
         nat.check(self.ctx.lib.lislam_batch_odometry_status(self.h, ctypes.byref(st)), self.ctx.h,
                   "lislam_batch_odometry_status")

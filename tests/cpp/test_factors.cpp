@@ -203,6 +203,42 @@ int main() {
       }
     }
     std::printf("batched: 2304 blocks, %d parameter points, 1 launch each\n", points);
+    // Ceres' evaluator points the parameter blocks into its own x / candidate-x vectors, so the
+    // pointers Evaluate sees change between evaluations of one problem: each point is evaluated
+    // from two buffers in turn (cost pass from one, Jacobian pass from the other, holding the same
+    // values), and a point seen before (an accepted candidate re-evaluated at x) is served from its
+    // batch.  Still one launch per new point, none for a repeated one.
+    double bufq[2][4], buft[2][3];
+    const long long before = lislam::FactorLaunches();
+    double prev_q[4] = {0, 0, 0, 1}, prev_t[3] = {0, 0, 0};
+    for (int pt = 0; pt < points; pt++) {
+      double qq[4] = {A(rng), A(rng), A(rng), 0.0}, tt[3] = {U(rng), U(rng), U(rng)};
+      qq[3] = std::sqrt(1.0 - qq[0] * qq[0] - qq[1] * qq[1] - qq[2] * qq[2]);
+      if (pt == points - 1) {  // the previous point again (from the other buffer)
+        std::memcpy(qq, prev_q, sizeof(qq));
+        std::memcpy(tt, prev_t, sizeof(tt));
+      }
+      for (int pass = 0; pass < 2; pass++) {
+        const int w = (pt + pass) % 2;
+        std::memcpy(bufq[w], qq, sizeof(qq));
+        std::memcpy(buft[w], tt, sizeof(tt));
+        const double* params[2] = {bufq[w], buft[w]};
+        for (size_t i = 0; i < pb.size(); i++) {
+          double res[3], jq[12], jt[9];
+          double* jacs[2] = {jq, jt};
+          if (!pb[i]->Evaluate(params, res, pass ? jacs : nullptr)) return 8;
+        }
+      }
+      std::memcpy(prev_q, qq, sizeof(qq));
+      std::memcpy(prev_t, tt, sizeof(tt));
+    }
+    const long long used = lislam::FactorLaunches() - before;
+    if (used != points - 1) {
+      std::fprintf(stderr, "alternating buffers: %lld launches for %d points (%d new; want 1 each)\n", used, points,
+                   points - 1);
+      g_fail++;
+    }
+    std::printf("alternating parameter buffers: %lld launches for %d points (%d new)\n", used, points, points - 1);
   }
   // Two problems alive at once, each over its own parameter blocks at its own pose (two Ceres
   // problems, evaluated in turn): each problem's pass is one launch of ITS blocks, the other's
