@@ -220,6 +220,9 @@ int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
  * re-runs that launch's chains on the per-round schedule (LISLAM_ENGINE_OFF, no device waits) before
  * it goes on, so the outputs are always those of a complete schedule.  Reading the count clears it. */
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
+/* Which schedule the batch's last odometry call ran: 0 per-round launches, 1 the single-launch
+ * engine (k_odom_chain), 2 the split engine (k_odom_roles + k_odom_items on CU-masked streams). */
+int lislam_batch_odometry_engine(lislam_batch* b, int32_t* kind);
 
 /* Order of equal sort keys in the two std::sort calls of the feature extraction:
  * - each segment's sort by curvature (scanRegistration.cpp:445), which decides which of two

@@ -653,6 +653,12 @@ int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
   return LISLAM_OK;
 }
 
+int lislam_batch_odometry_engine(lislam_batch* b, int32_t* kind) {
+  if (!b || !kind) return LISLAM_ERR_ARG;
+  *kind = !b->engine_ran ? 0 : b->eng_split == 1 ? 2 : 1;
+  return LISLAM_OK;
+}
+
 int lislam_batch_kernel_times(lislam_batch* b, float* ms_per_call, int32_t* launches_per_call, int32_t* calls) {
   if (!b || !ms_per_call) return LISLAM_ERR_ARG;
   SETTLE(b);

@@ -219,6 +219,17 @@ class Batch:
                   "lislam_batch_odometry_status")
         return int(st.value)
 
+    ENGINES = ("per-round launches (k_odom_assoc16 + k_odom_lm2)", "single-launch engine (k_odom_chain)",
+               "split engine (k_odom_roles + k_odom_items)")
+
+    def odometry_engine(self) -> int:
+        """The schedule of the last odometry call (lislam_batch_odometry_engine): 0 per-round
+        launches, 1 the single-launch engine, 2 the split engine (ENGINES names them)."""
+        k = ctypes.c_int32(0)
+        nat.check(self.ctx.lib.lislam_batch_odometry_engine(self.h, ctypes.byref(k)), self.ctx.h,
+                  "lislam_batch_odometry_engine")
+        return int(k.value)
+
     def skip_flags(self, n: int) -> np.ndarray:
         """use_aloam per scan from the ORB front end's results (intensity_odometry first): 1 where
         detectfeatures skipped the frame (the "skip_intensity" frame_id, scanRegistration.cpp:603-609)."""

@@ -66,8 +66,10 @@ write = pmc(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"))
 stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv")))}
 bench = json.load(open(os.path.join(src, "trace_bench.json")))
 bc = bench["config"]
+# the odometry schedule the PMC passes ran (bench.py matches it before citing the odometry's counters)
+pmc_cfg = json.load(open(os.path.join(src, "pmc_fetch.json"))).get("config", {})
 out = {"tag": tag, "config": {k: bc[k] for k in ("lines", "width", "scans_per_step_per_gpu", "chain_len") if k in bc},
-       "workload": bc.get("workload"),
+       "workload": bc.get("workload"), "odometry_engine": pmc_cfg.get("odometry_schedule"),
        "correction": "traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE "
                                  "half-count of wide reads, MI355X_MICROARCH.md HBM section)", "kernels": {}}
 for k in fetch:
