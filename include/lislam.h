@@ -223,6 +223,11 @@ int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
 /* Which schedule the batch's last odometry call ran: 0 per-round launches, 1 the single-launch
  * engine (k_odom_chain), 2 the split engine (k_odom_roles + k_odom_items on CU-masked streams). */
 int lislam_batch_odometry_engine(lislam_batch* b, int32_t* kind);
+/* The error word of the batch's last aborted engine launch (0: none since the batch's creation):
+ * which bounded wait gave up — 1 an association item waiting for the previous pass's items, 2 an
+ * item waiting for its pass's pose, 3 a solve role waiting for its pass's items, 4 / 5 the
+ * progressive gather's poll / loads, 0x57xx an overflow query out of range. */
+int lislam_batch_odometry_abort_code(lislam_batch* b, int32_t* code);
 
 /* Order of equal sort keys in the two std::sort calls of the feature extraction:
  * - each segment's sort by curvature (scanRegistration.cpp:445), which decides which of two

@@ -165,8 +165,10 @@ static int engine_settle(lislam_batch* b) {
   b->eng_check = false;
   // the host waits for the engine itself (not the context stream, which may hold later work)
   HIPCHK(c, hipEventSynchronize(b->eng_done));
-  if (*b->h_abort == 0) return LISLAM_OK;
-  *b->h_abort = 0;
+  // h_abort: the engine's error word (which wait gave up) and its sticky abort word
+  if (b->h_abort[1] == 0) return LISLAM_OK;
+  b->eng_abort_code = b->h_abort[0];
+  b->h_abort[0] = b->h_abort[1] = 0;
   HIPCHK(c, hipMemsetAsync(b->oa.eng_ctl + 3, 0, sizeof(unsigned), c->stream));
   b->eng_fallbacks++;
   // the per-round schedule has no device waits: it cannot abort
@@ -260,9 +262,9 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
   rc |= dalloc(b, &o.para, (size_t)S * 7);
   rc |= dalloc(b, &o.pose, (size_t)S * 7);
   rc |= dalloc(b, &o.stats, (size_t)S * 8);
-  rc |= dalloc(b, &o.eng_ctl, (size_t)8 + 6 * (size_t)S);
+  rc |= dalloc(b, &o.eng_ctl, (size_t)8 + 10 * (size_t)S);
   rc |= dalloc(b, &o.warm, (size_t)S * (b->cap_sharp + b->cap_flat) * 4);
-  rc |= dalloc(b, &o.eng_part, (size_t)S * lislam::engine_items(b->cap_sharp + b->cap_flat) * 32);  // [chains][items][32]
+  rc |= dalloc(b, &o.eng_part, (size_t)S * lislam::engine_part_rows(b->cap_sharp + b->cap_flat) * 32);  // [chains][rows][32]
   rc |= dalloc(b, &b->d_init, (size_t)S * 14);
   rc |= dalloc(b, &b->d_gate, (size_t)S);
   if (rc != LISLAM_OK) {
@@ -270,7 +272,7 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
     return LISLAM_ERR_DEVICE;
   }
   // the engine's control words (its sticky abort word is never cleared by a launch)
-  if (hipMemset(o.eng_ctl, 0, sizeof(unsigned) * ((size_t)8 + 6 * (size_t)S)) != hipSuccess) {
+  if (hipMemset(o.eng_ctl, 0, sizeof(unsigned) * ((size_t)8 + 10 * (size_t)S)) != hipSuccess) {
     lislam_batch_destroy(b);
     return LISLAM_ERR_DEVICE;
   }
@@ -595,8 +597,8 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_i, hipEventDisableTiming));
       }
       HIPCHK(c, hipEventCreateWithFlags(&b->eng_done, hipEventDisableTiming));
-      HIPCHK(c, hipHostMalloc((void**)&b->h_abort, sizeof(unsigned), hipHostMallocDefault));
-      *b->h_abort = 0;
+      HIPCHK(c, hipHostMalloc((void**)&b->h_abort, 2 * sizeof(unsigned), hipHostMallocDefault));
+      b->h_abort[0] = b->h_abort[1] = 0;
     }
     if (ev) { e0 = b->get_event(); e1 = b->get_event(); }
     hipStream_t tail = c->stream;  // where the engine ends
@@ -613,7 +615,7 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
       lislam::launch_odometry_chain(o, c->stream);
       if (ev) HIPCHK(c, hipEventRecord(e1, c->stream));
     }
-    HIPCHK(c, hipMemcpyAsync(b->h_abort, b->oa.eng_ctl + 3, sizeof(unsigned), hipMemcpyDeviceToHost, tail));
+    HIPCHK(c, hipMemcpyAsync(b->h_abort, b->oa.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, tail));
     HIPCHK(c, hipEventRecord(b->eng_done, tail));
     b->eng_args = o;
     b->eng_check = true;
@@ -650,6 +652,13 @@ int lislam_batch_odometry_status(lislam_batch* b, int32_t* status) {
   SETTLE(b);
   *status = b->eng_fallbacks;
   b->eng_fallbacks = 0;
+  return LISLAM_OK;
+}
+
+int lislam_batch_odometry_abort_code(lislam_batch* b, int32_t* code) {
+  if (!b || !code) return LISLAM_ERR_ARG;
+  SETTLE(b);
+  *code = (int32_t)b->eng_abort_code;
   return LISLAM_OK;
 }
 

@@ -63,6 +63,7 @@ struct lislam_batch {
   unsigned* h_abort = nullptr;
   OdomArgs eng_args{};
   int eng_fallbacks = 0;
+  unsigned eng_abort_code = 0;  // the error word of the last aborted launch (lislam_batch_odometry_abort_code)
   // recorded inside every lislam_batch_extract once the a1 images exist: the ORB front end waits
   // on it from its own stream, so it overlaps the rest of the extraction and whatever the caller
   // queued on the context stream after it.

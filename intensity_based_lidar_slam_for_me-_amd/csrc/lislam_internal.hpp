@@ -102,9 +102,10 @@ struct OdomArgs {
   const int* gate;  // [S] use_aloam per scan (laserOdometry.cpp:403-417), or null = every scan
   // chain engine (k_odom_chain): control words (zeroed before every launch) and the per-query
   // association of the first outer pass, the second pass's starting bounds
-  unsigned* eng_ctl;  // [8 + 6 S]
+  unsigned* eng_ctl;  // [8 + 10 S]
   int* warm;          // [n_chains][cap_sharp + cap_flat][4]
-  double* eng_part;   // [n_chains][items][32]: each association item's share of the first evaluation
+  double* eng_part;   // [n_chains][engine_part_rows][32]: each association item's (and overflow query's)
+                      // share of the first evaluation
 };
 
 // Batched evaluation of the cost functors (lislam_eval_factors).
@@ -161,6 +162,8 @@ bool use_chain_engine(const OdomArgs& a, int mode);
 // Association items per (pass, chain) of the engine for cap_queries = cap_sharp + cap_flat (the
 // size of OdomArgs::eng_part's per-chain rows).
 int engine_items(int cap_queries);
+// Rows per chain of OdomArgs::eng_part: the items' and the stolen overflow queries' (lislam_odometry.hip).
+int engine_part_rows(int cap_queries);
 void launch_factors(const FactorArgs& a, hipStream_t st);
 
 // AutoDiffCostFunction<F, R, 4, 3>::Evaluate of the functors of lidarFeaturePointsFunction.hpp:

@@ -1328,10 +1328,12 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
   }
 }
 
-// Developer profile of the engine (null in production): per ticket 8 u64 = s_memrealtime (100
-// MHz) at claim, inputs ready, records loaded (solve), done; summed evaluation and step ticks and
-// the evaluation count (solve).  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
+// Developer profile of the engine (null in production): per ticket kProfSlots u64 = s_memrealtime
+// (100 MHz) at claim, inputs ready, records loaded (solve), done; summed evaluation and step ticks and
+// the evaluation count (solve); items: 8 / 9 an overflow query's claim and end (eng_steal), 10 the
+// end of the item's last own query.  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
 // lislam_debug_engine_prof_read copies it out.
+constexpr int kProfSlots = 16;
 __device__ unsigned long long* g_eng_prof = nullptr;
 __device__ unsigned g_eng_prof_n = 0;  // tickets the buffer holds (writes past it are dropped)
 static unsigned long long* s_eng_prof = nullptr;
@@ -1341,8 +1343,8 @@ extern "C" int lislam_debug_engine_prof(int n_tickets) {
   s_eng_prof_n = 0;
   unsigned long long* d = nullptr;
   if (n_tickets > 0) {
-    if (hipMalloc((void**)&d, sizeof(unsigned long long) * 8 * n_tickets) != hipSuccess) return -2;
-    if (hipMemset(d, 0, sizeof(unsigned long long) * 8 * n_tickets) != hipSuccess) return -2;
+    if (hipMalloc((void**)&d, sizeof(unsigned long long) * kProfSlots * n_tickets) != hipSuccess) return -2;
+    if (hipMemset(d, 0, sizeof(unsigned long long) * kProfSlots * n_tickets) != hipSuccess) return -2;
     s_eng_prof = d;
     s_eng_prof_n = n_tickets;
   }
@@ -1353,7 +1355,7 @@ extern "C" int lislam_debug_engine_prof(int n_tickets) {
 extern "C" int lislam_debug_engine_prof_read(unsigned long long* out, int n_tickets) {
   if (!s_eng_prof || n_tickets > s_eng_prof_n) return -1;
   if (hipDeviceSynchronize() != hipSuccess) return -2;
-  return hipMemcpy(out, s_eng_prof, sizeof(unsigned long long) * 8 * n_tickets, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+  return hipMemcpy(out, s_eng_prof, sizeof(unsigned long long) * kProfSlots * n_tickets, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
 // LISLAM_ENG_PROF = 0 compiles the engine's developer timestamps out (rt_now() = 0, eng_prof a no-op).
 #ifndef LISLAM_ENG_PROF
@@ -1363,8 +1365,9 @@ __device__ __forceinline__ void eng_prof(unsigned tk, int slot, unsigned long lo
 #if LISLAM_ENG_PROF
   unsigned long long* p = g_eng_prof;
   if (!p || tk >= g_eng_prof_n) return;
-  if (add) p[(size_t)tk * 8 + slot] += v;
-  else p[(size_t)tk * 8 + slot] = v;
+  if (add) p[(size_t)tk * kProfSlots + slot] += v;
+  else if (slot == 10) atomicMax(p + (size_t)tk * kProfSlots + slot, v);  // the item's last own query
+  else p[(size_t)tk * kProfSlots + slot] = v;
 #endif
 }
 __device__ __forceinline__ unsigned long long rt_now() {
@@ -1410,7 +1413,10 @@ extern "C" int lislam_debug_engine_qlog(int* dev_buf, int pair) {
 #endif
 constexpr int kEngThreads = LISLAM_ENG_THREADS;
 constexpr int kEngWaves = kEngThreads / 64;
-constexpr int kEngQ = kEngWaves;      // queries per association item: one per wave (64 lanes)
+// Queries per association item: one per wave (64 lanes), EngCtl::Q = the item workgroup's waves —
+// kEngWaves in the single-launch engine (items share its workgroup size), up to kMaxItemWaves in the
+// split engine's items kernel (LISLAM_ENGINE_ITEM_WAVES).
+constexpr int kMaxItemWaves = 16;
 // A block record: 64 B = four 16-B quads, written by the association wave of its query (lanes 0..3,
 // write-through) and read by the solve with 16-B loads:
 //   q0 c.x c.y c.z a.x (float) | q1 a.y a.z (float) kind (int) - | q2 u.x u.y (double) | q3 u.z (double) -
@@ -1454,6 +1460,7 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // cleared by a launch: lislam_batch_odometry_status reads and clears it), [4, 4 + C) lm_gen, then
 // assoc_done[C][2 R]
 constexpr int kMaxShareItems = 256;  // 16 threads x 8 loads per item row: 32 rows per round x 8
+constexpr int kMaxShareRows = 512;   // eng_part rows per chain: items 0 .. 255, stolen overflow queries 256 + o
 struct EngCtl {
   unsigned* w;
   int C, R, I;
@@ -1463,14 +1470,45 @@ struct EngCtl {
   int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at
                  // once, and at most kMaxShareItems (the solve sums the shares in one round of loads)
   unsigned gen;  // this launch's number: with the pass, the tag of a complete item row (eng_tag)
+  int P;         // rows per chain of eng_part (engine_part_rows)
+  int steal;     // overflow queries are claimed by the pass's waves one at a time (split engine)
+  int Q;         // queries per association item = the item workgroup's waves
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
   __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
+  __device__ unsigned* ovf(int c, int ro) const { return w + 4 + C + (size_t)2 * R * C + (size_t)c * 2 * R + ro; }
 };
 // Word 31 of an item's eng_part row once its records and share of pass ro are written.
 __device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
   return ((uint64_t)ctl.gen << 32) | (uint64_t)(unsigned)(ro + 1);
+}
+
+// Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
+__device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& ctl, int k) {
+  if (a.gate && !a.gate[k]) return 0;
+  return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + ctl.Q - 1) / ctl.Q, ctl.budget));
+}
+
+// A pass's association: ieff items of Q queries; when the pair holds more queries than that
+// (the items are capped by EngCtl::budget, what the resident workgroups hold), the novf overflow
+// queries Q ieff + o are either claimed one at a time by whichever waves of the pass finish
+// first (steal: each is a row of its own, kMaxShareItems + o) or taken by the items in further rounds.
+struct PassShape {
+  int ieff, novf, rows;
+  bool steal;
+};
+__device__ __forceinline__ PassShape pass_shape(const OdomArgs& a, const EngCtl& ctl, int k) {
+  PassShape ps;
+  ps.ieff = eng_live_items(a, ctl, k);
+  const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
+  ps.novf = ps.ieff > 0 ? uni(max(0, nq - ctl.Q * ps.ieff)) : 0;
+  ps.steal = ctl.steal && ps.novf <= kMaxShareRows - kMaxShareItems;
+  ps.rows = ps.ieff;  // the items' rows; a stealing pass's overflow rows are kMaxShareItems + o, o < novf
+  return ps;
+}
+__device__ __forceinline__ double* part_row(const OdomArgs& a, const EngCtl& ctl, int c, int row) {
+  return a.eng_part + ((size_t)c * ctl.P + row) * 32;
 }
 
 // Developer trace of the engine (null in production): per workgroup {ticket, stage, LM passes,
@@ -1508,12 +1546,16 @@ __device__ __forceinline__ void eng_trace(int slot, unsigned v) {
 // workgroup's abort).  An expired bound raises this launch's abort word and the sticky one.
 // Arguments by value: a struct passed by reference would live in scratch, and values loaded from
 // scratch count as divergent, which would put the ticket loop's barriers in divergent control flow.
-__device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w, unsigned long long bound) {
+// code: which wait (EngCtl word 2 when its bound expires): 1 an item for the previous pass's items,
+// 2 an item for x, 3 a solve role for its pass's items.
+__device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w, unsigned long long bound,
+                                      unsigned code) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (ld_rlx(p) >= target) return true;
     if (ld_rlx(abort_w)) return false;
     if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {  // 100 MHz clock
+      st_rlx(abort_w + 1, code);  // the error word
       st_rlx(abort_w, 1u);
       st_rlx(abort_w + 2, 1u);  // sticky (EngCtl word 3)
       return false;
@@ -1524,14 +1566,16 @@ __device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* ab
 
 struct EngShared {
   double red[kEngWaves * 4][32];  // kAcc sums (+ 2 counts) per 16-lane row
-  double xw[kEngWaves][8];        // each wave's copy of its item's x (the item's queries read it here)
-  P4 prew[kEngWaves][4];          // each wave's ItemPre of its first query: qp, the seeds' points
-  int prei[kEngWaves][4];         // ... and the seeds' indices
+  double sred[kMaxItemWaves][30];  // each wave's share of the overflow query it stole (eng_steal)
+  double xw[kMaxItemWaves][8];     // each wave's copy of its item's x (the item's queries read it here)
+  P4 prew[kMaxItemWaves][4];       // each wave's ItemPre of its first query: qp, the seeds' points
+  int prei[kMaxItemWaves][4];      // ... and the seeds' indices
   double acc[kAcc];
   double x[7];
   double cx[7], cpw[7];  // solve role: the chain's x (para_q / para_t) and pose between passes
   int cnt[kEngWaves][2];
   unsigned ticket;
+  int ovc;  // eng_steal: the item's overflow queries claimed so far
   int flag, flag0, nc, np, pref;
   unsigned sink;
 };
@@ -1666,13 +1710,13 @@ __device__ __forceinline__ void eng_rt_x(const double* xs, double (&R)[9], D3& t
 __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& t) { eng_rt_x(sh.x, R, t); }
 
 // One association item, one query per wave (the 64-lane searches nn_wave / line_search: every round
-// trip looks at 64 candidates): query item * kEngQ + wave of pair k, at the pass's x (each wave's
+// trip looks at 64 candidates): query item * Q + wave of pair k, at the pass's x (each wave's
 // own copy).  Faster than four 16-lane rows per wave when one chain's ~2000 queries are all the
 // GPU runs (latency bound: 16.5 vs 34.9 us per round as separate launches).  The record goes out
 // write-through; the wave's share of the solve's first evaluation (its block's 28 sums at x and
 // the corner / plane counts) goes to sh.red[wave].
 __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int k, int w, Rsrc rec, int* warm, int outer,
-                                          unsigned tk, const ItemPre& pre, const double (&x)[7]) {
+                                          unsigned tk, const ItemPre& pre, const double (&x)[7], double* row) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id();
   const int ns = a.n_feat[k * 4 + 0];
@@ -1790,7 +1834,6 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
     eng_rt_x(x, R, t);
     eng_block(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, sb);
     if (lane == 0) {
-      double* row = sh.red[threadIdx.x >> 6];
 #pragma unroll
       for (int e = 0; e < kAcc; e++) row[e] += sb[e];
       row[28 + kind] += 1.0;
@@ -1798,18 +1841,84 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   }
 }
 
-// One association item: wave wv of item `item` takes queries (item + m ieff) kEngQ + wv, m = 0,
+// A bounds check of the engine's own index arithmetic (the rows it publishes, the records it
+// writes): a violation raises this launch's abort (and the sticky word) with `code` in the error
+// word instead of faulting, so the host re-runs the launch on the per-round schedule and the code
+// says which check fired.  Wave-uniform operands only.
+__device__ __forceinline__ bool eng_check(const EngCtl& ctl, bool ok, unsigned code) {
+  if (ok) return true;
+  if (lane_id() == 0) {
+    st_rlx(ctl.w + 2, code);
+    st_rlx(ctl.abort_w(), 1u);
+    st_rlx(ctl.w + 3, 1u);
+  }
+  return false;
+}
+
+// Every wave of a pass's live items, right after its own query: take the item's overflow queries
+// Q ieff + o, o = item, item + ieff, ... (< novf) one at a time, and publish each as row
+// kMaxShareItems + o (its record, seeds and share, then the row's tag).  The item's waves claim
+// them through an LDS counter, so the item's first waves to finish run them — the pass does not
+// wait for a second round of some items, and no global word is contended (a device-wide counter
+// read by every wave of the pass serialized ~2,000 requests on one line: 46.7 vs 27.5 ms, r05d).
+// The claim is one LDS atomic from the whole wave (lane 0 adds 1, the others 0) — no single-lane
+// branch anywhere in the loop: a loop opening with one can be rotated so that lane 0 runs the body
+// apart from the other lanes, and the searches' wave-wide ballots / permutes then see a partial
+// wave (the hang of the first version).
+__device__ __forceinline__ void eng_steal(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int c, int k, int ro,
+                                          int item, const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk,
+                                          const double (&x)[7]) {
+  const int ql = (int)(threadIdx.x >> 6), lane = lane_id();
+  auto claim = [&]() -> int {
+    const int j = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(&sh.ovc, lane == 0 ? 1 : 0, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
+    return item + j * ps.ieff;
+  };
+  const int e30 = lane < 30 ? lane : 29;  // no single-lane branches in this loop (lanes >= 30 repeat 29)
+  for (int ov = claim(); ov < ps.novf; ov = claim()) {
+    if (lane == 0) eng_prof(tk, 8, rt_now());
+    const int w = ctl.Q * ps.ieff + ov;
+    const int row_i = kMaxShareItems + ov;
+    if (!eng_check(ctl, w < a.cap_sharp + a.cap_flat && row_i < ctl.P, 0x5700u + (unsigned)min(ov, 255))) return;
+    sh.sred[ql][e30] = 0.0;
+#ifndef LISLAM_STEAL_NOQUERY
+    const ItemPre pre = eng_item_pre(a, k, w, warm, outer);
+    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.sred[ql]);
+#else  // developer bisect: no search, but a well-formed empty record (kind -1) and no seeds
+    {
+      const v4u q1 = v4u{0u, 0u, 0xffffffffu, 0u};
+      if (lane == 1) __builtin_amdgcn_raw_buffer_store_b128(q1, rec, w * kRecBytes + 16, 0, kAuxSc1);
+      if (outer == 0 && lane < 3)
+        __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's adds before the lanes' reads
+    __builtin_amdgcn_wave_barrier();
+    double* row = part_row(a, ctl, c, row_i);
+    st_sc1d(row + e30, sh.sred[ql][e30]);
+    drain_stores();  // the record, the seeds and the row
+    st_sc1(reinterpret_cast<uint64_t*>(row) + 31, eng_tag(ctl, ro));  // every lane, the same word
+    if (lane == 0) eng_prof(tk, 9, rt_now());
+  }
+}
+
+// One association item: wave wv of item `item` takes queries (item + m ieff) Q + wv, m = 0,
 // 1, ...: one each while the pair's queries fit ieff items (the common case), more when the pair
 // holds more queries than the engine keeps items in flight (EngCtl::budget), so that no item
-// waits for a workgroup to come free.  The wave's share of the first evaluation (its blocks' 28
-// sums at x, and the corner / plane counts) goes to sh.red[wave].
-__device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, int k, int item, int ieff, Rsrc rec,
-                                             int* warm, int outer, unsigned tk) {
+// waits for a workgroup to come free — or, when the pass steals (PassShape::steal), one each and
+// then the overflow queries as each wave comes free (eng_steal).  The wave's share of the first
+// evaluation (its blocks' 28 sums at x, and the corner / plane counts) goes to sh.red[wave].
+__device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int c, int k, int ro,
+                                             int item, const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk) {
   const int ql = (int)(threadIdx.x >> 6);
+  const int ieff = ps.ieff;
   const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
   if (lane_id() < 30) sh.red[ql][lane_id()] = 0.0;
-  for (int m = 0;; m++) {
-    const int w = (item + m * ieff) * kEngQ + ql;
+  double x[7];
+#pragma unroll
+  for (int e = 0; e < 7; e++) x[e] = sh.xw[ql][e];
+  for (int m = 0; m == 0 || !ps.steal; m++) {  // steal: the overflow queries go to eng_steal instead
+    const int w = (item + m * ieff) * ctl.Q + ql;
     if (w >= nq) break;  // wave-uniform
     ItemPre pre;
     if (m > 0) {
@@ -1819,11 +1928,12 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, EngShared& sh, i
 #pragma unroll
       for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][1 + e]; pre.wi[e] = sh.prei[ql][e]; }
     }
-    double x[7];
-#pragma unroll
-    for (int e = 0; e < 7; e++) x[e] = sh.xw[ql][e];
-    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x);
+    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
   }
+  if (lane_id() == 0) eng_prof(tk, 10, rt_now());
+#ifndef LISLAM_STEAL_NOCALL
+  if (ps.steal && item < ps.novf) eng_steal(a, ctl, sh, c, k, ro, item, ps, rec, warm, outer, tk, x);
+#endif
 }
 
 // The 28 sums of every thread -> sh.acc in lislam_lm.hpp's layout (cost, H upper, g).  Inside each
@@ -2359,11 +2469,6 @@ __device__ __forceinline__ void eng_gather_rows(EngShared& sh, double (&acc)[kAc
   for (int e = 0; e < kAcc; e++) acc[e] = sh.acc[e];
 }
 
-// Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
-__device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& ctl, int k) {
-  if (a.gate && !a.gate[k]) return 0;
-  return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + kEngQ - 1) / kEngQ, ctl.budget));
-}
 
 // ---- the solve role: one workgroup per chain, for the whole chain
 // Pass ro = 2 r + o of chain c (pair k): gather its association items' records and shares of the
@@ -2378,29 +2483,38 @@ __device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& c
 // Bulk (k_odom_chain): wait for every item (the assoc_done count), then load everything.
 // Both sum the shares in the same fixed tree: the results are identical.
 constexpr int kShareQuads = 15;  // doubles 0..29 of an item's row: 28 sums + 2 counts
+// quads per evaluating thread (gather_fill: quad Q = tp + kEvalThreads i)
+constexpr int kQuadRounds = (kMaxShareItems * kShareQuads + kEvalThreads - 1) / kEvalThreads;
 struct EngGather {
-  v4u shr[kMaxShareItems * kShareQuads];  // the items' rows, packed: quad q of item i at i * 15 + q
-  unsigned ready[kMaxShareItems];         // ro + 1 once item i's row of pass ro is complete
+  // the items' rows, packed: quad q of row i at i * 15 + q; sized to whole rounds of the evaluating
+  // waves, so every wave's LDS-DMA base lies inside it, and kept below 64 KiB of LDS (RolesLds puts it
+  // first): the DMA's M0 base is taken as 16 bits, as ds_write_addtid's is
+  v4u shr[kQuadRounds * kEvalThreads];
+  unsigned ready[kMaxShareRows];         // ro + 1 once row i of pass ro is complete (items', then overflow rows)
   int abort;
+  int all;  // wave 0 has seen every row of the pass (gather_fill then defers the last records)
 };
 
 // Wave 0: poll the tags of the pass's ieff items (lane l: items l, l + 64, ...) and publish each
 // complete one in gt.ready.  false = aborted (the bound expired here, or another workgroup's abort).
-__device__ __forceinline__ bool gather_poll(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro, int ieff) {
+__device__ __forceinline__ bool gather_poll(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro,
+                                            const PassShape& ps) {
+  constexpr int kJ = kMaxShareRows / 64, kJI = kMaxShareItems / 64;
   const int lane = lane_id();
   const uint64_t want = eng_tag(ctl, ro);
-  const uint64_t* tags = reinterpret_cast<const uint64_t*>(a.eng_part + (size_t)c * ctl.I * 32) + 31;
-  unsigned pend = 0u;
+  const uint64_t* tags = reinterpret_cast<const uint64_t*>(part_row(a, ctl, c, 0)) + 31;
+  const int nov = ps.steal ? ps.novf : 0;
+  unsigned pend = 0u;  // bit j: row lane + 64 j (items for j < kJI, then the overflow rows kMaxShareItems + ...)
 #pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (lane + 64 * j < ieff) pend |= 1u << j;
+  for (int j = 0; j < kJ; j++)
+    if (j < kJI ? lane + 64 * j < ps.ieff : lane + 64 * (j - kJI) < nov) pend |= 1u << j;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    uint64_t v[4];
+    uint64_t v[kJ];
 #pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = ((pend >> j) & 1u) ? ld_sc1(tags + (size_t)(lane + 64 * j) * 32) : 0ull;
+    for (int j = 0; j < kJ; j++) v[j] = ((pend >> j) & 1u) ? ld_sc1(tags + (size_t)(lane + 64 * j) * 32) : 0ull;
 #pragma unroll
-    for (int j = 0; j < 4; j++)
+    for (int j = 0; j < kJ; j++)
       if (((pend >> j) & 1u) && v[j] == want) {
         __hip_atomic_store(&gt.ready[lane + 64 * j], (unsigned)(ro + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         pend &= ~(1u << j);
@@ -2410,6 +2524,7 @@ __device__ __forceinline__ bool gather_poll(const OdomArgs& a, const EngCtl& ctl
     if (__builtin_amdgcn_s_memrealtime() - t0 > ctl.wait_ticks) {
       if (lane == 0) {
         st_rlx(ctl.abort_w(), 1u);
+        st_rlx(ctl.abort_w() + 1, 4u);  // error word: the progressive gather's poll
         st_rlx(ctl.abort_w() + 2, 1u);  // sticky (EngCtl word 3)
       }
       stop = true;
@@ -2430,15 +2545,18 @@ __device__ __forceinline__ void blk_absent(BlkReg& b) {
 }
 
 // Waves 1..: as gather_poll marks items complete, load their records into this thread's slots and
-// their share quads (quad Q = tp + 448 i of the packed rows) into gt.shr; returns once every load
-// is issued and landed (or on abort).
-__device__ __forceinline__ void gather_fill(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro, int ieff,
-                                            Rsrc rec, int ns, int nf, int tp, EvalSlots& S) {
-  const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
+// their share quads (quad Q = tp + 448 i of the packed rows) into gt.shr; returns once every share
+// quad is issued and landed (or on abort).  Once wave 0 has seen every row (gt.all) the records not
+// loaded yet are left out (the returned bits: bit k edge slot k, bit kEdgeSlots + k plane slot k):
+// step 0 needs only the shares, so gather_records loads those last records while wave 0 steps.
+__device__ __forceinline__ unsigned gather_fill(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro,
+                                            const PassShape& ps, Rsrc rec, int ns, int nf, int tp, EvalSlots& S) {
+  const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
   const unsigned pass = (unsigned)(ro + 1);
-  const int nquad = ieff * kShareQuads;
+  const int ieff = ps.ieff;
+  const int nquad = ps.rows * kShareQuads;
   const int wbase = uni(tp & ~63);  // this wave's first tp
-  unsigned pend = 0u;  // bits 0..1 edge slots, 2..5 plane slots, 6..14 share quads
+  unsigned pend = 0u;  // bits 0..1 edge slots, 2..5 plane slots, 6.. share quads
 #pragma unroll
   for (int k = 0; k < kEdgeSlots; k++) {
     blk_absent(S.e[k]);
@@ -2449,34 +2567,44 @@ __device__ __forceinline__ void gather_fill(const OdomArgs& a, const EngCtl& ctl
     blk_absent(S.p[k]);
     if (tp + k * kEvalThreads < nf) pend |= 1u << (kEdgeSlots + k);
   }
-  constexpr int kQ0 = kEdgeSlots + kPlaneSlots, kQuadRounds = (kMaxShareItems * kShareQuads + kEvalThreads - 1) / kEvalThreads;
+  constexpr int kQ0 = kEdgeSlots + kPlaneSlots;
+  static_assert(kQ0 + kQuadRounds <= 32, "pending bits");
+  static_assert(kQuadRounds * kEvalThreads * 16 <= 65536, "the DMA's LDS addresses below 64 KiB");
 #pragma unroll
   for (int i = 0; i < kQuadRounds; i++)
     if (tp + i * kEvalThreads < nquad) pend |= 1u << (kQ0 + i);
   auto ready = [&](int item) {
     return __hip_atomic_load(&gt.ready[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == pass;
   };
+  auto row_of = [&](int w) {  // the row whose tag covers query w's record
+    return w < ctl.Q * ieff ? w / ctl.Q : ps.steal ? kMaxShareItems + (w - ctl.Q * ieff) : (w / ctl.Q) % ieff;
+  };
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__ballot(pend != 0u) != 0ull) {
+  constexpr unsigned kRecBits = (1u << kQ0) - 1u;
+  while (__ballot((pend & ~kRecBits) != 0u) != 0ull) {  // share quads pending
+    const bool all = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&gt.all, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+    if (!all) {  // records of the rows complete so far (the rest wait for gather_records)
 #pragma unroll
-    for (int k = 0; k < kEdgeSlots; k++) {
-      const int w = tp + k * kEvalThreads;
-      if (((pend >> k) & 1u) && ready((w / kEngQ) % ieff)) {
-        rec_load(rec, w, true, S.e[k]);
-        pend &= ~(1u << k);
+      for (int k = 0; k < kEdgeSlots; k++) {
+        const int w = tp + k * kEvalThreads;
+        if (((pend >> k) & 1u) && ready(row_of(w))) {
+          rec_load(rec, w, true, S.e[k]);
+          pend &= ~(1u << k);
+        }
       }
-    }
 #pragma unroll
-    for (int k = 0; k < kPlaneSlots; k++) {
-      const int w = ns + tp + k * kEvalThreads;
-      if (((pend >> (kEdgeSlots + k)) & 1u) && ready((w / kEngQ) % ieff)) {
-        rec_load(rec, w, true, S.p[k]);
-        pend &= ~(1u << (kEdgeSlots + k));
+      for (int k = 0; k < kPlaneSlots; k++) {
+        const int w = ns + tp + k * kEvalThreads;
+        if (((pend >> (kEdgeSlots + k)) & 1u) && ready(row_of(w))) {
+          rec_load(rec, w, true, S.p[k]);
+          pend &= ~(1u << (kEdgeSlots + k));
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < kQuadRounds; i++) {
       const int Q = tp + i * kEvalThreads, item = Q / kShareQuads;
+      if (!uni(wbase + i * kEvalThreads < nquad)) continue;  // no lane of this wave has a quad in round i
       if (((pend >> (kQ0 + i)) & 1u) && ready(item)) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(parts, (__attribute__((address_space(3))) void*)&gt.shr[wbase + i * kEvalThreads], 16,
                                                  item * 256 + (Q - item * kShareQuads) * 16, 0, 0, kAuxSc1);
@@ -2486,6 +2614,7 @@ __device__ __forceinline__ void gather_fill(const OdomArgs& a, const EngCtl& ctl
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&gt.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * ctl.wait_ticks) {  // never expected: wave 0's bound is half
       if (lane_id() == 0) {
+        st_rlx(ctl.abort_w() + 1, 5u);
         st_rlx(ctl.abort_w(), 1u);
         st_rlx(ctl.abort_w() + 2, 1u);
       }
@@ -2495,43 +2624,90 @@ __device__ __forceinline__ void gather_fill(const OdomArgs& a, const EngCtl& ctl
   }
   S.tail = __ballot(tp + kEvalThreads < ns || tp + 3 * kEvalThreads < nf) != 0ull;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS writes have landed (and the records)
+  return pend & kRecBits;
+}
+
+// The records gather_fill left out (every row is complete by now), landed on return.
+__device__ __forceinline__ void gather_records(Rsrc rec, int ns, int tp, unsigned pend, EvalSlots& S) {
+#pragma unroll
+  for (int k = 0; k < kEdgeSlots; k++)
+    if ((pend >> k) & 1u) rec_load(rec, tp + k * kEvalThreads, true, S.e[k]);
+#pragma unroll
+  for (int k = 0; k < kPlaneSlots; k++)
+    if ((pend >> (kEdgeSlots + k)) & 1u) rec_load(rec, ns + tp + k * kEvalThreads, true, S.p[k]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <bool kProg>
 __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, EngGather* gt,
-                                               int c, int k, int ro, int ieff, Rsrc rec, bool wave0, unsigned tk) {
+                                               int c, int k, int ro, const PassShape& ps, Rsrc rec, bool wave0, unsigned tk) {
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const int lane = lane_id();
   const int tp = (int)threadIdx.x - 64;
+  const int ieff = ps.ieff;
   EvalSlots S;
-  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;  // share quad q of items g, g + 32, ..., g + 224
-  double d0[8], d1[8];
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;  // share quad q of rows g, g + 32, ..., g + 224 (+ 256 ..)
+  double d0[8], d1[8], e0 = 0.0, e1 = 0.0;
+  unsigned recpend = 0u;  // records gather_fill left for gather_records
+  // the stolen overflow queries' rows (complete once their pass is), straight from memory: their own
+  // pairwise tree over rows g + 32 j, added last
+  auto overflow_rows = [&](double& u0, double& u1) {
+    const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
+    v4u v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int o = g + 32 * j;
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(parts, (kMaxShareItems + (o < ps.novf ? o : 0)) * 256 + q * 16, 0, kAuxSc1);
+    }
+    double f0[8], f1[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const bool ok = g + 32 * j < ps.novf && q < kShareQuads;
+      f0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].y << 32) | v[j].x)) : 0.0;
+      f1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z)) : 0.0;
+    }
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+      for (int j = 0; j + h < 8; j += 2 * h) { f0[j] += f0[j + h]; f1[j] += f1[j + h]; }
+    u0 = f0[0];
+    u1 = f1[0];
+  };
   if constexpr (kProg) {
-    if (ieff > 0) {
+    if (ps.ieff > 0) {
       if (wave0) {
         eng_prof(tk, 1, rt_now());
-        const bool ok = gather_poll(a, ctl, *gt, c, ro, ieff);
-        if (lane == 0) sh.flag0 = ok;
+        const bool ok = gather_poll(a, ctl, *gt, c, ro, ps);
+        if (lane == 0) {
+          sh.flag0 = ok;
+          __hip_atomic_store(&gt->all, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // after the ready flags
+        }
         eng_prof(tk, 1, rt_now());
       } else {
-        gather_fill(a, ctl, *gt, c, ro, ieff, rec, ns, nf, tp, S);
+        recpend = gather_fill(a, ctl, *gt, c, ro, ps, rec, ns, nf, tp, S);
       }
     } else if (wave0 && lane == 0) {
       sh.flag0 = 1;
     }
     __syncthreads();
+    if (wave0 && lane == 0) __hip_atomic_store(&gt->all, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // next pass
     if (!uni(sh.flag0)) return false;
+    auto rows8 = [&](int r0, double (&u0)[8], double (&u1)[8]) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int it = g + 32 * j;
-      const bool ok = it < ieff && q < kShareQuads;
-      const v4u v = gt->shr[ok ? it * kShareQuads + q : 0];
-      d0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x)) : 0.0;
-      d1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z)) : 0.0;
-    }
+      for (int j = 0; j < 8; j++) {
+        const int it = r0 + g + 32 * j;
+        const bool ok = it < ps.rows && q < kShareQuads;
+        const v4u v = gt->shr[ok ? it * kShareQuads + q : 0];
+        u0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x)) : 0.0;
+        u1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z)) : 0.0;
+      }
+    };
+    if (ps.steal && ps.novf > 0) overflow_rows(e0, e1);
+    rows8(0, d0, d1);
   } else {
-    if (!wave0 && ieff > 0) eval_slots_load(rec, ns, nf, tp, S);  // in flight with the shares
-    const Rsrc parts = make_rsrc(a.eng_part + (size_t)c * ctl.I * 32, (unsigned)(ctl.I * 256));
+    // the items' rows (the records follow while wave 0 takes step 0: it needs only the shares)
+    if (ps.steal && ps.novf > 0) overflow_rows(e0, e1);
+    const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
     v4u v[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
@@ -2545,12 +2721,12 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
       d1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z)) : 0.0;
     }
   }
-  {  // the items' shares: pairwise tree over items g + 32 j, then (wave 0) over the 32 rows
+  {  // the rows' shares: pairwise tree over rows g + 32 j, then (wave 0) over the 32 sums
 #pragma unroll
     for (int h = 1; h < 8; h <<= 1)
 #pragma unroll
       for (int j = 0; j + h < 8; j += 2 * h) { d0[j] += d0[j + h]; d1[j] += d1[j + h]; }
-    if (q < kShareQuads) { sh.red[g][2 * q] = d0[0]; sh.red[g][2 * q + 1] = d1[0]; }
+    if (q < kShareQuads) { sh.red[g][2 * q] = d0[0] + e0; sh.red[g][2 * q + 1] = d1[0] + e1; }
   }
   __syncthreads();
   LdsLM& s = *(LdsLM*)&lm;
@@ -2620,6 +2796,9 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
       more = uni(sh.flag) != 0;
     }
   } else {
+    // the records not loaded yet, while wave 0 takes step 0
+    if constexpr (kProg) gather_records(rec, ns, tp, recpend, S);
+    else if (ieff > 0) eval_slots_load(rec, ns, nf, tp, S);
     __syncthreads();
     bool more = uni(sh.flag) != 0;
     while (more) {
@@ -2639,8 +2818,8 @@ __device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& 
                                                int c, bool wave0, unsigned tk) {
   const int lane = lane_id();
   if constexpr (kProg) {
-    for (int i = threadIdx.x; i < kMaxShareItems; i += kEngThreads) gt->ready[i] = 0u;
-    if (threadIdx.x == 0) gt->abort = 0;
+    for (int i = threadIdx.x; i < kMaxShareRows; i += kEngThreads) gt->ready[i] = 0u;
+    if (threadIdx.x == 0) { gt->abort = 0; gt->all = 0; }
     __syncthreads();
   }
   const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
@@ -2658,18 +2837,19 @@ __device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& 
     const int r = ro >> 1, o = ro & 1;
     int k;
     if (!pair_of(a, c, r, &k)) break;  // uniform: this chain is shorter
-    const int ieff = eng_live_items(a, ctl, k);
+    const PassShape ps = pass_shape(a, ctl, k);
+    const int ieff = ps.ieff;
     const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1)) + tk;  // profile slot of the pass (developer builds)
     if constexpr (!kProg) {
       if (wave0 && lane == 0) {
         eng_prof(ptk, 1, rt_now());
-        sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : 1;
+        sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 3u) : 1;
         eng_prof(ptk, 1, rt_now());
       }
       __syncthreads();
       if (!uni(sh.flag0)) return false;
     }
-    if (!eng_solve_pass<kProg>(a, ctl, sh, lm, gt, c, k, ro, ieff, rec, wave0, ptk)) return false;
+    if (!eng_solve_pass<kProg>(a, ctl, sh, lm, gt, c, k, ro, ps, rec, wave0, ptk)) return false;
     if (wave0 && lane == 0) {
       const int nc = sh.nc, np = sh.np;
       int* so = a.stats + (size_t)k * 8;
@@ -2767,8 +2947,10 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   if (wave0 && lead) eng_prof(ptk, 0, rt_now());
   int k;
   bool live = pair_of(a, c, r, &k);
-  // items holding queries of pair k: ceil((sharp + flat) / kEngQ), none for a gated-off scan
-  const int ieff = live ? eng_live_items(a, ctl, k) : 0;
+  // items holding queries of pair k: ceil((sharp + flat) / Q), none for a gated-off scan
+  PassShape ps{0, 0, 0, false};
+  if (live) ps = pass_shape(a, ctl, k);
+  const int ieff = ps.ieff;
   if (item >= ieff) live = false;  // an empty item: nothing to wait for or signal
   const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
   const Rsrc rec = make_rsrc(a.blk + (size_t)c * rec_stride, (unsigned)((a.cap_sharp + a.cap_flat) * kRecBytes));
@@ -2776,12 +2958,15 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   // An item of the second outer pass first waits for the first pass's items (its seeds), long
   // done in the common case; then every wave loads what needs no x while the lead waits for x.
   if (wave0) {
-    if (lead) sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks) : true;
+    if (lead) {
+      sh.ovc = 0;
+      sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 1u) : true;
+    }
   }
   __syncthreads();
   ok = uni(sh.flag0) != 0;
   if (ok && live) {  // each wave parks its first query's loads in its LDS slots
-    const ItemPre pre = eng_item_pre(a, k, item * kEngQ + (int)(threadIdx.x >> 6), warm, o);
+    const ItemPre pre = eng_item_pre(a, k, item * ctl.Q + (int)(threadIdx.x >> 6), warm, o);
     const int wv = (int)(threadIdx.x >> 6), l = lane_id();
     P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
     int wi = pre.wi[0];
@@ -2791,12 +2976,12 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
     if (l < 4) sh.prew[wv][l] = v;
     if (l < 3) sh.prei[wv][l] = wi;
   }
-  if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, kEngThreads - 64);
+  if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, (int)blockDim.x - 64);
   if (wave0) {
     if (lead) {
       if (ok && live) {
         eng_prof(ptk, 2, rt_now());  // the item's lead starts its wait for x
-        ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks);
+        ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks, 2u);
         eng_trace(1, ok ? 2u : 99u);
         eng_prof(ptk, 1, rt_now());
       }
@@ -2810,7 +2995,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
       const int l = lane_id();
       if (l < 7) sh.xw[threadIdx.x >> 6][l] = eng_x_word(a, c, r, o, l);
     }
-    eng_item_run(a, sh, k, item, ieff, rec, warm, o, ptk);
+    eng_item_run(a, ctl, sh, c, k, ro, item, ps, rec, warm, o, ptk);
     drain_stores();  // this wave's record (and seed) stores
     __syncthreads();
     if (wave0) {
@@ -2818,13 +3003,13 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
       if (lane_id() < 30) {  // the item's share: the sum of its waves' shares
         double v = 0.0;
 #pragma unroll
-        for (int w = 0; w < kEngWaves; w++) v += sh.red[w][lane_id()];
-        st_sc1d(a.eng_part + ((size_t)c * ctl.I + item) * 32 + lane_id(), v);
+        for (int w = 0; w < ctl.Q; w++) v += sh.red[w][lane_id()];
+        st_sc1d(part_row(a, ctl, c, item) + lane_id(), v);
       }
       drain_stores();
       if (lead) {
         eng_prof(ptk, 7, rt_now() - tp0);
-        st_sc1(reinterpret_cast<uint64_t*>(a.eng_part + ((size_t)c * ctl.I + item) * 32) + 31, eng_tag(ctl, ro));  // row complete
+        st_sc1(reinterpret_cast<uint64_t*>(part_row(a, ctl, c, item)) + 31, eng_tag(ctl, ro));  // row complete
         add_rlx(ctl.assoc_done(c, ro), 1u);
         eng_trace(1, 4u);
         eng_prof(ptk, 3, rt_now());
@@ -2887,16 +3072,28 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
 // roles on one reserved CU per XCD, the items on the others.  An item workgroup then leaves half
 // of its CU's registers and most of its LDS to whatever else runs (the next batch's extraction,
 // the ORB front end), and the roles always find a CU (launch_odometry_chain).
+// The roles' gather: 1 = progressive (wave 0 polls every row's tag, waves 1.. load each complete
+// row as it lands), 0 = bulk (wait for the pass's item count, then load every row at once).
+#ifndef LISLAM_ENG_PROG
+#define LISLAM_ENG_PROG 0
+#endif
+struct RolesLds {  // EngGather first: its DMA addresses stay below 64 KiB
+  EngGather gt;
+  EngShared sh;
+  EngLM lm;
+};
+
 __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
-  __shared__ EngShared sh;
-  __shared__ EngLM lm;
-  __shared__ EngGather gt;
+  __shared__ RolesLds L;
+  EngShared& sh = L.sh;
+  EngLM& lm = L.lm;
+  EngGather& gt = L.gt;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
   const int c = (int)blockIdx.x;
-  (void)eng_solve_role<true>(a, ctl, sh, lm, &gt, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+  (void)eng_solve_role<LISLAM_ENG_PROG != 0>(a, ctl, sh, lm, &gt, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
 }
 
-__global__ __launch_bounds__(kEngThreads, 4) void k_odom_items(OdomArgs a, EngCtl ctl) {
+__global__ __launch_bounds__(64 * kMaxItemWaves, 4) void k_odom_items(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
@@ -2924,14 +3121,26 @@ __global__ __launch_bounds__(kEngThreads, 4) void k_odom_items(OdomArgs a, EngCt
   }
 }
 
-extern "C" int lislam_debug_engine_items(int cap_queries) { return engine_items(cap_queries); }
+static int item_waves();
+// Items per (pass, chain) of the split engine (the developer profile's ticket layout).
+extern "C" int lislam_debug_engine_items(int cap_queries) { return (cap_queries + item_waves() - 1) / item_waves(); }
 // A number per engine launch (the item rows' tags tell this launch's passes from an earlier one's).
 static unsigned next_engine_gen() {
   static std::atomic<unsigned> gen{0};
   return ++gen;
 }
 
-int engine_items(int cap_queries) { return (cap_queries + kEngQ - 1) / kEngQ; }
+int engine_items(int cap_queries) { return (cap_queries + kEngWaves - 1) / kEngWaves; }  // rows: Q >= kEngWaves
+
+// Waves (= queries) per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (8 ..
+// kMaxItemWaves), default kDefaultItemWaves.
+constexpr int kDefaultItemWaves = 8;
+static int item_waves() {
+  const char* e = getenv("LISLAM_ENGINE_ITEM_WAVES");
+  const int q = e ? atoi(e) : kDefaultItemWaves;
+  return q >= kEngWaves && q <= kMaxItemWaves ? q : kDefaultItemWaves;
+}
+int engine_part_rows(int cap_queries) { return max(engine_items(cap_queries), kMaxShareRows); }
 
 bool use_chain_engine(const OdomArgs& a, int mode) {
   if (mode == 0 || a.n_chains < 1 || !a.eng_ctl) return false;
@@ -2955,12 +3164,15 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
   ctl.gen = next_engine_gen();
+  ctl.P = engine_part_rows(a.cap_sharp + a.cap_flat);
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
+  ctl.Q = kEngWaves;  // items run in the engine's own workgroups
   ctl.I = engine_items(a.cap_sharp + a.cap_flat);
   ctl.prefetch = 1;
   ctl.roles = ctl.C;
+  ctl.steal = 0;  // the bulk gather (k_odom_chain) reads the items' rows only
   // every device wait is bounded (2 s); LISLAM_ENGINE_WAIT_US shortens it (tests: a forced abort)
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
@@ -2974,7 +3186,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, (resident - ctl.C - 1) / ctl.C));
   // zero the control words of this launch, all but word 3 (the sticky abort)
-  const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
+  const size_t words = ((size_t)4 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
   (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
   // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)
@@ -3048,12 +3260,15 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
   ctl.gen = next_engine_gen();
+  ctl.P = engine_part_rows(a.cap_sharp + a.cap_flat);
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
-  ctl.I = engine_items(a.cap_sharp + a.cap_flat);
-  ctl.prefetch = 1;
+  ctl.Q = item_waves();
+  ctl.I = (a.cap_sharp + a.cap_flat + ctl.Q - 1) / ctl.Q;
+  ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
   ctl.roles = 0;
+  ctl.steal = getenv("LISLAM_ENGINE_STEAL") ? atoi(getenv("LISLAM_ENGINE_STEAL")) : 0;
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
   // One item workgroup per CU of the items' mask (all CUs but one per XCD): its 8 waves at <= 128
@@ -3070,7 +3285,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
-  const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;
+  const size_t words = ((size_t)4 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf
   EngineGate* gate = engine_gate(dev);
   std::unique_lock<std::mutex> lock;
   if (gate) {
@@ -3087,7 +3302,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(ctl.C), dim3(kEngThreads), 0, roles, a, ctl);
-  hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(kEngThreads), 0, items, a, ctl);
+  hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
   (void)hipEventRecord(join_r, roles);
   (void)hipEventRecord(join_i, items);
   (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do

@@ -230,6 +230,13 @@ class Batch:
                   "lislam_batch_odometry_engine")
         return int(k.value)
 
+    def odometry_abort_code(self) -> int:
+        """The error word of the last aborted engine launch (lislam_batch_odometry_abort_code)."""
+        k = ctypes.c_int32(0)
+        nat.check(self.ctx.lib.lislam_batch_odometry_abort_code(self.h, ctypes.byref(k)), self.ctx.h,
+                  "lislam_batch_odometry_abort_code")
+        return int(k.value)
+
     def skip_flags(self, n: int) -> np.ndarray:
         """use_aloam per scan from the ORB front end's results (intensity_odometry first): 1 where
         detectfeatures skipped the frame (the "skip_intensity" frame_id, scanRegistration.cpp:603-609)."""

@@ -45,10 +45,10 @@ with pkg.Context() as ctx:
     ctx.synchronize()
     nq = np.array([b.count(pkg.native.OUT_SHARP, k) + b.count(pkg.native.OUT_FLAT, k) for k in range(1, S)])
     sp = np.zeros(4, np.uint64)
-    buf = np.zeros((T, 8), np.uint64)
+    buf = np.zeros((T, 16), np.uint64)
     assert lib.lislam_debug_engine_prof_read(buf.ctypes.data, T) == 0
     lib.lislam_debug_engine_prof(0)
-    p = buf.reshape(2 * R, I + 1, 8).astype(np.int64)
+    p = buf.reshape(2 * R, I + 1, 16).astype(np.int64)
     us = 0.01
     items, lm = p[:, :I], p[:, I]
     valid = items[:, :, 3] > 0  # items that ran (all live ones)
@@ -107,6 +107,18 @@ with pkg.Context() as ctx:
               f"ready p50 {np.median(la[:, 2]):.1f}, run p50 {np.median(la[:, 3]):.1f}; item index p50 {np.median(la[:, 4]):.0f}")
         for row in la[np.argsort(-la[:, 2])][:8]:
             print("   late item: claim %.1f wait %.1f ready %.1f run %.1f item %d" % tuple(row))
+    # overflow queries taken by the items' first free waves (eng_steal): when the stealing wave
+    # claimed (its own query done), the stolen query's run, and the item's last own query
+    stl = items[:, :, 8] > 0
+    if stl.any():
+        rel = lambda col: np.concatenate([(items[i, stl[i], col] - a_start[i]) for i in range(2 * R)]) * us
+        rows["steal: claim after the pass's first ready"] = rel(8)
+        rows["steal: stolen query run (claim -> row published)"] = rel(9) - rel(8)
+        rows["steal: stealing item's last own query end (after first ready)"] = rel(10)
+        rows["steal: stolen rows per pass"] = stl.sum(1)
+        ok10 = valid & (items[:, :, 10] > 0)
+        rows["all items: last own query end (after first ready)"] = np.concatenate(
+            [(items[i, ok10[i], 10] - a_start[i]) for i in range(2 * R)]) * us
     for k, v in rows.items():
         print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")
     print(f"  evaluations per solve: mean {np.mean(npass):.2f}")

@@ -47,7 +47,8 @@ def test_pipelined_two_context_steps_match_the_oracle(pkg, sequences):
         worst = 0.0
         orb_pairs = 0
         for i, (b, (_, pose, rel, st, ost, oT)) in enumerate(zip(bats, sequences)):
-            assert b.odometry_status() == 0, i  # no engine launch gave up (none was re-run)
+            # no engine launch gave up (none was re-run): the error word names the wait if one did
+            assert b.odometry_status() == 0, (i, hex(b.odometry_abort_code()))
             snap = bench.snapshot_outputs(b, pkg, S, True)
             for k in range(1, S):
                 d = max(np.max(np.abs(snap["para"][k] - rel[k])), np.max(np.abs(snap["pose"][k] - pose[k])))
