@@ -459,14 +459,16 @@ int lislam_odom_fuse(lislam_odom_fuser* f, const double* aloam, const double* in
  * while recording).  lislam_map_kernel_times synchronizes, returns the total ms and launch count
  * per kernel since the previous read (arrays of LISLAM_MAP_NUM_KERNELS, in the order below) and
  * clears the record. */
-#define LISLAM_MAP_NUM_KERNELS 21 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
+#define LISLAM_MAP_NUM_KERNELS 22 /* k_knn, k_fit, k_lm_eval, k_lm_step, map rebuild (keys + sort +
                                      gather + cell table), Add_Points downsample (claim + resolve),
                                      k_orb_pyramid, k_orb_fast, k_orb_select, k_orb_finish,
                                      k_orb_blur (the padded-level blur of images too large for
                                      k_orb_pyramid), k_orb_desc, k_orb_match, k_orb_lm,
                                      k_ground_screen, k_ground_ransac, k_ground_extract,
                                      k_lc_step, k_lc_apply, k_fuse, k_orb_roiblur (the ROI blur +
-                                     border rows after k_orb_pyramid) */
+                                     border rows after k_orb_pyramid), k_lm_solve (a whole pose
+                                     solve in one launch; k_lm_eval / k_lm_step are no longer
+                                     launched) */
 int lislam_map_set_timing(lislam_ctx* ctx, int32_t enable);
 int lislam_map_kernel_times(lislam_ctx* ctx, float* ms, int32_t* launches);
 

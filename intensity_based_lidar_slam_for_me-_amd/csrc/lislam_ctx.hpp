@@ -53,7 +53,7 @@ enum {
   kT_knn = 0, kT_fit, kT_lm_eval, kT_lm_step, kT_rebuild, kT_downsample,
   kT_orb_pyramid, kT_orb_fast, kT_orb_select, kT_orb_finish, kT_orb_blur, kT_orb_desc, kT_orb_match, kT_orb_lm,
   kT_ground_screen, kT_ground_ransac, kT_ground_extract, kT_icp_step, kT_icp_apply, kT_fuse, kT_orb_roiblur,
-  kT_count
+  kT_lm_solve, kT_count
 };
 
 // Records HIP events around the launches of its scope when the context's timer is on.

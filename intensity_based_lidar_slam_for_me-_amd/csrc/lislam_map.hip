@@ -849,51 +849,92 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, con
   lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
 }
 
-// The trust-region step after an evaluation: sums the workgroup partials in order
-// (deterministic), then one thread advances the LM state (held in registers for the step).
-__global__ __launch_bounds__(64) void k_lm_step(LmDev* st, const double* partial, int nparts, int max_it) {
-  if (!st->flag) return;
-  __shared__ double acc[kPart];
-  // thread t sums parts t, t+64, ... (all loads in flight), then a fixed xor tree over the wave
-  double v[kPart];
-#pragma unroll
-  for (int e = 0; e < kPart; e++) v[e] = 0;
-  for (int p = threadIdx.x; p < nparts; p += 64) {
-#pragma unroll
-    for (int e = 0; e < kPart; e++) v[e] += partial[(size_t)p * kPart + e];
-  }
-#pragma unroll
-  for (int e = 0; e < kPart; e++) {
-    double x = v[e];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    if (threadIdx.x == 0) acc[e] = x;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  LM s = st->s;
-  bool cont;
-  if (st->phase == 0) {
-    st->nedge = (int)acc[kAcc];
-    st->nplane = (int)acc[kAcc + 1];
-    st->phase = 1;
-    if (st->nedge + st->nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
-      for (int e = 0; e < 7; e++) s.x[e] = st->x0[e];
-      s.it = 0;
-      s.term = 1;
-      cont = false;
-    } else {
-      double x0[7];
-      for (int e = 0; e < 7; e++) x0[e] = st->x0[e];
-      cont = lm_start(s, x0, acc, max_it);
+// The whole ceres::Solve of solve_device in one launch of one workgroup: the initial evaluation
+// and one per iteration over the records (every thread a strided share; a fixed-order reduction:
+// 16-lane DPP rows, then the rows in order), the trust-region step on thread 0 between them
+// (lm_start / lm_next), the state left in st for k_mapopt_pose, and k_lm_finish's outputs when x_out
+// is given.  One workgroup is enough at laserMapping's sizes (20k
+// blocks: 40 per thread per evaluation); the earlier multi-workgroup evaluation + one-thread step
+// launches paid two launches per evaluation (2 x 5 evaluations per registration).
+constexpr int kSolveThreads = 512;
+// Thread 0's trust-region step between evaluations (not inlined: the evaluation loop every thread
+// runs keeps its own registers).  e = the evaluation just summed into acc.
+__device__ __noinline__ bool lm_solve_step(LM* s, int e, const double* acc, const double* x0, int max_it, int* nedge,
+                                           int* nplane) {
+  if (e == 0) {
+    *nedge = (int)acc[kAcc];
+    *nplane = (int)acc[kAcc + 1];
+    if (*nedge + *nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
+      for (int k = 0; k < 7; k++) s->x[k] = x0[k];
+      s->it = 0;
+      s->term = 1;
+      return false;
     }
-  } else {
-    cont = lm_next(s, acc, max_it);
+    double xs[7];
+    for (int k = 0; k < 7; k++) xs[k] = x0[k];
+    return lm_start(*s, xs, acc, max_it);
   }
-  st->s = s;
-  st->flag = cont;
-  if (cont)
-    for (int e = 0; e < 7; e++) st->xe[e] = s.xc[e];
+  return lm_next(*s, acc, max_it);
+}
+__global__ __launch_bounds__(kSolveThreads) void k_lm_solve(const double* rec, const int* kind, const int* ncount, int n,
+                                                            const double* x0, int max_it, LmDev* st, double* x_out,
+                                                            int* summary) {
+  __shared__ double red[kSolveThreads / 16][kPart];
+  __shared__ double acc[kPart];
+  __shared__ double xe[7];
+  __shared__ int flag;
+  const int nn = ncount ? min(*ncount, n) : n;
+  const int tid = threadIdx.x;
+  if (tid < 7) xe[tid] = x0[tid];
+  if (tid == 0) flag = 1;
+  __syncthreads();
+  LM s;  // thread 0's
+  int nedge = 0, nplane = 0;
+  for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
+    if (!flag) break;  // uniform: written by thread 0 before the barrier
+    double a[kPart];
+#pragma unroll
+    for (int k = 0; k < kPart; k++) a[k] = 0;
+    const DQ q{xe[0], xe[1], xe[2], xe[3]};
+    const D3 t{xe[4], xe[5], xe[6]};
+    for (int i = tid; i < nn; i += kSolveThreads) {
+      const int kd = kind[i];
+      if (kd < 0) continue;
+      block_accum(kd, rec + (size_t)i * 9, q, t, a);
+      a[kAcc + (kd == 0 ? 0 : 1)] += 1.0;
+    }
+    const int row = tid >> 4;
+#pragma unroll
+    for (int k = 0; k < kPart; k++) {
+      const double v = row_sum(a[k]);
+      if ((tid & 15) == 0) red[row][k] = v;
+    }
+    __syncthreads();
+    if (tid < kPart) {
+      double v = 0;
+      for (int w = 0; w < kSolveThreads / 16; w++) v += red[w][tid];
+      acc[tid] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const bool cont = lm_solve_step(&s, e, acc, x0, max_it, &nedge, &nplane);
+      flag = cont;
+      if (cont)
+        for (int k = 0; k < 7; k++) xe[k] = s.xc[k];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    st->s = s;
+    for (int k = 0; k < 7; k++) { st->x0[k] = x0[k]; st->xe[k] = xe[k]; }
+    st->flag = 0;
+    st->phase = 1;
+    st->nedge = nedge;
+    st->nplane = nplane;
+    if (x_out)
+      for (int k = 0; k < 7; k++) x_out[k] = s.x[k];
+    if (summary) { summary[0] = s.it; summary[1] = s.term; summary[2] = nedge; summary[3] = nplane; }
+  }
 }
 
 // x_out = solved pose; summary = iterations, termination, edge blocks, plane blocks
@@ -1199,22 +1240,16 @@ int associate_device(lislam_map* m, int match, const float* q, int stride, const
 }
 
 // ceres::Solve over n device records; result stays in the LmDev (device).
+// (x_out / summary: k_lm_finish's outputs, written by the same launch when given)
 int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* kind, const int* ncount, int n,
-                 const double* x0_dev, int max_it) {
+                 const double* x0_dev, int max_it, double* x_out, int* summary) {
   hipStream_t st = stream_of(c);
   MCHK(c, sc.lm.reserve(sizeof(LmDev)));
-  MCHK(c, sc.partial.reserve((size_t)kMaxParts * kPart * 8));
   LmDev* lm = sc.lm.as<LmDev>();
-  const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
-  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev);
-  for (int e = 0; e <= max_it; e++) {  // initial evaluation + at most one per iteration
-    {
-      TimedScope ts(c, kT_lm_eval);
-      hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
-                         sc.partial.as<double>());
-    }
-    TimedScope ts(c, kT_lm_step);
-    hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(64), 0, st, lm, sc.partial.as<double>(), parts, max_it);
+  {
+    TimedScope ts(c, kT_lm_solve);
+    hipLaunchKernelGGL(k_lm_solve, dim3(1), dim3(kSolveThreads), 0, st, rec, kind, ncount, n, x0_dev, max_it, lm, x_out,
+                       summary);
   }
   MCHK(c, hipGetLastError());
   return LISLAM_OK;
@@ -1472,9 +1507,9 @@ int lislam_pose_solve(lislam_ctx* c, const double* rec, const int32_t* kind, int
     MCHK(c, hipMemcpyAsync(sc.kind.p, kind, (size_t)n * 4, hipMemcpyDefault, st));
   }
   MCHK(c, hipMemcpyAsync(sc.x.p, x, 56, hipMemcpyDefault, st));
-  MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, sc.x.as<double>(), max_iterations));
   int* dsum = reinterpret_cast<int*>(sc.x.as<double>() + 8);
-  hipLaunchKernelGGL(k_lm_finish, dim3(1), dim3(64), 0, st, sc.lm.as<LmDev>(), sc.x.as<double>(), dsum);
+  MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, sc.x.as<double>(), max_iterations,
+                   sc.x.as<double>(), dsum));
   int hs[4];
   MCHK(c, hipMemcpyAsync(x, sc.x.p, 56, hipMemcpyDefault, st));
   MCHK(c, hipMemcpyAsync(hs, dsum, 16, hipMemcpyDeviceToHost, st));
@@ -1574,7 +1609,7 @@ int lislam_mapopt_step_corner(lislam_map* m, lislam_map* cm, const float* ground
     MCHK(c, sc.rec.reserve((size_t)std::max(n, 1) * 72));
     MCHK(c, sc.kind.reserve((size_t)std::max(n, 1) * 4));
     MRC(associate_device(m, 1, voxbuf.as<float>(), 4, nvox, n, dp + 16, sc.rec.as<double>(), sc.kind.as<int>()));
-    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nvox, n, dp + 16, 10));
+    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nvox, n, dp + 16, 10, nullptr, nullptr));
     LmDev* lm = sc.lm.as<LmDev>();
     hipLaunchKernelGGL(k_mapopt_pose, dim3(1), dim3(64), 0, st, 1, dp, dp + 8, dp + 16, lm, dp + 24);
     int* dsum = reinterpret_cast<int*>(dp + 32);
@@ -1628,8 +1663,7 @@ int lislam_laser_mapping(lislam_map* mc, lislam_map* ms, const float* corner, in
     MRC(associate_device(mc, 0, qc.as<float>(), 4, nullptr, nc, dp, sc.rec.as<double>(), sc.kind.as<int>()));
     MRC(associate_device(ms, 1, qs.as<float>(), 4, nullptr, ns, dp, sc.rec.as<double>() + (size_t)nc * 9,
                          sc.kind.as<int>() + nc));
-    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, dp, 4));
-    hipLaunchKernelGGL(k_lm_finish, dim3(1), dim3(64), 0, st, sc.lm.as<LmDev>(), dp, dsum + outer * 4);
+    MRC(solve_device(c, sc, sc.rec.as<double>(), sc.kind.as<int>(), nullptr, n, dp, 4, dp, dsum + outer * 4));
   }
   MCHK(c, hipMemcpyAsync(x, dp, 56, hipMemcpyDefault, st));
   MCHK(c, hipMemcpyAsync(hs, dsum, 32, hipMemcpyDeviceToHost, st));

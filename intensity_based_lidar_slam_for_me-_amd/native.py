@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
 MAP_KERNELS = ("k_knn", "k_fit", "k_lm_eval", "k_lm_step", "map_rebuild", "map_downsample", "k_orb_pyramid",
                "k_orb_fast", "k_orb_select", "k_orb_finish", "k_orb_blur", "k_orb_desc", "k_orb_match", "k_orb_lm",
                "k_ground_screen", "k_ground_ransac", "k_ground_extract", "k_lc_step", "k_lc_apply", "k_fuse",
-               "k_orb_roiblur")
+               "k_orb_roiblur", "k_lm_solve")
 
 MATCH_LINE, MATCH_PLANE = 0, 1
 
