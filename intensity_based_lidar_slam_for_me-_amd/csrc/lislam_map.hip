@@ -849,17 +849,10 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, con
   lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
 }
 
-// The whole ceres::Solve of solve_device in one launch of one workgroup: the initial evaluation
-// and one per iteration over the records (every thread a strided share; a fixed-order reduction:
-// 16-lane DPP rows, then the rows in order), the trust-region step on thread 0 between them
-// (lm_start / lm_next), the state left in st for k_mapopt_pose, and k_lm_finish's outputs when x_out
-// is given.  One workgroup is enough at laserMapping's sizes (20k
-// blocks: 40 per thread per evaluation); the earlier multi-workgroup evaluation + one-thread step
-// launches paid two launches per evaluation (2 x 5 evaluations per registration).
-constexpr int kSolveThreads = 512;
-// Thread 0's trust-region step between evaluations (not inlined: the evaluation loop every thread
-// runs keeps its own registers).  e = the evaluation just summed into acc.
-__device__ __noinline__ bool lm_solve_step(LM* s, int e, const double* acc, const double* x0, int max_it, int* nedge,
+// Thread 0's trust-region step after evaluation e (summed into acc).  Inlined: its registers are
+// live only after the evaluation's, so the kernel stays within 256 VGPRs without scratch (a
+// non-inlined call kept LM in scratch memory, every access a memory round trip).
+__device__ __forceinline__ bool lm_solve_step(LM* s, int e, const double* acc, const double* x0, int max_it, int* nedge,
                                            int* nplane) {
   if (e == 0) {
     *nedge = (int)acc[kAcc];
@@ -876,63 +869,71 @@ __device__ __noinline__ bool lm_solve_step(LM* s, int e, const double* acc, cons
   }
   return lm_next(*s, acc, max_it);
 }
-__global__ __launch_bounds__(kSolveThreads) void k_lm_solve(const double* rec, const int* kind, const int* ncount, int n,
-                                                            const double* x0, int max_it, LmDev* st, double* x_out,
-                                                            int* summary) {
-  __shared__ double red[kSolveThreads / 16][kPart];
-  __shared__ double acc[kPart];
-  __shared__ double xe[7];
-  __shared__ int flag;
-  const int nn = ncount ? min(*ncount, n) : n;
-  const int tid = threadIdx.x;
-  if (tid < 7) xe[tid] = x0[tid];
-  if (tid == 0) flag = 1;
+
+// One evaluation of ceres::Solve with its trust-region step (solve_device launches it max_it + 1
+// times; a launch after the solve has ended returns at once): every workgroup sums its strided share
+// of the records (lm_eval_partial) and counts itself in; the last one sums the partials in workgroup
+// order (deterministic) and takes the step on thread 0 — the separate one-thread step launch per
+// evaluation is gone.  x_out / summary (k_lm_finish's outputs) are written when the solve ends.
+__global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec, const int* kind, const int* ncount, int n,
+                                                              LmDev* st, double* partial, unsigned* arrive, int max_it,
+                                                              double* x_out, int* summary) {
+  if (!st->flag) return;
+  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
+  __shared__ int last;
+  __threadfence();  // this workgroup's partial before its arrival
   __syncthreads();
-  LM s;  // thread 0's
-  int nedge = 0, nplane = 0;
-  for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
-    if (!flag) break;  // uniform: written by thread 0 before the barrier
-    double a[kPart];
+  if (threadIdx.x == 0) last = atomicAdd(arrive, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every other workgroup's partial is visible after the count
+  // The partials summed in a fixed two-level order: lane group g (of kSumGroups) sums parts
+  // g, g + kSumGroups, ... of column e with every load issued before the first add (a serial chain
+  // of L2 round trips cost more than the evaluation), then thread e sums the groups in order.
+  constexpr int kSumGroups = kEvalThreads / 32;
+  __shared__ double gsum[kSumGroups][kPart];
+  __shared__ double acc[kPart];
+  {
+    const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
+    if (e < kPart) {
+      constexpr int kLoads = kMaxParts / kSumGroups;
+      double v[kLoads];
 #pragma unroll
-    for (int k = 0; k < kPart; k++) a[k] = 0;
-    const DQ q{xe[0], xe[1], xe[2], xe[3]};
-    const D3 t{xe[4], xe[5], xe[6]};
-    for (int i = tid; i < nn; i += kSolveThreads) {
-      const int kd = kind[i];
-      if (kd < 0) continue;
-      block_accum(kd, rec + (size_t)i * 9, q, t, a);
-      a[kAcc + (kd == 0 ? 0 : 1)] += 1.0;
-    }
-    const int row = tid >> 4;
+      for (int j = 0; j < kLoads; j++) {
+        const int w = g + j * kSumGroups;
+        v[j] = w < (int)gridDim.x ? __hip_atomic_load(partial + (size_t)w * kPart + e, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0.0;
+      }
+      double s = 0;
 #pragma unroll
-    for (int k = 0; k < kPart; k++) {
-      const double v = row_sum(a[k]);
-      if ((tid & 15) == 0) red[row][k] = v;
+      for (int j = 0; j < kLoads; j++) s += v[j];
+      gsum[g][e] = s;
     }
-    __syncthreads();
-    if (tid < kPart) {
-      double v = 0;
-      for (int w = 0; w < kSolveThreads / 16; w++) v += red[w][tid];
-      acc[tid] = v;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const bool cont = lm_solve_step(&s, e, acc, x0, max_it, &nedge, &nplane);
-      flag = cont;
-      if (cont)
-        for (int k = 0; k < 7; k++) xe[k] = s.xc[k];
-    }
-    __syncthreads();
   }
-  if (tid == 0) {
-    st->s = s;
-    for (int k = 0; k < 7; k++) { st->x0[k] = x0[k]; st->xe[k] = xe[k]; }
-    st->flag = 0;
-    st->phase = 1;
-    st->nedge = nedge;
-    st->nplane = nplane;
+  __syncthreads();
+  if (threadIdx.x < kPart) {
+    double v = 0;
+#pragma unroll
+    for (int g = 0; g < kSumGroups; g++) v += gsum[g][threadIdx.x];
+    acc[threadIdx.x] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  *arrive = 0u;  // the next evaluation's count (its launch follows this one on the stream)
+  LM s = st->s;
+  int nedge = st->nedge, nplane = st->nplane;
+  const bool cont = lm_solve_step(&s, st->phase, acc, st->x0, max_it, &nedge, &nplane);
+  st->s = s;
+  st->nedge = nedge;
+  st->nplane = nplane;
+  st->phase++;
+  st->flag = cont;
+  if (cont)
+    for (int e = 0; e < 7; e++) st->xe[e] = s.xc[e];
+  if (!cont || st->phase > max_it) {  // the solve's end (or its last launch)
     if (x_out)
-      for (int k = 0; k < 7; k++) x_out[k] = s.x[k];
+      for (int e = 0; e < 7; e++) x_out[e] = s.x[e];
     if (summary) { summary[0] = s.it; summary[1] = s.term; summary[2] = nedge; summary[3] = nplane; }
   }
 }
@@ -1240,16 +1241,21 @@ int associate_device(lislam_map* m, int match, const float* q, int stride, const
 }
 
 // ceres::Solve over n device records; result stays in the LmDev (device).
-// (x_out / summary: k_lm_finish's outputs, written by the same launch when given)
+// (x_out / summary: k_lm_finish's outputs, written by the evaluation that ends the solve, when given)
 int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* kind, const int* ncount, int n,
                  const double* x0_dev, int max_it, double* x_out, int* summary) {
   hipStream_t st = stream_of(c);
   MCHK(c, sc.lm.reserve(sizeof(LmDev)));
+  MCHK(c, sc.partial.reserve((size_t)kMaxParts * kPart * 8 + 64));
   LmDev* lm = sc.lm.as<LmDev>();
-  {
+  unsigned* arrive = reinterpret_cast<unsigned*>(sc.partial.as<char>() + (size_t)kMaxParts * kPart * 8);
+  const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
+  MCHK(c, hipMemsetAsync(arrive, 0, sizeof(unsigned), st));
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev);
+  for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
     TimedScope ts(c, kT_lm_solve);
-    hipLaunchKernelGGL(k_lm_solve, dim3(1), dim3(kSolveThreads), 0, st, rec, kind, ncount, n, x0_dev, max_it, lm, x_out,
-                       summary);
+    hipLaunchKernelGGL(k_lm_evalstep, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
+                       sc.partial.as<double>(), arrive, max_it, x_out, summary);
   }
   MCHK(c, hipGetLastError());
   return LISLAM_OK;

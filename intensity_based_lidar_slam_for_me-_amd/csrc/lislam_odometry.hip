@@ -1478,6 +1478,7 @@ struct EngCtl {
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
   __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
   __device__ unsigned* ovf(int c, int ro) const { return w + 4 + C + (size_t)2 * R * C + (size_t)c * 2 * R + ro; }
+  __device__ unsigned* role_ticket() const { return w + 4 + C + (size_t)4 * R * C; }
 };
 // Word 31 of an item's eng_part row once its records and share of pass ro are written.
 __device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
@@ -3083,17 +3084,28 @@ struct RolesLds {  // EngGather first: its DMA addresses stay below 64 KiB
   EngLM lm;
 };
 
+// The grid is one workgroup per role CU (at least C): a workgroup takes the next chain from a ticket
+// when it starts, so the chains go to whichever role CUs are free (another engine may hold some:
+// LISLAM_ENGINE_DEPTH), and the workgroups left over exit at once.
 __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
   __shared__ RolesLds L;
   EngShared& sh = L.sh;
   EngLM& lm = L.lm;
   EngGather& gt = L.gt;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
-  const int c = (int)blockIdx.x;
+  if (wave0) {
+    if (lane_id() == 0) sh.ticket = add_rlx(ctl.role_ticket(), 1u);
+  }
+  __syncthreads();
+  const int c = uni((int)sh.ticket);
+  if (c >= ctl.C) return;
   (void)eng_solve_role<LISLAM_ENG_PROG != 0>(a, ctl, sh, lm, &gt, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
 }
 
-__global__ __launch_bounds__(64 * kMaxItemWaves, 4) void k_odom_items(OdomArgs a, EngCtl ctl) {
+#ifndef LISLAM_ITEM_WPE
+#define LISLAM_ITEM_WPE 4  // waves per SIMD the items are compiled for: 4 = 128 VGPRs
+#endif
+__global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_items(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
@@ -3247,8 +3259,10 @@ bool work_stream(int dev, hipStream_t* s) {
 // wait on the previous engine and the re-record of the event are one critical section (the mutex),
 // so two host threads launching on different contexts cannot both pass the gate.
 struct EngineGate {
+  static constexpr int kMaxDepth = 4;
   std::mutex mu;
-  hipEvent_t ev = nullptr;
+  hipEvent_t ev[kMaxDepth] = {};
+  int next = 0;
 };
 static EngineGate* engine_gate(int dev) {
   static EngineGate gates[64];
@@ -3285,14 +3299,21 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
-  const size_t words = ((size_t)4 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf
+  const size_t words = ((size_t)5 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf, role ticket
+  // engines in flight per device: LISLAM_ENGINE_DEPTH (default 2: a launch waits for the one before
+  // the last, so two chains run together — two item workgroups per CU at 128 VGPRs — and each
+  // chain's idle association slots, while its solve runs, serve the other chain)
+  const int depth = getenv("LISLAM_ENGINE_DEPTH") ? std::min(EngineGate::kMaxDepth, std::max(1, atoi(getenv("LISLAM_ENGINE_DEPTH")))) : 2;
   EngineGate* gate = engine_gate(dev);
   std::unique_lock<std::mutex> lock;
+  hipEvent_t prev = nullptr;
   if (gate) {
     lock = std::unique_lock<std::mutex>(gate->mu);
-    if (!gate->ev) (void)hipEventCreateWithFlags(&gate->ev, hipEventDisableTiming);
+    gate->next = (gate->next + 1) % depth;
+    hipEvent_t& e = gate->ev[gate->next];
+    if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    prev = e;  // recorded by the launch depth launches ago; re-recorded below
   }
-  const hipEvent_t prev = gate ? gate->ev : nullptr;
   (void)hipStreamWaitEvent(roles, ready, 0);
   if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
   if (t0) (void)hipEventRecord(t0, roles);
@@ -3301,7 +3322,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), roles);
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
-  hipLaunchKernelGGL(k_odom_roles, dim3(ctl.C), dim3(kEngThreads), 0, roles, a, ctl);
+  hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
   hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
   (void)hipEventRecord(join_r, roles);
   (void)hipEventRecord(join_i, items);
