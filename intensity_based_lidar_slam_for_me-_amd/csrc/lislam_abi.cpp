@@ -45,6 +45,14 @@ int dalloc(lislam_batch* b, T** p, size_t count) {
   if (e != hipSuccess) return fail(b->ctx, LISLAM_ERR_DEVICE, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
   b->allocs.push_back(q);
   *p = static_cast<T*>(q);
+  // developer: LISLAM_POISON=<byte> fills every new batch buffer with that byte (a read-before-write
+  // hunt: 255 = NaN doubles / -1 ints); LISLAM_POISON_LO / _HI: only buffers lo .. hi (1-based order)
+  if (const char* e = getenv("LISLAM_POISON")) {
+    const int lo = getenv("LISLAM_POISON_LO") ? atoi(getenv("LISLAM_POISON_LO")) : 0;
+    const int hi = getenv("LISLAM_POISON_HI") ? atoi(getenv("LISLAM_POISON_HI")) : 1 << 30;
+    const int i = (int)b->allocs.size();
+    if (i >= lo && i <= hi) (void)hipMemset(q, atoi(e), std::max<size_t>(count, 1) * sizeof(T));
+  }
   return LISLAM_OK;
 }
 

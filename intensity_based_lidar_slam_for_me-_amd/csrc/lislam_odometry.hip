@@ -747,38 +747,68 @@ __device__ __forceinline__ dkey row_min(dkey v) {
 }
 __device__ __forceinline__ uint32_t row_bits(uint64_t m) { return (uint32_t)(m >> (lane_id() & 48)) & 0xffffu; }
 
-// Best-first over the 16 chunks of super-chunk u (u < 0: the row takes no part), the two
-// smallest pending bounds per round trip (evaluating a chunk too many never changes a minimum).
+// The 16-lane searches take up to K chunks per round trip (lane r loads point r of each): the
+// row's pending chunks whose bound can still beat its best, the first K of them in chunk order.
+// Which pending chunks a round takes never changes a minimum (every chunk whose bound is not
+// above the best is evaluated before a search ends); K only trades loads per lane for round trips.
+#ifndef LISLAM_NN16_K
+#define LISLAM_NN16_K 8
+#endif
+#ifndef LISLAM_LS16_K
+#define LISLAM_LS16_K 8
+#endif
+constexpr int kNn16K = LISLAM_NN16_K, kLs16K = LISLAM_LS16_K;
+
+// The K lowest set bits of m (16-bit, the row's), lowest first; -1 past the last.
+template <int K>
+__device__ __forceinline__ void first_bits(uint32_t m, int (&pc)[K]) {
+#pragma unroll
+  for (int t = 0; t < K; t++) {
+    pc[t] = m ? (int)__builtin_ctz(m) : -1;
+    m &= m - 1u;
+  }
+}
+
+// Every chunk of super-chunk u (u < 0: the row takes no part) whose bound is not above the row's
+// best, K per round trip.
 __device__ __forceinline__ void nn16_super(const P4* sorted, int n, int nch, const float4* chm, int u, const P4& q,
                                            dkey& best) {
+  constexpr int K = kNn16K;
   const int lr = lane_id() & 15;
   const int c = u * kChunk + lr;
   bool cp = u >= 0 && c < nch;
   float clb = 3.4e38f;
   if (cp) clb = box_lb(ldg(chm + 2 * c), ldg(chm + 2 * c + 1), q);
   for (;;) {
-    const bool cand = cp && !(clb > dk_d(best));
-    const dkey m1 = row_min(cand ? dk(clb, lr) : kIdent);
-    const bool ev1 = m1 != kIdent;
-    if (!__ballot(ev1)) break;
-    const int p1 = ev1 ? dk_key(m1) : -1;
-    const dkey m2 = row_min(cand && lr != p1 ? dk(clb, lr) : kIdent);
-    const bool ev2 = m2 != kIdent;
-    const int p2 = ev2 ? dk_key(m2) : -1;
-    if (lr == p1 || lr == p2) cp = false;
-    const int j1 = (u * kChunk + p1) * kChunk + lr, j2 = (u * kChunk + p2) * kChunk + lr;
-    const bool ok1 = ev1 && j1 < n, ok2 = ev2 && j2 < n;
-    const P4 a1 = ld4(sorted + (ok1 ? j1 : 0)), a2 = ld4(sorted + (ok2 ? j2 : 0));
-    const float d1 = d2f(q, a1), d2 = d2f(q, a2);
-    const dkey v = dmin(ok1 && d1 < 25.f ? dk(d1, __float_as_int(a1.i)) : kIdent,
-                        ok2 && d2 < 25.f ? dk(d2, __float_as_int(a2.i)) : kIdent);
+    const uint32_t m = row_bits(__ballot(cp && !(clb > dk_d(best))));
+    if (!__ballot(m != 0u)) break;
+    int pc[K];
+    first_bits<K>(m, pc);
+    bool took = false;
+#pragma unroll
+    for (int t = 0; t < K; t++) took = took || pc[t] == lr;
+    if (took) cp = false;
+    P4 p[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+      const int j = (u * kChunk + pc[t]) * kChunk + lr;
+      p[t] = ld4(sorted + (pc[t] >= 0 && j < n ? j : 0));
+    }
+    dkey v = kIdent;
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+      const int j = (u * kChunk + pc[t]) * kChunk + lr;
+      const float d = d2f(q, p[t]);
+      if (pc[t] >= 0 && j < n && d < 25.f) v = dmin(v, dk(d, __float_as_int(p[t].i)));
+    }
     best = dmin(best, row_min(v));
   }
 }
 
-// Exact 1-NN (d < 25) of the row's query in the Morton-ordered copy; -1 = none.
+// Exact 1-NN (d < 25) of the row's query in the Morton-ordered copy; -1 = none.  seed: a known
+// point (d < 25) that only tightens the pruning.
 __device__ __forceinline__ int nn16(const P4* sorted, int n, const float4* chm, const float4* sum, const P4& q,
-                                    bool act) {
+                                    bool act, dkey seed = kIdent) {
   const int lr = lane_id() & 15;
   const int nch = (n + kChunk - 1) / kChunk, nsu = act && n > 0 ? (nch + kChunk - 1) / kChunk : 0;
   dkey ub = kIdent;
@@ -786,20 +816,27 @@ __device__ __forceinline__ int nn16(const P4* sorted, int n, const float4* chm, 
   const int kmax = (int)wave_umax((uint32_t)((nsu + 15) >> 4));
 #pragma unroll
   for (int kk = 0; kk < 4; kk++) slb[kk] = 3.4e38f;
-  for (int k = 0; k < kmax; k++) {
-    const int u = lr + 16 * k;
-    if (u < nsu) {
-      const float lb = box_lb(ldg(sum + 2 * u), ldg(sum + 2 * u + 1), q);
-      ub = dmin(ub, dk(lb, u));
+  for (int k0 = 0; k0 < kmax; k0 += 4) {  // four super-chunk bounds per lane per round trip
+    float4 lo[4], hi[4];
 #pragma unroll
-      for (int kk = 0; kk < 4; kk++)
-        if (k == kk) slb[kk] = lb;
+    for (int kk = 0; kk < 4; kk++) {
+      const int u = lr + 16 * (k0 + kk);
+      if (u < nsu) { lo[kk] = ldg(sum + 2 * u); hi[kk] = ldg(sum + 2 * u + 1); }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      const int u = lr + 16 * (k0 + kk);
+      if (u < nsu) {
+        const float lb = box_lb(lo[kk], hi[kk], q);
+        ub = dmin(ub, dk(lb, u));
+        if (k0 == 0) slb[kk] = lb;
+      }
     }
   }
   ub = row_min(ub);
   const bool go = nsu > 0 && dk_d(ub) < 25.f;
   const int u0 = go ? dk_key(ub) : -1;
-  dkey best = dk(25.f, kNone);
+  dkey best = dmin(dk(25.f, kNone), seed);
   nn16_super(sorted, n, nch, chm, u0, q, best);
   // the other super-chunks, 64 per window (four per lane), in bound order while <= best
   const int wmax = (int)wave_umax((uint32_t)(go ? (nsu + 63) >> 6 : 0));
@@ -840,9 +877,11 @@ __device__ __forceinline__ bool ls16_need(bool corner, bool up, int lmin, int lm
 }
 
 // The scan-line searches of the row (corner: b2; surf: b2, b3) around `closest` in the target
-// cloud L (scan-line order, labels non-decreasing), windows of 16 chunks up and down.
+// cloud L (scan-line order, labels non-decreasing), windows of 16 chunks up and down; every round
+// trip takes up to K pending chunks, nearest the home chunk first, split between the directions.
 __device__ __forceinline__ void ls16(const P4* L, const float4* chm, int n, int closest, int cid, const P4& sel,
                                      bool corner, bool act, dkey& b2, dkey& b3) {
+  constexpr int K = kLs16K;
   const int lr = lane_id() & 15;
   const int nch = (n + kChunk - 1) / kChunk;
   const int hc = act ? closest / kChunk : 0;
@@ -864,33 +903,47 @@ __device__ __forceinline__ void ls16(const P4* L, const float4* chm, int n, int 
       const float bd2 = dk_d(b2), bd3 = dk_d(b3);
       const bool nu = upend && ls16_need(corner, true, (int)ulo.w, (int)uhi.w, cid, ulb, bd2, bd3);
       const bool nd = dpend && ls16_need(corner, false, (int)dlo.w, (int)dhi.w, cid, dlb, bd2, bd3);
-      const dkey cu1 = nu ? dk(ulb, 2 * lr) : kIdent, cd1 = nd ? dk(dlb, 2 * lr + 1) : kIdent;
-      const dkey m1 = row_min(dmin(cu1, cd1));
-      const bool ev1 = m1 != kIdent;
-      if (!__ballot(ev1)) break;
-      const int k1 = ev1 ? dk_key(m1) : -1;
-      const dkey m2 = row_min(dmin(2 * lr == k1 ? kIdent : cu1, 2 * lr + 1 == k1 ? kIdent : cd1));
-      const bool ev2 = m2 != kIdent;
-      const int k2 = ev2 ? dk_key(m2) : -1;
-      if (k1 == 2 * lr || k2 == 2 * lr) upend = false;
-      if (k1 == 2 * lr + 1 || k2 == 2 * lr + 1) dpend = false;
+      uint32_t mu = row_bits(__ballot(nu)), md = row_bits(__ballot(nd));
+      if (!__ballot((mu | md) != 0u)) break;
+      // ku from the up walk, the rest from the down walk (half each unless one side has fewer)
+      const int ku = min(__builtin_popcount(mu), max(K / 2, K - __builtin_popcount(md)));
+      int pk[K];
+      bool pup[K];
+#pragma unroll
+      for (int t = 0; t < K; t++) {
+        const bool up = t < ku;
+        const uint32_t mm = up ? mu : md;
+        pk[t] = mm ? (int)__builtin_ctz(mm) : -1;
+        if (up) mu &= mu - 1u;
+        else md &= md - 1u;
+        pup[t] = up;
+      }
+#pragma unroll
+      for (int t = 0; t < K; t++) {
+        if (pk[t] == lr && pup[t]) upend = false;
+        if (pk[t] == lr && !pup[t]) dpend = false;
+      }
+      P4 p[K];
+      int jj[K];
+#pragma unroll
+      for (int t = 0; t < K; t++) {
+        const int c = pup[t] ? hc + 16 * win + pk[t] : hc - 16 * win - pk[t];
+        jj[t] = c * kChunk + lr;
+        const bool valid = pk[t] >= 0 && jj[t] >= 0 && jj[t] < n && (pup[t] ? jj[t] > closest : jj[t] < closest);
+        if (!valid) jj[t] = -1;
+        p[t] = ld4(L + (valid ? jj[t] : 0));
+      }
       dkey v2 = kIdent, v3 = kIdent;
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const bool ev = h == 0 ? ev1 : ev2;
-        const int key = h == 0 ? k1 : k2;
-        const bool up = (key & 1) == 0;
-        const int pl = key >> 1;
-        const int c = up ? hc + 16 * win + pl : hc - 16 * win - pl;
-        const int j = c * kChunk + lr;
-        const bool valid = ev && j >= 0 && j < n && (up ? j > closest : j < closest);
-        const P4 p = ld4(L + (valid ? j : 0));
-        const int pid = int(p.i);
+      for (int t = 0; t < K; t++) {
+        const bool up = pup[t];
+        const int j = jj[t];
+        const int pid = int(p[t].i);
+        bool v = j >= 0;
         // the walk's break inside this chunk: up, the first point past cid + 2; down, the last below cid - 2
-        const uint32_t bm = row_bits(__ballot(valid && (up ? pid > cid + 2 : pid < cid - 2)));
-        bool v = valid;
+        const uint32_t bm = row_bits(__ballot(v && (up ? pid > cid + 2 : pid < cid - 2)));
         if (bm) v = v && (up ? lr < (int)__builtin_ctz(bm) : lr > 31 - (int)__builtin_clz(bm));
-        const float d = d2f(sel, p);
+        const float d = d2f(sel, p[t]);
         const int rk = up ? j - closest : n + closest - j;
         if (v && d < 25.f) {
           if (corner) {
@@ -1330,8 +1383,7 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
 
 // Developer profile of the engine (null in production): per ticket kProfSlots u64 = s_memrealtime
 // (100 MHz) at claim, inputs ready, records loaded (solve), done; summed evaluation and step ticks and
-// the evaluation count (solve); items: 8 / 9 an overflow query's claim and end (eng_steal), 10 the
-// end of the item's last own query.  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
+// the evaluation count (solve); items: 10 the end of the item's last query.  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
 // lislam_debug_engine_prof_read copies it out.
 constexpr int kProfSlots = 16;
 __device__ unsigned long long* g_eng_prof = nullptr;
@@ -1460,7 +1512,6 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // cleared by a launch: lislam_batch_odometry_status reads and clears it), [4, 4 + C) lm_gen, then
 // assoc_done[C][2 R]
 constexpr int kMaxShareItems = 256;  // 16 threads x 8 loads per item row: 32 rows per round x 8
-constexpr int kMaxShareRows = 512;   // eng_part rows per chain: items 0 .. 255, stolen overflow queries 256 + o
 struct EngCtl {
   unsigned* w;
   int C, R, I;
@@ -1471,14 +1522,14 @@ struct EngCtl {
                  // once, and at most kMaxShareItems (the solve sums the shares in one round of loads)
   unsigned gen;  // this launch's number: with the pass, the tag of a complete item row (eng_tag)
   int P;         // rows per chain of eng_part (engine_part_rows)
-  int steal;     // overflow queries are claimed by the pass's waves one at a time (split engine)
-  int Q;         // queries per association item = the item workgroup's waves
+  int Q;         // the association item workgroup's waves
+  int qpw;       // queries per wave: 1 (the 64-lane searches) or 4 (one per 16-lane row)
+  __host__ __device__ int qpi() const { return Q * qpw; }  // queries per item
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
   __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
-  __device__ unsigned* ovf(int c, int ro) const { return w + 4 + C + (size_t)2 * R * C + (size_t)c * 2 * R + ro; }
-  __device__ unsigned* role_ticket() const { return w + 4 + C + (size_t)4 * R * C; }
+  __device__ unsigned* role_ticket() const { return w + 4 + C + (size_t)2 * R * C; }
 };
 // Word 31 of an item's eng_part row once its records and share of pass ro are written.
 __device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
@@ -1488,24 +1539,20 @@ __device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
 // Association items of pair k that hold queries (the rest of the ctl.I items are skipped).
 __device__ __forceinline__ int eng_live_items(const OdomArgs& a, const EngCtl& ctl, int k) {
   if (a.gate && !a.gate[k]) return 0;
-  return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + ctl.Q - 1) / ctl.Q, ctl.budget));
+  return uni(min((a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2] + ctl.qpi() - 1) / ctl.qpi(), ctl.budget));
 }
 
-// A pass's association: ieff items of Q queries; when the pair holds more queries than that
-// (the items are capped by EngCtl::budget, what the resident workgroups hold), the novf overflow
-// queries Q ieff + o are either claimed one at a time by whichever waves of the pass finish
-// first (steal: each is a row of its own, kMaxShareItems + o) or taken by the items in further rounds.
+// A pass's association: ieff items of qpi() queries; when the pair holds more queries than that
+// (the items are capped by EngCtl::budget, what the resident workgroups hold), the items take the
+// novf overflow queries in further rounds (eng_item_run).
 struct PassShape {
-  int ieff, novf, rows;
-  bool steal;
+  int ieff, novf;
 };
 __device__ __forceinline__ PassShape pass_shape(const OdomArgs& a, const EngCtl& ctl, int k) {
   PassShape ps;
   ps.ieff = eng_live_items(a, ctl, k);
   const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
-  ps.novf = ps.ieff > 0 ? uni(max(0, nq - ctl.Q * ps.ieff)) : 0;
-  ps.steal = ctl.steal && ps.novf <= kMaxShareRows - kMaxShareItems;
-  ps.rows = ps.ieff;  // the items' rows; a stealing pass's overflow rows are kMaxShareItems + o, o < novf
+  ps.novf = ps.ieff > 0 ? uni(max(0, nq - ctl.qpi() * ps.ieff)) : 0;
   return ps;
 }
 __device__ __forceinline__ double* part_row(const OdomArgs& a, const EngCtl& ctl, int c, int row) {
@@ -1567,16 +1614,14 @@ __device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* ab
 
 struct EngShared {
   double red[kEngWaves * 4][32];  // kAcc sums (+ 2 counts) per 16-lane row
-  double sred[kMaxItemWaves][30];  // each wave's share of the overflow query it stole (eng_steal)
   double xw[kMaxItemWaves][8];     // each wave's copy of its item's x (the item's queries read it here)
-  P4 prew[kMaxItemWaves][4];       // each wave's ItemPre of its first query: qp, the seeds' points
-  int prei[kMaxItemWaves][4];      // ... and the seeds' indices
+  P4 prew[kMaxItemWaves][4][4];    // each wave's ItemPre of its first query per row: qp, the seeds' points
+  int prei[kMaxItemWaves][4][4];   // ... and the seeds' indices
   double acc[kAcc];
   double x[7];
   double cx[7], cpw[7];  // solve role: the chain's x (para_q / para_t) and pose between passes
   int cnt[kEngWaves][2];
   unsigned ticket;
-  int ovc;  // eng_steal: the item's overflow queries claimed so far
   int flag, flag0, nc, np, pref;
   unsigned sink;
 };
@@ -1809,9 +1854,10 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   if (outer == 0 && lane < 3)  // seeds of the second pass (write-through: another workgroup reads them)
     __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), (unsigned)(lane == 0 ? closest : lane == 1 ? i2 : i3),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the record: four 16-B write-through stores (lanes 0..3; the kind word always, the rest with a
-  // correspondence) -- layout of rec_unpack
-  if (lane < 4 && (lane == 1 || kind >= 0)) {
+  // the record: four 16-B write-through stores (lanes 0..3) -- layout of rec_unpack.  All four even
+  // without a correspondence (zeros): the evaluation weighs an absent block by 0, and 0 x a stale
+  // non-finite word from an earlier use of the buffer would be NaN (a read-before-write)
+  if (lane < 4) {
     v4u q;
     if (lane == 0) q = v4u{__float_as_uint(cur.x), __float_as_uint(cur.y), __float_as_uint(cur.z), __float_as_uint(pa.x)};
     else if (lane == 1) q = v4u{__float_as_uint(pa.y), __float_as_uint(pa.z), (unsigned)kind, 0u};
@@ -1842,6 +1888,128 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   }
 }
 
+// One association query per 16-lane row, four per wave (EngCtl::qpw = 4): the searches of the
+// per-round schedule (nn16 / ls16: a round trip looks at 16 candidates per query) with eng_query's
+// seeds, record, second-pass seeds and share.  A quarter of eng_query's waves per pass, so a pass's
+// queries fit the resident item waves in one round and leave the SIMDs room for whatever runs
+// beside the engine.  has: this row holds a query (w < the pair's queries).
+__device__ __forceinline__ void eng_query16(const OdomArgs& a, int k, int w, bool has, Rsrc rec, int* warm, int outer,
+                                            unsigned tk, const ItemPre& pre, const double (&x)[7], double* row) {
+  const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
+  const int lane = lane_id(), lr = lane & 15;
+  const int ns = a.n_feat[k * 4 + 0];
+  const bool corner = w < ns;
+  const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
+  const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
+  const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
+  const int nL = a.n_feat[(k - 1) * 4 + (corner ? 1 : 3)];
+  const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
+  const P4 cur{pre.qp.x, pre.qp.y, pre.qp.z, 0.f};
+  const P4 sel = transform_to_start(cur, x);
+  const int (&wi)[3] = pre.wi;
+  const P4 (&wp)[3] = pre.wp;
+  dkey seed = kIdent;  // the first pass's matches (second pass): candidates of the minimum they seed
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    const float d = d2f(sel, wp[e]);
+    if (wi[e] >= 0 && wi[e] < nL && d < 25.f) seed = dmin(seed, dk(d, wi[e]));
+  }
+  const unsigned long long tq1 = threadIdx.x == 0 ? rt_now() : 0ull;
+  const int closest = nn16(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, has, seed);
+  const unsigned long long tq2 = threadIdx.x == 0 ? rt_now() : 0ull;
+  const bool act = has && closest >= 0;
+  P4 pa = ld4(L + (act ? closest : 0));
+  if (!act) pa = P4{0.f, 0.f, 0.f, 0.f};  // the record's defined zeros (no correspondence)
+  const int cid = act ? int(pa.i) : 0;
+  dkey b2 = dk(25.f, kNone), b3 = dk(25.f, kNone);
+  if (act) {
+#pragma unroll
+    for (int e = 0; e < 3; e++) {  // seeds of the walks under this closest (as eng_query)
+      const int j = wi[e];
+      if (j < 0 || j >= nL || j == closest) continue;
+      const int lab = int(wp[e].i);
+      const bool up = j > closest;
+      if (up ? lab > cid + 2 : lab < cid - 2) continue;
+      const float d = d2f(sel, wp[e]);
+      if (!(d < 25.f)) continue;
+      const dkey kd2 = dk(d, up ? j - closest : nL + closest - j);
+      const bool other = up ? lab > cid : lab < cid;
+      if (corner) {
+        if (other) b2 = dmin(b2, kd2);
+      } else {
+        if (other) b3 = dmin(b3, kd2);
+        else b2 = dmin(b2, kd2);
+      }
+    }
+  }
+  ls16(L, ix.chunk + mo, nL, act ? closest : 0, cid, sel, corner, act, b2, b3);
+  auto idx_of = [&](dkey b) { const int kk = dk_key(b); return kk < nL ? closest + kk : closest - (kk - nL); };
+  int kind = -1, i2 = -1, i3 = -1;
+  D3 u{0.0, 0.0, 0.0};
+  if (act && dk_key(b2) != kNone) i2 = idx_of(b2);
+  if (act && !corner && dk_key(b3) != kNone) i3 = idx_of(b3);
+  if (act && corner && i2 >= 0) {  // LidarEdgeFactor(curr, a, b)
+    const P4 pb = ld4(L + i2);
+    const D3 de{(double)pa.x - (double)pb.x, (double)pa.y - (double)pb.y, (double)pa.z - (double)pb.z};
+    const double inv = 1.0 / sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
+    u = D3{de.x * inv, de.y * inv, de.z * inv};
+    kind = 0;
+  } else if (act && !corner && i2 >= 0 && i3 >= 0) {  // LidarPlaneFactor(curr, j, l, m)
+    const P4 pl = ld4(L + i2), pm = ld4(L + i3);
+    u = plane_normal(D3{pa.x, pa.y, pa.z}, D3{pl.x, pl.y, pl.z}, D3{pm.x, pm.y, pm.z});
+    kind = 1;
+  }
+  if (threadIdx.x == 0) {  // the wave's four queries together (developer profile)
+    const unsigned long long tq3 = rt_now();
+    eng_prof(tk, 4, tq1 - tq0);
+    eng_prof(tk, 5, tq2 - tq1);
+    eng_prof(tk, 6, tq3 - tq2);
+  }
+  if (has && outer == 0 && lr < 3)  // seeds of the second pass (write-through: another workgroup reads them)
+    __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lr), (unsigned)(lr == 0 ? closest : lr == 1 ? i2 : i3),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the record (rec_unpack's layout): lanes 0..3 of the row, 16 B each, all four always (eng_query)
+  if (has && lr < 4) {
+    v4u q;
+    if (lr == 0) q = v4u{__float_as_uint(cur.x), __float_as_uint(cur.y), __float_as_uint(cur.z), __float_as_uint(pa.x)};
+    else if (lr == 1) q = v4u{__float_as_uint(pa.y), __float_as_uint(pa.z), (unsigned)kind, 0u};
+    else if (lr == 2) {
+      const uint64_t ux = (uint64_t)__double_as_longlong(u.x), uy = (uint64_t)__double_as_longlong(u.y);
+      q = v4u{(unsigned)ux, (unsigned)(ux >> 32), (unsigned)uy, (unsigned)(uy >> 32)};
+    } else {
+      const uint64_t uz = (uint64_t)__double_as_longlong(u.z);
+      q = v4u{(unsigned)uz, (unsigned)(uz >> 32), 0u, 0u};
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(q, rec, w * kRecBytes + lr * 16, 0, kAuxSc1);
+  }
+  // the rows' shares of the first evaluation: every lane of a row computes its row's block, and lane
+  // 0 adds the four rows' sums (rows 0 + 1, 2 + 3, then the two) to the wave's row of sh.red
+  double sb[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) sb[e] = 0.0;
+  if (kind >= 0) {
+    double R[9];
+    D3 t;
+    eng_rt_x(x, R, t);
+    eng_block(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, sb);
+  }
+  const uint64_t mc = __ballot(lr == 0 && kind == 0), mp = __ballot(lr == 0 && kind == 1);
+  auto rd = [](double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)(unsigned)hi << 32) | (unsigned)lo));
+  };
+  double tot[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) tot[e] = (rd(sb[e], 0) + rd(sb[e], 16)) + (rd(sb[e], 32) + rd(sb[e], 48));
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < kAcc; e++) row[e] += tot[e];
+    row[28] += (double)__builtin_popcountll(mc);
+    row[29] += (double)__builtin_popcountll(mp);
+  }
+}
+
 // A bounds check of the engine's own index arithmetic (the rows it publishes, the records it
 // writes): a violation raises this launch's abort (and the sticky word) with `code` in the error
 // word instead of faulting, so the host re-runs the launch on the per-round schedule and the code
@@ -1856,85 +2024,39 @@ __device__ __forceinline__ bool eng_check(const EngCtl& ctl, bool ok, unsigned c
   return false;
 }
 
-// Every wave of a pass's live items, right after its own query: take the item's overflow queries
-// Q ieff + o, o = item, item + ieff, ... (< novf) one at a time, and publish each as row
-// kMaxShareItems + o (its record, seeds and share, then the row's tag).  The item's waves claim
-// them through an LDS counter, so the item's first waves to finish run them — the pass does not
-// wait for a second round of some items, and no global word is contended (a device-wide counter
-// read by every wave of the pass serialized ~2,000 requests on one line: 46.7 vs 27.5 ms, r05d).
-// The claim is one LDS atomic from the whole wave (lane 0 adds 1, the others 0) — no single-lane
-// branch anywhere in the loop: a loop opening with one can be rotated so that lane 0 runs the body
-// apart from the other lanes, and the searches' wave-wide ballots / permutes then see a partial
-// wave (the hang of the first version).
-__device__ __forceinline__ void eng_steal(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int c, int k, int ro,
-                                          int item, const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk,
-                                          const double (&x)[7]) {
-  const int ql = (int)(threadIdx.x >> 6), lane = lane_id();
-  auto claim = [&]() -> int {
-    const int j = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(&sh.ovc, lane == 0 ? 1 : 0, __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
-    return item + j * ps.ieff;
-  };
-  const int e30 = lane < 30 ? lane : 29;  // no single-lane branches in this loop (lanes >= 30 repeat 29)
-  for (int ov = claim(); ov < ps.novf; ov = claim()) {
-    if (lane == 0) eng_prof(tk, 8, rt_now());
-    const int w = ctl.Q * ps.ieff + ov;
-    const int row_i = kMaxShareItems + ov;
-    if (!eng_check(ctl, w < a.cap_sharp + a.cap_flat && row_i < ctl.P, 0x5700u + (unsigned)min(ov, 255))) return;
-    sh.sred[ql][e30] = 0.0;
-#ifndef LISLAM_STEAL_NOQUERY
-    const ItemPre pre = eng_item_pre(a, k, w, warm, outer);
-    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.sred[ql]);
-#else  // developer bisect: no search, but a well-formed empty record (kind -1) and no seeds
-    {
-      const v4u q1 = v4u{0u, 0u, 0xffffffffu, 0u};
-      if (lane == 1) __builtin_amdgcn_raw_buffer_store_b128(q1, rec, w * kRecBytes + 16, 0, kAuxSc1);
-      if (outer == 0 && lane < 3)
-        __hip_atomic_store((gu32*)(warm + (size_t)w * 4 + lane), 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // lane 0's adds before the lanes' reads
-    __builtin_amdgcn_wave_barrier();
-    double* row = part_row(a, ctl, c, row_i);
-    st_sc1d(row + e30, sh.sred[ql][e30]);
-    drain_stores();  // the record, the seeds and the row
-    st_sc1(reinterpret_cast<uint64_t*>(row) + 31, eng_tag(ctl, ro));  // every lane, the same word
-    if (lane == 0) eng_prof(tk, 9, rt_now());
-  }
-}
-
-// One association item: wave wv of item `item` takes queries (item + m ieff) Q + wv, m = 0,
-// 1, ...: one each while the pair's queries fit ieff items (the common case), more when the pair
-// holds more queries than the engine keeps items in flight (EngCtl::budget), so that no item
-// waits for a workgroup to come free — or, when the pass steals (PassShape::steal), one each and
-// then the overflow queries as each wave comes free (eng_steal).  The wave's share of the first
-// evaluation (its blocks' 28 sums at x, and the corner / plane counts) goes to sh.red[wave].
-__device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int c, int k, int ro,
-                                             int item, const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk) {
+// One association item: wave wv of item `item` takes queries (item + m ieff) qpi + wv qpw (+ the
+// row, four 16-lane rows per wave when qpw = 4), m = 0, 1, ...: one round while the pair's queries
+// fit ieff items (the common case), more when the pair holds more queries than the engine keeps
+// items in flight (EngCtl::budget), so that no item waits for a workgroup to come free.  The wave's
+// share of the first evaluation (its blocks' 28 sums at x, and the corner / plane counts) goes to
+// sh.red[wave].
+template <int kQpw>
+__device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int k, int item,
+                                             const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk) {
   const int ql = (int)(threadIdx.x >> 6);
+  const int row = kQpw == 4 ? lane_id() >> 4 : 0;
   const int ieff = ps.ieff;
   const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
   if (lane_id() < 30) sh.red[ql][lane_id()] = 0.0;
   double x[7];
 #pragma unroll
   for (int e = 0; e < 7; e++) x[e] = sh.xw[ql][e];
-  for (int m = 0; m == 0 || !ps.steal; m++) {  // steal: the overflow queries go to eng_steal instead
-    const int w = (item + m * ieff) * ctl.Q + ql;
-    if (w >= nq) break;  // wave-uniform
+  for (int m = 0;; m++) {
+    const int w0 = (item + m * ieff) * ctl.Q * kQpw + ql * kQpw;  // the wave's first query
+    if (w0 >= nq) break;  // wave-uniform
+    const int w = w0 + row;
     ItemPre pre;
     if (m > 0) {
       pre = eng_item_pre(a, k, w, warm, outer);
     } else {  // loaded before x existed, parked in this wave's LDS slots
-      pre.qp = sh.prew[ql][0];
+      pre.qp = sh.prew[ql][row][0];
 #pragma unroll
-      for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][1 + e]; pre.wi[e] = sh.prei[ql][e]; }
+      for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][row][1 + e]; pre.wi[e] = sh.prei[ql][row][e]; }
     }
-    eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
+    if constexpr (kQpw == 4) eng_query16(a, k, w, w < nq, rec, warm, outer, tk, pre, x, sh.red[ql]);
+    else eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
   }
   if (lane_id() == 0) eng_prof(tk, 10, rt_now());
-#ifndef LISLAM_STEAL_NOCALL
-  if (ps.steal && item < ps.novf) eng_steal(a, ctl, sh, c, k, ro, item, ps, rec, warm, outer, tk, x);
-#endif
 }
 
 // The 28 sums of every thread -> sh.acc in lislam_lm.hpp's layout (cost, H upper, g).  Inside each
@@ -2477,237 +2599,21 @@ __device__ __forceinline__ void eng_gather_rows(EngShared& sh, double (&acc)[kAc
 // iteration), then publish x (para_q / para_t, write-through) and lm_gen[c] = ro + 1.  The chain's
 // x and pose stay in LDS.
 //
-// Gather, progressive (k_odom_roles, kProg): every item tags its eng_part row (eng_tag) once its
-// records and share are written; wave 0 polls the tags and marks each complete item in LDS, and
-// waves 1.. load that item's records into their slots and its share quads straight into LDS
-// (buffer_load ... lds) as it lands — so when the last item finishes only its own loads remain.
-// Bulk (k_odom_chain): wait for every item (the assoc_done count), then load everything.
-// Both sum the shares in the same fixed tree: the results are identical.
+// The solve's gather: wait for every item of the pass (the assoc_done count), then load every
+// item's share row at once (summed in a fixed tree) and, while wave 0 takes step 0 from the shares,
+// the records into the evaluating waves' slots.
 constexpr int kShareQuads = 15;  // doubles 0..29 of an item's row: 28 sums + 2 counts
-// quads per evaluating thread (gather_fill: quad Q = tp + kEvalThreads i)
-constexpr int kQuadRounds = (kMaxShareItems * kShareQuads + kEvalThreads - 1) / kEvalThreads;
-struct EngGather {
-  // the items' rows, packed: quad q of row i at i * 15 + q; sized to whole rounds of the evaluating
-  // waves, so every wave's LDS-DMA base lies inside it, and kept below 64 KiB of LDS (RolesLds puts it
-  // first): the DMA's M0 base is taken as 16 bits, as ds_write_addtid's is
-  v4u shr[kQuadRounds * kEvalThreads];
-  unsigned ready[kMaxShareRows];         // ro + 1 once row i of pass ro is complete (items', then overflow rows)
-  int abort;
-  int all;  // wave 0 has seen every row of the pass (gather_fill then defers the last records)
-};
 
-// Wave 0: poll the tags of the pass's ieff items (lane l: items l, l + 64, ...) and publish each
-// complete one in gt.ready.  false = aborted (the bound expired here, or another workgroup's abort).
-__device__ __forceinline__ bool gather_poll(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro,
-                                            const PassShape& ps) {
-  constexpr int kJ = kMaxShareRows / 64, kJI = kMaxShareItems / 64;
-  const int lane = lane_id();
-  const uint64_t want = eng_tag(ctl, ro);
-  const uint64_t* tags = reinterpret_cast<const uint64_t*>(part_row(a, ctl, c, 0)) + 31;
-  const int nov = ps.steal ? ps.novf : 0;
-  unsigned pend = 0u;  // bit j: row lane + 64 j (items for j < kJI, then the overflow rows kMaxShareItems + ...)
-#pragma unroll
-  for (int j = 0; j < kJ; j++)
-    if (j < kJI ? lane + 64 * j < ps.ieff : lane + 64 * (j - kJI) < nov) pend |= 1u << j;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    uint64_t v[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; j++) v[j] = ((pend >> j) & 1u) ? ld_sc1(tags + (size_t)(lane + 64 * j) * 32) : 0ull;
-#pragma unroll
-    for (int j = 0; j < kJ; j++)
-      if (((pend >> j) & 1u) && v[j] == want) {
-        __hip_atomic_store(&gt.ready[lane + 64 * j], (unsigned)(ro + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        pend &= ~(1u << j);
-      }
-    if (__ballot(pend != 0u) == 0ull) return true;
-    bool stop = ld_rlx(ctl.abort_w()) != 0u;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > ctl.wait_ticks) {
-      if (lane == 0) {
-        st_rlx(ctl.abort_w(), 1u);
-        st_rlx(ctl.abort_w() + 1, 4u);  // error word: the progressive gather's poll
-        st_rlx(ctl.abort_w() + 2, 1u);  // sticky (EngCtl word 3)
-      }
-      stop = true;
-    }
-    if (__builtin_amdgcn_readfirstlane((int)stop)) {
-      if (lane == 0) __hip_atomic_store(&gt.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-__device__ __forceinline__ void blk_absent(BlkReg& b) {
-  b.c[0] = b.c[1] = b.c[2] = 0.f;
-  b.a[0] = b.a[1] = b.a[2] = 0.f;
-  b.u[0] = b.u[1] = b.u[2] = 0.0;
-  b.kd = -1;
-}
-
-// Waves 1..: as gather_poll marks items complete, load their records into this thread's slots and
-// their share quads (quad Q = tp + 448 i of the packed rows) into gt.shr; returns once every share
-// quad is issued and landed (or on abort).  Once wave 0 has seen every row (gt.all) the records not
-// loaded yet are left out (the returned bits: bit k edge slot k, bit kEdgeSlots + k plane slot k):
-// step 0 needs only the shares, so gather_records loads those last records while wave 0 steps.
-__device__ __forceinline__ unsigned gather_fill(const OdomArgs& a, const EngCtl& ctl, EngGather& gt, int c, int ro,
-                                            const PassShape& ps, Rsrc rec, int ns, int nf, int tp, EvalSlots& S) {
-  const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
-  const unsigned pass = (unsigned)(ro + 1);
-  const int ieff = ps.ieff;
-  const int nquad = ps.rows * kShareQuads;
-  const int wbase = uni(tp & ~63);  // this wave's first tp
-  unsigned pend = 0u;  // bits 0..1 edge slots, 2..5 plane slots, 6.. share quads
-#pragma unroll
-  for (int k = 0; k < kEdgeSlots; k++) {
-    blk_absent(S.e[k]);
-    if (tp + k * kEvalThreads < ns) pend |= 1u << k;
-  }
-#pragma unroll
-  for (int k = 0; k < kPlaneSlots; k++) {
-    blk_absent(S.p[k]);
-    if (tp + k * kEvalThreads < nf) pend |= 1u << (kEdgeSlots + k);
-  }
-  constexpr int kQ0 = kEdgeSlots + kPlaneSlots;
-  static_assert(kQ0 + kQuadRounds <= 32, "pending bits");
-  static_assert(kQuadRounds * kEvalThreads * 16 <= 65536, "the DMA's LDS addresses below 64 KiB");
-#pragma unroll
-  for (int i = 0; i < kQuadRounds; i++)
-    if (tp + i * kEvalThreads < nquad) pend |= 1u << (kQ0 + i);
-  auto ready = [&](int item) {
-    return __hip_atomic_load(&gt.ready[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == pass;
-  };
-  auto row_of = [&](int w) {  // the row whose tag covers query w's record
-    return w < ctl.Q * ieff ? w / ctl.Q : ps.steal ? kMaxShareItems + (w - ctl.Q * ieff) : (w / ctl.Q) % ieff;
-  };
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  constexpr unsigned kRecBits = (1u << kQ0) - 1u;
-  while (__ballot((pend & ~kRecBits) != 0u) != 0ull) {  // share quads pending
-    const bool all = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&gt.all, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
-    if (!all) {  // records of the rows complete so far (the rest wait for gather_records)
-#pragma unroll
-      for (int k = 0; k < kEdgeSlots; k++) {
-        const int w = tp + k * kEvalThreads;
-        if (((pend >> k) & 1u) && ready(row_of(w))) {
-          rec_load(rec, w, true, S.e[k]);
-          pend &= ~(1u << k);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kPlaneSlots; k++) {
-        const int w = ns + tp + k * kEvalThreads;
-        if (((pend >> (kEdgeSlots + k)) & 1u) && ready(row_of(w))) {
-          rec_load(rec, w, true, S.p[k]);
-          pend &= ~(1u << (kEdgeSlots + k));
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < kQuadRounds; i++) {
-      const int Q = tp + i * kEvalThreads, item = Q / kShareQuads;
-      if (!uni(wbase + i * kEvalThreads < nquad)) continue;  // no lane of this wave has a quad in round i
-      if (((pend >> (kQ0 + i)) & 1u) && ready(item)) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(parts, (__attribute__((address_space(3))) void*)&gt.shr[wbase + i * kEvalThreads], 16,
-                                                 item * 256 + (Q - item * kShareQuads) * 16, 0, 0, kAuxSc1);
-        pend &= ~(1u << (kQ0 + i));
-      }
-    }
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&gt.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * ctl.wait_ticks) {  // never expected: wave 0's bound is half
-      if (lane_id() == 0) {
-        st_rlx(ctl.abort_w() + 1, 5u);
-        st_rlx(ctl.abort_w(), 1u);
-        st_rlx(ctl.abort_w() + 2, 1u);
-      }
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  S.tail = __ballot(tp + kEvalThreads < ns || tp + 3 * kEvalThreads < nf) != 0ull;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' LDS writes have landed (and the records)
-  return pend & kRecBits;
-}
-
-// The records gather_fill left out (every row is complete by now), landed on return.
-__device__ __forceinline__ void gather_records(Rsrc rec, int ns, int tp, unsigned pend, EvalSlots& S) {
-#pragma unroll
-  for (int k = 0; k < kEdgeSlots; k++)
-    if ((pend >> k) & 1u) rec_load(rec, tp + k * kEvalThreads, true, S.e[k]);
-#pragma unroll
-  for (int k = 0; k < kPlaneSlots; k++)
-    if ((pend >> (kEdgeSlots + k)) & 1u) rec_load(rec, ns + tp + k * kEvalThreads, true, S.p[k]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <bool kProg>
-__device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, EngGather* gt,
+__device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm,
                                                int c, int k, int ro, const PassShape& ps, Rsrc rec, bool wave0, unsigned tk) {
   const int ns = a.n_feat[k * 4 + 0], nf = a.n_feat[k * 4 + 2];
   const int lane = lane_id();
   const int tp = (int)threadIdx.x - 64;
   const int ieff = ps.ieff;
   EvalSlots S;
-  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;  // share quad q of rows g, g + 32, ..., g + 224 (+ 256 ..)
-  double d0[8], d1[8], e0 = 0.0, e1 = 0.0;
-  unsigned recpend = 0u;  // records gather_fill left for gather_records
-  // the stolen overflow queries' rows (complete once their pass is), straight from memory: their own
-  // pairwise tree over rows g + 32 j, added last
-  auto overflow_rows = [&](double& u0, double& u1) {
-    const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
-    v4u v[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int o = g + 32 * j;
-      v[j] = __builtin_amdgcn_raw_buffer_load_b128(parts, (kMaxShareItems + (o < ps.novf ? o : 0)) * 256 + q * 16, 0, kAuxSc1);
-    }
-    double f0[8], f1[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const bool ok = g + 32 * j < ps.novf && q < kShareQuads;
-      f0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].y << 32) | v[j].x)) : 0.0;
-      f1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v[j].w << 32) | v[j].z)) : 0.0;
-    }
-#pragma unroll
-    for (int h = 1; h < 8; h <<= 1)
-#pragma unroll
-      for (int j = 0; j + h < 8; j += 2 * h) { f0[j] += f0[j + h]; f1[j] += f1[j + h]; }
-    u0 = f0[0];
-    u1 = f1[0];
-  };
-  if constexpr (kProg) {
-    if (ps.ieff > 0) {
-      if (wave0) {
-        eng_prof(tk, 1, rt_now());
-        const bool ok = gather_poll(a, ctl, *gt, c, ro, ps);
-        if (lane == 0) {
-          sh.flag0 = ok;
-          __hip_atomic_store(&gt->all, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // after the ready flags
-        }
-        eng_prof(tk, 1, rt_now());
-      } else {
-        recpend = gather_fill(a, ctl, *gt, c, ro, ps, rec, ns, nf, tp, S);
-      }
-    } else if (wave0 && lane == 0) {
-      sh.flag0 = 1;
-    }
-    __syncthreads();
-    if (wave0 && lane == 0) __hip_atomic_store(&gt->all, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // next pass
-    if (!uni(sh.flag0)) return false;
-    auto rows8 = [&](int r0, double (&u0)[8], double (&u1)[8]) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int it = r0 + g + 32 * j;
-        const bool ok = it < ps.rows && q < kShareQuads;
-        const v4u v = gt->shr[ok ? it * kShareQuads + q : 0];
-        u0[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x)) : 0.0;
-        u1[j] = ok ? __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z)) : 0.0;
-      }
-    };
-    if (ps.steal && ps.novf > 0) overflow_rows(e0, e1);
-    rows8(0, d0, d1);
-  } else {
-    // the items' rows (the records follow while wave 0 takes step 0: it needs only the shares)
-    if (ps.steal && ps.novf > 0) overflow_rows(e0, e1);
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;  // share quad q of rows g, g + 32, ..., g + 224
+  double d0[8], d1[8];
+  {  // the items' rows (the records follow while wave 0 takes step 0: it needs only the shares)
     const Rsrc parts = make_rsrc(part_row(a, ctl, c, 0), (unsigned)(ctl.P * 256));
     v4u v[8];
 #pragma unroll
@@ -2727,7 +2633,7 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
     for (int h = 1; h < 8; h <<= 1)
 #pragma unroll
       for (int j = 0; j + h < 8; j += 2 * h) { d0[j] += d0[j + h]; d1[j] += d1[j + h]; }
-    if (q < kShareQuads) { sh.red[g][2 * q] = d0[0] + e0; sh.red[g][2 * q + 1] = d1[0] + e1; }
+    if (q < kShareQuads) { sh.red[g][2 * q] = d0[0]; sh.red[g][2 * q + 1] = d1[0]; }
   }
   __syncthreads();
   LdsLM& s = *(LdsLM*)&lm;
@@ -2798,8 +2704,7 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
     }
   } else {
     // the records not loaded yet, while wave 0 takes step 0
-    if constexpr (kProg) gather_records(rec, ns, tp, recpend, S);
-    else if (ieff > 0) eval_slots_load(rec, ns, nf, tp, S);
+    if (ieff > 0) eval_slots_load(rec, ns, nf, tp, S);
     __syncthreads();
     bool more = uni(sh.flag) != 0;
     while (more) {
@@ -2813,16 +2718,9 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
 }
 
 // The solve role of chain c (ticket c): every pass of the chain, in order.  false = aborted.
-// gt: the progressive gather's LDS (kProg), else null.
-template <bool kProg>
-__device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, EngGather* gt,
-                                               int c, bool wave0, unsigned tk) {
+__device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, EngLM& lm, int c,
+                                               bool wave0, unsigned tk) {
   const int lane = lane_id();
-  if constexpr (kProg) {
-    for (int i = threadIdx.x; i < kMaxShareRows; i += kEngThreads) gt->ready[i] = 0u;
-    if (threadIdx.x == 0) { gt->abort = 0; gt->all = 0; }
-    __syncthreads();
-  }
   const size_t rec_stride = (size_t)(a.cap_sharp + a.cap_flat) * 9;  // doubles per chain (a.blk)
   const Rsrc rec = make_rsrc(a.blk + (size_t)c * rec_stride, (unsigned)((a.cap_sharp + a.cap_flat) * kRecBytes));
   double* st = a.state + (size_t)c * 16;
@@ -2841,16 +2739,14 @@ __device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& 
     const PassShape ps = pass_shape(a, ctl, k);
     const int ieff = ps.ieff;
     const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1)) + tk;  // profile slot of the pass (developer builds)
-    if constexpr (!kProg) {
-      if (wave0 && lane == 0) {
-        eng_prof(ptk, 1, rt_now());
-        sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 3u) : 1;
-        eng_prof(ptk, 1, rt_now());
-      }
-      __syncthreads();
-      if (!uni(sh.flag0)) return false;
+    if (wave0 && lane == 0) {
+      eng_prof(ptk, 1, rt_now());
+      sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 3u) : 1;
+      eng_prof(ptk, 1, rt_now());
     }
-    if (!eng_solve_pass<kProg>(a, ctl, sh, lm, gt, c, k, ro, ps, rec, wave0, ptk)) return false;
+    __syncthreads();
+    if (!uni(sh.flag0)) return false;
+    if (!eng_solve_pass(a, ctl, sh, lm, c, k, ro, ps, rec, wave0, ptk)) return false;
     if (wave0 && lane == 0) {
       const int nc = sh.nc, np = sh.np;
       int* so = a.stats + (size_t)k * 8;
@@ -2939,6 +2835,7 @@ __device__ __forceinline__ int eng_wants_prefetch(const OdomArgs& a, const EngCt
 
 // One association item ticket (pass ro, chain c, item): wait for the pass's x, run the item's
 // queries, publish its records and share.  false = aborted.
+template <int kQpw>
 __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, bool wave0, bool lead,
                                                 const ItemTicket& it) {
   bool ok = true;
@@ -2949,7 +2846,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   int k;
   bool live = pair_of(a, c, r, &k);
   // items holding queries of pair k: ceil((sharp + flat) / Q), none for a gated-off scan
-  PassShape ps{0, 0, 0, false};
+  PassShape ps{0, 0};
   if (live) ps = pass_shape(a, ctl, k);
   const int ieff = ps.ieff;
   if (item >= ieff) live = false;  // an empty item: nothing to wait for or signal
@@ -2960,22 +2857,21 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   // done in the common case; then every wave loads what needs no x while the lead waits for x.
   if (wave0) {
     if (lead) {
-      sh.ovc = 0;
       sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 1u) : true;
     }
   }
   __syncthreads();
   ok = uni(sh.flag0) != 0;
   if (ok && live) {  // each wave parks its first query's loads in its LDS slots
-    const ItemPre pre = eng_item_pre(a, k, item * ctl.Q + (int)(threadIdx.x >> 6), warm, o);
-    const int wv = (int)(threadIdx.x >> 6), l = lane_id();
+    const int wv = (int)(threadIdx.x >> 6), row = kQpw == 4 ? lane_id() >> 4 : 0, l = lane_id() & 15;
+    const ItemPre pre = eng_item_pre(a, k, (item * ctl.Q + wv) * kQpw + row, warm, o);
     P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
     int wi = pre.wi[0];
     if (l == 1) { v = pre.wp[0]; wi = pre.wi[1]; }
     if (l == 2) { v = pre.wp[1]; wi = pre.wi[2]; }
     if (l == 3) v = pre.wp[2];
-    if (l < 4) sh.prew[wv][l] = v;
-    if (l < 3) sh.prei[wv][l] = wi;
+    if (l < 4 && (kQpw == 4 || lane_id() < 4)) sh.prew[wv][row][l] = v;
+    if (l < 3 && (kQpw == 4 || lane_id() < 3)) sh.prei[wv][row][l] = wi;
   }
   if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, (int)blockDim.x - 64);
   if (wave0) {
@@ -2996,7 +2892,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
       const int l = lane_id();
       if (l < 7) sh.xw[threadIdx.x >> 6][l] = eng_x_word(a, c, r, o, l);
     }
-    eng_item_run(a, ctl, sh, c, k, ro, item, ps, rec, warm, o, ptk);
+    eng_item_run<kQpw>(a, ctl, sh, k, item, ps, rec, warm, o, ptk);
     drain_stores();  // this wave's record (and seed) stores
     __syncthreads();
     if (wave0) {
@@ -3032,6 +2928,11 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
 __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   __shared__ EngLM lm;
+#ifdef LISLAM_ENG_ZERO_LDS  // developer: start from zeroed LDS (a read-before-write hunt)
+  for (int i = threadIdx.x; i < (int)(sizeof(EngShared) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&sh)[i] = 0u;
+  for (int i = threadIdx.x; i < (int)(sizeof(EngLM) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&lm)[i] = 0u;
+  __syncthreads();
+#endif
   const unsigned per_ro = (unsigned)ctl.C * ctl.I;
   const unsigned total = (unsigned)ctl.roles + per_ro * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
@@ -3050,9 +2951,9 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
     bool ok = true;
     if (tk < (unsigned)ctl.roles) {
       const int c = uni((int)tk);
-      ok = eng_solve_role<false>(a, ctl, sh, lm, nullptr, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+      ok = eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
     } else {
-      ok = eng_item_ticket(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
+      ok = eng_item_ticket<1>(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
     }
     if (wave0) {
       if (lead) {
@@ -3073,25 +2974,18 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
 // roles on one reserved CU per XCD, the items on the others.  An item workgroup then leaves half
 // of its CU's registers and most of its LDS to whatever else runs (the next batch's extraction,
 // the ORB front end), and the roles always find a CU (launch_odometry_chain).
-// The roles' gather: 1 = progressive (wave 0 polls every row's tag, waves 1.. load each complete
-// row as it lands), 0 = bulk (wait for the pass's item count, then load every row at once).
-#ifndef LISLAM_ENG_PROG
-#define LISLAM_ENG_PROG 0
-#endif
-struct RolesLds {  // EngGather first: its DMA addresses stay below 64 KiB
-  EngGather gt;
-  EngShared sh;
-  EngLM lm;
-};
 
 // The grid is one workgroup per role CU (at least C): a workgroup takes the next chain from a ticket
 // when it starts, so the chains go to whichever role CUs are free (another engine may hold some:
 // LISLAM_ENGINE_DEPTH), and the workgroups left over exit at once.
 __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
-  __shared__ RolesLds L;
-  EngShared& sh = L.sh;
-  EngLM& lm = L.lm;
-  EngGather& gt = L.gt;
+  __shared__ EngShared sh;
+  __shared__ EngLM lm;
+#ifdef LISLAM_ENG_ZERO_LDS  // developer: start from zeroed LDS (a read-before-write hunt)
+  for (int i = threadIdx.x; i < (int)(sizeof(EngShared) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&sh)[i] = 0u;
+  for (int i = threadIdx.x; i < (int)(sizeof(EngLM) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&lm)[i] = 0u;
+  __syncthreads();
+#endif
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
   if (wave0) {
     if (lane_id() == 0) sh.ticket = add_rlx(ctl.role_ticket(), 1u);
@@ -3099,12 +2993,13 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl c
   __syncthreads();
   const int c = uni((int)sh.ticket);
   if (c >= ctl.C) return;
-  (void)eng_solve_role<LISLAM_ENG_PROG != 0>(a, ctl, sh, lm, &gt, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+  (void)eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
 }
 
 #ifndef LISLAM_ITEM_WPE
 #define LISLAM_ITEM_WPE 4  // waves per SIMD the items are compiled for: 4 = 128 VGPRs
 #endif
+template <int kQpw>
 __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_items(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
@@ -3120,7 +3015,7 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
   __syncthreads();
   unsigned tk = (unsigned)uni((int)sh.ticket);
   while (tk < total) {
-    const bool ok = eng_item_ticket(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
+    const bool ok = eng_item_ticket<kQpw>(a, ctl, sh, wave0, lead, item_ticket(ctl, tk));
     if (wave0) {
       if (lead) {
         const unsigned t = add_rlx(ctl.ticket(), 1u);
@@ -3133,9 +3028,13 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
   }
 }
 
-static int item_waves();
+static int item_waves(int qpw);
+static int engine_qpw();
 // Items per (pass, chain) of the split engine (the developer profile's ticket layout).
-extern "C" int lislam_debug_engine_items(int cap_queries) { return (cap_queries + item_waves() - 1) / item_waves(); }
+extern "C" int lislam_debug_engine_items(int cap_queries) {
+  const int qpi = item_waves(engine_qpw()) * engine_qpw();
+  return (cap_queries + qpi - 1) / qpi;
+}
 // A number per engine launch (the item rows' tags tell this launch's passes from an earlier one's).
 static unsigned next_engine_gen() {
   static std::atomic<unsigned> gen{0};
@@ -3144,15 +3043,21 @@ static unsigned next_engine_gen() {
 
 int engine_items(int cap_queries) { return (cap_queries + kEngWaves - 1) / kEngWaves; }  // rows: Q >= kEngWaves
 
-// Waves (= queries) per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (8 ..
-// kMaxItemWaves), default kDefaultItemWaves.
-constexpr int kDefaultItemWaves = 8;
-static int item_waves() {
-  const char* e = getenv("LISLAM_ENGINE_ITEM_WAVES");
-  const int q = e ? atoi(e) : kDefaultItemWaves;
-  return q >= kEngWaves && q <= kMaxItemWaves ? q : kDefaultItemWaves;
+// Queries per wave of the split engine's items: LISLAM_ENGINE_QPW = 4 (four 16-lane rows), else 1
+// (the 64-lane searches).
+static int engine_qpw() {
+  const char* e = getenv("LISLAM_ENGINE_QPW");
+  return e && atoi(e) == 4 ? 4 : 1;
 }
-int engine_part_rows(int cap_queries) { return max(engine_items(cap_queries), kMaxShareRows); }
+// Waves per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (up to kMaxItemWaves, and
+// at least kEngWaves queries per item: the share rows are sized for that), default 8 / 4 (qpw 1 / 4).
+static int item_waves(int qpw) {
+  const int def = qpw == 4 ? 4 : 8;
+  const char* e = getenv("LISLAM_ENGINE_ITEM_WAVES");
+  const int q = e ? atoi(e) : def;
+  return q * qpw >= kEngWaves && q <= kMaxItemWaves ? q : def;
+}
+int engine_part_rows(int cap_queries) { return max(engine_items(cap_queries), kMaxShareItems); }
 
 bool use_chain_engine(const OdomArgs& a, int mode) {
   if (mode == 0 || a.n_chains < 1 || !a.eng_ctl) return false;
@@ -3184,7 +3089,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   ctl.I = engine_items(a.cap_sharp + a.cap_flat);
   ctl.prefetch = 1;
   ctl.roles = ctl.C;
-  ctl.steal = 0;  // the bulk gather (k_odom_chain) reads the items' rows only
+  ctl.qpw = 1;
   // every device wait is bounded (2 s); LISLAM_ENGINE_WAIT_US shortens it (tests: a forced abort)
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
@@ -3198,7 +3103,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, (resident - ctl.C - 1) / ctl.C));
   // zero the control words of this launch, all but word 3 (the sticky abort)
-  const size_t words = ((size_t)4 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf
+  const size_t words = ((size_t)4 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), st);
   (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), st);
   // LISLAM_ENGINE_WGS caps the grid (tests: one workgroup drains the whole queue)
@@ -3278,11 +3183,11 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
-  ctl.Q = item_waves();
-  ctl.I = (a.cap_sharp + a.cap_flat + ctl.Q - 1) / ctl.Q;
+  ctl.qpw = engine_qpw();
+  ctl.Q = item_waves(ctl.qpw);
+  ctl.I = (a.cap_sharp + a.cap_flat + ctl.qpi() - 1) / ctl.qpi();
   ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
   ctl.roles = 0;
-  ctl.steal = getenv("LISLAM_ENGINE_STEAL") ? atoi(getenv("LISLAM_ENGINE_STEAL")) : 0;
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
   // One item workgroup per CU of the items' mask (all CUs but one per XCD): its 8 waves at <= 128
@@ -3299,7 +3204,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
-  const size_t words = ((size_t)5 + ctl.C + (size_t)4 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, ovf, role ticket
+  const size_t words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
   // engines in flight per device: LISLAM_ENGINE_DEPTH (default 2: a launch waits for the one before
   // the last, so two chains run together — two item workgroups per CU at 128 VGPRs — and each
   // chain's idle association slots, while its solve runs, serve the other chain)
@@ -3323,7 +3228,8 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
-  hipLaunchKernelGGL(k_odom_items, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
+  if (ctl.qpw == 4) hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
+  else hipLaunchKernelGGL(k_odom_items<1>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
   (void)hipEventRecord(join_r, roles);
   (void)hipEventRecord(join_i, items);
   (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do

@@ -75,7 +75,7 @@ with pkg.Context() as ctx:
     w0 = items[:, :, 5] > 0
     med = lambda col: np.array([np.median(items[i, w0[i], col]) for i in range(2 * R)]) * us
     rows["association wave 0: query load + transform + seeds"] = med(4)
-    rows["association wave 0: 1-NN (nn_wave)"] = med(5)
+    rows["association wave 0: 1-NN (nn_wave / nn16)"] = med(5)
     rows["association wave 0: line searches + record"] = med(6)
     rows["association item: first-evaluation share (wave 0)"] = med(7)
     rows["association wave 0: 1-NN, outer 1 (seeded)"] = med(5)[1::2]
@@ -107,17 +107,10 @@ with pkg.Context() as ctx:
               f"ready p50 {np.median(la[:, 2]):.1f}, run p50 {np.median(la[:, 3]):.1f}; item index p50 {np.median(la[:, 4]):.0f}")
         for row in la[np.argsort(-la[:, 2])][:8]:
             print("   late item: claim %.1f wait %.1f ready %.1f run %.1f item %d" % tuple(row))
-    # overflow queries taken by the items' first free waves (eng_steal): when the stealing wave
-    # claimed (its own query done), the stolen query's run, and the item's last own query
-    stl = items[:, :, 8] > 0
-    if stl.any():
-        rel = lambda col: np.concatenate([(items[i, stl[i], col] - a_start[i]) for i in range(2 * R)]) * us
-        rows["steal: claim after the pass's first ready"] = rel(8)
-        rows["steal: stolen query run (claim -> row published)"] = rel(9) - rel(8)
-        rows["steal: stealing item's last own query end (after first ready)"] = rel(10)
-        rows["steal: stolen rows per pass"] = stl.sum(1)
-        ok10 = valid & (items[:, :, 10] > 0)
-        rows["all items: last own query end (after first ready)"] = np.concatenate(
+    # the end of each item's last query (slot 10), after the pass's first ready item
+    ok10 = valid & (items[:, :, 10] > 0)
+    if ok10.any():
+        rows["all items: last query end (after first ready)"] = np.concatenate(
             [(items[i, ok10[i], 10] - a_start[i]) for i in range(2 * R)]) * us
     for k, v in rows.items():
         print(f"  {k:62s} mean {np.mean(v):7.2f} us  p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}")

@@ -279,3 +279,31 @@ def test_odom_step_recovers_from_an_engine_abort(pkg, oracle, synth):
     finally:
         odo.close()
         c.close()
+
+
+@pytest.mark.parametrize("qpw", ["1", "4"])
+def test_engine_over_poisoned_buffers(pkg, oracle, synth, qpw):
+    """Every batch buffer filled with 0xFF bytes (NaN doubles, -1 words) before first use
+    (LISLAM_POISON, the library's read-before-write probe): the engine's records are written whole
+    for every query, with or without a correspondence, so a stale non-finite word from an earlier
+    use of the memory never enters an evaluation (weighted by 0 it would still be NaN).  Before the
+    fix the first pair's second solve diverged (para off by 4.8e-3) whenever such words were left."""
+    os.environ["LISLAM_POISON"] = "255"
+    os.environ["LISLAM_ENGINE_QPW"] = qpw
+    try:
+        c = pkg.Context(n_scans=64, width=1024)
+        scans = synth.make_sequence(5, start=40)
+        b = pkg.Batch(c, 5)
+        b.upload(scans)
+        b.extract(5)
+        b.odometry(5, 4)
+        c.synchronize()
+        feats = [oracle.scan_registration(s) for s in scans]
+        pose, rel, st = oracle.odometry_chain(feats)
+        assert b.odometry_engine() != 0
+        check_chain(pkg, b, feats, pose, rel, st)
+        b.close()
+        c.close()
+    finally:
+        del os.environ["LISLAM_POISON"]
+        del os.environ["LISLAM_ENGINE_QPW"]
