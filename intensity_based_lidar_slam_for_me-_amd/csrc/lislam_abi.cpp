@@ -108,6 +108,9 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
     const int m = atoi(e);
     if (m >= LISLAM_ENGINE_OFF && m <= LISLAM_ENGINE_ON) c->odom_engine = m;
   }
+  // LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed the engine's shape (lislam_set_engine_shape)
+  if (const char* e = getenv("LISLAM_ENGINE_QPW")) c->eng_qpw = atoi(e) == 4 ? 4 : 1;
+  if (const char* e = getenv("LISLAM_ENGINE_DEPTH")) c->eng_depth = std::min(4, std::max(1, atoi(e)));
   *out = c;
   return LISLAM_OK;
 }
@@ -591,6 +594,8 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
   }
   o.c0 = 0;
   o.cn = o.n_chains;
+  o.eng_qpw = c->eng_qpw;
+  o.eng_depth = c->eng_depth;
   if (lislam::use_chain_engine(o, c->odom_engine)) {
     // few long chains: one persistent launch sequences every round on the device
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1030,6 +1035,14 @@ int lislam_eval_factors(lislam_ctx* c, int32_t n, const int32_t* kind, const dou
 int lislam_set_odometry_schedule(lislam_ctx* c, int32_t mode) {
   if (!c || mode < LISLAM_ENGINE_OFF || mode > LISLAM_ENGINE_ON) return LISLAM_ERR_ARG;
   c->odom_engine = mode;
+  return LISLAM_OK;
+}
+
+int lislam_set_engine_shape(lislam_ctx* c, int32_t queries_per_wave, int32_t depth) {
+  if (!c || (queries_per_wave != 0 && queries_per_wave != 1 && queries_per_wave != 4) || depth < 0 || depth > 4)
+    return LISLAM_ERR_ARG;
+  if (queries_per_wave) c->eng_qpw = queries_per_wave;
+  if (depth) c->eng_depth = depth;
   return LISLAM_OK;
 }
 

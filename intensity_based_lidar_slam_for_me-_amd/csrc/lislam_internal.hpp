@@ -103,6 +103,7 @@ struct OdomArgs {
   // chain engine (k_odom_chain): control words (zeroed before every launch) and the per-query
   // association of the first outer pass, the second pass's starting bounds
   unsigned* eng_ctl;  // [8 + 10 S]
+  int eng_qpw, eng_depth;  // the split engine's shape (lislam_set_engine_shape)
   int* warm;          // [n_chains][cap_sharp + cap_flat][4]
   double* eng_part;   // [n_chains][engine_part_rows][32]: each association item's (and overflow query's)
                       // share of the first evaluation

@@ -3029,10 +3029,10 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
 }
 
 static int item_waves(int qpw);
-static int engine_qpw();
-// Items per (pass, chain) of the split engine (the developer profile's ticket layout).
-extern "C" int lislam_debug_engine_items(int cap_queries) {
-  const int qpi = item_waves(engine_qpw()) * engine_qpw();
+// Items per (pass, chain) of the split engine at qpw queries per wave (the developer profile's
+// ticket layout).
+extern "C" int lislam_debug_engine_items(int cap_queries, int qpw) {
+  const int qpi = item_waves(qpw) * qpw;
   return (cap_queries + qpi - 1) / qpi;
 }
 // A number per engine launch (the item rows' tags tell this launch's passes from an earlier one's).
@@ -3043,12 +3043,6 @@ static unsigned next_engine_gen() {
 
 int engine_items(int cap_queries) { return (cap_queries + kEngWaves - 1) / kEngWaves; }  // rows: Q >= kEngWaves
 
-// Queries per wave of the split engine's items: LISLAM_ENGINE_QPW = 4 (four 16-lane rows), else 1
-// (the 64-lane searches).
-static int engine_qpw() {
-  const char* e = getenv("LISLAM_ENGINE_QPW");
-  return e && atoi(e) == 4 ? 4 : 1;
-}
 // Waves per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (up to kMaxItemWaves, and
 // at least kEngWaves queries per item: the share rows are sized for that), default 8 / 4 (qpw 1 / 4).
 static int item_waves(int qpw) {
@@ -3183,7 +3177,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
-  ctl.qpw = engine_qpw();
+  ctl.qpw = a.eng_qpw == 4 ? 4 : 1;  // lislam_set_engine_shape
   ctl.Q = item_waves(ctl.qpw);
   ctl.I = (a.cap_sharp + a.cap_flat + ctl.qpi() - 1) / ctl.qpi();
   ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
@@ -3205,10 +3199,10 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
   const size_t words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
-  // engines in flight per device: LISLAM_ENGINE_DEPTH (default 2: a launch waits for the one before
-  // the last, so two chains run together — two item workgroups per CU at 128 VGPRs — and each
-  // chain's idle association slots, while its solve runs, serve the other chain)
-  const int depth = getenv("LISLAM_ENGINE_DEPTH") ? std::min(EngineGate::kMaxDepth, std::max(1, atoi(getenv("LISLAM_ENGINE_DEPTH")))) : 2;
+  // engines in flight per device (lislam_set_engine_shape; 2 by default: a launch waits for the one
+  // before the last, so two chains run together — at one query per wave, two item workgroups per
+  // CU at 128 VGPRs — and each chain's idle association slots, while its solve runs, serve the other)
+  const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
   EngineGate* gate = engine_gate(dev);
   std::unique_lock<std::mutex> lock;
   hipEvent_t prev = nullptr;

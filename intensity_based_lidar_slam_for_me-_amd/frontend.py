@@ -52,6 +52,15 @@ class Context:
         launch, k_odom_chain) or ENGINE_AUTO.  Results are the same."""
         nat.check(self.lib.lislam_set_odometry_schedule(self.h, int(mode)), self.h, "lislam_set_odometry_schedule")
 
+    SHAPE_LATENCY = (1, 2)     # lislam_set_engine_shape: one query per wavefront, two engines in flight
+    SHAPE_THROUGHPUT = (4, 4)  # four queries per wavefront, four engines in flight (pipelined contexts)
+
+    def set_engine_shape(self, queries_per_wave: int = 0, depth: int = 0):
+        """lislam_set_engine_shape: the chain engine's queries per wavefront (1 or 4) and engines in
+        flight per device (1..4) for this context's launches; 0 keeps a value.  Results are the same."""
+        nat.check(self.lib.lislam_set_engine_shape(self.h, int(queries_per_wave), int(depth)), self.h,
+                  "lislam_set_engine_shape")
+
     def set_tie_order(self, order: int):
         """Order of equal voxels in the a7 VoxelGrid (lislam_set_tie_order): TIES_REFERENCE
         (default, PCL 1.10's std::sort order, bit-exact) or TIES_INDEX (input order, faster)."""

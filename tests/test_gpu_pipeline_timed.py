@@ -1,12 +1,14 @@
 """The configuration the headline times, checked against the oracle: bench.py's pipelined schedule
 (bench.pipeline) over two contexts, each with its own batch of 61 scans (one continuous 60-pair
-chain, laserOdometry.cpp:130-135,417-717), for four steps.  Step s's chain runs in the split engine
-(k_odom_roles + k_odom_items on their CU-masked streams) while step s + 1's extraction and step s's
-ORB cascade run beside it on the same CUs, and the context stream joins the engine only at the
-batch's next call: the co-residency, deferred join and agent-scope hand-offs the engine was built
-for.  Afterwards each context holds its last step's outputs (context 0: step 2, context 1: step 3),
-and every pair's pose, para, correspondence counts and LM iterations, and the ORB front end's stats
-and T_s2s, must equal the oracle's over the same scans."""
+chain, laserOdometry.cpp:130-135,417-717), each context queued from its own host thread.  Step s's
+chain runs in the split engine (k_odom_roles + k_odom_items on their CU-masked streams) while other
+steps' chains, extraction and ORB cascades run beside it on the same CUs, and the context stream
+joins the engine only at the batch's next call: the co-residency, deferred join and agent-scope
+hand-offs the engine was built for.  Two engine shapes (lislam_set_engine_shape): latency (one
+query per wavefront, two engines in flight, two contexts, four steps) and throughput (four queries
+per wavefront, four engines in flight, four contexts, eight steps: bench.py's default).  Afterwards
+each context holds its last step's outputs, and every pair's pose, para, correspondence counts and
+LM iterations, and the ORB front end's stats and T_s2s, must equal the oracle's over the same scans."""
 import numpy as np
 import pytest
 
@@ -14,13 +16,13 @@ pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-4  # BASELINE.json north_star: <= 1e-4 m / <= 1e-4 rad
 S = 61
-STEPS = 4
+STARTS = (100, 400, 700, 1000)  # a different stretch of the corridor per context
 
 
 @pytest.fixture(scope="module")
 def sequences(oracle, synth):
     out = []
-    for start in (100, 400):  # a different stretch of the corridor per context
+    for start in STARTS:
         scans = synth.make_sequence(S, start=start)
         feats = [oracle.scan_registration(s) for s in scans]
         pose, rel, st = oracle.odometry_chain(feats)
@@ -31,17 +33,19 @@ def sequences(oracle, synth):
     return out
 
 
-def test_pipelined_two_context_steps_match_the_oracle(pkg, sequences):
+@pytest.mark.parametrize("shape,k,steps", [("latency", 2, 4), ("throughput", 4, 8)])
+def test_pipelined_steps_match_the_oracle(pkg, sequences, shape, k, steps):
     import bench
 
-    nat = pkg.native
-    ctxs = [pkg.Context(n_scans=64, width=1024) for _ in range(2)]
+    ctxs = [pkg.Context(n_scans=64, width=1024) for _ in range(k)]
+    for c in ctxs:
+        c.set_engine_shape(*(c.SHAPE_LATENCY if shape == "latency" else c.SHAPE_THROUGHPUT))
     bats = [pkg.Batch(c, S) for c in ctxs]
     try:
         for b, seq in zip(bats, sequences):
             b.upload(seq[0])
         mask = pkg.intensity.set_mask(64, 1024)
-        bench.pipeline(bats, S, STEPS, S - 1, 2, (1000, mask))
+        bench.pipeline(bats, S, steps, S - 1, k, (1000, mask))
         for c in ctxs:
             c.synchronize()
         worst = 0.0
@@ -64,7 +68,7 @@ def test_pipelined_two_context_steps_match_the_oracle(pkg, sequences):
             pd = bench.pose_delta(snap, chains, True)
             assert pd["within_tolerance"] and pd["stats_mismatches"] == 0 and pd["orb_stats_mismatches"] == 0
         assert orb_pairs > 0
-        print(f"pipelined 2-context steps: max |pose - oracle| = {worst:.3g} over {2 * (S - 1)} pairs, "
+        print(f"pipelined {k}-context steps ({shape}): max |pose - oracle| = {worst:.3g} over {k * (S - 1)} pairs, "
               f"{orb_pairs} ORB-optimized pairs")
     finally:
         for b in bats:
