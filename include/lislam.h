@@ -215,13 +215,14 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
 int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
 /* The chain engine's shape for this context's launches (results are the same).
  * queries_per_wave: 1 = one association query per wavefront (64-lane searches: the shortest chain,
- * but one engine's association waves fill half of every CU), 4 = four per wavefront (16-lane rows:
- * each query is slower, the engine holds a quarter of the waves, so several engines and the next
- * batches' extraction share the GPU); 0 = keep.  depth = engines in flight per device when a launch
- * of this context enters the device's queue (1..4; a launch waits for the one `depth` launches
- * before it); 0 = keep.  Latency (one sequence at a time): 1 / 2, the default.  Throughput (several
- * pipelined contexts, e.g. bench.py): 4 / 4.  LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed a new
- * context's shape. */
+ * but one engine's association waves fill half of every CU); 2, 3 = that many 64-lane queries one
+ * after another per wavefront; 4 = four at once, one per 16-lane row.  Above 1 each chain is
+ * slower but an engine holds a fraction of the waves, so several engines and the next batches'
+ * extraction share the GPU.  0 = keep.  depth = engines in flight per device when a launch of this
+ * context enters the device's queue (1..4; a launch waits for the one `depth` launches before it);
+ * 0 = keep.  Latency (one sequence at a time): 1 / 2, the default.  Throughput (several pipelined
+ * contexts, e.g. bench.py): 3 / 4.  LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed a new context's
+ * shape. */
 int lislam_set_engine_shape(lislam_ctx* ctx, int32_t queries_per_wave, int32_t depth);
 /* status = the number of engine launches of the batch that gave up since the previous status call
  * (one of the engine's bounded device waits expired, e.g. when its two launches could not run

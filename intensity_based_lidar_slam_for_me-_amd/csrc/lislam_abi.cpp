@@ -109,7 +109,7 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
     if (m >= LISLAM_ENGINE_OFF && m <= LISLAM_ENGINE_ON) c->odom_engine = m;
   }
   // LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed the engine's shape (lislam_set_engine_shape)
-  if (const char* e = getenv("LISLAM_ENGINE_QPW")) c->eng_qpw = atoi(e) == 4 ? 4 : 1;
+  if (const char* e = getenv("LISLAM_ENGINE_QPW")) c->eng_qpw = std::min(4, std::max(1, atoi(e)));
   if (const char* e = getenv("LISLAM_ENGINE_DEPTH")) c->eng_depth = std::min(4, std::max(1, atoi(e)));
   *out = c;
   return LISLAM_OK;
@@ -1039,7 +1039,7 @@ int lislam_set_odometry_schedule(lislam_ctx* c, int32_t mode) {
 }
 
 int lislam_set_engine_shape(lislam_ctx* c, int32_t queries_per_wave, int32_t depth) {
-  if (!c || (queries_per_wave != 0 && queries_per_wave != 1 && queries_per_wave != 4) || depth < 0 || depth > 4)
+  if (!c || queries_per_wave < 0 || queries_per_wave > 4 || depth < 0 || depth > 4)
     return LISLAM_ERR_ARG;
   if (queries_per_wave) c->eng_qpw = queries_per_wave;
   if (depth) c->eng_depth = depth;

@@ -752,10 +752,10 @@ __device__ __forceinline__ uint32_t row_bits(uint64_t m) { return (uint32_t)(m >
 // Which pending chunks a round takes never changes a minimum (every chunk whose bound is not
 // above the best is evaluated before a search ends); K only trades loads per lane for round trips.
 #ifndef LISLAM_NN16_K
-#define LISLAM_NN16_K 8
+#define LISLAM_NN16_K 4
 #endif
 #ifndef LISLAM_LS16_K
-#define LISLAM_LS16_K 8
+#define LISLAM_LS16_K 4
 #endif
 constexpr int kNn16K = LISLAM_NN16_K, kLs16K = LISLAM_LS16_K;
 
@@ -1523,7 +1523,7 @@ struct EngCtl {
   unsigned gen;  // this launch's number: with the pass, the tag of a complete item row (eng_tag)
   int P;         // rows per chain of eng_part (engine_part_rows)
   int Q;         // the association item workgroup's waves
-  int qpw;       // queries per wave: 1 (the 64-lane searches) or 4 (one per 16-lane row)
+  int qpw;       // queries per wave: 1..3 (64-lane searches, one after another) or 4 (one per 16-lane row)
   __host__ __device__ int qpi() const { return Q * qpw; }  // queries per item
   __device__ unsigned* ticket() const { return w; }
   __device__ unsigned* abort_w() const { return w + 1; }
@@ -2024,12 +2024,12 @@ __device__ __forceinline__ bool eng_check(const EngCtl& ctl, bool ok, unsigned c
   return false;
 }
 
-// One association item: wave wv of item `item` takes queries (item + m ieff) qpi + wv qpw (+ the
-// row, four 16-lane rows per wave when qpw = 4), m = 0, 1, ...: one round while the pair's queries
-// fit ieff items (the common case), more when the pair holds more queries than the engine keeps
-// items in flight (EngCtl::budget), so that no item waits for a workgroup to come free.  The wave's
-// share of the first evaluation (its blocks' 28 sums at x, and the corner / plane counts) goes to
-// sh.red[wave].
+// One association item: wave wv of item `item` takes queries (item + m ieff) qpi + wv qpw + s,
+// s < qpw (four 16-lane rows at once when qpw = 4, else one 64-lane query after another), m = 0,
+// 1, ...: one round while the pair's queries fit ieff items (the common case), more when the pair
+// holds more queries than the engine keeps items in flight (EngCtl::budget), so that no item waits
+// for a workgroup to come free.  The wave's share of the first evaluation (its blocks' 28 sums at
+// x, and the corner / plane counts) goes to sh.red[wave].
 template <int kQpw>
 __device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ctl, EngShared& sh, int k, int item,
                                              const PassShape& ps, Rsrc rec, int* warm, int outer, unsigned tk) {
@@ -2044,17 +2044,32 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ct
   for (int m = 0;; m++) {
     const int w0 = (item + m * ieff) * ctl.Q * kQpw + ql * kQpw;  // the wave's first query
     if (w0 >= nq) break;  // wave-uniform
-    const int w = w0 + row;
-    ItemPre pre;
-    if (m > 0) {
-      pre = eng_item_pre(a, k, w, warm, outer);
-    } else {  // loaded before x existed, parked in this wave's LDS slots
-      pre.qp = sh.prew[ql][row][0];
+    if constexpr (kQpw == 4) {
+      const int w = w0 + row;
+      ItemPre pre;
+      if (m > 0) {
+        pre = eng_item_pre(a, k, w, warm, outer);
+      } else {  // loaded before x existed, parked in this wave's LDS slots
+        pre.qp = sh.prew[ql][row][0];
 #pragma unroll
-      for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][row][1 + e]; pre.wi[e] = sh.prei[ql][row][e]; }
+        for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][row][1 + e]; pre.wi[e] = sh.prei[ql][row][e]; }
+      }
+      eng_query16(a, k, w, w < nq, rec, warm, outer, tk, pre, x, sh.red[ql]);
+    } else {
+      for (int s = 0; s < kQpw; s++) {  // the wave's queries one after another (slot s: parked by row s)
+        const int w = w0 + s;
+        if (w >= nq) break;  // wave-uniform
+        ItemPre pre;
+        if (m > 0) {
+          pre = eng_item_pre(a, k, w, warm, outer);
+        } else {
+          pre.qp = sh.prew[ql][s][0];
+#pragma unroll
+          for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][s][1 + e]; pre.wi[e] = sh.prei[ql][s][e]; }
+        }
+        eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
+      }
     }
-    if constexpr (kQpw == 4) eng_query16(a, k, w, w < nq, rec, warm, outer, tk, pre, x, sh.red[ql]);
-    else eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
   }
   if (lane_id() == 0) eng_prof(tk, 10, rt_now());
 }
@@ -2863,15 +2878,17 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   __syncthreads();
   ok = uni(sh.flag0) != 0;
   if (ok && live) {  // each wave parks its first query's loads in its LDS slots
-    const int wv = (int)(threadIdx.x >> 6), row = kQpw == 4 ? lane_id() >> 4 : 0, l = lane_id() & 15;
+    // lane group `row` (16 lanes) loads the wave's query row: its 16-lane row (qpw 4) or its row-th
+    // query in turn (qpw 2, 3)
+    const int wv = (int)(threadIdx.x >> 6), row = kQpw > 1 ? min(lane_id() >> 4, kQpw - 1) : 0, l = lane_id() & 15;
     const ItemPre pre = eng_item_pre(a, k, (item * ctl.Q + wv) * kQpw + row, warm, o);
     P4 v = pre.qp;  // selects, not a lane-indexed array (which would live in scratch)
     int wi = pre.wi[0];
     if (l == 1) { v = pre.wp[0]; wi = pre.wi[1]; }
     if (l == 2) { v = pre.wp[1]; wi = pre.wi[2]; }
     if (l == 3) v = pre.wp[2];
-    if (l < 4 && (kQpw == 4 || lane_id() < 4)) sh.prew[wv][row][l] = v;
-    if (l < 3 && (kQpw == 4 || lane_id() < 3)) sh.prei[wv][row][l] = wi;
+    if (l < 4 && lane_id() < 16 * kQpw) sh.prew[wv][row][l] = v;
+    if (l < 3 && lane_id() < 16 * kQpw) sh.prei[wv][row][l] = wi;
   }
   if (!wave0 && ok && live && uni(sh.pref)) eng_prefetch(a, sh, k, threadIdx.x - 64, (int)blockDim.x - 64);
   if (wave0) {
@@ -3044,7 +3061,7 @@ static unsigned next_engine_gen() {
 int engine_items(int cap_queries) { return (cap_queries + kEngWaves - 1) / kEngWaves; }  // rows: Q >= kEngWaves
 
 // Waves per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (up to kMaxItemWaves, and
-// at least kEngWaves queries per item: the share rows are sized for that), default 8 / 4 (qpw 1 / 4).
+// at least kEngWaves queries per item: the share rows are sized for that), default 8 (qpw 1..3) / 4.
 static int item_waves(int qpw) {
   const int def = qpw == 4 ? 4 : 8;
   const char* e = getenv("LISLAM_ENGINE_ITEM_WAVES");
@@ -3177,7 +3194,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
-  ctl.qpw = a.eng_qpw == 4 ? 4 : 1;  // lislam_set_engine_shape
+  ctl.qpw = a.eng_qpw >= 1 && a.eng_qpw <= 4 ? a.eng_qpw : 1;  // lislam_set_engine_shape
   ctl.Q = item_waves(ctl.qpw);
   ctl.I = (a.cap_sharp + a.cap_flat + ctl.qpi() - 1) / ctl.qpi();
   ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
@@ -3222,8 +3239,12 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
-  if (ctl.qpw == 4) hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
-  else hipLaunchKernelGGL(k_odom_items<1>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
+  switch (ctl.qpw) {
+    case 4: hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    case 3: hipLaunchKernelGGL(k_odom_items<3>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    case 2: hipLaunchKernelGGL(k_odom_items<2>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    default: hipLaunchKernelGGL(k_odom_items<1>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+  }
   (void)hipEventRecord(join_r, roles);
   (void)hipEventRecord(join_i, items);
   (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do

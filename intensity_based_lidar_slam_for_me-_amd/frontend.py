@@ -53,10 +53,10 @@ class Context:
         nat.check(self.lib.lislam_set_odometry_schedule(self.h, int(mode)), self.h, "lislam_set_odometry_schedule")
 
     SHAPE_LATENCY = (1, 2)     # lislam_set_engine_shape: one query per wavefront, two engines in flight
-    SHAPE_THROUGHPUT = (4, 4)  # four queries per wavefront, four engines in flight (pipelined contexts)
+    SHAPE_THROUGHPUT = (3, 4)  # three queries per wavefront, four engines in flight (pipelined contexts)
 
     def set_engine_shape(self, queries_per_wave: int = 0, depth: int = 0):
-        """lislam_set_engine_shape: the chain engine's queries per wavefront (1 or 4) and engines in
+        """lislam_set_engine_shape: the chain engine's queries per wavefront (1..4) and engines in
         flight per device (1..4) for this context's launches; 0 keeps a value.  Results are the same."""
         nat.check(self.lib.lislam_set_engine_shape(self.h, int(queries_per_wave), int(depth)), self.h,
                   "lislam_set_engine_shape")
