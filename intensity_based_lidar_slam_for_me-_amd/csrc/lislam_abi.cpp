@@ -350,7 +350,8 @@ static int output_source(lislam_batch* b, int what, int scan, const void** src_o
 
 int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
-  SETTLE(b);
+  // no engine settle: the chain engine (and its per-round re-run) reads the features, never the
+  // points, so the next batch's bytes move while the engine runs
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   const size_t n = (size_t)n_scans * b->N;
@@ -377,7 +378,8 @@ int lislam_batch_upload(lislam_batch* b, const void* points, int32_t n_scans, co
 
 int lislam_batch_upload_async(lislam_batch* b, const void* points, int32_t n_scans, const lislam_point_layout* layout) {
   if (!b || !points || n_scans < 1 || n_scans > b->max_scans) return LISLAM_ERR_ARG;
-  SETTLE(b);
+  // no engine settle: the chain engine (and its per-round re-run) reads the features, never the
+  // points, so the next batch's bytes move while the engine runs
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   static const lislam_point_layout kPacked{16, 0, 4, 8, 12};
@@ -497,7 +499,8 @@ int lislam_batch_download_cloud(lislam_batch* b, int32_t what, int32_t scan, voi
 
 int lislam_batch_input_device_ptr(lislam_batch* b, void** dptr) {
   if (!b || !dptr) return LISLAM_ERR_ARG;
-  SETTLE(b);
+  // no engine settle: the chain engine (and its per-round re-run) reads the features, never the
+  // points, so the next batch's bytes move while the engine runs
   *dptr = (void*)b->fa.pts;
   return LISLAM_OK;
 }

@@ -35,6 +35,7 @@
 #include "lislam_ctx.hpp"
 #include "lislam_device.hpp"
 #include "lislam_lm.hpp"
+#include "lislam_lm_wave.hpp"
 
 namespace lislam {
 namespace mapk {
@@ -799,7 +800,7 @@ constexpr int kMaxParts = 256;
 constexpr int kPart = kAcc + 2;  // acc + edge / plane block counts
 
 struct LmDev {
-  LM s;
+  EngLM s;  // the step state (lislam_lm_wave.hpp), staged through LDS by the launch that steps
   double x0[7], xe[7];
   int flag, phase, nedge, nplane;
 };
@@ -849,31 +850,11 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, con
   lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
 }
 
-// Thread 0's trust-region step after evaluation e (summed into acc).  Inlined: its registers are
-// live only after the evaluation's, so the kernel stays within 256 VGPRs without scratch (a
-// non-inlined call kept LM in scratch memory, every access a memory round trip).
-__device__ __forceinline__ bool lm_solve_step(LM* s, int e, const double* acc, const double* x0, int max_it, int* nedge,
-                                           int* nplane) {
-  if (e == 0) {
-    *nedge = (int)acc[kAcc];
-    *nplane = (int)acc[kAcc + 1];
-    if (*nedge + *nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
-      for (int k = 0; k < 7; k++) s->x[k] = x0[k];
-      s->it = 0;
-      s->term = 1;
-      return false;
-    }
-    double xs[7];
-    for (int k = 0; k < 7; k++) xs[k] = x0[k];
-    return lm_start(*s, xs, acc, max_it);
-  }
-  return lm_next(*s, acc, max_it);
-}
-
 // One evaluation of ceres::Solve with its trust-region step (solve_device launches it max_it + 1
 // times; a launch after the solve has ended returns at once): every workgroup sums its strided share
 // of the records (lm_eval_partial) and counts itself in; the last one sums the partials in workgroup
-// order (deterministic) and takes the step on thread 0 — the separate one-thread step launch per
+// order (deterministic) and takes the step on its wave 0 (lislam_lm_wave.hpp, the chain engine's
+// step: a short fp64 chain, the state through LDS) — the separate one-thread step launch per
 // evaluation is gone.  x_out / summary (k_lm_finish's outputs) are written when the solve ends.
 __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec, const int* kind, const int* ncount, int n,
                                                               LmDev* st, double* partial, unsigned* arrive, int max_it,
@@ -919,22 +900,54 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
     acc[threadIdx.x] = v;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  *arrive = 0u;  // the next evaluation's count (its launch follows this one on the stream)
-  LM s = st->s;
+  if (threadIdx.x >= 64) return;  // wave 0 takes the step (lislam_lm_wave.hpp: every lane alike)
+  const int lane = threadIdx.x;
+  if (lane == 0) *arrive = 0u;  // the next evaluation's count (its launch follows this one on the stream)
+  __shared__ EngLM sl;
+  constexpr int kWords = (int)(sizeof(EngLM) / 4);
+  for (int i = lane; i < kWords; i += 64) reinterpret_cast<unsigned*>(&sl)[i] = reinterpret_cast<const unsigned*>(&st->s)[i];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  LdsLM& s = *(LdsLM*)&sl;
+  const int phase = st->phase;
   int nedge = st->nedge, nplane = st->nplane;
-  const bool cont = lm_solve_step(&s, st->phase, acc, st->x0, max_it, &nedge, &nplane);
-  st->s = s;
+  double a[kAcc];
+#pragma unroll
+  for (int e = 0; e < kAcc; e++) a[e] = acc[e];
+  bool cont;
+  if (phase == 0) {
+    nedge = (int)acc[kAcc];
+    nplane = (int)acc[kAcc + 1];
+    double x0[7];
+#pragma unroll
+    for (int e = 0; e < 7; e++) x0[e] = st->x0[e];
+    if (nedge + nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
+#pragma unroll
+      for (int e = 0; e < 7; e++) s.x[e] = x0[e];
+      s.it = 0;
+      s.term = 1;
+      cont = false;
+    } else {
+      cont = eng_step(s, x0, a, true, max_it);
+    }
+  } else {
+    cont = eng_step(s, nullptr, a, false, max_it);
+  }
+  if (cont) eng_step_post(s);  // the candidate's parameter tolerance and 1 / model cost change
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < kWords; i += 64) reinterpret_cast<unsigned*>(&st->s)[i] = reinterpret_cast<const unsigned*>(&sl)[i];
+  if (lane != 0) return;
   st->nedge = nedge;
   st->nplane = nplane;
-  st->phase++;
+  st->phase = phase + 1;
   st->flag = cont;
   if (cont)
-    for (int e = 0; e < 7; e++) st->xe[e] = s.xc[e];
-  if (!cont || st->phase > max_it) {  // the solve's end (or its last launch)
+    for (int e = 0; e < 7; e++) st->xe[e] = sl.xc[e];
+  if (!cont || phase + 1 > max_it) {  // the solve's end (or its last launch)
     if (x_out)
-      for (int e = 0; e < 7; e++) x_out[e] = s.x[e];
-    if (summary) { summary[0] = s.it; summary[1] = s.term; summary[2] = nedge; summary[3] = nplane; }
+      for (int e = 0; e < 7; e++) x_out[e] = sl.x[e];
+    if (summary) { summary[0] = sl.it; summary[1] = sl.term; summary[2] = nedge; summary[3] = nplane; }
   }
 }
 
