@@ -40,7 +40,7 @@ struct lislam_ctx {
   lislam_ktimer mtimer;            // mapping-kernel timing
   int ties = LISLAM_TIES_REFERENCE;  // lislam_set_tie_order
   int odom_engine = LISLAM_ENGINE_AUTO;     // lislam_set_odometry_schedule
-  int eng_qpw = 1, eng_depth = 2;           // lislam_set_engine_shape
+  int eng_qpw = 1, eng_depth = 1;           // lislam_set_engine_shape (the latency shape)
   // lislam_eval_factors(_raw): one grow-only device buffer for the blocks, the parameters and the
   // outputs, reused across calls; the mutex serializes callers (Ceres evaluates residual blocks
   // from num_threads threads)

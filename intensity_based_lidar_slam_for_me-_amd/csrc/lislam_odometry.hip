@@ -2771,11 +2771,11 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
   }
 }
 
-static int item_waves(int qpw);
-// Items per (pass, chain) of the split engine at qpw queries per wave (the developer profile's
-// ticket layout).
-extern "C" int lislam_debug_engine_items(int cap_queries, int qpw) {
-  const int qpi = item_waves(qpw) * qpw;
+static int item_waves(int qpw, int depth);
+// Items per (pass, chain) of the split engine at qpw queries per wave and `depth` engines in flight
+// (the developer profile's ticket layout).
+extern "C" int lislam_debug_engine_items(int cap_queries, int qpw, int depth) {
+  const int qpi = item_waves(qpw, depth) * qpw;
   return (cap_queries + qpi - 1) / qpi;
 }
 // A number per engine launch (the item rows' tags tell this launch's passes from an earlier one's).
@@ -2787,9 +2787,12 @@ static unsigned next_engine_gen() {
 int engine_items(int cap_queries) { return (cap_queries + kEngWaves - 1) / kEngWaves; }  // rows: Q >= kEngWaves
 
 // Waves per item workgroup of the split engine: LISLAM_ENGINE_ITEM_WAVES (up to kMaxItemWaves, and
-// at least kEngWaves queries per item: the share rows are sized for that), default 8 (qpw 1..3) / 4.
-static int item_waves(int qpw) {
-  const int def = qpw == 4 ? 4 : 8;
+// at least kEngWaves queries per item: the share rows are sized for that); by default 12 for one
+// engine at a time at one query per wave (248 x 12 waves hold a pass's ~2,100 queries in one
+// round: no overflow round, 25.0 vs 26.9 ms per chain), else 8 (qpw 1..3: two engines' items fit
+// a CU's 16 wave slots at 128 VGPRs) / 4 (qpw 4).
+static int item_waves(int qpw, int depth) {
+  const int def = qpw == 4 ? 4 : (qpw == 1 && depth == 1) ? 12 : 8;
   const char* e = getenv("LISLAM_ENGINE_ITEM_WAVES");
   const int q = e ? atoi(e) : def;
   return q * qpw >= kEngWaves && q <= kMaxItemWaves ? q : def;
@@ -2921,7 +2924,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   ctl.C = a.n_chains;
   ctl.R = min(a.chain_len, a.S - 1);
   ctl.qpw = a.eng_qpw >= 1 && a.eng_qpw <= 4 ? a.eng_qpw : 1;  // lislam_set_engine_shape
-  ctl.Q = item_waves(ctl.qpw);
+  ctl.Q = item_waves(ctl.qpw, std::max(1, a.eng_depth));
   ctl.I = (a.cap_sharp + a.cap_flat + ctl.qpi() - 1) / ctl.qpi();
   ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
   ctl.roles = 0;

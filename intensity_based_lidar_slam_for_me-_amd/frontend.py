@@ -52,7 +52,7 @@ class Context:
         launch, k_odom_chain) or ENGINE_AUTO.  Results are the same."""
         nat.check(self.lib.lislam_set_odometry_schedule(self.h, int(mode)), self.h, "lislam_set_odometry_schedule")
 
-    SHAPE_LATENCY = (1, 2)     # lislam_set_engine_shape: one query per wavefront, two engines in flight
+    SHAPE_LATENCY = (1, 1)     # lislam_set_engine_shape: one query per wavefront, one engine at a time
     SHAPE_THROUGHPUT = (3, 4)  # three queries per wavefront, four engines in flight (pipelined contexts)
 
     def set_engine_shape(self, queries_per_wave: int = 0, depth: int = 0):

@@ -37,7 +37,8 @@ with pkg.Context() as ctx:
     b.extract(S)
     b.odometry(S, S - 1)
     ctx.synchronize()
-    I = lib.lislam_debug_engine_items(12 * 64 + 24 * 64, 4 if os.environ.get("LISLAM_ENGINE_QPW") == "4" else 1)
+    I = lib.lislam_debug_engine_items(12 * 64 + 24 * 64, int(os.environ.get("LISLAM_ENGINE_QPW", "1")),
+                                      int(os.environ.get("LISLAM_ENGINE_DEPTH", "1")))
     R = S - 1
     T = 2 * R * (I + 1)
     assert lib.lislam_debug_engine_prof(T) == 0

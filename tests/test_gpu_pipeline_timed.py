@@ -5,7 +5,7 @@ chain runs in the split engine (k_odom_roles + k_odom_items on their CU-masked s
 steps' chains, extraction and ORB cascades run beside it on the same CUs, and the context stream
 joins the engine only at the batch's next call: the co-residency, deferred join and agent-scope
 hand-offs the engine was built for.  Two engine shapes (lislam_set_engine_shape): latency (one
-query per wavefront, two engines in flight, two contexts, four steps) and throughput (three queries
+query per wavefront, one engine in flight, two contexts, four steps) and throughput (three queries
 per wavefront, four engines in flight, four contexts, eight steps: bench.py's default).  Afterwards
 each context holds its last step's outputs, and every pair's pose, para, correspondence counts and
 LM iterations, and the ORB front end's stats and T_s2s, must equal the oracle's over the same scans."""
