@@ -2926,7 +2926,10 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   ctl.qpw = a.eng_qpw >= 1 && a.eng_qpw <= 4 ? a.eng_qpw : 1;  // lislam_set_engine_shape
   ctl.Q = item_waves(ctl.qpw, std::max(1, a.eng_depth));
   ctl.I = (a.cap_sharp + a.cap_flat + ctl.qpi() - 1) / ctl.qpi();
-  ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : 1;
+  // waiting items warm their XCD's L2 with the pair's target structures: with one engine in flight
+  // (with several, each warming all eight L2s for its own pair evicts the others': 18.9k vs 17.9k
+  // scans/s over three alternating runs at the throughput shape, profiles/r05_shape_ab.txt)
+  ctl.prefetch = getenv("LISLAM_ENGINE_PREFETCH") ? atoi(getenv("LISLAM_ENGINE_PREFETCH")) : (a.eng_depth <= 1 ? 1 : 0);
   ctl.roles = 0;
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;

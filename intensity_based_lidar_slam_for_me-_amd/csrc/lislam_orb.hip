@@ -65,7 +65,7 @@ constexpr int kFastT = 20;
 #define LISLAM_SEL_THREADS 512
 #endif
 constexpr int kSelThreads = LISLAM_SEL_THREADS;  // k_orb_select workgroup
-constexpr int kPairThreads = 1024;
+constexpr int kPairThreads = 512;  // k_orb_match: 8 waves, so a workgroup finds room beside the chain engines
 constexpr int kLmThreads = 256;
 constexpr int kNoMatch = 0x7f7f7f7f;
 #ifndef LISLAM_FAST_BAND
@@ -1376,11 +1376,11 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 // The same result on the matrix cores: Hamming(q, t) = |q| + |t| - 2 <q, t> with the 256
 // descriptor bits as 0/1 int8 vectors and <q, t> from v_mfma_i32_16x16x64_i8 (four k-steps of 64
 // bits; A and B fragments use one and the same lane -> k map, so the dot product does not depend
-// on the hardware's k order).  A workgroup = 16 waves x 16 trains; each 256-query tile is expanded
-// to 0/1 bytes in LDS once and read by the 16 waves.  By the C/D layout lane l owns train column
+// on the hardware's k order).  A workgroup = kXmWaves waves x 16 trains; each 256-query tile is expanded
+// to 0/1 bytes in LDS once and read by all the waves.  By the C/D layout lane l owns train column
 // l & 15 and query rows 4 (l >> 4) .. +3 of every 16-query tile, so its running first minimum
 // follows query order; the four lanes of a column merge by (distance, query) at the end.
-constexpr int kXmWaves = 16;                // waves per workgroup
+constexpr int kXmWaves = 8;                 // waves per workgroup (8: room beside the chain engines)
 constexpr int kXmTrains = 16 * kXmWaves;    // trains per workgroup (16 per wave)
 constexpr int kXmQTile = 256;   // queries expanded per LDS tile
 constexpr int kXmRow = 272;     // LDS bytes per expanded query (256 + 16: rows start on distinct banks)
