@@ -136,6 +136,21 @@ const char* lislam_last_error(const lislam_ctx* c) { return c ? c->err.c_str() :
 
 static int engine_settle(lislam_batch* b);
 
+// The per-round schedule's chain groups: 2 streams, so one group's solves overlap another's
+// association (a solve occupies one workgroup per chain, far from filling the device).  Made when
+// that schedule first runs (or an engine launch is recovered on it): a batch that only runs the
+// engine holds no extra hardware queue.
+static int round_streams(lislam_batch* b) {
+  lislam_ctx* c = b->ctx;
+  b->odo_stream[0] = c->stream;
+  for (int g = 1; g < lislam_batch::kGroups; g++) {
+    if (!b->odo_stream[g] && !lislam::work_stream(c->device, &b->odo_stream[g])) return fail(c, LISLAM_ERR_DEVICE, "stream");
+    if (!b->odo_join[g]) HIPCHK(c, hipEventCreateWithFlags(&b->odo_join[g], hipEventDisableTiming));
+  }
+  if (lislam_batch::kGroups > 1 && !b->odo_fork) HIPCHK(c, hipEventCreateWithFlags(&b->odo_fork, hipEventDisableTiming));
+  return LISLAM_OK;
+}
+
 int lislam_synchronize(lislam_ctx* c) {
   if (!c) return LISLAM_ERR_ARG;
   hipSetDevice(c->device);
@@ -183,6 +198,7 @@ static int engine_settle(lislam_batch* b) {
   HIPCHK(c, hipMemsetAsync(b->oa.eng_ctl + 3, 0, sizeof(unsigned), c->stream));
   b->eng_fallbacks++;
   // the per-round schedule has no device waits: it cannot abort
+  if (round_streams(b) != LISLAM_OK) return LISLAM_ERR_DEVICE;
   lislam::launch_odometry(b->eng_args, b->odo_stream, lislam_batch::kGroups, b->odo_fork, b->odo_join, nullptr,
                           &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
@@ -580,16 +596,7 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     HIPCHK(c, hipEventRecord(b->stage_ev, c->stream));
     b->stage_busy = true;
   }
-  // chain groups: 2 streams, so one group's solves overlap another's
-  // association (a solve occupies one workgroup per chain, far from filling the device); the engine's
-  // abort recovery runs the same schedule, so the streams exist before any engine launch
   const int G = lislam_batch::kGroups;
-  b->odo_stream[0] = c->stream;
-  for (int g = 1; g < G; g++) {
-    if (!b->odo_stream[g] && !lislam::work_stream(c->device, &b->odo_stream[g])) return fail(c, LISLAM_ERR_DEVICE, "stream");
-    if (!b->odo_join[g]) HIPCHK(c, hipEventCreateWithFlags(&b->odo_join[g], hipEventDisableTiming));
-  }
-  if (G > 1 && !b->odo_fork) HIPCHK(c, hipEventCreateWithFlags(&b->odo_fork, hipEventDisableTiming));
   std::vector<lislam::OdoTimed>* ev = nullptr;
   if (b->timing) {
     b->odo_ev.emplace_back();
@@ -641,6 +648,7 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
     return LISLAM_OK;
   }
   b->engine_ran = false;
+  if (round_streams(b) != LISLAM_OK) return LISLAM_ERR_DEVICE;
   launch_odometry(o, b->odo_stream, G, b->odo_fork, b->odo_join, ev, &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
   return LISLAM_OK;
