@@ -310,8 +310,10 @@ int lislam_batch_create(lislam_ctx* c, int32_t max_scans, lislam_batch** out) {
 int lislam_batch_destroy(lislam_batch* b) {
   if (!b) return LISLAM_OK;
   hipSetDevice(b->ctx->device);
-  if (b->eng_roles) hipStreamSynchronize(b->eng_roles);
-  if (b->eng_items) hipStreamSynchronize(b->eng_items);
+  if (b->eng_pending) {  // the batch's last engine launch (its streams are the device's, shared)
+    hipEventSynchronize(b->eng_join_r);
+    hipEventSynchronize(b->eng_join_i);
+  }
   hipStreamSynchronize(b->ctx->stream);
   {
     auto& v = b->ctx->batches;
@@ -326,8 +328,6 @@ int lislam_batch_destroy(lislam_batch* b) {
     if (b->odo_join[g]) hipEventDestroy(b->odo_join[g]);
   }
   if (b->odo_fork) hipEventDestroy(b->odo_fork);
-  if (b->eng_roles) { hipStreamSynchronize(b->eng_roles); hipStreamDestroy(b->eng_roles); }
-  if (b->eng_items) { hipStreamSynchronize(b->eng_items); hipStreamDestroy(b->eng_items); }
   for (hipEvent_t e : {b->eng_fork, b->eng_join_r, b->eng_join_i}) if (e) hipEventDestroy(e);
   for (hipEvent_t e : b->pool) hipEventDestroy(e);
   if (b->orb) lislam_free_orb(b->orb);
@@ -613,7 +613,7 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
       // LISLAM_ENGINE_SINGLE=1: the single-launch engine (k_odom_chain) even where CU masks exist
       // (read once per batch: the tests run both engines in one process)
       const bool single = getenv("LISLAM_ENGINE_SINGLE") && atoi(getenv("LISLAM_ENGINE_SINGLE")) == 1;
-      b->eng_split = !single && lislam::engine_streams(c->device, &b->eng_roles, &b->eng_items) ? 1 : 0;
+      b->eng_split = !single && lislam::engine_streams_available(c->device) ? 1 : 0;
       if (b->eng_split) {
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_fork, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&b->eng_join_r, hipEventDisableTiming));
@@ -624,22 +624,21 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
       b->h_abort[0] = b->h_abort[1] = 0;
     }
     if (ev) { e0 = b->get_event(); e1 = b->get_event(); }
-    hipStream_t tail = c->stream;  // where the engine ends
     if (b->eng_split) {
       // the inputs: everything queued on the context stream so far (the last extract, any per-round
-      // odometry queued after it, the staging copies just queued)
+      // odometry queued after it, the staging copies just queued); the launch copies its abort words
+      // to h_abort and records eng_done on its own stream
       HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
-      lislam::launch_odometry_chain_split(o, b->eng_roles, b->eng_items, b->eng_ready, b->eng_fork, b->eng_join_r,
-                                          b->eng_join_i, e0, e1);
+      lislam::launch_odometry_chain_split(o, b->eng_ready, b->eng_fork, b->eng_join_r, b->eng_join_i, e0, e1,
+                                          b->h_abort, b->eng_done);
       b->eng_pending = true;
-      tail = b->eng_items;  // joined with the roles stream
     } else {
       if (ev) HIPCHK(c, hipEventRecord(e0, c->stream));
       lislam::launch_odometry_chain(o, c->stream);
       if (ev) HIPCHK(c, hipEventRecord(e1, c->stream));
+      HIPCHK(c, hipMemcpyAsync(b->h_abort, b->oa.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipEventRecord(b->eng_done, c->stream));
     }
-    HIPCHK(c, hipMemcpyAsync(b->h_abort, b->oa.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, tail));
-    HIPCHK(c, hipEventRecord(b->eng_done, tail));
     b->eng_args = o;
     b->eng_check = true;
     b->engine_ran = true;

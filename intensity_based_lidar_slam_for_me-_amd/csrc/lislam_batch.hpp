@@ -40,10 +40,10 @@ struct lislam_batch {
   std::vector<hipEvent_t> pool;
   int extracted = 0;
   bool engine_ran = false;  // the last odometry call ran the chain engine (lislam_batch_odometry_status)
-  // the engine's two CU-masked streams (roles / items) and their fork / join events; split: -1 not
-  // tried yet, 0 unavailable (single-launch engine), 1 ready
+  // the split engine's fork / join events (its two CU-masked streams are the device's: a pair per
+  // engine slot, shared by every batch); split: -1 not tried yet, 0 unavailable (single-launch
+  // engine), 1 ready
   int eng_split = -1;
-  hipStream_t eng_roles = nullptr, eng_items = nullptr;
   hipEvent_t eng_fork = nullptr, eng_join_r = nullptr, eng_join_i = nullptr;
   // the split engine is not joined back into the context stream at launch (a join there would also
   // hold back whatever another context queued behind it on a shared hardware queue): eng_pending

@@ -146,14 +146,16 @@ void launch_odometry(const OdomArgs& a, const hipStream_t* streams, int ngroups,
 // The same schedule as ONE persistent launch (k_odom_chain, lislam_odometry.hip): every round of
 // the a.n_chains chains, association and solve, sequenced on the device.  Returns the grid size.
 int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
-// The same engine as two launches (k_odom_roles on `roles`, k_odom_items on `items`, CU-masked
-// streams from engine_streams), forked from and joined back into st by the three events.
-// Nothing is queued on the context stream: the roles stream waits for `ready` (the inputs) and for
-// the previous engine of the device, the items stream forks from it; join_r / join_i mark the end
-// (the caller makes its stream wait for them later); t0 / t1 (nullable): timing events.
-int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_t items, hipEvent_t ready, hipEvent_t fork,
-                                hipEvent_t join_r, hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1);
-bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items);
+// The same engine as two launches (k_odom_roles / k_odom_items on a CU-masked stream pair).
+// Nothing is queued on the context stream: the launch takes the device's next engine slot (its
+// stream pair, shared by every batch: engine_streams_available), the roles stream waits for `ready`
+// (the inputs) and for the launch `depth` before it, the items stream forks from it; join_r /
+// join_i mark the end (the caller makes its stream wait for them later); t0 / t1 (nullable): timing
+// events; h_abort (nullable): pinned host words the launch's error / sticky abort words are copied
+// to at its end, `done` (nullable) recorded after that copy.  0 = no launch (no CU masks).
+int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
+                                hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done);
+bool engine_streams_available(int dev);  // the device has CU-masked streams for the split engine
 // A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).
 bool work_stream(int dev, hipStream_t* s);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's

@@ -2855,14 +2855,14 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   return grid;
 }
 
-// The engine as two launches (k_odom_roles / k_odom_items) on streams of their own, made once per
-// batch (engine_streams); false = unavailable on this device (the caller runs the single-launch
-// engine instead).  CU-masked streams: a mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950,
-// measured: scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD unmasked), the
-// roles one CU in every XCD, the items every other CU, so an item workgroup never takes the CU a
-// solve role needs whole (256 VGPRs x 8 waves).  (Unmasked priority streams were measured to starve
-// the role of a whole CU under the pipelined extraction, r04i, and are not offered.)
-bool engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
+// The engine as two launches (k_odom_roles / k_odom_items) on a pair of CU-masked streams
+// (make_engine_streams); false = unavailable on this device (the caller runs the single-launch
+// engine instead).  A mask bit i selects a CU of XCD i % 8 (gfx942 / gfx950, measured:
+// scripts/micro/cumask.hip; a mask with no bit of some XCD leaves that XCD unmasked), the roles one
+// CU in every XCD, the items every other CU, so an item workgroup never takes the CU a solve role
+// needs whole (256 VGPRs x 8 waves).  (Unmasked priority streams were measured to starve the role
+// of a whole CU under the pipelined extraction, r04i, and are not offered.)
+static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
@@ -2903,19 +2903,37 @@ bool work_stream(int dev, hipStream_t* s) {
 // one, so two pipelined batches' chains do not split the CUs the extraction beside them needs.  The
 // wait on the previous engine and the re-record of the event are one critical section (the mutex),
 // so two host threads launching on different contexts cannot both pass the gate.
+// Slot s of the ring also owns a pair of engine streams, shared by every batch of the device: the
+// launches of all contexts run on kMaxDepth stream pairs, not one pair per batch, so five or six
+// pipelined contexts do not push the process past the device's hardware queues (past ~20 masked
+// queues every launch slowed: the isolated chain 34.7 -> 47-50 ms with six contexts, r05c56).
 struct EngineGate {
   static constexpr int kMaxDepth = 4;
   std::mutex mu;
   hipEvent_t ev[kMaxDepth] = {};
+  hipStream_t roles[kMaxDepth] = {}, items[kMaxDepth] = {};
   int next = 0;
+  int avail = -1;  // -1 not probed, 0 no CU masks on this device, 1 ready
 };
 static EngineGate* engine_gate(int dev) {
   static EngineGate gates[64];
   return dev >= 0 && dev < 64 ? &gates[dev] : nullptr;
 }
 
-int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_t items, hipEvent_t ready, hipEvent_t fork,
-                                hipEvent_t join_r, hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1) {
+bool engine_streams_available(int dev) {
+  EngineGate* g = engine_gate(dev);
+  if (!g) return false;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->avail < 0) {
+    g->avail = 1;
+    for (int s = 0; s < EngineGate::kMaxDepth && g->avail; s++)
+      if (!make_engine_streams(dev, &g->roles[s], &g->items[s])) g->avail = 0;
+  }
+  return g->avail == 1;
+}
+
+int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
+                                hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
   if (a.n_chains <= 0) return 0;
   EngCtl ctl;
   ctl.gen = next_engine_gen();
@@ -2953,15 +2971,13 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   // CU at 128 VGPRs — and each chain's idle association slots, while its solve runs, serve the other)
   const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
   EngineGate* gate = engine_gate(dev);
-  std::unique_lock<std::mutex> lock;
-  hipEvent_t prev = nullptr;
-  if (gate) {
-    lock = std::unique_lock<std::mutex>(gate->mu);
-    gate->next = (gate->next + 1) % depth;
-    hipEvent_t& e = gate->ev[gate->next];
-    if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    prev = e;  // recorded by the launch depth launches ago; re-recorded below
-  }
+  if (!gate || gate->avail != 1) return 0;
+  std::unique_lock<std::mutex> lock(gate->mu);
+  gate->next = (gate->next + 1) % depth;
+  hipEvent_t& e = gate->ev[gate->next];
+  if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  hipEvent_t prev = e;  // recorded by the launch depth launches ago; re-recorded below
+  hipStream_t roles = gate->roles[gate->next], items = gate->items[gate->next];  // the slot's streams
   (void)hipStreamWaitEvent(roles, ready, 0);
   if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
   if (t0) (void)hipEventRecord(t0, roles);
@@ -2981,7 +2997,11 @@ int launch_odometry_chain_split(const OdomArgs& a, hipStream_t roles, hipStream_
   (void)hipEventRecord(join_i, items);
   (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do
   if (t1) (void)hipEventRecord(t1, items);
-  if (prev) (void)hipEventRecord(prev, items);
+  // the launch's error and sticky abort words to the host, and its end, before the slot's next
+  // launch can queue behind it (still under the gate's lock)
+  if (h_abort) (void)hipMemcpyAsync(h_abort, a.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, items);
+  if (done) (void)hipEventRecord(done, items);
+  (void)hipEventRecord(prev, items);
   return grid;
 }
 
