@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -84,6 +85,9 @@ void timeline_print(int dev, const char* who, const void* obj, int kernel, hipEv
 
 extern "C" {
 
+// live contexts per device: the device's shared engine streams go with the last one
+static std::atomic<int> g_ctx_count[64];
+
 int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out) {
   if (!cfg || !out) return LISLAM_ERR_ARG;
   *out = nullptr;
@@ -111,6 +115,7 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
   // LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed the engine's shape (lislam_set_engine_shape)
   if (const char* e = getenv("LISLAM_ENGINE_QPW")) c->eng_qpw = std::min(4, std::max(1, atoi(e)));
   if (const char* e = getenv("LISLAM_ENGINE_DEPTH")) c->eng_depth = std::min(4, std::max(1, atoi(e)));
+  if (device < 64) ++g_ctx_count[device];
   *out = c;
   return LISLAM_OK;
 }
@@ -128,7 +133,9 @@ int lislam_ctx_destroy(lislam_ctx* c) {
     (void)hipFree(c->factor_buf);
   }
   if (c->own_stream) hipStreamDestroy(c->own_stream);
+  const int dev = c->device;
   delete c;
+  if (dev >= 0 && dev < 64 && --g_ctx_count[dev] == 0) lislam::release_engine_streams(dev);
   return LISLAM_OK;
 }
 
@@ -953,6 +960,37 @@ static int put_frame(lislam_batch* b, int slot, const lislam_frame* fr) {
   return rc ? LISLAM_ERR_DEVICE : LISLAM_OK;
 }
 
+// Slot `from` of the node batch becomes slot `to` on the device (the frame's clouds, counts, line
+// offsets and its target index): the current frame turns into the last frame without a second
+// upload and index build.
+static int copy_slot(lislam_batch* b, int from, int to) {
+  lislam_ctx* c = b->ctx;
+  const hipStream_t st = c->stream;
+  auto cp = [&](const void* base, size_t per_slot) -> int {
+    const char* p = static_cast<const char*>(base);
+    HIPCHK(c, hipMemcpyAsync(const_cast<char*>(p) + (size_t)to * per_slot, p + (size_t)from * per_slot, per_slot,
+                             hipMemcpyDeviceToDevice, st));
+    return LISLAM_OK;
+  };
+  const FeatureArgs& f = b->fa;
+  const OdomArgs& o = b->oa;
+  int rc = 0;
+  rc |= cp(f.sharp, (size_t)b->cap_sharp * 16);
+  rc |= cp(f.less_sharp, (size_t)b->cap_less_sharp * 16);
+  rc |= cp(f.flat, (size_t)b->cap_flat * 16);
+  rc |= cp(f.less_flat, (size_t)b->N * 16);
+  rc |= cp(f.n_feat, 4 * sizeof(int));
+  rc |= cp(f.feat_loff, (size_t)2 * (b->H + 1) * sizeof(int));
+  for (const TargetIndex* ti : {&o.idx_ls, &o.idx_lf}) {
+    rc |= cp(ti->chunk, (size_t)ti->nchunk * 2 * 16);
+    rc |= cp(ti->super, (size_t)ti->nsuper * 2 * 16);
+    rc |= cp(ti->nn_chunk, (size_t)ti->nchunk * 2 * 16);
+    rc |= cp(ti->nn_super, (size_t)ti->nsuper * 2 * 16);
+    rc |= cp(ti->sorted, (size_t)ti->cap * 16);
+  }
+  return rc ? LISLAM_ERR_DEVICE : LISLAM_OK;
+}
+
 static int odom_step(lislam_odom* od, const lislam_frame* fr, int use_aloam, double* para_out, double* pose_out,
                      int32_t* stats_out) {
   if (!od || !fr) return LISLAM_ERR_ARG;
@@ -969,12 +1007,21 @@ static int odom_step(lislam_odom* od, const lislam_frame* fr, int use_aloam, dou
     b->extracted = 2;
     od->gate[1] = use_aloam != 0;
     if ((rc = run_odometry(b, 2, 1, od->state, use_aloam < 0 ? nullptr : od->gate))) return rc;
-    int n;
-    if ((rc = lislam_batch_download(b, LISLAM_OUT_PARA, 1, od->state, 7, &n))) return rc;
-    if ((rc = lislam_batch_download(b, LISLAM_OUT_POSE, 1, od->state + 7, 7, &n))) return rc;
-    if ((rc = lislam_batch_download(b, LISLAM_OUT_STATS, 1, st, 8, &n))) return rc;
-    // the current frame becomes the last frame (laserOdometry.cpp:793-808)
-    if ((rc = put_frame(b, 0, fr))) return rc;
+    // para, pose and stats of the pair: three copies on the context stream, one wait
+    SETTLE(b);
+    const struct { int what; void* dst; int cap; } outs[3] = {
+        {LISLAM_OUT_PARA, od->state, 7}, {LISLAM_OUT_POSE, od->state + 7, 7}, {LISLAM_OUT_STATS, st, 8}};
+    for (const auto& o : outs) {
+      const void* src = nullptr;
+      int cnt = 0;
+      size_t esz = 0;
+      if ((rc = output_source(b, o.what, 1, &src, &cnt, &esz))) return rc;
+      if (cnt > o.cap) return fail(c, LISLAM_ERR_CAPACITY, "output %d needs %d elements", o.what, cnt);
+      if (cnt > 0) HIPCHK(c, hipMemcpyAsync(o.dst, src, (size_t)cnt * esz, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the current frame becomes the last frame (laserOdometry.cpp:793-808), on the device
+    if ((rc = copy_slot(b, 1, 0))) return rc;
   }
   od->frames++;
   if (para_out) std::memcpy(para_out, od->state, 7 * sizeof(double));

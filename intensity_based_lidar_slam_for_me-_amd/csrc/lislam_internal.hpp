@@ -156,6 +156,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
                                 hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done);
 bool engine_streams_available(int dev);  // the device has CU-masked streams for the split engine
+void release_engine_streams(int dev);    // with the device's last context
 // A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).
 bool work_stream(int dev, hipStream_t* s);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's

@@ -2932,6 +2932,23 @@ bool engine_streams_available(int dev) {
   return g->avail == 1;
 }
 
+// The device's engine streams and slot events are released with its last context (a stream left to
+// the process's exit is torn down after the runtime, which a profiler's exit path trips over).
+void release_engine_streams(int dev) {
+  EngineGate* g = engine_gate(dev);
+  if (!g) return;
+  std::lock_guard<std::mutex> lk(g->mu);
+  for (int s = 0; s < EngineGate::kMaxDepth; s++) {
+    if (g->items[s]) { (void)hipStreamSynchronize(g->items[s]); (void)hipStreamDestroy(g->items[s]); }
+    if (g->roles[s]) { (void)hipStreamSynchronize(g->roles[s]); (void)hipStreamDestroy(g->roles[s]); }
+    if (g->ev[s]) (void)hipEventDestroy(g->ev[s]);
+    g->items[s] = g->roles[s] = nullptr;
+    g->ev[s] = nullptr;
+  }
+  g->next = 0;
+  g->avail = -1;
+}
+
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
                                 hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
   if (a.n_chains <= 0) return 0;
