@@ -853,21 +853,31 @@ int lislam_scan_registration(lislam_ctx* c, const void* points, const lislam_poi
   lislam_batch* b = c->single;
   if ((rc = lislam_batch_upload(b, points, 1, layout))) return rc;
   if ((rc = lislam_batch_extract(b, 1))) return rc;
-  int n = 0;
-  struct Item { int what; float* dst; int cap; int* n; };
-  Item items[] = {{LISLAM_OUT_LASER_CLOUD, out->laser_cloud, out->cap_laser_cloud, &out->n_laser_cloud},
-                  {LISLAM_OUT_SHARP, out->sharp, out->cap_sharp, &out->n_sharp},
-                  {LISLAM_OUT_LESS_SHARP, out->less_sharp, out->cap_less_sharp, &out->n_less_sharp},
-                  {LISLAM_OUT_FLAT, out->flat, out->cap_flat, &out->n_flat},
-                  {LISLAM_OUT_LESS_FLAT, out->less_flat, out->cap_less_flat, &out->n_less_flat}};
+  // every output of the scan in one pass: the counts once, then the copies, one wait at the end
+  const FeatureArgs& f = b->fa;
+  const int N = b->N;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int ncloud = 0, nfeat[4] = {0, 0, 0, 0};
+  HIPCHK(c, hipMemcpy(&ncloud, f.n_cloud, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(nfeat, f.n_feat, sizeof(nfeat), hipMemcpyDeviceToHost));
+  struct Item { const void* src; int cnt; size_t esz; void* dst; int cap; int* n; const char* name; };
+  const Item items[] = {
+      {f.cloud, ncloud, 16, out->laser_cloud, out->cap_laser_cloud, &out->n_laser_cloud, "laser_cloud"},
+      {f.sharp, nfeat[0], 16, out->sharp, out->cap_sharp, &out->n_sharp, "sharp"},
+      {f.less_sharp, nfeat[1], 16, out->less_sharp, out->cap_less_sharp, &out->n_less_sharp, "less_sharp"},
+      {f.flat, nfeat[2], 16, out->flat, out->cap_flat, &out->n_flat, "flat"},
+      {f.less_flat, nfeat[3], 16, out->less_flat, out->cap_less_flat, &out->n_less_flat, "less_flat"},
+      {f.img_range, N, 1, out->image_range, N, nullptr, "image_range"},
+      {f.img_int, N, 1, out->image_intensity, N, nullptr, "image_intensity"},
+      {f.track, N, 16, out->cloud_track, N, nullptr, "cloud_track"}};
   for (const Item& it : items) {
     if (!it.dst) continue;
-    if ((rc = lislam_batch_download(b, it.what, 0, it.dst, it.cap, it.n))) return rc;
+    if (!it.src) return fail(c, LISLAM_ERR_STATE, "%s unavailable (context created without images)", it.name);
+    if (it.cnt > it.cap) return fail(c, LISLAM_ERR_CAPACITY, "%s needs %d elements, cap %d", it.name, it.cnt, it.cap);
+    if (it.n) *it.n = it.cnt;
+    if (it.cnt > 0) HIPCHK(c, hipMemcpyAsync(it.dst, it.src, (size_t)it.cnt * it.esz, hipMemcpyDeviceToHost, c->stream));
   }
-  const int N = b->N;
-  if (out->image_range && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_RANGE, 0, out->image_range, N, &n))) return rc;
-  if (out->image_intensity && (rc = lislam_batch_download(b, LISLAM_OUT_IMAGE_INTENSITY, 0, out->image_intensity, N, &n))) return rc;
-  if (out->cloud_track && (rc = lislam_batch_download(b, LISLAM_OUT_CLOUD_TRACK, 0, out->cloud_track, N, &n))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return LISLAM_OK;
 }
 
