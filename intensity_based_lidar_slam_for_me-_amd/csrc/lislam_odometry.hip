@@ -1384,7 +1384,7 @@ __global__ __launch_bounds__(256) void k_eval_factors_raw(RawFactorArgs a) {
 
 // Developer profile of the engine (null in production): per ticket kProfSlots u64 = s_memrealtime
 // (100 MHz) at claim, inputs ready, records loaded (solve), done; summed evaluation and step ticks and
-// the evaluation count (solve); items: 10 the end of the item's last query.  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
+// the evaluation count (solve), 11 step 0's share sum; items: 10 the end of the item's last query.  lislam_debug_engine_prof(n) arms it (n tickets; 0 disarms),
 // lislam_debug_engine_prof_read copies it out.
 constexpr int kProfSlots = 16;
 __device__ unsigned long long* g_eng_prof = nullptr;
@@ -2401,6 +2401,7 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    const unsigned long long tfa = rt_now();  // the shares summed
     const int nc = uni(sh.cnt[0][0]), np = uni(sh.cnt[0][1]);
     bool cont = false;
     if (nc + np > 0) {  // no residual blocks: Ceres leaves the parameters untouched
@@ -2419,6 +2420,7 @@ __device__ __forceinline__ bool eng_solve_pass(const OdomArgs& a, const EngCtl& 
     __syncthreads();
     if (lane == 0) {
       eng_prof(tk, 0, tf1 - tf0);          // step 0 (wave 0)
+      eng_prof(tk, 11, tfa - tf0);         // ... of which the shares' sum
       eng_prof(tk, 7, rt_now() - tf0);     // step 0 and the blocks' load (to the first barrier)
       eng_prof(tk, 2, tf0);                // shares summed
     }

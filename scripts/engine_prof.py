@@ -70,6 +70,8 @@ with pkg.Context() as ctx:
         "solve steps (sum)": st * us,
         "solve: step 0 beside the blocks' load (to the first barrier)": lm[:, 7] * us,
         "solve: step 0 alone (wave 0)": lm[:, 0] * us,
+        "solve: step 0, the 32 share rows' sum": lm[:, 11] * us,
+        "solve: step 0, the LM step (lm_start + propose)": (lm[:, 0] - lm[:, 11]) * us,
         "solve total (ready -> done)": (lm_done - lm_ready) * us,
         "hand-off solve -> assoc (solve done -> next first item ready)": (a_start[1:] - lm_done[:-1]) * us,
     }
