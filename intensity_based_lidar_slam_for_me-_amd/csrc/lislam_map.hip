@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -72,7 +73,19 @@ struct MapView {
   float cell, inv_cell;
   int n;
   int scan_shell;  // after this shell a query scans the whole map: the shells' cell probes would cost more
+  float near2;     // first pass of the 3x3x3 block: the cells within this squared distance (< 0: all 27)
 };
+
+// The 3x3x3 block's first pass probes only the cells whose box is within LISLAM_KNN_NEAR metres of
+// the query (default half a cell: the query's own cell and the 7 or fewer nearest); a second pass
+// takes the block's other cells that could still beat the k-th best.  A negative value probes the
+// whole block in one pass.  Either way the k-best is exact (same (distance, id) order).  Read at
+// every launch (the parity tests run each setting in one process).
+inline float knn_near2(float cell) {
+  const char* e = getenv("LISLAM_KNN_NEAR");
+  const float near = e && *e ? (float)atof(e) : 0.5f * cell;
+  return near < 0 ? -1.f : near * near;
+}
 
 // first shell s whose cells walked so far (27 + sum_{j=2..s} 24 j^2 + 2) reach n / 4 point loads
 inline int scan_shell_for(int64_t n) {
@@ -285,21 +298,28 @@ __device__ __forceinline__ int xcd_block(int b, int nblk) {
 }
 
 // One pass over `total` cells (the 3x3x3 block for s == 1, else the shell at radius s): lanes
-// probe one cell each (skipping cells whose box cannot beat `bound`), then the points of the
-// probed cells are dealt evenly over the 64 lanes (exclusive prefix of the counts + a 6-step
-// binary search per point), four loads in flight per lane.
+// probe one cell each (skipping cells whose box cannot beat `bound`, and those within `skip` — a
+// pass over them already ran; skip < 0: none; s == 1 with bound = inf: every cell, no box test),
+// then the points of the probed cells are dealt evenly over the 64 lanes (exclusive prefix of the
+// counts + a 6-step binary search per point), four loads in flight per lane.
 template <int K>
-__device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int cx, int cy, int cz, int s, float bound,
-                                         float max_d2, KBest<K>& b) {
+__device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int cx, int cy, int cz, int s, float skip,
+                                         float bound, float max_d2, KBest<K>& b) {
   const int lane = threadIdx.x & 63;
   const int total = s == 1 ? 27 : 24 * s * s + 2;
+  const bool all = s == 1 && bound == kInf && skip < 0;
   for (int j0 = 0; j0 < total; j0 += 64) {
     const int j = j0 + lane;
     int cnt = 0, beg = 0;
     if (j < total) {
       int dx, dy, dz;
       shell_cell(s, j, dx, dy, dz);
-      if (s == 1 || cell_lb2(q, cx + dx, cy + dy, cz + dz, m.cell) <= (double)bound) {
+      bool probe = all;
+      if (!all) {
+        const double lb = cell_lb2(q, cx + dx, cy + dy, cz + dz, m.cell);
+        probe = lb <= (double)bound && !(skip >= 0 && lb <= (double)skip);
+      }
+      if (probe) {
         const int2 r = cell_lookup(m, pack_cell(cx + dx, cy + dy, cz + dz));
         beg = r.x;
         cnt = r.y;
@@ -360,9 +380,22 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
   const double maxd = sqrt((double)max_d2);
   for (int s = 1;; s++) {
     // a cell is probed only if its (conservative) box distance can beat the current k-th best
-    const float bound = fminf(max_d2, s == 1 ? kInf : kth_of(mg, k));
-    knn_pass(m, q, cx, cy, cz, s, bound, max_d2, b);
-    group_merge(b, mg);
+    if (s == 1 && m.near2 >= 0) {
+      // the block's near cells first; then its other cells that can still beat the k-th best
+      // (cells within near2 are in exactly one of the two passes: the same test decides both)
+      const float b1 = fminf(max_d2, m.near2);
+      knn_pass(m, q, cx, cy, cz, 1, -1.f, b1, max_d2, b);
+      group_merge(b, mg);
+      const float b2 = fminf(max_d2, kth_of(mg, k));
+      if (max_d2 > m.near2 && b2 > m.near2) {
+        knn_pass(m, q, cx, cy, cz, 1, m.near2, b2, max_d2, b);
+        group_merge(b, mg);
+      }
+    } else {
+      const float bound = fminf(max_d2, s == 1 ? kInf : kth_of(mg, k));
+      knn_pass(m, q, cx, cy, cz, s, -1.f, bound, max_d2, b);
+      group_merge(b, mg);
+    }
     const float kth = kth_of(mg, k);
     const double gap = fmin(block_gap(q.x, cx, s, m.cell), fmin(block_gap(q.y, cy, s, m.cell), block_gap(q.z, cz, s, m.cell)));
     if (gap >= maxd * (1.0 + 1e-6)) break;                                  // every point within max_dist seen
@@ -805,8 +838,10 @@ struct LmDev {
   int flag, phase, nedge, nplane;
 };
 
-__global__ void k_lm_init(LmDev* st, const double* x0) {
+// ctl (nullable): k_lm_solve's arrival count, generation and give-up words, zeroed here
+__global__ void k_lm_init(LmDev* st, const double* x0, unsigned* ctl) {
   if (threadIdx.x != 0) return;
+  if (ctl) { ctl[0] = 0u; ctl[1] = 0u; ctl[2] = 0u; }
   for (int e = 0; e < 7; e++) { st->x0[e] = x0[e]; st->xe[e] = x0[e]; }
   st->flag = 1;
   st->phase = 0;
@@ -815,16 +850,40 @@ __global__ void k_lm_init(LmDev* st, const double* x0) {
   st->s.term = 1;
 }
 
-// This workgroup's partial (acc + block counts) of the evaluation at st->xe.
-__device__ __forceinline__ void lm_eval_partial(const double* rec, const int* kind, int nn, const LmDev* st,
-                                                double* partial) {
+// Agent-scope (sc1) accesses of the solve state and the partials: inside one launch of k_lm_solve
+// another workgroup (on another XCD, behind another L2) reads what a workgroup wrote, so these bypass
+// the non-coherent caches instead of fencing the whole L2 (the chain engine's hand-offs,
+// lislam_odometry.hip).  The stores are drained (s_waitcnt vmcnt(0)) before the count or the
+// generation word that publishes them.
+typedef __attribute__((address_space(1))) unsigned long long gmu64;
+typedef __attribute__((address_space(1))) unsigned gmu32;
+__device__ __forceinline__ double ld_ag(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((gmu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_ag(double* p, double v) {
+  __hip_atomic_store((gmu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_ag(const unsigned* p) {
+  return __hip_atomic_load((gmu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag(unsigned* p, unsigned v) {
+  __hip_atomic_store((gmu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_ag(const int* p) { return (int)ld_ag((const unsigned*)p); }
+__device__ __forceinline__ void st_ag(int* p, int v) { st_ag((unsigned*)p, (unsigned)v); }
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Partial blk (of nblk: the records blk * kEvalThreads + threadIdx.x, strided by nblk * kEvalThreads)
+// of the evaluation at xe (acc + block counts), stored agent-scope (ag) or plainly.
+__device__ __forceinline__ void lm_eval_partial(const double* rec, const int* kind, int nn, const double* xe, int blk,
+                                                int nblk, double* partial, bool ag) {
   __shared__ double red[kEvalThreads / 16][kPart];
   double acc[kPart];
 #pragma unroll
   for (int e = 0; e < kPart; e++) acc[e] = 0;
-  const DQ q{st->xe[0], st->xe[1], st->xe[2], st->xe[3]};
-  const D3 t{st->xe[4], st->xe[5], st->xe[6]};
-  for (int i = blockIdx.x * kEvalThreads + threadIdx.x; i < nn; i += gridDim.x * kEvalThreads) {
+  const DQ q{xe[0], xe[1], xe[2], xe[3]};
+  const D3 t{xe[4], xe[5], xe[6]};
+  for (int i = blk * kEvalThreads + threadIdx.x; i < nn; i += nblk * kEvalThreads) {
     const int kd = kind[i];
     if (kd < 0) continue;
     block_accum(kd, rec + (size_t)i * 9, q, t, acc);
@@ -840,37 +899,26 @@ __device__ __forceinline__ void lm_eval_partial(const double* rec, const int* ki
   if (threadIdx.x < kPart) {
     double v = 0;
     for (int w = 0; w < kEvalThreads / 16; w++) v += red[w][threadIdx.x];
-    partial[(size_t)blockIdx.x * kPart + threadIdx.x] = v;
+    double* o = partial + (size_t)blk * kPart + threadIdx.x;
+    if (ag) st_ag(o, v);
+    else *o = v;
   }
 }
 
 __global__ __launch_bounds__(kEvalThreads) void k_lm_eval(const double* rec, const int* kind, const int* ncount, int n,
                                                           LmDev* st, double* partial) {
   if (!st->flag) return;
-  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
+  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st->xe, blockIdx.x, gridDim.x, partial, false);
 }
 
-// One evaluation of ceres::Solve with its trust-region step (solve_device launches it max_it + 1
-// times; a launch after the solve has ended returns at once): every workgroup sums its strided share
-// of the records (lm_eval_partial) and counts itself in; the last one sums the partials in workgroup
-// order (deterministic) and takes the step on its wave 0 (lislam_lm_wave.hpp, the chain engine's
-// step: a short fp64 chain, the state through LDS) — the separate one-thread step launch per
-// evaluation is gone.  x_out / summary (k_lm_finish's outputs) are written when the solve ends.
-__global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec, const int* kind, const int* ncount, int n,
-                                                              LmDev* st, double* partial, unsigned* arrive, int max_it,
-                                                              double* x_out, int* summary) {
-  if (!st->flag) return;
-  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st, partial);
-  __shared__ int last;
-  __threadfence();  // this workgroup's partial before its arrival
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(arrive, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // every other workgroup's partial is visible after the count
-  // The partials summed in a fixed two-level order: lane group g (of kSumGroups) sums parts
-  // g, g + kSumGroups, ... of column e with every load issued before the first add (a serial chain
-  // of L2 round trips cost more than the evaluation), then thread e sums the groups in order.
+// The G partials summed in a fixed two-level order, then the trust-region step on wave 0
+// (lislam_lm_wave.hpp, the chain engine's step: a short fp64 chain, the state through LDS); every
+// thread of the workgroup calls it.  Lane group g (of kSumGroups) sums parts g, g + kSumGroups, ... of
+// column e with every load issued before the first add (a serial chain of L2 round trips cost more
+// than the evaluation), then thread e sums the groups in order.  The state is read and written
+// agent-scope.  x_out / summary (k_lm_finish's outputs) are written when the solve ends.
+__device__ __forceinline__ void lm_sum_step(const double* partial, int G, LmDev* st, int max_it, double* x_out,
+                                            int* summary) {
   constexpr int kSumGroups = kEvalThreads / 32;
   __shared__ double gsum[kSumGroups][kPart];
   __shared__ double acc[kPart];
@@ -882,9 +930,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
 #pragma unroll
       for (int j = 0; j < kLoads; j++) {
         const int w = g + j * kSumGroups;
-        v[j] = w < (int)gridDim.x ? __hip_atomic_load(partial + (size_t)w * kPart + e, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0.0;
+        v[j] = w < G ? ld_ag(partial + (size_t)w * kPart + e) : 0.0;
       }
       double s = 0;
 #pragma unroll
@@ -900,17 +946,17 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
     acc[threadIdx.x] = v;
   }
   __syncthreads();
-  if (threadIdx.x >= 64) return;  // wave 0 takes the step (lislam_lm_wave.hpp: every lane alike)
+  if (threadIdx.x >= 64) return;  // wave 0 takes the step (every lane alike)
   const int lane = threadIdx.x;
-  if (lane == 0) *arrive = 0u;  // the next evaluation's count (its launch follows this one on the stream)
   __shared__ EngLM sl;
   constexpr int kWords = (int)(sizeof(EngLM) / 4);
-  for (int i = lane; i < kWords; i += 64) reinterpret_cast<unsigned*>(&sl)[i] = reinterpret_cast<const unsigned*>(&st->s)[i];
+  for (int i = lane; i < kWords; i += 64)
+    reinterpret_cast<unsigned*>(&sl)[i] = ld_ag(reinterpret_cast<const unsigned*>(&st->s) + i);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   LdsLM& s = *(LdsLM*)&sl;
-  const int phase = st->phase;
-  int nedge = st->nedge, nplane = st->nplane;
+  const int phase = ld_ag(&st->phase);
+  int nedge = ld_ag(&st->nedge), nplane = ld_ag(&st->nplane);
   double a[kAcc];
 #pragma unroll
   for (int e = 0; e < kAcc; e++) a[e] = acc[e];
@@ -920,7 +966,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
     nplane = (int)acc[kAcc + 1];
     double x0[7];
 #pragma unroll
-    for (int e = 0; e < 7; e++) x0[e] = st->x0[e];
+    for (int e = 0; e < 7; e++) x0[e] = ld_ag(&st->x0[e]);
     if (nedge + nplane == 0) {  // no residual blocks: Ceres leaves the parameters untouched
 #pragma unroll
       for (int e = 0; e < 7; e++) s.x[e] = x0[e];
@@ -936,18 +982,118 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
   if (cont) eng_step_post(s);  // the candidate's parameter tolerance and 1 / model cost change
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < kWords; i += 64) reinterpret_cast<unsigned*>(&st->s)[i] = reinterpret_cast<const unsigned*>(&sl)[i];
+  for (int i = lane; i < kWords; i += 64)
+    st_ag(reinterpret_cast<unsigned*>(&st->s) + i, reinterpret_cast<const unsigned*>(&sl)[i]);
   if (lane != 0) return;
-  st->nedge = nedge;
-  st->nplane = nplane;
-  st->phase = phase + 1;
-  st->flag = cont;
+  st_ag(&st->nedge, nedge);
+  st_ag(&st->nplane, nplane);
+  st_ag(&st->phase, phase + 1);
+  st_ag(&st->flag, (int)cont);
   if (cont)
-    for (int e = 0; e < 7; e++) st->xe[e] = sl.xc[e];
-  if (!cont || phase + 1 > max_it) {  // the solve's end (or its last launch)
+    for (int e = 0; e < 7; e++) st_ag(&st->xe[e], sl.xc[e]);
+  if (!cont || phase + 1 > max_it) {  // the solve's end (or its last evaluation)
     if (x_out)
       for (int e = 0; e < 7; e++) x_out[e] = sl.x[e];
     if (summary) { summary[0] = sl.it; summary[1] = sl.term; summary[2] = nedge; summary[3] = nplane; }
+  }
+}
+
+// One evaluation of ceres::Solve with its trust-region step per launch (LISLAM_MAP_SOLVE=launches:
+// solve_device launches it max_it + 1 times; a launch after the solve has ended returns at once):
+// every workgroup sums its strided share of the records and counts itself in; the last one sums the
+// partials and takes the step.
+__global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec, const int* kind, const int* ncount, int n,
+                                                              LmDev* st, double* partial, unsigned* arrive, int max_it,
+                                                              double* x_out, int* summary) {
+  if (!st->flag) return;
+  lm_eval_partial(rec, kind, ncount ? min(*ncount, n) : n, st->xe, blockIdx.x, gridDim.x, partial, true);
+  __shared__ int last;
+  drain_vm();  // this workgroup's partial before its arrival
+  __syncthreads();
+  if (threadIdx.x == 0) last = __hip_atomic_fetch_add((gmu32*)arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) *arrive = 0u;  // the next evaluation's count (its launch follows this one on the stream)
+  lm_sum_step(partial, gridDim.x, st, max_it, x_out, summary);
+}
+
+// ceres::Solve in one launch (the default): the workgroups run every evaluation (at most max_it + 1),
+// one grid-wide hand-off apart.  Each workgroup stores its partial, drains and counts itself in
+// (ctl[0], monotonic over the launch); the last arrival of evaluation e sums and steps
+// (lm_sum_step), drains and publishes generation e + 1 (ctl[1]); the others wait for it on one lane
+// with s_sleep, then read the new state.  Every wait is bounded (wait_ticks of the 100 MHz clock):
+// a workgroup that gives up sets ctl[2] and leaves, every waiting workgroup sees it and leaves, and
+// k_lm_rescue (next on the stream) finishes the solve from the last completed step — the same
+// partials and the same sum order, so the same bits.  (The workgroups need not be resident
+// together: a late one only delays the hand-off.)
+__global__ __launch_bounds__(kEvalThreads) void k_lm_solve(const double* rec, const int* kind, const int* ncount, int n,
+                                                           LmDev* st, double* partial, unsigned* ctl, int max_it,
+                                                           double* x_out, int* summary, unsigned long long wait_ticks) {
+  const int nn = ncount ? min(*ncount, n) : n;
+  const unsigned G = gridDim.x;
+  __shared__ int s_go, s_last;
+  __shared__ double s_xe[7];
+  for (int e = 0; e <= max_it; e++) {
+    if (threadIdx.x == 0) s_go = ld_ag(&st->flag) != 0 && ld_ag(ctl + 2) == 0u;
+    if (threadIdx.x < 7) s_xe[threadIdx.x] = ld_ag(&st->xe[threadIdx.x]);
+    __syncthreads();
+    if (!s_go) return;
+    lm_eval_partial(rec, kind, nn, s_xe, blockIdx.x, G, partial, true);
+    drain_vm();  // this workgroup's partial before its arrival
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add((gmu32*)ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(e + 1) * G - 1u;
+    __syncthreads();
+    if (s_last) {
+      lm_sum_step(partial, G, st, max_it, x_out, summary);
+      drain_vm();  // the new state before its generation
+      __syncthreads();
+      if (threadIdx.x == 0) st_ag(ctl + 1, (unsigned)(e + 1));
+    } else {
+      if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (ld_ag(ctl + 1) < (unsigned)(e + 1)) {
+          if (ld_ag(ctl + 2) != 0u) { ok = 0; break; }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > wait_ticks) {
+            st_ag(ctl + 2, 1u);
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        s_go = ok;
+      }
+      __syncthreads();
+      if (!s_go) return;
+    }
+  }
+}
+
+// After k_lm_solve: nothing unless it gave up (ctl[2]); then one workgroup finishes the solve from
+// the last completed step, computing every partial as its workgroup would have (same records, same
+// order) and the same sum and step.
+__global__ __launch_bounds__(kEvalThreads) void k_lm_rescue(const double* rec, const int* kind, const int* ncount, int n,
+                                                            LmDev* st, double* partial, const unsigned* ctl, int parts,
+                                                            int max_it, double* x_out, int* summary) {
+  if (ctl[2] == 0u) return;
+  const int nn = ncount ? min(*ncount, n) : n;
+  __shared__ int s_go;
+  __shared__ double s_xe[7];
+  for (;;) {
+    if (threadIdx.x == 0) s_go = ld_ag(&st->flag) != 0 && ld_ag(&st->phase) <= max_it;
+    if (threadIdx.x < 7) s_xe[threadIdx.x] = ld_ag(&st->xe[threadIdx.x]);
+    __syncthreads();
+    if (!s_go) return;
+    for (int w = 0; w < parts; w++) {
+      lm_eval_partial(rec, kind, nn, s_xe, w, parts, partial, true);
+      __syncthreads();
+    }
+    drain_vm();
+    __syncthreads();
+    lm_sum_step(partial, parts, st, max_it, x_out, summary);
+    drain_vm();
+    __syncthreads();
   }
 }
 
@@ -1083,6 +1229,7 @@ struct lislam_map {
     v.inv_cell = 1.0f / cell;
     v.n = (int)n;
     v.scan_shell = mapk::scan_shell_for(n);
+    v.near2 = mapk::knn_near2(cell);
     return v;
   }
 };
@@ -1253,6 +1400,19 @@ int associate_device(lislam_map* m, int match, const float* q, int stride, const
   return LISLAM_OK;
 }
 
+// LISLAM_MAP_SOLVE=launches: one k_lm_evalstep launch per evaluation instead of k_lm_solve.
+// (Both read at every solve: the parity tests run each setting in one process.)
+bool map_solve_launches() {
+  const char* e = getenv("LISLAM_MAP_SOLVE");
+  return e && strcmp(e, "launches") == 0;
+}
+// Bound of k_lm_solve's hand-off waits (100 MHz ticks): LISLAM_MAP_SOLVE_WAIT_US, default 2 s.
+unsigned long long map_solve_wait_ticks() {
+  const char* e = getenv("LISLAM_MAP_SOLVE_WAIT_US");
+  const double us = e && *e ? atof(e) : 2e6;
+  return (unsigned long long)(us * 100.0);
+}
+
 // ceres::Solve over n device records; result stays in the LmDev (device).
 // (x_out / summary: k_lm_finish's outputs, written by the evaluation that ends the solve, when given)
 int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* kind, const int* ncount, int n,
@@ -1261,14 +1421,21 @@ int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* ki
   MCHK(c, sc.lm.reserve(sizeof(LmDev)));
   MCHK(c, sc.partial.reserve((size_t)kMaxParts * kPart * 8 + 64));
   LmDev* lm = sc.lm.as<LmDev>();
-  unsigned* arrive = reinterpret_cast<unsigned*>(sc.partial.as<char>() + (size_t)kMaxParts * kPart * 8);
+  unsigned* ctl = reinterpret_cast<unsigned*>(sc.partial.as<char>() + (size_t)kMaxParts * kPart * 8);
   const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
-  MCHK(c, hipMemsetAsync(arrive, 0, sizeof(unsigned), st));
-  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev);
-  for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev, ctl);
+  if (map_solve_launches()) {  // one launch per evaluation (the round-4 schedule, for A/B)
+    for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
+      TimedScope ts(c, kT_lm_solve);
+      hipLaunchKernelGGL(k_lm_evalstep, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
+                         sc.partial.as<double>(), ctl, max_it, x_out, summary);
+    }
+  } else {
     TimedScope ts(c, kT_lm_solve);
-    hipLaunchKernelGGL(k_lm_evalstep, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
-                       sc.partial.as<double>(), arrive, max_it, x_out, summary);
+    hipLaunchKernelGGL(k_lm_solve, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,
+                       sc.partial.as<double>(), ctl, max_it, x_out, summary, map_solve_wait_ticks());
+    hipLaunchKernelGGL(k_lm_rescue, dim3(1), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm, sc.partial.as<double>(),
+                       ctl, parts, max_it, x_out, summary);
   }
   MCHK(c, hipGetLastError());
   return LISLAM_OK;
@@ -1497,7 +1664,7 @@ int lislam_normal_equations(lislam_ctx* c, const double* rec, const int32_t* kin
   }
   MCHK(c, hipMemcpyAsync(sc.x.p, x, 56, hipMemcpyDefault, st));
   LmDev* lm = sc.lm.as<LmDev>();
-  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, sc.x.as<double>());
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, sc.x.as<double>(), (unsigned*)nullptr);
   const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
   hipLaunchKernelGGL(k_lm_eval, dim3(parts), dim3(kEvalThreads), 0, st, sc.rec.as<double>(), sc.kind.as<int>(), nullptr,
                      n, lm, sc.partial.as<double>());

@@ -70,6 +70,27 @@ def test_knn_corridor_and_far_queries(pkg, oracle, ctx, synth):
     g.close()
 
 
+@pytest.mark.parametrize("near", ["-1", "0", "0.02", "0.1", "0.3", "2"])
+@pytest.mark.parametrize("cell", [0.1, 0.3])
+def test_knn_near_first_pass(pkg, oracle, ctx, synth, monkeypatch, near, cell):
+    """The 3x3x3 block's near-cells-first split (LISLAM_KNN_NEAR, metres; -1: one pass) returns the
+    same k-best as the oracle's k-d tree for every radius, including radii that cover no cell but
+    the query's own (0), part of the block (0.02 .. 0.3) and all of it (2), with and without a
+    max distance."""
+    monkeypatch.setenv("LISLAM_KNN_NEAR", near)
+    M = synth.make_corridor_map(200_000, spacing=0.05)
+    g = pkg.mapping.IkdMap(ctx, 0.4, cell)
+    g.build(M)
+    o = oracle.IkdMap(0.4)
+    o.build(M)
+    rng = np.random.default_rng(11)
+    Q = _f32(M[rng.choice(len(M), 2000, replace=False), :3] + rng.normal(0, 0.08, (2000, 3)))
+    _knn_equal(g.nearest_search(Q, 5), o.knn(Q, 5), 5)
+    _knn_equal(g.nearest_search(Q, 8), o.knn(Q, 8), 8)
+    _knn_equal(g.nearest_search(Q, 5, 0.01), o.knn(Q, 5, 0.01), 5)
+    g.close()
+
+
 def test_knn_small_and_empty_maps(pkg, oracle, ctx):
     g = pkg.mapping.IkdMap(ctx, 0.2)
     Q = _f32([[0.1, 0, 0], [5, 5, 5]])
@@ -313,6 +334,39 @@ def test_laser_mapping(pkg, oracle, ctx, synth):
     assert np.linalg.norm(xg[4:] - truth[4:]) < np.linalg.norm(x0[4:] - truth[4:])
     gs.close()
     gc.close()
+
+
+def test_map_solve_modes_agree(pkg, oracle, ctx, synth, monkeypatch):
+    """The pose solve in one launch (k_lm_solve, default), one launch per evaluation
+    (LISLAM_MAP_SOLVE=launches) and the give-up path (a zero wait bound: every workgroup that has to
+    wait gives up at once and k_lm_rescue finishes the solve on one workgroup) return the same bits,
+    and the oracle's pose.  20k records: 79 workgroups per evaluation."""
+    M = synth.make_corridor_map(400_000, spacing=0.05)
+    gs = pkg.mapping.IkdMap(ctx, 0.4, 0.3)
+    gs.build(M)
+    os_ = oracle.IkdMap(0.4)
+    os_.build(M)
+    rng = np.random.default_rng(17)
+    truth = np.array([0, 0, 0, 1, 4.0, 0.2, 0.0])
+    x0 = synth.perturb_pose(truth[:4], truth[4:], 0.05, 0.5, seed=9)
+    Qs = M[rng.choice(len(M), 20000, replace=False)].copy()
+    Qs[:, :3] -= truth[4:7].astype(np.float32)
+    empty = np.zeros((0, 4), np.float32)
+    out = {}
+    for mode, env in (("persistent", {}), ("launches", {"LISLAM_MAP_SOLVE": "launches"}),
+                      ("rescue", {"LISLAM_MAP_SOLVE_WAIT_US": "0"})):
+        for k in ("LISLAM_MAP_SOLVE", "LISLAM_MAP_SOLVE_WAIT_US"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out[mode] = pkg.mapping.laser_mapping(gs, gs, empty, Qs, x0)
+    for mode in ("launches", "rescue"):
+        assert np.array_equal(out[mode][0], out["persistent"][0]), (mode, out[mode][0], out["persistent"][0])
+        assert list(out[mode][1]) == list(out["persistent"][1]), mode
+    xo, sto = oracle.laser_mapping(os_, os_, empty, Qs, x0)
+    assert np.max(np.abs(out["persistent"][0] - xo)) < POSE_TOL
+    assert list(out["persistent"][1]) == list(sto)
+    gs.close()
 
 
 def test_mapopt_fed_from_batch(pkg, oracle, ctx, synth):
