@@ -998,8 +998,8 @@ __device__ __forceinline__ void lm_sum_step(const double* partial, int G, LmDev*
   }
 }
 
-// One evaluation of ceres::Solve with its trust-region step per launch (LISLAM_MAP_SOLVE=launches:
-// solve_device launches it max_it + 1 times; a launch after the solve has ended returns at once):
+// One evaluation of ceres::Solve with its trust-region step per launch (the default: solve_device
+// launches it max_it + 1 times; a launch after the solve has ended returns at once):
 // every workgroup sums its strided share of the records and counts itself in; the last one sums the
 // partials and takes the step.
 __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec, const int* kind, const int* ncount, int n,
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_lm_evalstep(const double* rec,
   lm_sum_step(partial, gridDim.x, st, max_it, x_out, summary);
 }
 
-// ceres::Solve in one launch (the default): the workgroups run every evaluation (at most max_it + 1),
+// ceres::Solve in one launch (LISLAM_MAP_SOLVE=persistent): the workgroups run every evaluation (at most max_it + 1),
 // one grid-wide hand-off apart.  Each workgroup stores its partial, drains and counts itself in
 // (ctl[0], monotonic over the launch); the last arrival of evaluation e sums and steps
 // (lm_sum_step), drains and publishes generation e + 1 (ctl[1]); the others wait for it on one lane
@@ -1400,11 +1400,14 @@ int associate_device(lislam_map* m, int match, const float* q, int stride, const
   return LISLAM_OK;
 }
 
-// LISLAM_MAP_SOLVE=launches: one k_lm_evalstep launch per evaluation instead of k_lm_solve.
-// (Both read at every solve: the parity tests run each setting in one process.)
+// The solve's schedule: one k_lm_evalstep launch per evaluation (default), or LISLAM_MAP_SOLVE=persistent:
+// k_lm_solve, every evaluation in one launch.  The two measure the same on config 5 (a grid-wide
+// hand-off costs what a kernel boundary does: 2.59k / 2.63k vs 2.64k / 2.70k registrations/s,
+// profiles/r05_map_ab.txt), so the default needs no co-residency at all.
+// (Both knobs are read at every solve: the parity tests run each setting in one process.)
 bool map_solve_launches() {
   const char* e = getenv("LISLAM_MAP_SOLVE");
-  return e && strcmp(e, "launches") == 0;
+  return !(e && strcmp(e, "persistent") == 0);
 }
 // Bound of k_lm_solve's hand-off waits (100 MHz ticks): LISLAM_MAP_SOLVE_WAIT_US, default 2 s.
 unsigned long long map_solve_wait_ticks() {
@@ -1424,7 +1427,7 @@ int solve_device(lislam_ctx* c, MapScratch& sc, const double* rec, const int* ki
   unsigned* ctl = reinterpret_cast<unsigned*>(sc.partial.as<char>() + (size_t)kMaxParts * kPart * 8);
   const int parts = std::min(kMaxParts, blocks(std::max(n, 1), kEvalThreads));
   hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, st, lm, x0_dev, ctl);
-  if (map_solve_launches()) {  // one launch per evaluation (the round-4 schedule, for A/B)
+  if (map_solve_launches()) {  // one launch per evaluation
     for (int e = 0; e <= max_it; e++) {  // the initial evaluation + at most one per iteration
       TimedScope ts(c, kT_lm_solve);
       hipLaunchKernelGGL(k_lm_evalstep, dim3(parts), dim3(kEvalThreads), 0, st, rec, kind, ncount, n, lm,

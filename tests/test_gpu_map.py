@@ -337,10 +337,11 @@ def test_laser_mapping(pkg, oracle, ctx, synth):
 
 
 def test_map_solve_modes_agree(pkg, oracle, ctx, synth, monkeypatch):
-    """The pose solve in one launch (k_lm_solve, default), one launch per evaluation
-    (LISLAM_MAP_SOLVE=launches) and the give-up path (a zero wait bound: every workgroup that has to
-    wait gives up at once and k_lm_rescue finishes the solve on one workgroup) return the same bits,
-    and the oracle's pose.  20k records: 79 workgroups per evaluation."""
+    """The pose solve with one launch per evaluation (k_lm_evalstep, default), in one launch
+    (LISLAM_MAP_SOLVE=persistent: k_lm_solve) and on that launch's give-up path (a zero wait bound:
+    every workgroup that has to wait gives up at once and k_lm_rescue finishes the solve on one
+    workgroup) return the same bits, and the oracle's pose.  20k records: 79 workgroups per
+    evaluation."""
     M = synth.make_corridor_map(400_000, spacing=0.05)
     gs = pkg.mapping.IkdMap(ctx, 0.4, 0.3)
     gs.build(M)
@@ -353,19 +354,19 @@ def test_map_solve_modes_agree(pkg, oracle, ctx, synth, monkeypatch):
     Qs[:, :3] -= truth[4:7].astype(np.float32)
     empty = np.zeros((0, 4), np.float32)
     out = {}
-    for mode, env in (("persistent", {}), ("launches", {"LISLAM_MAP_SOLVE": "launches"}),
-                      ("rescue", {"LISLAM_MAP_SOLVE_WAIT_US": "0"})):
+    for mode, env in (("launches", {}), ("persistent", {"LISLAM_MAP_SOLVE": "persistent"}),
+                      ("rescue", {"LISLAM_MAP_SOLVE": "persistent", "LISLAM_MAP_SOLVE_WAIT_US": "0"})):
         for k in ("LISLAM_MAP_SOLVE", "LISLAM_MAP_SOLVE_WAIT_US"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         out[mode] = pkg.mapping.laser_mapping(gs, gs, empty, Qs, x0)
-    for mode in ("launches", "rescue"):
-        assert np.array_equal(out[mode][0], out["persistent"][0]), (mode, out[mode][0], out["persistent"][0])
-        assert list(out[mode][1]) == list(out["persistent"][1]), mode
+    for mode in ("persistent", "rescue"):
+        assert np.array_equal(out[mode][0], out["launches"][0]), (mode, out[mode][0], out["launches"][0])
+        assert list(out[mode][1]) == list(out["launches"][1]), mode
     xo, sto = oracle.laser_mapping(os_, os_, empty, Qs, x0)
-    assert np.max(np.abs(out["persistent"][0] - xo)) < POSE_TOL
-    assert list(out["persistent"][1]) == list(sto)
+    assert np.max(np.abs(out["launches"][0] - xo)) < POSE_TOL
+    assert list(out["launches"][1]) == list(sto)
     gs.close()
 
 
