@@ -42,7 +42,6 @@ namespace lislam {
 namespace mapk {
 
 constexpr uint64_t kEmptyKey = ~0ull;
-constexpr int kG = 64;          // lanes per query in k_knn (one wavefront)
 constexpr int kMaxShell = 24;   // beyond this the search scans the whole map (exact either way)
 constexpr float kInf = __builtin_huge_valf();
 
@@ -194,24 +193,24 @@ __device__ __forceinline__ void kb_insert(KBest<K>& b, float d, int id, int ix) 
   }
 }
 
-// Merge the k-best lists of the 16 lanes of each group: afterwards every lane of the group
+// Merge the k-best lists of the G lanes of each group (a wave, or a 16-lane row): afterwards every lane of the group
 // returns the merged list in `out`; the group leader keeps it in b, the others are cleared.
-template <int K>
+template <int K, int G>
 __device__ __forceinline__ void group_merge(KBest<K>& b, KBest<K>& out) {
 #pragma unroll
   for (int r = 0; r < K; r++) {
     float md = b.d[0];
     int mi = b.id[0];
 #pragma unroll
-    for (int o = 1; o < kG; o <<= 1) {
-      const float od = __shfl_xor(md, o, kG);
-      const int oi = __shfl_xor(mi, o, kG);
+    for (int o = 1; o < G; o <<= 1) {
+      const float od = __shfl_xor(md, o, G);
+      const int oi = __shfl_xor(mi, o, G);
       if (lex_less(od, oi, md, mi)) { md = od; mi = oi; }
     }
     const bool own = b.d[0] == md && b.id[0] == mi && md != kInf;
     int ox = own ? b.ix[0] : 0;
 #pragma unroll
-    for (int o = 1; o < kG; o <<= 1) ox += __shfl_xor(ox, o, kG);
+    for (int o = 1; o < G; o <<= 1) ox += __shfl_xor(ox, o, G);
     out.d[r] = md; out.id[r] = mi; out.ix[r] = md == kInf ? -1 : ox;
     if (own) {
 #pragma unroll
@@ -219,7 +218,7 @@ __device__ __forceinline__ void group_merge(KBest<K>& b, KBest<K>& out) {
       b.d[K - 1] = kInf; b.id[K - 1] = 0x7fffffff; b.ix[K - 1] = -1;
     }
   }
-  if ((threadIdx.x & (kG - 1)) == 0) b = out;
+  if ((threadIdx.x & (G - 1)) == 0) b = out;
   else kb_clear(b);
 }
 
@@ -301,14 +300,15 @@ __device__ __forceinline__ int xcd_block(int b, int nblk) {
 // probe one cell each (skipping cells whose box cannot beat `bound`, and those within `skip` — a
 // pass over them already ran; skip < 0: none; s == 1 with bound = inf: every cell, no box test),
 // then the points of the probed cells are dealt evenly over the 64 lanes (exclusive prefix of the
-// counts + a 6-step binary search per point), four loads in flight per lane.
-template <int K>
+// counts + a log2(G)-step binary search per point), four loads in flight per lane.  G lanes per
+// query: a wave (64) or a 16-lane row (four queries per wave; every group-wide step is a row op).
+template <int K, int G>
 __device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int cx, int cy, int cz, int s, float skip,
                                          float bound, float max_d2, KBest<K>& b) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & (G - 1);
   const int total = s == 1 ? 27 : 24 * s * s + 2;
   const bool all = s == 1 && bound == kInf && skip < 0;
-  for (int j0 = 0; j0 < total; j0 += 64) {
+  for (int j0 = 0; j0 < total; j0 += G) {
     const int j = j0 + lane;
     int cnt = 0, beg = 0;
     if (j < total) {
@@ -327,24 +327,24 @@ __device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int 
     }
     int incl = cnt;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o, 64);
+    for (int o = 1; o < G; o <<= 1) {
+      const int v = __shfl_up(incl, o, G);
       if (lane >= o) incl += v;
     }
-    const int T = __shfl(incl, 63, 64);
+    const int T = __shfl(incl, G - 1, G);
     const int excl = incl - cnt;
-    for (int t0 = 0; t0 < T; t0 += 4 * 64) {
+    for (int t0 = 0; t0 < T; t0 += 4 * G) {
       int pi[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const int t = t0 + u * 64 + lane;
+        const int t = t0 + u * G + lane;
         int lo = 0;
 #pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-          const int e = __shfl(excl, lo + st, 64);
+        for (int st = G / 2; st > 0; st >>= 1) {
+          const int e = __shfl(excl, lo + st, G);
           if (e <= t) lo += st;
         }
-        const int bb = __shfl(beg, lo, 64), ee = __shfl(excl, lo, 64);
+        const int bb = __shfl(beg, lo, G), ee = __shfl(excl, lo, G);
         pi[u] = t < T ? bb + (t - ee) : -1;
       }
       float4 v[4];
@@ -362,14 +362,14 @@ __device__ __forceinline__ void knn_pass(const MapView& m, const float4& q, int 
 
 // queries: n points of `stride` floats (optionally counted on the device: *qcount); pose
 // (device, nullable): queries are sensor-frame points mapped by pointAssociateToMap first.
-template <int K>
+template <int K, int G>
 __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, int stride, const int* qcount, int nq,
                                              const double* pose, int k, float max_d2, float4* out_pts, float* out_d2,
                                              int* out_found) {
-  const int qi = xcd_block(blockIdx.x, gridDim.x) * (256 / kG) + (int)(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  const int qi = xcd_block(blockIdx.x, gridDim.x) * (256 / G) + (int)(threadIdx.x / G);
+  const int lane = threadIdx.x & (G - 1);
   const int n = qcount ? min(*qcount, nq) : nq;
-  if (qi >= n) return;  // whole waves leave
+  if (qi >= n) return;  // whole groups leave
   const float* qp = queries + (size_t)qi * stride;
   float4 q = make_float4(qp[0], qp[1], qp[2], 0.f);
   if (pose) q = to_world(pose, q.x, q.y, q.z);
@@ -384,17 +384,17 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
       // the block's near cells first; then its other cells that can still beat the k-th best
       // (cells within near2 are in exactly one of the two passes: the same test decides both)
       const float b1 = fminf(max_d2, m.near2);
-      knn_pass(m, q, cx, cy, cz, 1, -1.f, b1, max_d2, b);
-      group_merge(b, mg);
+      knn_pass<K, G>(m, q, cx, cy, cz, 1, -1.f, b1, max_d2, b);
+      group_merge<K, G>(b, mg);
       const float b2 = fminf(max_d2, kth_of(mg, k));
       if (max_d2 > m.near2 && b2 > m.near2) {
-        knn_pass(m, q, cx, cy, cz, 1, m.near2, b2, max_d2, b);
-        group_merge(b, mg);
+        knn_pass<K, G>(m, q, cx, cy, cz, 1, m.near2, b2, max_d2, b);
+        group_merge<K, G>(b, mg);
       }
     } else {
       const float bound = fminf(max_d2, s == 1 ? kInf : kth_of(mg, k));
-      knn_pass(m, q, cx, cy, cz, s, -1.f, bound, max_d2, b);
-      group_merge(b, mg);
+      knn_pass<K, G>(m, q, cx, cy, cz, s, -1.f, bound, max_d2, b);
+      group_merge<K, G>(b, mg);
     }
     const float kth = kth_of(mg, k);
     const double gap = fmin(block_gap(q.x, cx, s, m.cell), fmin(block_gap(q.y, cy, s, m.cell), block_gap(q.z, cz, s, m.cell)));
@@ -402,12 +402,12 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
     if (kth != kInf && (double)kth < gap * gap * (1.0 - 1e-6)) break;  // none closer outside
     if (s >= m.scan_shell) {                                                // far from the map: scan it all
       kb_clear(b);
-      for (int p = lane; p < m.n; p += 64) {
+      for (int p = lane; p < m.n; p += G) {
         const float4 v = m.pts[p];
         const float d = calc_dist(q.x, q.y, q.z, v.x, v.y, v.z);
         if (d <= max_d2) kb_insert(b, d, __float_as_int(v.w), p);
       }
-      group_merge(b, mg);
+      group_merge<K, G>(b, mg);
       break;
     }
   }
@@ -1359,20 +1359,37 @@ int add_packed(lislam_map* m, int64_t nin, bool downsample, int64_t* n_added) {
   return rebuild(m, (int64_t)h[0] + h[1]);
 }
 
-// k-NN of n queries (device buffer, stride floats, optional device count / pose).
+// k-NN of n queries (device buffer, stride floats, optional device count / pose).  Lanes per query:
+// LISLAM_KNN_LANES = 64 (a wave, the default) or 16 (a 16-lane row: four queries per wave), read at
+// every launch.  Four queries per wave measured slower on config 5 (k_knn 0.213 vs 0.195 ms per
+// step, profiles/r05_map_ab.txt): the search is issue-bound, not latency-bound per wave.
+int knn_lanes() {
+  const char* e = getenv("LISLAM_KNN_LANES");
+  return e && atoi(e) == 16 ? 16 : 64;
+}
 int knn_device(lislam_map* m, const float* q, int stride, const int* qcount, int n, const double* pose, int k, float max_d2,
                float4* out_pts, float* out_d2, int* out_found) {
   lislam_ctx* c = m->ctx;
   if (n <= 0) return LISLAM_OK;
-  const int nb = blocks((int64_t)n * kG);  // one wavefront per query
+  const int G = knn_lanes();
+  const int nb = blocks((int64_t)n * G);  // G lanes per query, 256-thread workgroups
   MapView v = m->view();
   TimedScope ts(c, kT_knn);
-  if (k <= 5)
-    hipLaunchKernelGGL(k_knn<5>, dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2, out_pts,
-                       out_d2, out_found);
-  else
-    hipLaunchKernelGGL(k_knn<8>, dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2, out_pts,
-                       out_d2, out_found);
+  if (G == 16) {
+    if (k <= 5)
+      hipLaunchKernelGGL((k_knn<5, 16>), dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2,
+                         out_pts, out_d2, out_found);
+    else
+      hipLaunchKernelGGL((k_knn<8, 16>), dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2,
+                         out_pts, out_d2, out_found);
+  } else {
+    if (k <= 5)
+      hipLaunchKernelGGL((k_knn<5, 64>), dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2,
+                         out_pts, out_d2, out_found);
+    else
+      hipLaunchKernelGGL((k_knn<8, 64>), dim3(nb), dim3(256), 0, stream_of(c), v, q, stride, qcount, n, pose, k, max_d2,
+                         out_pts, out_d2, out_found);
+  }
   MCHK(c, hipGetLastError());
   return LISLAM_OK;
 }

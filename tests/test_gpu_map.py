@@ -70,14 +70,47 @@ def test_knn_corridor_and_far_queries(pkg, oracle, ctx, synth):
     g.close()
 
 
+@pytest.mark.parametrize("cell", [0.0, 0.1, 1.0])
+def test_knn_16_lane_groups_bit_exact(pkg, oracle, ctx, synth, monkeypatch, cell):
+    """Four queries per wave (LISLAM_KNN_LANES=16: one 16-lane row per query, every group-wide step
+    a row op, groups leaving the shell loop at different shells) against the oracle: random map and
+    queries (some outside the map's box), k 1 / 5 / 8, max distances, and the corridor map with
+    far queries that take the whole-map scan."""
+    monkeypatch.setenv("LISLAM_KNN_LANES", "16")
+    rng = np.random.default_rng(21)
+    P = _f32(rng.uniform(-6, 6, (50000, 3)))
+    Q = _f32(rng.uniform(-8, 8, (4000, 3)))
+    g = pkg.mapping.IkdMap(ctx, 0.4, cell)
+    g.build(P)
+    o = oracle.IkdMap(0.4)
+    o.build(P)
+    for k in (1, 5, 8):
+        _knn_equal(g.nearest_search(Q, k), o.knn(Q, k), k)
+    for md in (0.05, 0.3, 1.0):
+        _knn_equal(g.nearest_search(Q, 5, md), o.knn(Q, 5, md), 5)
+    g.close()
+    M = synth.make_corridor_map(300_000, spacing=0.05)
+    g = pkg.mapping.IkdMap(ctx, 0.4, 0.1)
+    g.build(M)
+    o = oracle.IkdMap(0.4)
+    o.build(M)
+    Q = M[rng.choice(len(M), 3001, replace=False), :3] + rng.normal(0, 0.03, (3001, 3))
+    far = _f32(np.array([[500.0, 30.0, 9.0], [-50.0, 0.0, 0.0], [2.0, 0.0, 40.0]]))
+    Q = _f32(np.concatenate([Q, far]))  # 3004 queries: the last workgroup is partly empty
+    _knn_equal(g.nearest_search(Q, 5), o.knn(Q, 5), 5)
+    g.close()
+
+
+@pytest.mark.parametrize("lanes", ["16", "64"])
 @pytest.mark.parametrize("near", ["-1", "0", "0.02", "0.1", "0.3", "2"])
 @pytest.mark.parametrize("cell", [0.1, 0.3])
-def test_knn_near_first_pass(pkg, oracle, ctx, synth, monkeypatch, near, cell):
+def test_knn_near_first_pass(pkg, oracle, ctx, synth, monkeypatch, near, cell, lanes):
     """The 3x3x3 block's near-cells-first split (LISLAM_KNN_NEAR, metres; -1: one pass) returns the
     same k-best as the oracle's k-d tree for every radius, including radii that cover no cell but
     the query's own (0), part of the block (0.02 .. 0.3) and all of it (2), with and without a
-    max distance."""
+    max distance, with 64 and 16 lanes per query."""
     monkeypatch.setenv("LISLAM_KNN_NEAR", near)
+    monkeypatch.setenv("LISLAM_KNN_LANES", lanes)
     M = synth.make_corridor_map(200_000, spacing=0.05)
     g = pkg.mapping.IkdMap(ctx, 0.4, cell)
     g.build(M)
