@@ -428,12 +428,17 @@ __global__ __launch_bounds__(256) void k_knn(MapView m, const float* queries, in
 // Eigen::ColPivHouseholderQR<Matrix<double,5,3>>::compute + solve(-1): column-pivoted
 // Householder QR with norm downdating, rank from the threshold, R^-1 Q^T b, un-permuted.
 __device__ __forceinline__ void colpiv_qr_solve_5x3(double (&A)[5][3], double* x) {
-  const int R = 5, C = 3;
+  // Every loop has a constant trip count and every data-dependent index (the pivot column, the
+  // rank) is a predicate over unrolled indices, so A and the work arrays stay in registers (a
+  // dynamic index puts them in LDS or scratch); the arithmetic and its order are Eigen's.
+  constexpr int R = 5, C = 3;
   double upd[3], dir[3], tau[3];
   int trans[3];
   double maxn = 0;
+#pragma unroll
   for (int j = 0; j < C; j++) {
     double s = 0;
+#pragma unroll
     for (int i = 0; i < R; i++) s += A[i][j] * A[i][j];
     upd[j] = dir[j] = sqrt(s);
     maxn = fmax(maxn, upd[j]);
@@ -442,40 +447,54 @@ __device__ __forceinline__ void colpiv_qr_solve_5x3(double (&A)[5][3], double* x
   const double thr = (maxn * eps) * (maxn * eps) / R;
   const double downdate = sqrt(eps);
   int nonzero = C;
+#pragma unroll
   for (int k = 0; k < C; k++) {
     int big = k;
+    double ub = upd[k];
+#pragma unroll
     for (int j = k + 1; j < C; j++)
-      if (upd[j] > upd[big]) big = j;
-    const double bsq = upd[big] * upd[big];
+      if (upd[j] > ub) { big = j; ub = upd[j]; }
+    const double bsq = ub * ub;
     if (nonzero == C && bsq < thr * (R - k)) nonzero = k;
     trans[k] = big;
-    if (k != big) {
-      for (int i = 0; i < R; i++) { const double t = A[i][k]; A[i][k] = A[i][big]; A[i][big] = t; }
-      double t = upd[k]; upd[k] = upd[big]; upd[big] = t;
-      t = dir[k]; dir[k] = dir[big]; dir[big] = t;
+#pragma unroll
+    for (int j = k + 1; j < C; j++) {
+      if (j == big) {
+#pragma unroll
+        for (int i = 0; i < R; i++) { const double t = A[i][k]; A[i][k] = A[i][j]; A[i][j] = t; }
+        double t = upd[k]; upd[k] = upd[j]; upd[j] = t;
+        t = dir[k]; dir[k] = dir[j]; dir[j] = t;
+      }
     }
     const double c0 = A[k][k];
     double tail = 0;
+#pragma unroll
     for (int i = k + 1; i < R; i++) tail += A[i][k] * A[i][k];
     double beta;
     if (tail <= 2.2250738585072014e-308) {
       tau[k] = 0;
       beta = c0;
+#pragma unroll
       for (int i = k + 1; i < R; i++) A[i][k] = 0;
     } else {
       beta = sqrt(c0 * c0 + tail);
       if (c0 >= 0) beta = -beta;
+#pragma unroll
       for (int i = k + 1; i < R; i++) A[i][k] = A[i][k] / (c0 - beta);
       tau[k] = (beta - c0) / beta;
     }
     A[k][k] = beta;
+#pragma unroll
     for (int j = k + 1; j < C; j++) {
       if (tau[k] == 0) continue;
       double t = A[k][j];
+#pragma unroll
       for (int i = k + 1; i < R; i++) t += A[i][k] * A[i][j];
       A[k][j] -= tau[k] * t;
+#pragma unroll
       for (int i = k + 1; i < R; i++) A[i][j] -= tau[k] * A[i][k] * t;
     }
+#pragma unroll
     for (int j = k + 1; j < C; j++) {
       if (upd[j] == 0) continue;
       double t = fabs(A[k][j]) / upd[j];
@@ -484,6 +503,7 @@ __device__ __forceinline__ void colpiv_qr_solve_5x3(double (&A)[5][3], double* x
       const double t2 = t * (upd[j] / dir[j]) * (upd[j] / dir[j]);
       if (t2 <= downdate) {
         double s = 0;
+#pragma unroll
         for (int i = k + 1; i < R; i++) s += A[i][j] * A[i][j];
         dir[j] = upd[j] = sqrt(s);
       } else {
@@ -491,21 +511,39 @@ __device__ __forceinline__ void colpiv_qr_solve_5x3(double (&A)[5][3], double* x
       }
     }
   }
+  // perm: the transpositions applied in order (perm[k] <-> perm[trans[k]])
   int perm[3] = {0, 1, 2};
-  for (int k = 0; k < C; k++) { const int t = perm[k]; perm[k] = perm[trans[k]]; perm[trans[k]] = t; }
+#pragma unroll
+  for (int k = 0; k < C; k++) {
+#pragma unroll
+    for (int j = k + 1; j < C; j++)
+      if (j == trans[k]) { const int t = perm[k]; perm[k] = perm[j]; perm[j] = t; }
+  }
   double c[5] = {-1, -1, -1, -1, -1};
-  for (int k = 0; k < nonzero; k++) {
-    if (tau[k] == 0) continue;
+#pragma unroll
+  for (int k = 0; k < C; k++) {
+    if (k >= nonzero || tau[k] == 0) continue;
     double t = c[k];
+#pragma unroll
     for (int i = k + 1; i < R; i++) t += A[i][k] * c[i];
     c[k] -= tau[k] * t;
+#pragma unroll
     for (int i = k + 1; i < R; i++) c[i] -= tau[k] * A[i][k] * t;
   }
-  for (int i = nonzero - 1; i >= 0; i--) {
+#pragma unroll
+  for (int i = C - 1; i >= 0; i--) {
+    if (i >= nonzero) continue;
     c[i] /= A[i][i];
+#pragma unroll
     for (int r = 0; r < i; r++) c[r] -= A[r][i] * c[i];
   }
-  for (int i = 0; i < C; i++) x[perm[i]] = i < nonzero ? c[i] : 0.0;
+#pragma unroll
+  for (int i = 0; i < C; i++) {
+    const double v = i < nonzero ? c[i] : 0.0;
+#pragma unroll
+    for (int j = 0; j < C; j++)
+      if (perm[i] == j) x[j] = v;
+  }
 }
 
 // laserMapping.cpp:756-788, mapOptimization.cpp:398-420
@@ -521,29 +559,38 @@ __device__ __forceinline__ bool plane_fit(const float4* nb, double* n, double* d
   return true;
 }
 
-// symmetric 3x3 eigen-decomposition, cyclic Jacobi; ascending eigenvalues, V[:, k] vectors
+// symmetric 3x3 eigen-decomposition, cyclic Jacobi; ascending eigenvalues, V[:, k] vectors.  Loops
+// unrolled and the final ordering a compare-swap network on (eigenvalue, column) pairs, so nothing
+// is indexed by data (the arrays stay in registers).
 __device__ __forceinline__ void sym_eig3(double (&a)[3][3], double* w, double (&V)[3][3]) {
+#pragma unroll
   for (int i = 0; i < 3; i++)
+#pragma unroll
     for (int j = 0; j < 3; j++) V[i][j] = i == j ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 32; sweep++) {
     const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
     if (off == 0.0) break;
+#pragma unroll
     for (int p = 0; p < 2; p++)
+#pragma unroll
       for (int q = p + 1; q < 3; q++) {
         if (a[p][q] == 0.0) continue;
         const double theta = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
         const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
         const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           const double akp = a[k][p], akq = a[k][q];
           a[k][p] = c * akp - s * akq;
           a[k][q] = s * akp + c * akq;
         }
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           const double apk = a[p][k], aqk = a[q][k];
           a[p][k] = c * apk - s * aqk;
           a[q][k] = s * apk + c * aqk;
         }
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           const double vkp = V[k][p], vkq = V[k][q];
           V[k][p] = c * vkp - s * vkq;
@@ -551,17 +598,29 @@ __device__ __forceinline__ void sym_eig3(double (&a)[3][3], double* w, double (&
         }
       }
   }
-  int ord[3] = {0, 1, 2};
+  // ascending order: the index sort of the round-4 code (ord[i] <-> ord[j] when a[ord[j]][ord[j]] <
+  // a[ord[i]][ord[i]], i < j) applied to the (eigenvalue, column) pairs themselves
+  double d[3] = {a[0][0], a[1][1], a[2][2]};
+  double col[3][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+#pragma unroll
+    for (int i = 0; i < 3; i++) col[k][i] = V[i][k];
+#pragma unroll
   for (int i = 0; i < 3; i++)
+#pragma unroll
     for (int j = i + 1; j < 3; j++)
-      if (a[ord[j]][ord[j]] < a[ord[i]][ord[i]]) { const int t = ord[i]; ord[i] = ord[j]; ord[j] = t; }
-  double W[3][3];
+      if (d[j] < d[i]) {
+        const double t = d[i]; d[i] = d[j]; d[j] = t;
+#pragma unroll
+        for (int r = 0; r < 3; r++) { const double u = col[i][r]; col[i][r] = col[j][r]; col[j][r] = u; }
+      }
+#pragma unroll
   for (int k = 0; k < 3; k++) {
-    w[k] = a[ord[k]][ord[k]];
-    for (int i = 0; i < 3; i++) W[i][k] = V[i][ord[k]];
+    w[k] = d[k];
+#pragma unroll
+    for (int i = 0; i < 3; i++) V[i][k] = col[k][i];
   }
-  for (int i = 0; i < 3; i++)
-    for (int j = 0; j < 3; j++) V[i][j] = W[i][j];
 }
 
 // laserMapping.cpp:681-723
