@@ -1469,7 +1469,10 @@ constexpr int kEngWaves = kEngThreads / 64;
 // Queries per association item: one per wave (64 lanes), EngCtl::Q = the item workgroup's waves —
 // kEngWaves in the single-launch engine (items share its workgroup size), up to kMaxItemWaves in the
 // split engine's items kernel (LISLAM_ENGINE_ITEM_WAVES).
-constexpr int kMaxItemWaves = 16;
+#ifndef LISLAM_MAX_ITEM_WAVES
+#define LISLAM_MAX_ITEM_WAVES 16
+#endif
+constexpr int kMaxItemWaves = LISLAM_MAX_ITEM_WAVES;
 // A block record: 64 B = four 16-B quads, written by the association wave of its query (lanes 0..3,
 // write-through) and read by the solve with 16-B loads:
 //   q0 c.x c.y c.z a.x (float) | q1 a.y a.z (float) kind (int) - | q2 u.x u.y (double) | q3 u.z (double) -
