@@ -299,7 +299,7 @@ __device__ __forceinline__ int xcd_block(int b, int nblk) {
 // One pass over `total` cells (the 3x3x3 block for s == 1, else the shell at radius s): lanes
 // probe one cell each (skipping cells whose box cannot beat `bound`, and those within `skip` — a
 // pass over them already ran; skip < 0: none; s == 1 with bound = inf: every cell, no box test),
-// then the points of the probed cells are dealt evenly over the 64 lanes (exclusive prefix of the
+// then the points of the probed cells are dealt evenly over the G lanes (exclusive prefix of the
 // counts + a log2(G)-step binary search per point), four loads in flight per lane.  G lanes per
 // query: a wave (64) or a 16-lane row (four queries per wave; every group-wide step is a row op).
 template <int K, int G>
