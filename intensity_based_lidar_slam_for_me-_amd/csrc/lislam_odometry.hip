@@ -2748,7 +2748,7 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl c
 #define LISLAM_ITEM_WPE 4  // waves per SIMD the items are compiled for: 4 = 128 VGPRs
 #endif
 template <int kQpw>
-__global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_items(OdomArgs a, EngCtl ctl) {
+__device__ __forceinline__ void eng_items_body(const OdomArgs& a, const EngCtl& ctl) {
   __shared__ EngShared sh;
   const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
@@ -2774,6 +2774,18 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
     __syncthreads();
     tk = ok ? (unsigned)uni((int)sh.ticket) : total;
   }
+}
+template <int kQpw>
+__global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_items(OdomArgs a, EngCtl ctl) {
+  eng_items_body<kQpw>(a, ctl);
+}
+// One engine at a time (the latency shape: qpw 1, depth 1, 12-wave items): the same items compiled
+// for 3 waves per SIMD (168 VGPRs: no spills, where the 128-VGPR build spills 36 VGPRs and ~180
+// SGPRs).  With several engines in flight the 128-VGPR build stays: two item workgroups per CU beat
+// spill-free ones (profiles/r05_shape_ab.txt, r05wpe).  LISLAM_ENGINE_SOLO_ITEMS=1 selects it (A/B).
+constexpr int kSoloItemWaves = 12;
+__global__ __launch_bounds__(64 * kSoloItemWaves, 3) void k_odom_items_solo(OdomArgs a, EngCtl ctl) {
+  eng_items_body<1>(a, ctl);
 }
 
 static int item_waves(int qpw, int depth);
@@ -3009,7 +3021,10 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
-  switch (ctl.qpw) {
+  static const bool solo_ok = getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 1;
+  const bool solo = solo_ok && depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
+  if (solo) hipLaunchKernelGGL(k_odom_items_solo, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
+  else switch (ctl.qpw) {
     case 4: hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
     case 3: hipLaunchKernelGGL(k_odom_items<3>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
     case 2: hipLaunchKernelGGL(k_odom_items<2>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
