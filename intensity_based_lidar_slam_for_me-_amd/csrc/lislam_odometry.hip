@@ -2782,7 +2782,8 @@ __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_it
 // One engine at a time (the latency shape: qpw 1, depth 1, 12-wave items): the same items compiled
 // for 3 waves per SIMD (168 VGPRs: no spills, where the 128-VGPR build spills 36 VGPRs and ~180
 // SGPRs).  With several engines in flight the 128-VGPR build stays: two item workgroups per CU beat
-// spill-free ones (profiles/r05_shape_ab.txt, r05wpe).  LISLAM_ENGINE_SOLO_ITEMS=1 selects it (A/B).
+// spill-free ones (profiles/r05_shape_ab.txt, r05wpe); one engine gains 2-3 % (single sequence 10.40k /
+// 10.43k vs 10.20k / 10.10k, r05solo).  LISLAM_ENGINE_SOLO_ITEMS=0: the 128-VGPR build (A/B).
 constexpr int kSoloItemWaves = 12;
 __global__ __launch_bounds__(64 * kSoloItemWaves, 3) void k_odom_items_solo(OdomArgs a, EngCtl ctl) {
   eng_items_body<1>(a, ctl);
@@ -3021,7 +3022,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
-  static const bool solo_ok = getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 1;
+  static const bool solo_ok = !(getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 0);
   const bool solo = solo_ok && depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
   if (solo) hipLaunchKernelGGL(k_odom_items_solo, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
   else switch (ctl.qpw) {
