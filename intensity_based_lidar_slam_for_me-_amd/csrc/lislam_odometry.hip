@@ -148,8 +148,11 @@ __device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kK], int P, uint64_t*
 // which: 0 less-sharp, 1 less-flat (targets), 2 sharp, 3 flat (queries: permutation only);
 // blockIdx.x -> (scan, w0 / w1 / w2 of the launch).  kW waves of kK keys per lane (64 kK kW keys in
 // registers).
+#ifndef LISLAM_TI_WPE32
+#define LISLAM_TI_WPE32 4  // waves per SIMD the 32-keys-per-lane build is compiled for (4: 128 VGPRs)
+#endif
 template <int kW, int kK>
-__global__ __launch_bounds__(64 * kW, 4) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+__global__ __launch_bounds__(64 * kW, kK >= 32 ? LISLAM_TI_WPE32 : 4) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
   constexpr int kKeysPerLane = kK, kPer = 64 * kK;
   __shared__ uint64_t xch[kW * 8 * 64];
   __shared__ float red[6][kW];
