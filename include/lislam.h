@@ -227,10 +227,16 @@ int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
 int lislam_set_engine_shape(lislam_ctx* ctx, int32_t queries_per_wave, int32_t depth);
 /* status = the number of engine launches of the batch that gave up since the previous status call
  * (one of the engine's bounded device waits expired, e.g. when its two launches could not run
- * together).  An aborted launch is recovered, not refused: the next call on the batch (any
- * lislam_batch_* call, lislam_odom_step, lislam_synchronize) waits for the engine on the host and
- * re-runs that launch's chains on the per-round schedule (LISLAM_ENGINE_OFF, no device waits) before
- * it goes on, so the outputs are always those of a complete schedule.  Reading the count clears it. */
+ * together).  An aborted launch is recovered, not refused: the next call that reads or replaces the
+ * batch's outputs waits for the engine on the host and re-runs that launch's chains on the
+ * per-round schedule (LISLAM_ENGINE_OFF, no device waits) before it goes on, so the outputs are
+ * always those of a complete schedule.  Those calls ("settling" calls): lislam_batch_extract,
+ * lislam_batch_odometry(_gated), lislam_batch_download, lislam_batch_download_cloud,
+ * lislam_batch_kernel_times, lislam_batch_odometry_status / _engine / _abort_code,
+ * lislam_batch_mapopt(_corner), lislam_odom_step(_gated) and lislam_synchronize.  The calls that
+ * touch only the input points or the ORB / ground stages do not wait for the engine:
+ * lislam_batch_upload(_async), lislam_batch_input_device_ptr, lislam_batch_set_timing,
+ * lislam_batch_ground, lislam_batch_intensity_odometry.  Reading the count clears it. */
 int lislam_batch_odometry_status(lislam_batch* b, int32_t* status);
 /* Which schedule the batch's last odometry call ran: 0 per-round launches, 1 the single-launch
  * engine (k_odom_chain), 2 the split engine (k_odom_roles + k_odom_items on CU-masked streams). */
@@ -240,6 +246,11 @@ int lislam_batch_odometry_engine(lislam_batch* b, int32_t* kind);
  * item waiting for its pass's pose, 3 a solve role waiting for its pass's items, 4 / 5 the
  * progressive gather's poll / loads, 0x57xx an overflow query out of range. */
 int lislam_batch_odometry_abort_code(lislam_batch* b, int32_t* code);
+/* The CU-masked streams the library holds on a device (*masked_queues).  Each is a hardware queue
+ * of its own, and past about 20 of them in one process every launch slows: a context holds one
+ * (its stream, which its ORB front end shares), the chain engine's 4 stream pairs and the per-round
+ * schedule's group stream belong to the device (shared by all batches). */
+int lislam_device_queue_count(int32_t device, int32_t* masked_queues);
 
 /* Order of equal sort keys in the two std::sort calls of the feature extraction:
  * - each segment's sort by curvature (scanRegistration.cpp:445), which decides which of two

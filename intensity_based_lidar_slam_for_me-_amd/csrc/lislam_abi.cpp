@@ -132,7 +132,7 @@ int lislam_ctx_destroy(lislam_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->factor_buf);
   }
-  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  if (c->own_stream) lislam::destroy_stream(c->own_stream);
   const int dev = c->device;
   delete c;
   if (dev >= 0 && dev < 64 && --g_ctx_count[dev] == 0) lislam::release_engine_streams(dev);
@@ -144,14 +144,16 @@ const char* lislam_last_error(const lislam_ctx* c) { return c ? c->err.c_str() :
 static int engine_settle(lislam_batch* b);
 
 // The per-round schedule's chain groups: 2 streams, so one group's solves overlap another's
-// association (a solve occupies one workgroup per chain, far from filling the device).  Made when
-// that schedule first runs (or an engine launch is recovered on it): a batch that only runs the
-// engine holds no extra hardware queue.
+// association (a solve occupies one workgroup per chain, far from filling the device).  Group 0
+// runs on the context stream; the other groups' streams belong to the device (lislam::round_stream,
+// made when that schedule first runs, shared by every batch): running that schedule adds one
+// hardware queue to the process, not one per batch.
 static int round_streams(lislam_batch* b) {
   lislam_ctx* c = b->ctx;
   b->odo_stream[0] = c->stream;
   for (int g = 1; g < lislam_batch::kGroups; g++) {
-    if (!b->odo_stream[g] && !lislam::work_stream(c->device, &b->odo_stream[g])) return fail(c, LISLAM_ERR_DEVICE, "stream");
+    if (!b->odo_stream[g] && !(b->odo_stream[g] = lislam::round_stream(c->device, g)))
+      return fail(c, LISLAM_ERR_DEVICE, "stream");
     if (!b->odo_join[g]) HIPCHK(c, hipEventCreateWithFlags(&b->odo_join[g], hipEventDisableTiming));
   }
   if (lislam_batch::kGroups > 1 && !b->odo_fork) HIPCHK(c, hipEventCreateWithFlags(&b->odo_fork, hipEventDisableTiming));
@@ -195,20 +197,25 @@ static int engine_settle(lislam_batch* b) {
     b->eng_pending = false;
   }
   if (!b->eng_check) return LISLAM_OK;
-  b->eng_check = false;
   // the host waits for the engine itself (not the context stream, which may hold later work)
   HIPCHK(c, hipEventSynchronize(b->eng_done));
   // h_abort: the engine's error word (which wait gave up) and its sticky abort word
-  if (b->h_abort[1] == 0) return LISLAM_OK;
-  b->eng_abort_code = b->h_abort[0];
-  b->h_abort[0] = b->h_abort[1] = 0;
+  if (b->h_abort[1] == 0) {
+    b->eng_check = false;
+    return LISLAM_OK;
+  }
+  // eng_check stays set until the re-run is queued: a failure below leaves the recovery to the
+  // batch's next call instead of losing it
   HIPCHK(c, hipMemsetAsync(b->oa.eng_ctl + 3, 0, sizeof(unsigned), c->stream));
-  b->eng_fallbacks++;
   // the per-round schedule has no device waits: it cannot abort
   if (round_streams(b) != LISLAM_OK) return LISLAM_ERR_DEVICE;
   lislam::launch_odometry(b->eng_args, b->odo_stream, lislam_batch::kGroups, b->odo_fork, b->odo_join, nullptr,
                           &lislam_batch::event_cb, b);
   HIPCHK(c, hipGetLastError());
+  b->eng_abort_code = b->h_abort[0];
+  b->h_abort[0] = b->h_abort[1] = 0;
+  b->eng_fallbacks++;
+  b->eng_check = false;
   return LISLAM_OK;
 }
 #define SETTLE(b)                           \
@@ -331,7 +338,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   for (auto& v : b->ext_ev) for (hipEvent_t e : v) hipEventDestroy(e);
   for (auto& v : b->odo_ev) for (auto& t : v) { hipEventDestroy(t.b); hipEventDestroy(t.e); }
   for (int g = 1; g < lislam_batch::kMaxGroups; g++) {
-    if (b->odo_stream[g]) hipStreamDestroy(b->odo_stream[g]);
+    // odo_stream[g]: the device's (lislam::round_stream), joined into the context stream synchronized above
     if (b->odo_join[g]) hipEventDestroy(b->odo_join[g]);
   }
   if (b->odo_fork) hipEventDestroy(b->odo_fork);
@@ -631,15 +638,18 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
       b->h_abort[0] = b->h_abort[1] = 0;
     }
     if (ev) { e0 = b->get_event(); e1 = b->get_event(); }
+    bool queued = false;
     if (b->eng_split) {
       // the inputs: everything queued on the context stream so far (the last extract, any per-round
       // odometry queued after it, the staging copies just queued); the launch copies its abort words
       // to h_abort and records eng_done on its own stream
       HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
-      lislam::launch_odometry_chain_split(o, b->eng_ready, b->eng_fork, b->eng_join_r, b->eng_join_i, e0, e1,
-                                          b->h_abort, b->eng_done);
-      b->eng_pending = true;
-    } else {
+      queued = lislam::launch_odometry_chain_split(o, b->eng_ready, b->eng_fork, b->eng_join_r, b->eng_join_i, e0, e1,
+                                                   b->h_abort, b->eng_done) > 0;
+      if (queued) b->eng_pending = true;
+      else b->eng_split = 0;  // no engine streams on this device after all: the single launch below
+    }
+    if (!queued) {
       if (ev) HIPCHK(c, hipEventRecord(e0, c->stream));
       lislam::launch_odometry_chain(o, c->stream);
       if (ev) HIPCHK(c, hipEventRecord(e1, c->stream));
@@ -689,6 +699,12 @@ int lislam_batch_odometry_abort_code(lislam_batch* b, int32_t* code) {
   if (!b || !code) return LISLAM_ERR_ARG;
   SETTLE(b);
   *code = (int32_t)b->eng_abort_code;
+  return LISLAM_OK;
+}
+
+int lislam_device_queue_count(int32_t device, int32_t* masked_queues) {
+  if (!masked_queues || device < 0) return LISLAM_ERR_ARG;
+  *masked_queues = lislam::masked_queue_count(device);
   return LISLAM_OK;
 }
 

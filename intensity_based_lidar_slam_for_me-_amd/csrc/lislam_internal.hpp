@@ -152,13 +152,22 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 // (the inputs) and for the launch `depth` before it, the items stream forks from it; join_r /
 // join_i mark the end (the caller makes its stream wait for them later); t0 / t1 (nullable): timing
 // events; h_abort (nullable): pinned host words the launch's error / sticky abort words are copied
-// to at its end, `done` (nullable) recorded after that copy.  0 = no launch (no CU masks).
+// to at its end, `done` (nullable) recorded after that copy.  0 = nothing queued (no CU masks on
+// this device): the caller must run the single-launch engine instead.
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
                                 hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done);
 bool engine_streams_available(int dev);  // the device has CU-masked streams for the split engine
-void release_engine_streams(int dev);    // with the device's last context
+void release_engine_streams(int dev);    // with the device's last context (also the round-stream pool)
 // A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).
+// Every CU-masked stream is a hardware queue of its own; the library counts them per device
+// (masked_queue_count) and destroys them with destroy_stream.
 bool work_stream(int dev, hipStream_t* s);
+void destroy_stream(hipStream_t s);
+int masked_queue_count(int dev);
+// The per-round schedule's extra chain-group stream g (>= 1): one per device and group, shared by
+// every batch (two pipelined contexts' group-g launches then queue on one hardware queue instead of
+// one each); null if it cannot be made.
+hipStream_t round_stream(int dev, int g);
 // Whether the engine serves a.n_chains chains (launch_odometry otherwise): mode = the context's
 // lislam_set_odometry_schedule (LISLAM_ENGINE_*; a context starts from the environment's
 // LISLAM_ENGINE if set); AUTO = on for at most 4 chains.

@@ -2883,6 +2883,39 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
 // CU in every XCD, the items every other CU, so an item workgroup never takes the CU a solve role
 // needs whole (256 VGPRs x 8 waves).  (Unmasked priority streams were measured to starve the role
 // of a whole CU under the pipelined extraction, r04i, and are not offered.)
+// Every CU-masked stream is a hardware queue of its own, and past about 20 of them in one process
+// every launch slows (r05c56: the isolated chain 34.7 -> 47-50 ms).  The library's masked streams
+// are registered here, so the count is known (lislam_device_queue_count, bench.py's config) and kept
+// low by construction: a context holds one (its stream, which its ORB front end shares), the
+// engine's kMaxDepth pairs and the per-round schedule's group streams belong to the device.
+namespace {
+std::mutex g_masked_mu;
+std::vector<std::pair<hipStream_t, int>> g_masked;  // (stream, device)
+bool masked_stream(int dev, hipStream_t* s, int words, const uint32_t* mask) {
+  if (hipExtStreamCreateWithCUMask(s, words, mask) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(g_masked_mu);
+  g_masked.emplace_back(*s, dev);
+  return true;
+}
+}  // namespace
+
+void destroy_stream(hipStream_t s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> lk(g_masked_mu);
+    for (size_t i = 0; i < g_masked.size(); i++)
+      if (g_masked[i].first == s) { g_masked.erase(g_masked.begin() + i); break; }
+  }
+  (void)hipStreamDestroy(s);
+}
+
+int masked_queue_count(int dev) {
+  std::lock_guard<std::mutex> lk(g_masked_mu);
+  int n = 0;
+  for (const auto& e : g_masked) n += e.second == dev;
+  return n;
+}
+
 static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
@@ -2892,9 +2925,9 @@ static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items)
   const int words = (cus + 31) / 32;
   std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
   for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);
-  if (hipExtStreamCreateWithCUMask(roles, words, mr.data()) != hipSuccess) return false;
-  if (hipExtStreamCreateWithCUMask(items, words, mi.data()) != hipSuccess) {
-    (void)hipStreamDestroy(*roles);
+  if (!masked_stream(dev, roles, words, mr.data())) return false;
+  if (!masked_stream(dev, items, words, mi.data())) {
+    destroy_stream(*roles);
     *roles = nullptr;
     return false;
   }
@@ -2914,7 +2947,7 @@ bool work_stream(int dev, hipStream_t* s) {
       const int words = (cus + 31) / 32;
       std::vector<uint32_t> m(words, 0u);
       for (int i = nx; i < cus; i++) m[i / 32] |= 1u << (i % 32);
-      if (hipExtStreamCreateWithCUMask(s, words, m.data()) == hipSuccess) return true;
+      if (masked_stream(dev, s, words, m.data())) return true;
     }
   }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
@@ -2928,23 +2961,27 @@ bool work_stream(int dev, hipStream_t* s) {
 // launches of all contexts run on kMaxDepth stream pairs, not one pair per batch, so five or six
 // pipelined contexts do not push the process past the device's hardware queues (past ~20 masked
 // queues every launch slowed: the isolated chain 34.7 -> 47-50 ms with six contexts, r05c56).
+// Launch n takes slot n % kMaxDepth (its stream pair) and waits for the event of launch n - depth,
+// whatever slot that one used: with contexts of different depths on one device, a depth-1 launch
+// still waits for the launch just before it (a per-depth ring would wait for the last launch that
+// used its slot instead).
 struct EngineGate {
   static constexpr int kMaxDepth = 4;
   std::mutex mu;
   hipEvent_t ev[kMaxDepth] = {};
   hipStream_t roles[kMaxDepth] = {}, items[kMaxDepth] = {};
-  int next = 0;
+  unsigned long long launches = 0;
   int avail = -1;  // -1 not probed, 0 no CU masks on this device, 1 ready
+  static constexpr int kRoundGroups = 4;
+  hipStream_t round[kRoundGroups] = {};  // the per-round schedule's group streams (round_stream)
 };
 static EngineGate* engine_gate(int dev) {
   static EngineGate gates[64];
   return dev >= 0 && dev < 64 ? &gates[dev] : nullptr;
 }
 
-bool engine_streams_available(int dev) {
-  EngineGate* g = engine_gate(dev);
-  if (!g) return false;
-  std::lock_guard<std::mutex> lk(g->mu);
+// g->mu held
+static bool probe_engine_streams(EngineGate* g, int dev) {
   if (g->avail < 0) {
     g->avail = 1;
     for (int s = 0; s < EngineGate::kMaxDepth && g->avail; s++)
@@ -2953,20 +2990,40 @@ bool engine_streams_available(int dev) {
   return g->avail == 1;
 }
 
-// The device's engine streams and slot events are released with its last context (a stream left to
-// the process's exit is torn down after the runtime, which a profiler's exit path trips over).
+bool engine_streams_available(int dev) {
+  EngineGate* g = engine_gate(dev);
+  if (!g) return false;
+  std::lock_guard<std::mutex> lk(g->mu);
+  return probe_engine_streams(g, dev);
+}
+
+hipStream_t round_stream(int dev, int grp) {
+  EngineGate* g = engine_gate(dev);
+  if (!g || grp < 1 || grp >= EngineGate::kRoundGroups) return nullptr;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (!g->round[grp] && !work_stream(dev, &g->round[grp])) g->round[grp] = nullptr;
+  return g->round[grp];
+}
+
+// The device's engine streams, round streams and slot events are released with its last context
+// (a stream left to the process's exit is torn down after the runtime, which a profiler's exit
+// path trips over).
 void release_engine_streams(int dev) {
   EngineGate* g = engine_gate(dev);
   if (!g) return;
   std::lock_guard<std::mutex> lk(g->mu);
   for (int s = 0; s < EngineGate::kMaxDepth; s++) {
-    if (g->items[s]) { (void)hipStreamSynchronize(g->items[s]); (void)hipStreamDestroy(g->items[s]); }
-    if (g->roles[s]) { (void)hipStreamSynchronize(g->roles[s]); (void)hipStreamDestroy(g->roles[s]); }
+    if (g->items[s]) { (void)hipStreamSynchronize(g->items[s]); destroy_stream(g->items[s]); }
+    if (g->roles[s]) { (void)hipStreamSynchronize(g->roles[s]); destroy_stream(g->roles[s]); }
     if (g->ev[s]) (void)hipEventDestroy(g->ev[s]);
     g->items[s] = g->roles[s] = nullptr;
     g->ev[s] = nullptr;
   }
-  g->next = 0;
+  for (int r = 1; r < EngineGate::kRoundGroups; r++) {
+    if (g->round[r]) { (void)hipStreamSynchronize(g->round[r]); destroy_stream(g->round[r]); }
+    g->round[r] = nullptr;
+  }
+  g->launches = 0;
   g->avail = -1;
 }
 
@@ -3009,15 +3066,20 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   // CU at 128 VGPRs — and each chain's idle association slots, while its solve runs, serve the other)
   const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
   EngineGate* gate = engine_gate(dev);
-  if (!gate || gate->avail != 1) return 0;
+  if (!gate) return 0;
   std::unique_lock<std::mutex> lock(gate->mu);
-  gate->next = (gate->next + 1) % depth;
-  hipEvent_t& e = gate->ev[gate->next];
-  if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  hipEvent_t prev = e;  // recorded by the launch depth launches ago; re-recorded below
-  hipStream_t roles = gate->roles[gate->next], items = gate->items[gate->next];  // the slot's streams
+  // the streams may have been released (the device's last context went away) since the caller
+  // probed them: probe again under the lock
+  if (!probe_engine_streams(gate, dev)) return 0;
+  const unsigned long long n = gate->launches++;
+  const int slot = (int)(n % EngineGate::kMaxDepth);
+  for (hipEvent_t& e : gate->ev)
+    if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  hipStream_t roles = gate->roles[slot], items = gate->items[slot];  // the slot's streams
   (void)hipStreamWaitEvent(roles, ready, 0);
-  if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
+  // launch n - depth (its event is re-recorded only by launch n - depth + kMaxDepth > n)
+  if (n >= (unsigned long long)depth) (void)hipStreamWaitEvent(roles, gate->ev[(n - depth) % EngineGate::kMaxDepth], 0);
+  hipEvent_t mine = gate->ev[slot];
   if (t0) (void)hipEventRecord(t0, roles);
   // zero the control words of this launch, all but word 3 (the sticky abort)
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);
@@ -3042,7 +3104,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   // launch can queue behind it (still under the gate's lock)
   if (h_abort) (void)hipMemcpyAsync(h_abort, a.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, items);
   if (done) (void)hipEventRecord(done, items);
-  (void)hipEventRecord(prev, items);
+  (void)hipEventRecord(mine, items);
   return grid;
 }
 

@@ -2214,7 +2214,12 @@ struct OrbBatch {
   std::vector<void*> allocs;
   double* outT = nullptr;   // [S][7]
   int* outS = nullptr;      // [S][8]
-  hipStream_t side = nullptr;  // the batch front end runs here, concurrently with the odometry chain
+  // The batch front end runs on the context stream: the split chain engine queues nothing there, so
+  // the ORB kernels still overlap the chain, and a context holds one hardware queue, not two (past
+  // ~20 CU-masked queues per process every launch slows; six pipelined contexts used to hold twelve
+  // here).  LISLAM_ORB_SIDE_STREAM=1: a stream of the batch's own, ordered only after the a1 images.
+  hipStream_t side = nullptr;
+  hipStream_t st(const lislam_ctx* c) const { return side ? side : c->stream; }
   hipEvent_t done = nullptr;
   // the device-decided re-detection cascade (k_orb_decide): state, lists, and its verdict copied
   // to pinned host memory; `pending` until a reader of the outputs has checked it
@@ -2226,7 +2231,7 @@ struct OrbBatch {
   int info[2] = {-1, 0};     // lislam_batch_orb_cascade_info
   ~OrbBatch() {
     if (side) (void)hipStreamSynchronize(side);
-    if (side) (void)hipStreamDestroy(side);
+    if (side) destroy_stream(side);
     if (done) (void)hipEventDestroy(done);
     if (settled) (void)hipEventDestroy(settled);
     if (h_status) (void)hipHostFree(h_status);
@@ -2257,7 +2262,8 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
     ob->has_mask = mask != nullptr;
     ob->e1 = new OrbEngine();
     ob->e2 = new OrbEngine();
-    if (!work_stream(c->device, &ob->side)) return ofail(c, LISLAM_ERR_DEVICE, "ORB stream");
+    static const bool own_side = getenv("LISLAM_ORB_SIDE_STREAM") && atoi(getenv("LISLAM_ORB_SIDE_STREAM")) == 1;
+    if (own_side && !work_stream(c->device, &ob->side)) return ofail(c, LISLAM_ERR_DEVICE, "ORB stream");
     OCHK(c, hipEventCreateWithFlags(&ob->done, hipEventDisableTiming));
     // the engines' tables and mask pyramids are uploaded / built on the side stream, where the
     // front end that reads them runs
@@ -2266,7 +2272,7 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
       hipStream_t keep;
       ~StreamSwap() { c->stream = keep; }
     } swap{c, c->stream};
-    c->stream = ob->side;
+    c->stream = ob->st(c);
     ORC(engine_init(ob->e1, c, b->H, b->W, b->max_scans, nfeatures, mask));
     ORC(engine_init(ob->e2, c, b->H, b->W, b->max_scans, 2 * nfeatures, mask));
     ORC(ob->pb.init(c, b->max_scans, std::max(ob->e1->g.cap, ob->e2->g.cap), false));
@@ -2299,7 +2305,8 @@ int orb_batch_get(lislam_batch* b, int nfeatures, const uint8_t* mask, OrbBatch*
 
 namespace {
 
-// Body of lislam_batch_intensity_odometry; runs with c->stream switched to the batch's side stream.
+// Body of lislam_batch_intensity_odometry; runs with c->stream switched to the batch's ORB stream
+// (OrbBatch::st: the context stream unless LISLAM_ORB_SIDE_STREAM=1).
 int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
   lislam_ctx* c = b->ctx;
   hipStream_t st = c->stream;
@@ -2435,8 +2442,9 @@ int orb_settle(lislam_batch* b) {
   ob->info[1] = ob->h_status[1];
   if (ob->h_status[0] == 1) return LISLAM_OK;
   const hipStream_t main_stream = c->stream;
-  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_images, 0));
-  c->stream = ob->side;
+  const hipStream_t side = ob->st(c);
+  if (side != main_stream) OCHK(c, hipStreamWaitEvent(side, b->ev_images, 0));
+  c->stream = side;
   const int rc = batch_intensity_odometry(b, ob, ob->pending_n);
   c->stream = main_stream;
   return rc;
@@ -2444,10 +2452,11 @@ int orb_settle(lislam_batch* b) {
 
 extern "C" {
 
-// The ORB front end of every scan pair.  It runs on its own stream, ordered only after the
-// images of the last lislam_batch_extract, so it overlaps the rest of the extraction and the
-// odometry chain the caller may already have queued on the context stream; on return all of its work is done and the context stream is
-// ordered after it.
+// The ORB front end of every scan pair.  It is queued on the context stream, after the last
+// lislam_batch_extract (with LISLAM_ORB_SIDE_STREAM=1 on a stream of the batch's own, ordered only
+// after that extract's images); the split chain engine the caller may already have queued runs on
+// the device's engine streams, so the two overlap.  On return the context stream is ordered after
+// all of its work.
 int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nfeatures, const uint8_t* mask) {
   if (!b || n_scans < 1 || n_scans > b->max_scans || nfeatures < 1 || nfeatures > 16384) return LISLAM_ERR_ARG;
   lislam_ctx* c = b->ctx;
@@ -2458,16 +2467,19 @@ int lislam_batch_intensity_odometry(lislam_batch* b, int32_t n_scans, int32_t nf
   OrbBatch* ob = nullptr;
   ORC(orb_batch_get(b, nfeatures, mask, &ob));
   const hipStream_t main_stream = c->stream;
-  OCHK(c, hipStreamWaitEvent(ob->side, b->ev_images, 0));
-  c->stream = ob->side;
+  const hipStream_t side = ob->st(c);
+  if (side != main_stream) OCHK(c, hipStreamWaitEvent(side, b->ev_images, 0));
+  c->stream = side;
   ob->pending = false;  // a newer batch replaces results nobody read
   ob->info[0] = -1;
   ob->info[1] = 0;
   const int rc = (n_scans < 2 || n_scans > kCascadeMax) ? batch_intensity_odometry(b, ob, n_scans)
                                                                                : batch_intensity_odometry_dev(b, ob, n_scans);
   c->stream = main_stream;
-  OCHK(c, hipEventRecord(ob->done, ob->side));
-  OCHK(c, hipStreamWaitEvent(main_stream, ob->done, 0));
+  if (side != main_stream) {
+    OCHK(c, hipEventRecord(ob->done, side));
+    OCHK(c, hipStreamWaitEvent(main_stream, ob->done, 0));
+  }
   return rc;
 }
 

@@ -28,7 +28,7 @@ class Context:
     def __init__(self, n_scans: int = 64, width: int = 1024, min_range: float = 0.3, max_iterations: int = 4,
                  want_images: bool = True, device: int = 0):
         self.lib = nat.load()
-        self.n_scans, self.width = n_scans, width
+        self.n_scans, self.width, self.device = n_scans, width, device
         cfg = nat.Config(n_scans, width, min_range, max_iterations, int(want_images))
         h = ctypes.c_void_p()
         rc = self.lib.lislam_ctx_create(ctypes.byref(cfg), device, ctypes.byref(h))
@@ -60,6 +60,14 @@ class Context:
         flight per device (1..4) for this context's launches; 0 keeps a value.  Results are the same."""
         nat.check(self.lib.lislam_set_engine_shape(self.h, int(queries_per_wave), int(depth)), self.h,
                   "lislam_set_engine_shape")
+
+    def masked_queues(self) -> int:
+        """CU-masked streams (hardware queues) the library holds on this context's device
+        (lislam_device_queue_count)."""
+        n = ctypes.c_int32(0)
+        nat.check(self.lib.lislam_device_queue_count(int(self.device), ctypes.byref(n)), self.h,
+                  "lislam_device_queue_count")
+        return int(n.value)
 
     def set_tie_order(self, order: int):
         """Order of equal voxels in the a7 VoxelGrid (lislam_set_tie_order): TIES_REFERENCE

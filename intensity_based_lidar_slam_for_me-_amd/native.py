@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "lislam_batch_upload", "lislam_batch_upload_async", "lislam_batch_download_cloud", "lislam_batch_input_device_ptr", "lislam_batch_extract",
     "lislam_batch_odometry", "lislam_batch_set_timing", "lislam_batch_kernel_times",
     "lislam_batch_download", "lislam_eval_factors", "lislam_eval_factors_raw", "lislam_set_tie_order", "lislam_set_odometry_schedule", "lislam_set_engine_shape", "lislam_batch_odometry_status",
-    "lislam_batch_odometry_engine", "lislam_batch_odometry_abort_code",
+    "lislam_batch_odometry_engine", "lislam_batch_odometry_abort_code", "lislam_device_queue_count",
     "lislam_map_create", "lislam_map_destroy", "lislam_map_build", "lislam_map_add_points", "lislam_map_size",
     "lislam_map_points", "lislam_map_nearest_search", "lislam_map_associate", "lislam_normal_equations",
     "lislam_pose_solve", "lislam_voxel_grid", "lislam_mapopt_step", "lislam_mapopt_step_corner", "lislam_laser_mapping",
@@ -156,6 +156,7 @@ def load(path: str = LIB_PATH):
     L.lislam_batch_odometry_status.argtypes = [vp, ctypes.POINTER(_i32)]
     L.lislam_batch_odometry_engine.argtypes = [vp, ctypes.POINTER(_i32)]
     L.lislam_batch_odometry_abort_code.argtypes = [vp, ctypes.POINTER(_i32)]
+    L.lislam_device_queue_count.argtypes = [_i32, ctypes.POINTER(_i32)]
     i64, i64p = ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)
     L.lislam_map_create.argtypes = [vp, ctypes.POINTER(MapConfig), ctypes.POINTER(vp)]
     L.lislam_map_destroy.argtypes = [vp]

@@ -1,7 +1,9 @@
 """Config 4's sharded path on the GPU: `bench.py --gpus 2 --total-scans T` starts two ranks
 (they share the box's one GPU round-robin), each runs its contiguous shard with chains restarting
 at the shard boundary (laserOdometry.cpp:130-135 within a shard), and every
-rank's poses, stats and feature counts equal the oracle's chains over the same shard."""
+rank's poses, stats and feature counts equal the oracle's chains over the same shard.  The line
+itself carries the CPU baseline and every rank's pose delta (bench.py's CPU stage runs on every rank
+before it touches the GPU)."""
 import json
 import os
 import subprocess
@@ -20,13 +22,19 @@ def test_two_ranks_config4_shards_match_oracle(tmp_path, oracle, synth):
     T, L = 14, 4
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--total-scans", str(T),
-                          "--chain", str(L), "--steps", "2", "--warmup", "1", "--cpu-budget", "0", "--sustain-s", "0",
-                          "--workers", "1", "--dump-dir", str(tmp_path)],
+                          "--chain", str(L), "--steps", "2", "--warmup", "1", "--cpu-budget", "2", "--cpu-workers", "2",
+                          "--sustain-s", "0", "--workers", "1", "--dump-dir", str(tmp_path)],
                          capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([l for l in out.stdout.splitlines() if l.strip()][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["total_scans_per_step"] == T
+    # the multi-GPU line carries the CPU baseline (rank 0's shard, timed before it touched the GPU)
+    # and every rank's pose delta against the oracle over its own shard
+    cpu, pd = line["cpu_baseline"], line["pose_delta_vs_cpu"]
+    assert cpu is not None and cpu["kind"] == "port" and cpu["value"] > 0
+    assert pd is not None and pd["ranks_compared"] == 2 and pd["within_tolerance"], pd
+    assert pd["stats_mismatches"] == 0 and pd["pairs_compared"] >= 2 * (7 - 1), pd
     for r in range(2):
         d = np.load(tmp_path / f"rank{r}.npz")
         start, n = int(d["start"]), int(d["n"])
