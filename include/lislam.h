@@ -219,10 +219,10 @@ int lislam_set_odometry_schedule(lislam_ctx* ctx, int32_t mode);
  * after another per wavefront; 4 = four at once, one per 16-lane row.  Above 1 each chain is
  * slower but an engine holds a fraction of the waves, so several engines and the next batches'
  * extraction share the GPU.  0 = keep.  depth = engines in flight per device when a launch of this
- * context enters the device's queue (1..4; a launch waits for the one `depth` launches before it);
+ * context enters the device's queue (1..6; a launch waits for the one `depth` launches before it);
  * 0 = keep.  Latency (one sequence at a time): 1 / 1, the default (one engine in flight, its item
  * workgroups 12 waves: a pass's queries in one round).  Throughput (several pipelined
- * contexts, e.g. bench.py): 3 / 4.  LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed a new context's
+ * contexts, e.g. bench.py): 3 / 5.  LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed a new context's
  * shape. */
 int lislam_set_engine_shape(lislam_ctx* ctx, int32_t queries_per_wave, int32_t depth);
 /* status = the number of engine launches of the batch that gave up since the previous status call

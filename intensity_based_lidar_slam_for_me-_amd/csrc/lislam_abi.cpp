@@ -114,7 +114,7 @@ int lislam_ctx_create(const lislam_config* cfg, int32_t device, lislam_ctx** out
   }
   // LISLAM_ENGINE_QPW / LISLAM_ENGINE_DEPTH seed the engine's shape (lislam_set_engine_shape)
   if (const char* e = getenv("LISLAM_ENGINE_QPW")) c->eng_qpw = std::min(4, std::max(1, atoi(e)));
-  if (const char* e = getenv("LISLAM_ENGINE_DEPTH")) c->eng_depth = std::min(4, std::max(1, atoi(e)));
+  if (const char* e = getenv("LISLAM_ENGINE_DEPTH")) c->eng_depth = std::min(lislam::kMaxEngineDepth, std::max(1, atoi(e)));
   if (device < 64) ++g_ctx_count[device];
   *out = c;
   return LISLAM_OK;
@@ -1122,7 +1122,7 @@ int lislam_set_odometry_schedule(lislam_ctx* c, int32_t mode) {
 }
 
 int lislam_set_engine_shape(lislam_ctx* c, int32_t queries_per_wave, int32_t depth) {
-  if (!c || queries_per_wave < 0 || queries_per_wave > 4 || depth < 0 || depth > 4)
+  if (!c || queries_per_wave < 0 || queries_per_wave > 4 || depth < 0 || depth > lislam::kMaxEngineDepth)
     return LISLAM_ERR_ARG;
   if (queries_per_wave) c->eng_qpw = queries_per_wave;
   if (depth) c->eng_depth = depth;

@@ -13,6 +13,7 @@ constexpr int kMaxLines = 128;               // N_SCANS in {16, 32, 64, 128}
 constexpr int kCapSharpPerLine = 12;         // 2 per segment x 6 (scanRegistration.cpp:459)
 constexpr int kCapLessSharpPerLine = 120;    // 20 per segment x 6 (:466)
 constexpr int kCapFlatPerLine = 24;          // 4 per segment x 6 (:530)
+constexpr int kMaxEngineDepth = 6;           // engines in flight per device (lislam_set_engine_shape)
 
 // Device-resident batch of S organized scans and every per-scan output of a1..a7.
 struct FeatureArgs {

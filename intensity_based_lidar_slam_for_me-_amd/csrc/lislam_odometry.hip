@@ -2966,7 +2966,7 @@ bool work_stream(int dev, hipStream_t* s) {
 // still waits for the launch just before it (a per-depth ring would wait for the last launch that
 // used its slot instead).
 struct EngineGate {
-  static constexpr int kMaxDepth = 4;
+  static constexpr int kMaxDepth = kMaxEngineDepth;  // pairs are made per slot used
   std::mutex mu;
   hipEvent_t ev[kMaxDepth] = {};
   hipStream_t roles[kMaxDepth] = {}, items[kMaxDepth] = {};
@@ -2980,13 +2980,11 @@ static EngineGate* engine_gate(int dev) {
   return dev >= 0 && dev < 64 ? &gates[dev] : nullptr;
 }
 
-// g->mu held
+// g->mu held.  Slot 0's pair is made on the first probe (it tells whether CU masks work here); the
+// other slots' pairs when a launch first takes them, so a device holds 2 x (the deepest depth used)
+// engine queues.
 static bool probe_engine_streams(EngineGate* g, int dev) {
-  if (g->avail < 0) {
-    g->avail = 1;
-    for (int s = 0; s < EngineGate::kMaxDepth && g->avail; s++)
-      if (!make_engine_streams(dev, &g->roles[s], &g->items[s])) g->avail = 0;
-  }
+  if (g->avail < 0) g->avail = make_engine_streams(dev, &g->roles[0], &g->items[0]) ? 1 : 0;
   return g->avail == 1;
 }
 
@@ -3072,14 +3070,17 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   // probed them: probe again under the lock
   if (!probe_engine_streams(gate, dev)) return 0;
   const unsigned long long n = gate->launches++;
-  const int slot = (int)(n % EngineGate::kMaxDepth);
+  // slot n % depth: the launch it waits for (n - depth) used the same slot, so a slot's pair holds
+  // one engine at a time
+  int slot = (int)(n % depth);
+  if (!gate->roles[slot] && !make_engine_streams(dev, &gate->roles[slot], &gate->items[slot])) slot = 0;
   for (hipEvent_t& e : gate->ev)
     if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   hipStream_t roles = gate->roles[slot], items = gate->items[slot];  // the slot's streams
   (void)hipStreamWaitEvent(roles, ready, 0);
   // launch n - depth (its event is re-recorded only by launch n - depth + kMaxDepth > n)
   if (n >= (unsigned long long)depth) (void)hipStreamWaitEvent(roles, gate->ev[(n - depth) % EngineGate::kMaxDepth], 0);
-  hipEvent_t mine = gate->ev[slot];
+  hipEvent_t mine = gate->ev[n % EngineGate::kMaxDepth];
   if (t0) (void)hipEventRecord(t0, roles);
   // zero the control words of this launch, all but word 3 (the sticky abort)
   (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);

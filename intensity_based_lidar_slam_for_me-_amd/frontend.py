@@ -53,11 +53,11 @@ class Context:
         nat.check(self.lib.lislam_set_odometry_schedule(self.h, int(mode)), self.h, "lislam_set_odometry_schedule")
 
     SHAPE_LATENCY = (1, 1)     # lislam_set_engine_shape: one query per wavefront, one engine at a time
-    SHAPE_THROUGHPUT = (3, 4)  # three queries per wavefront, four engines in flight (pipelined contexts)
+    SHAPE_THROUGHPUT = (3, 5)  # three queries per wavefront, five engines in flight (pipelined contexts)
 
     def set_engine_shape(self, queries_per_wave: int = 0, depth: int = 0):
         """lislam_set_engine_shape: the chain engine's queries per wavefront (1..4) and engines in
-        flight per device (1..4) for this context's launches; 0 keeps a value.  Results are the same."""
+        flight per device (1..6) for this context's launches; 0 keeps a value.  Results are the same."""
         nat.check(self.lib.lislam_set_engine_shape(self.h, int(queries_per_wave), int(depth)), self.h,
                   "lislam_set_engine_shape")
 

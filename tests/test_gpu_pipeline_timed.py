@@ -6,8 +6,8 @@ steps' chains, extraction and ORB cascades run beside it on the same CUs, and th
 joins the engine only at the batch's next call: the co-residency, deferred join and agent-scope
 hand-offs the engine was built for.  Two engine shapes (lislam_set_engine_shape): latency (one
 query per wavefront, one engine in flight, two contexts, four steps) and throughput (three queries
-per wavefront, four engines in flight, four contexts, eight steps; and six contexts, twelve steps:
-bench.py's default schedule).  Afterwards
+per wavefront, five engines in flight, four contexts, eight steps; and eight contexts, sixteen
+steps: bench.py's default schedule).  Afterwards
 each context holds its last step's outputs, and every pair's pose, para, correspondence counts and
 LM iterations, and the ORB front end's stats and T_s2s, must equal the oracle's over the same scans."""
 import numpy as np
@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-4  # BASELINE.json north_star: <= 1e-4 m / <= 1e-4 rad
 S = 61
-STARTS = (100, 400, 700, 1000, 1300, 1600)  # a different stretch of the corridor per context
+STARTS = (100, 400, 700, 1000, 1300, 1600, 250, 550)  # a different stretch of the corridor per context
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +34,7 @@ def sequences(oracle, synth):
     return out
 
 
-@pytest.mark.parametrize("shape,k,steps", [("latency", 2, 4), ("throughput", 4, 8), ("throughput", 6, 12)])
+@pytest.mark.parametrize("shape,k,steps", [("latency", 2, 4), ("throughput", 4, 8), ("throughput", 8, 16)])
 def test_pipelined_steps_match_the_oracle(pkg, sequences, shape, k, steps):
     import bench
 
@@ -49,9 +49,10 @@ def test_pipelined_steps_match_the_oracle(pkg, sequences, shape, k, steps):
         bench.pipeline(bats, S, steps, S - 1, k, (1000, mask))
         for c in ctxs:
             c.synchronize()
-        # one hardware queue per context (its ORB front end shares it) + the engine's 4 stream pairs:
-        # well below the ~20 masked queues past which every launch slows
-        assert ctxs[0].masked_queues() <= k + 8, ctxs[0].masked_queues()
+        # one hardware queue per context (its ORB front end shares it) + one stream pair per engine
+        # slot in use (depth 5 at the throughput shape): at most 18 at bench.py's default, below the
+        # ~20 masked queues past which every launch slows
+        assert ctxs[0].masked_queues() <= k + 10, ctxs[0].masked_queues()
         worst = 0.0
         orb_pairs = 0
         for i, (b, (_, pose, rel, st, ost, oT)) in enumerate(zip(bats, sequences)):
