@@ -1523,6 +1523,7 @@ struct EngCtl {
   unsigned* w;
   int C, R, I;
   unsigned long long wait_ticks;  // bound of every device wait (s_memrealtime ticks, 100 MHz)
+  unsigned backoff;               // eng_wait's longest sleep between polls (x 64 cycles)
   int prefetch;  // waiting association tickets warm this XCD's L2 with their pair's target structures
   int roles;     // solve-role tickets ahead of the items in this launch's queue (C, or 0: roles in their own launch)
   int budget;    // association items per (pass, chain) at most: what the resident workgroups can hold at
@@ -1603,20 +1604,45 @@ __device__ __forceinline__ void eng_trace(int slot, unsigned v) {
 // scratch count as divergent, which would put the ticket loop's barriers in divergent control flow.
 // code: which wait (EngCtl word 2 when its bound expires): 1 an item for the previous pass's items,
 // 2 an item for x, 3 a solve role for its pass's items.
+// Developer builds (LISLAM_ENG_PROF=1) count every wait's polls per wait code (g_eng_polls[code],
+// g_eng_polls[8 + code] the waits): each poll is two agent-scope loads (the word, the abort word),
+// the traffic attribution of DESIGN.md §5 (lislam_debug_engine_polls reads and clears them).
+__device__ unsigned long long g_eng_polls[16];
+extern "C" int lislam_debug_engine_polls(unsigned long long* out16) {
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_eng_polls), sizeof(g_eng_polls)) != hipSuccess) return -2;
+  static const unsigned long long zero[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_eng_polls), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+}
+__device__ __forceinline__ void eng_count_polls(unsigned code, unsigned long long polls) {
+#if LISLAM_ENG_PROF
+  __hip_atomic_fetch_add(&g_eng_polls[code & 7], polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(&g_eng_polls[8 + (code & 7)], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+// backoff: the sleep between polls doubles from 64 cycles up to `backoff` x 64 (1 = a fixed 64).
 __device__ __noinline__ bool eng_wait(unsigned* p, unsigned target, unsigned* abort_w, unsigned long long bound,
-                                      unsigned code) {
+                                      unsigned code, unsigned backoff) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long polls = 0;
+  unsigned nap = 1;
+  bool ok;
   for (;;) {
-    if (ld_rlx(p) >= target) return true;
-    if (ld_rlx(abort_w)) return false;
+    polls++;
+    if (ld_rlx(p) >= target) { ok = true; break; }
+    if (ld_rlx(abort_w)) { ok = false; break; }
     if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {  // 100 MHz clock
       st_rlx(abort_w + 1, code);  // the error word
       st_rlx(abort_w, 1u);
       st_rlx(abort_w + 2, 1u);  // sticky (EngCtl word 3)
-      return false;
+      ok = false;
+      break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    for (unsigned i = 0; i < nap; i++) __builtin_amdgcn_s_sleep(1);
+    nap = nap * 2 > backoff ? backoff : nap * 2;
   }
+  eng_count_polls(code, polls);
+  return ok;
 }
 
 struct EngShared {
@@ -1639,17 +1665,16 @@ __device__ __forceinline__ double eng_x_word(const OdomArgs& a, int c, int r, in
   if (r == 0 && o == 0) return a.init_state ? a.init_state[(size_t)c * 14 + e] : (e == 3 ? 1.0 : 0.0);
   return ld_sc1d(a.state + (size_t)c * 16 + e);
 }
-__device__ __forceinline__ void eng_load_x(const OdomArgs& a, int c, int r, int o, double* x) {
-#pragma unroll
-  for (int e = 0; e < 7; e++) x[e] = eng_x_word(a, c, r, o, e);
-}
 
-// One block's 28 sums (see the engine comment) at p = R c, lp = p + t (R, t uniform).
-// Edge blocks: M (rank 2) and each row of T folded into the sums (and into U) as soon as it exists,
-// to keep few doubles live.  Plane blocks are rank 1: with a = p x n, M = w n n^T, T = [p]x M =
-// w a n^T, U = T [p]x = -w a a^T, v = w r n, p x v = w r a (39 multiply-adds instead of ~90).
-__device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
-                                          double (&s)[kAcc]) {
+
+// One block's 28 sums (see the engine comment) at p = R c, lp = p + t (R, t uniform): emit(e, v)
+// receives each block's contribution v to sum e once (a fresh sum's accumulate, fma(a, b, 0) ==
+// a * b).  Edge blocks: M (rank 2) and each row of T emitted as soon as it exists, to keep few
+// doubles live.  Plane blocks are rank 1: with a = p x n, M = w n n^T, T = [p]x M = w a n^T,
+// U = T [p]x = -w a a^T, v = w r n, p x v = w r a (39 multiplies instead of ~90).
+template <class Emit>
+__device__ __forceinline__ void eng_block_emit(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
+                                               Emit&& emit) {
   const D3 p{fma(R[0], c.x, fma(R[1], c.y, R[2] * c.z)), fma(R[3], c.x, fma(R[4], c.y, R[5] * c.z)),
              fma(R[6], c.x, fma(R[7], c.y, R[8] * c.z))};
   const D3 e{(p.x + t.x) - pa.x, (p.y + t.y) - pa.y, (p.z + t.z) - pa.z};
@@ -1664,24 +1689,24 @@ __device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, con
   double w = 1.0;
   if (s2 > 0.01) {  // HuberLoss(0.1): rho = 2 a sqrt(s) - a^2, rho' = a / sqrt(s)
     const double rr = sqrt(s2);
-    s[0] += 0.5 * (0.2 * rr - 0.01);
+    emit(0, 0.5 * (0.2 * rr - 0.01));
     w = fmax(2.2250738585072014e-308, 0.1 / rr);
   } else {
-    s[0] += 0.5 * s2;
+    emit(0, 0.5 * s2);
   }
   const double wx = w * u.x, wy = w * u.y, wz = w * u.z;
   if (kd != 0) {
     const D3 av{fma(p.y, u.z, -p.z * u.y), fma(p.z, u.x, -p.x * u.z), fma(p.x, u.y, -p.y * u.x)};
     const double ax = w * av.x, ay = w * av.y, az = w * av.z;
-    s[1] = fma(wx, u.x, s[1]); s[2] = fma(wx, u.y, s[2]); s[3] = fma(wx, u.z, s[3]);
-    s[4] = fma(wy, u.y, s[4]); s[5] = fma(wy, u.z, s[5]); s[6] = fma(wz, u.z, s[6]);
-    s[7] = fma(ax, u.x, s[7]); s[8] = fma(ax, u.y, s[8]); s[9] = fma(ax, u.z, s[9]);
-    s[10] = fma(ay, u.x, s[10]); s[11] = fma(ay, u.y, s[11]); s[12] = fma(ay, u.z, s[12]);
-    s[13] = fma(az, u.x, s[13]); s[14] = fma(az, u.y, s[14]); s[15] = fma(az, u.z, s[15]);
-    s[16] = fma(-ax, av.x, s[16]); s[17] = fma(-ax, av.y, s[17]); s[18] = fma(-ax, av.z, s[18]);
-    s[19] = fma(-ay, av.y, s[19]); s[20] = fma(-ay, av.z, s[20]); s[21] = fma(-az, av.z, s[21]);
-    s[22] = fma(rp, wx, s[22]); s[23] = fma(rp, wy, s[23]); s[24] = fma(rp, wz, s[24]);
-    s[25] = fma(rp, ax, s[25]); s[26] = fma(rp, ay, s[26]); s[27] = fma(rp, az, s[27]);
+    emit(1, wx * u.x); emit(2, wx * u.y); emit(3, wx * u.z);
+    emit(4, wy * u.y); emit(5, wy * u.z); emit(6, wz * u.z);
+    emit(7, ax * u.x); emit(8, ax * u.y); emit(9, ax * u.z);
+    emit(10, ay * u.x); emit(11, ay * u.y); emit(12, ay * u.z);
+    emit(13, az * u.x); emit(14, az * u.y); emit(15, az * u.z);
+    emit(16, -ax * av.x); emit(17, -ax * av.y); emit(18, -ax * av.z);
+    emit(19, -ay * av.y); emit(20, -ay * av.z); emit(21, -az * av.z);
+    emit(22, rp * wx); emit(23, rp * wy); emit(24, rp * wz);
+    emit(25, rp * ax); emit(26, rp * ay); emit(27, rp * az);
     return;
   }
   double m00, m01, m02, m11, m12, m22, v0, v1, v2;
@@ -1692,29 +1717,34 @@ __device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, con
     // v = w (u x r)
     v0 = w * fma(u.y, r2, -u.z * r1); v1 = w * fma(u.z, r0, -u.x * r2); v2 = w * fma(u.x, r1, -u.y * r0);
   }
-  s[1] += m00; s[2] += m01; s[3] += m02; s[4] += m11; s[5] += m12; s[6] += m22;
-  s[22] += v0; s[23] += v1; s[24] += v2;
-  s[25] += fma(p.y, v2, -p.z * v1); s[26] += fma(p.z, v0, -p.x * v2); s[27] += fma(p.x, v1, -p.y * v0);
+  emit(1, m00); emit(2, m01); emit(3, m02); emit(4, m11); emit(5, m12); emit(6, m22);
+  emit(22, v0); emit(23, v1); emit(24, v2);
+  emit(25, fma(p.y, v2, -p.z * v1)); emit(26, fma(p.z, v0, -p.x * v2)); emit(27, fma(p.x, v1, -p.y * v0));
   // T = [p]x M row by row; U = T [p]x (symmetric): U[i][0] = T[i][1] pz - T[i][2] py,
   // U[i][1] = T[i][2] px - T[i][0] pz, U[i][2] = T[i][0] py - T[i][1] px
   {
     const double t0 = fma(-p.z, m01, p.y * m02), t1 = fma(-p.z, m11, p.y * m12), t2 = fma(-p.z, m12, p.y * m22);
-    s[7] += t0; s[8] += t1; s[9] += t2;
-    s[16] += fma(t1, p.z, -t2 * p.y);
-    s[17] += fma(t2, p.x, -t0 * p.z);
-    s[18] += fma(t0, p.y, -t1 * p.x);
+    emit(7, t0); emit(8, t1); emit(9, t2);
+    emit(16, fma(t1, p.z, -t2 * p.y));
+    emit(17, fma(t2, p.x, -t0 * p.z));
+    emit(18, fma(t0, p.y, -t1 * p.x));
   }
   {
     const double t0 = fma(p.z, m00, -p.x * m02), t1 = fma(p.z, m01, -p.x * m12), t2 = fma(p.z, m02, -p.x * m22);
-    s[10] += t0; s[11] += t1; s[12] += t2;
-    s[19] += fma(t2, p.x, -t0 * p.z);
-    s[20] += fma(t0, p.y, -t1 * p.x);
+    emit(10, t0); emit(11, t1); emit(12, t2);
+    emit(19, fma(t2, p.x, -t0 * p.z));
+    emit(20, fma(t0, p.y, -t1 * p.x));
   }
   {
     const double t0 = fma(-p.y, m00, p.x * m01), t1 = fma(-p.y, m01, p.x * m11), t2 = fma(-p.y, m02, p.x * m12);
-    s[13] += t0; s[14] += t1; s[15] += t2;
-    s[21] += fma(t0, p.y, -t1 * p.x);
+    emit(13, t0); emit(14, t1); emit(15, t2);
+    emit(21, fma(t0, p.y, -t1 * p.x));
   }
+}
+// The 28 sums of one block into a fresh s (zeros).
+__device__ __forceinline__ void eng_block(int kd, const D3& c, const D3& pa, const D3& u, const double* R, const D3& t,
+                                          double (&s)[kAcc]) {
+  eng_block_emit(kd, c, pa, u, R, t, [&](int e, double v) { s[e] += v; });
 }
 
 // What an association item loads before its pass's x exists (all waves, while the lead waits):
@@ -1769,12 +1799,12 @@ __device__ __forceinline__ void eng_rt(const EngShared& sh, double (&R)[9], D3& 
 // write-through; the wave's share of the solve's first evaluation (its block's 28 sums at x and
 // the corner / plane counts) goes to sh.red[wave].
 __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int k, int w, Rsrc rec, int* warm, int outer,
-                                          unsigned tk, const ItemPre& pre, const double (&x)[7], double* row) {
+                                          unsigned tk, const P4* pw, const int* pi, const double* x, double* row) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id();
   const int ns = a.n_feat[k * 4 + 0];
   const bool corner = w < ns;
-  const P4 qp = pre.qp;
+  const P4 qp = pw[0];
   const TargetIndex& ix = corner ? a.idx_ls : a.idx_lf;
   const P4* L = corner ? a.less_sharp + (size_t)(k - 1) * a.cap_less_sharp : a.less_flat + (size_t)(k - 1) * a.N;
   const P4* sorted = reinterpret_cast<const P4*>(ix.sorted + (size_t)(k - 1) * ix.cap);
@@ -1782,20 +1812,22 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   const size_t mo = (size_t)(k - 1) * ix.nchunk * 2, so = (size_t)(k - 1) * ix.nsuper * 2;
   const P4 cur{qp.x, qp.y, qp.z, 0.f};
   const P4 sel = transform_to_start(cur, x);
-  // Second outer pass: the first pass's closest / second / third points (pre.wi / pre.wp, loaded
-  // before x existed) seed the searches (the pose moved little).  A seed is one of the candidates
-  // of the minimum it seeds, so every result is unchanged; only the pruning starts tighter.
-  const int (&wi)[3] = pre.wi;
-  const P4 (&wp)[3] = pre.wp;
+  // Second outer pass: the first pass's closest / second / third points (pi / pw[1..3], loaded
+  // before x existed into the wave's LDS slot) seed the searches (the pose moved little).  A seed is
+  // one of the candidates of the minimum it seeds, so every result is unchanged; only the pruning
+  // starts tighter.  The seeds (and x) are read from LDS where they are used, not held in
+  // registers across the 1-NN search.
   dkey seed = kIdent;
 #pragma unroll
   for (int e = 0; e < 3; e++) {
-    const float d = d2f(sel, wp[e]);
-    if (wi[e] >= 0 && wi[e] < nL && d < 25.f) seed = dmin(seed, dk(d, wi[e]));
+    const int wi = pi[e];
+    const float d = d2f(sel, pw[1 + e]);
+    if (wi >= 0 && wi < nL && d < 25.f) seed = dmin(seed, dk(d, wi));
   }
   const bool qlog = g_eng_qlog && g_eng_qlog_pair == k;
   const unsigned long long tq1 = (threadIdx.x == 0 || qlog) ? rt_now() : 0ull;
   const int closest = nn_wave(sorted, nL, ix.nn_chunk + mo, ix.nn_super + so, sel, seed);
+  asm volatile("" ::: "memory");  // re-read the LDS seeds below rather than keep them live
   const unsigned long long tq2 = (threadIdx.x == 0 || qlog) ? rt_now() : 0ull;
   int kind = -1;
   D3 u{0.0, 0.0, 0.0};
@@ -1807,12 +1839,13 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
     dkey s2 = dk(25.f, kNone), s3 = dk(25.f, kNone);
 #pragma unroll
     for (int e = 0; e < 3; e++) {  // seeds of the walks (:467-520 / :589-646) under this closest
-      const int j = wi[e];
+      const int j = pi[e];
       if (j < 0 || j >= nL || j == closest) continue;
-      const int lab = int(wp[e].i);
+      const P4 wpe = pw[1 + e];
+      const int lab = int(wpe.i);
       const bool up = j > closest;
       if (up ? lab > cid + 2 : lab < cid - 2) continue;  // past the walk's break
-      const float d = d2f(sel, wp[e]);
+      const float d = d2f(sel, wpe);
       if (!(d < 25.f)) continue;
       const dkey kd2 = dk(d, up ? j - closest : nL + closest - j);
       const bool other = up ? lab > cid : lab < cid;  // another scan line
@@ -1879,19 +1912,12 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
   }
   // the share of the first evaluation, added to the wave's row sh.red[wave] (kind is wave-uniform;
   // every lane computes, lane 0 adds; a wave's LDS accesses stay in order)
-  if (kind >= 0) {
-    double sb[kAcc];
-#pragma unroll
-    for (int e = 0; e < kAcc; e++) sb[e] = 0.0;
+  if (kind >= 0 && lane == 0) {  // one lane: each sum straight into the row (few doubles live)
     double R[9];
     D3 t;
     eng_rt_x(x, R, t);
-    eng_block(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, sb);
-    if (lane == 0) {
-#pragma unroll
-      for (int e = 0; e < kAcc; e++) row[e] += sb[e];
-      row[28 + kind] += 1.0;
-    }
+    eng_block_emit(kind, D3{cur.x, cur.y, cur.z}, D3{pa.x, pa.y, pa.z}, u, R, t, [&](int e, double v) { row[e] += v; });
+    row[28 + kind] += 1.0;
   }
 }
 
@@ -1901,7 +1927,7 @@ __device__ __forceinline__ void eng_query(const OdomArgs& a, EngShared& sh, int 
 // queries fit the resident item waves in one round and leave the SIMDs room for whatever runs
 // beside the engine.  has: this row holds a query (w < the pair's queries).
 __device__ __forceinline__ void eng_query16(const OdomArgs& a, int k, int w, bool has, Rsrc rec, int* warm, int outer,
-                                            unsigned tk, const ItemPre& pre, const double (&x)[7], double* row) {
+                                            unsigned tk, const ItemPre& pre, const double* x, double* row) {
   const unsigned long long tq0 = threadIdx.x == 0 ? rt_now() : 0ull;
   const int lane = lane_id(), lr = lane & 15;
   const int ns = a.n_feat[k * 4 + 0];
@@ -2045,9 +2071,9 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ct
   const int ieff = ps.ieff;
   const int nq = a.n_feat[k * 4 + 0] + a.n_feat[k * 4 + 2];
   if (lane_id() < 30) sh.red[ql][lane_id()] = 0.0;
-  double x[7];
-#pragma unroll
-  for (int e = 0; e < 7; e++) x[e] = sh.xw[ql][e];
+  // the pass's x stays in the wave's LDS copy: read where a query needs it (its transform, its
+  // share), not held in 14 VGPRs across the searches
+  const double* x = sh.xw[ql];
   for (int m = 0;; m++) {
     const int w0 = (item + m * ieff) * ctl.Q * kQpw + ql * kQpw;  // the wave's first query
     if (w0 >= nq) break;  // wave-uniform
@@ -2066,15 +2092,15 @@ __device__ __forceinline__ void eng_item_run(const OdomArgs& a, const EngCtl& ct
       for (int s = 0; s < kQpw; s++) {  // the wave's queries one after another (slot s: parked by row s)
         const int w = w0 + s;
         if (w >= nq) break;  // wave-uniform
-        ItemPre pre;
-        if (m > 0) {
-          pre = eng_item_pre(a, k, w, warm, outer);
-        } else {
-          pre.qp = sh.prew[ql][s][0];
+        if (m > 0) {  // an overflow query: its loads parked in the slot now (a wave's LDS accesses stay in order)
+          const ItemPre pre = eng_item_pre(a, k, w, warm, outer);
+          if (lane_id() == 0) {
+            sh.prew[ql][s][0] = pre.qp;
 #pragma unroll
-          for (int e = 0; e < 3; e++) { pre.wp[e] = sh.prew[ql][s][1 + e]; pre.wi[e] = sh.prei[ql][s][e]; }
+            for (int e = 0; e < 3; e++) { sh.prew[ql][s][1 + e] = pre.wp[e]; sh.prei[ql][s][e] = pre.wi[e]; }
+          }
         }
-        eng_query(a, sh, k, w, rec, warm, outer, tk, pre, x, sh.red[ql]);
+        eng_query(a, sh, k, w, rec, warm, outer, tk, sh.prew[ql][s], sh.prei[ql][s], x, sh.red[ql]);
       }
     }
   }
@@ -2490,7 +2516,7 @@ __device__ __forceinline__ bool eng_solve_role(const OdomArgs& a, const EngCtl& 
     const unsigned ptk = (unsigned)(ro * ctl.C * (ctl.I + 1)) + tk;  // profile slot of the pass (developer builds)
     if (wave0 && lane == 0) {
       eng_prof(ptk, 1, rt_now());
-      sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 3u) : 1;
+      sh.flag0 = ieff > 0 ? eng_wait(ctl.assoc_done(c, ro), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 3u, ctl.backoff) : 1;
       eng_prof(ptk, 1, rt_now());
     }
     __syncthreads();
@@ -2606,7 +2632,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
   // done in the common case; then every wave loads what needs no x while the lead waits for x.
   if (wave0) {
     if (lead) {
-      sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 1u) : true;
+      sh.flag0 = (live && o == 1) ? eng_wait(ctl.assoc_done(c, ro - 1), (unsigned)ieff, ctl.abort_w(), ctl.wait_ticks, 1u, ctl.backoff) : true;
     }
   }
   __syncthreads();
@@ -2629,7 +2655,7 @@ __device__ __forceinline__ bool eng_item_ticket(const OdomArgs& a, const EngCtl&
     if (lead) {
       if (ok && live) {
         eng_prof(ptk, 2, rt_now());  // the item's lead starts its wait for x
-        ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks, 2u);
+        ok = eng_wait(ctl.lm_gen(c), (unsigned)ro, ctl.abort_w(), ctl.wait_ticks, 2u, ctl.backoff);
         eng_trace(1, ok ? 2u : 99u);
         eng_prof(ptk, 1, rt_now());
       }
@@ -2793,6 +2819,13 @@ __global__ __launch_bounds__(64 * kSoloItemWaves, 3) void k_odom_items_solo(Odom
 }
 
 static int item_waves(int qpw, int depth);
+// eng_wait's longest sleep between polls in units of 64 cycles: 1 (a fixed 64) with one engine in
+// flight, whose wake-up latency is the chain's; 8 with several, whose waiting items would otherwise
+// poll 1.5x as often (profiles/r06b_backoff_ab.txt).  LISLAM_ENGINE_BACKOFF overrides (1..64).
+static unsigned engine_backoff(int depth) {
+  static const int env = getenv("LISLAM_ENGINE_BACKOFF") ? std::max(1, std::min(64, atoi(getenv("LISLAM_ENGINE_BACKOFF")))) : 0;
+  return env ? (unsigned)env : depth <= 1 ? 1u : 8u;
+}
 // Items per (pass, chain) of the split engine at qpw queries per wave and `depth` engines in flight
 // (the developer profile's ticket layout).
 extern "C" int lislam_debug_engine_items(int cap_queries, int qpw, int depth) {
@@ -2854,6 +2887,7 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st) {
   // every device wait is bounded (2 s); LISLAM_ENGINE_WAIT_US shortens it (tests: a forced abort)
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
+  ctl.backoff = engine_backoff(a.eng_depth);
   // Items per (pass, chain): the workgroups resident at once, less the chains' solve roles and one
   // spare, shared by the chains.  More queries than
   // that are dealt as second queries to the items' waves (eng_item_run).  LISLAM_ENGINE_BUDGET
@@ -2946,7 +2980,11 @@ bool work_stream(int dev, hipStream_t* s) {
     if (multi_xcd && cus >= 4 * nx && cus % nx == 0) {
       const int words = (cus + 31) / 32;
       std::vector<uint32_t> m(words, 0u);
-      for (int i = nx; i < cus; i++) m[i / 32] |= 1u << (i % 32);
+      // LISLAM_WORK_XCDS=n (developer: traffic attribution) keeps the stream on the first n XCDs
+      const char* xe = getenv("LISLAM_WORK_XCDS");
+      const int nxu = xe ? std::max(1, std::min(nx, atoi(xe))) : nx;
+      for (int i = nx; i < cus; i++)
+        if (i % nx < nxu) m[i / 32] |= 1u << (i % 32);
       if (masked_stream(dev, s, words, m.data())) return true;
     }
   }
@@ -3044,6 +3082,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   ctl.roles = 0;
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
+  ctl.backoff = engine_backoff(a.eng_depth);
   // One item workgroup per CU of the items' mask (all CUs but one per XCD): its 8 waves at <= 128
   // VGPRs take half of each SIMD's registers, so the next batch's extraction and ORB kernels run
   // beside the engine instead of queueing behind it.  LISLAM_ENGINE_WGS caps the grid (tests: one

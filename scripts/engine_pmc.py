@@ -40,6 +40,8 @@ def main():
         scans = bench.generate(0, B, H, W, 16)
         np.save(cache, scans)
     pkg = importlib.import_module(bench.PKG)
+    if os.environ.get("LISLAM_ALT_LIB"):  # developer A/B: a variant build of the library
+        pkg.native.load(os.environ["LISLAM_ALT_LIB"])
     ctx = pkg.Context(n_scans=H, width=W)
     b = pkg.Batch(ctx, B)
     b.upload(scans)
