@@ -2950,12 +2950,24 @@ int masked_queue_count(int dev) {
   return n;
 }
 
+// XCDs of the device (hipDeviceAttributeNumberOfXccs: 8 on an MI355X in SPX mode, 1 per device in
+// CPX mode); a CU mask bit i selects a CU of XCD i % xccs (measured on gfx942 / gfx950 in SPX:
+// scripts/micro/cumask.hip).  0 = unknown.
+static int device_xccs(int dev) {
+  int x = 0;
+  if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    x = 0;
+  }
+  return x;
+}
+
 static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
-  const int cus = prop.multiProcessorCount, nx = 8;
-  if (!multi_xcd || cus < 4 * nx || cus % nx) return false;
+  const int cus = prop.multiProcessorCount, nx = device_xccs(dev);
+  if (!multi_xcd || nx < 1 || cus < 4 * nx || cus % nx) return false;
   const int words = (cus + 31) / 32;
   std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
   for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);
@@ -2976,8 +2988,8 @@ bool work_stream(int dev, hipStream_t* s) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
     const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
-    const int cus = prop.multiProcessorCount, nx = 8;
-    if (multi_xcd && cus >= 4 * nx && cus % nx == 0) {
+    const int cus = prop.multiProcessorCount, nx = device_xccs(dev);
+    if (multi_xcd && nx >= 1 && cus >= 4 * nx && cus % nx == 0) {
       const int words = (cus + 31) / 32;
       std::vector<uint32_t> m(words, 0u);
       // LISLAM_WORK_XCDS=n (developer: traffic attribution) keeps the stream on the first n XCDs
@@ -3063,6 +3075,29 @@ void release_engine_streams(int dev) {
   g->avail = -1;
 }
 
+// Item workgroups of one build (qpw 1..4, or 0: the solo build) that fit one CU, per device build
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor: registers, LDS, waves), cached.
+static int item_occupancy(int qpw, int threads) {
+  static int cache[5][17] = {};
+  const int w = std::min(16, std::max(1, threads / 64));
+  int& r = cache[qpw][w];
+  if (r) return r;
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (qpw) {
+    case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_odom_items_solo, threads, 0); break;
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_odom_items<1>, threads, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_odom_items<2>, threads, 0); break;
+    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_odom_items<3>, threads, 0); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_odom_items<4>, threads, 0); break;
+  }
+  if (e != hipSuccess || n < 1) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return r = n;
+}
+
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
                                 hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
   if (a.n_chains <= 0) return 0;
@@ -3091,17 +3126,23 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   (void)hipGetDevice(&dev);
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
+  static const bool solo_ok = !(getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 0);
+  const bool solo = solo_ok && depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
+  // Co-residency, checked at launch rather than assumed: the item workgroups one engine may hold at
+  // once = the item CUs (all but one per XCD) x the workgroups of this item build that fit a CU
+  // (hipOccupancyMaxActiveBlocksPerMultiprocessor), shared by the `depth` engines in flight.  The
+  // grid and the items per (pass, chain) never exceed it, so a pass's items are all resident.
+  const int per_cu = item_occupancy(solo ? 0 : ctl.qpw, 64 * ctl.Q);
+  const int item_cus = std::max(1, cus - std::max(1, device_xccs(dev)));
+  const int resident = std::max(1, item_cus * per_cu / depth);
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
-  const int cap = cap_env ? atoi(cap_env) : max(1, cus - 8);
+  const int cap = cap_env ? atoi(cap_env) : std::min(item_cus, resident);
   int grid = ctl.C * ctl.I;
   if (cap > 0) grid = min(grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
   const size_t words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
-  // engines in flight per device (lislam_set_engine_shape; 2 by default: a launch waits for the one
-  // before the last, so two chains run together — at one query per wave, two item workgroups per
-  // CU at 128 VGPRs — and each chain's idle association slots, while its solve runs, serve the other)
-  const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
   EngineGate* gate = engine_gate(dev);
   if (!gate) return 0;
   std::unique_lock<std::mutex> lock(gate->mu);
@@ -3126,9 +3167,7 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), roles);
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
-  hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, 8)), dim3(kEngThreads), 0, roles, a, ctl);
-  static const bool solo_ok = !(getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 0);
-  const bool solo = solo_ok && depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
+  hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, std::max(1, device_xccs(dev)))), dim3(kEngThreads), 0, roles, a, ctl);
   if (solo) hipLaunchKernelGGL(k_odom_items_solo, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
   else switch (ctl.qpw) {
     case 4: hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
