@@ -1,6 +1,6 @@
 """A/B timing of library variants (developer tool, GPU box).
 
-    python scripts/ab_lines.py [--scans 300] [--chain 10] [--odometry] main scripts/_ab/liblislam_x.so ...
+    python scripts/archive/ab_lines.py [--scans 300] [--chain 10] [--odometry] main scripts/_ab/liblislam_x.so ...
 
 Generates the seeded 300-scan batch once (spawn pool, cached in /tmp), then runs each library in
 its own child process: extraction (and odometry with --odometry) repeated, per-kernel HIP-event

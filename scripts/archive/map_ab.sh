@@ -1,6 +1,6 @@
 #!/bin/bash
 # Config-5 map bench under several environment settings ("NAME=V,NAME2=V2" each; "DEF" = none),
-# alternating, after the map parity tests.  Usage (GPU box): bash scripts/map_ab.sh <tag> [NOTEST] setting...
+# alternating, after the map parity tests.  Usage (GPU box): bash scripts/archive/map_ab.sh <tag> [NOTEST] setting...
 cd $GRAFT_REPO_ROOT
 D=gpurun_out/${1:-mapab}
 shift

@@ -2,7 +2,7 @@
 # Round-6 A/B of eng_wait's poll backoff (LISLAM_ENGINE_BACKOFF = longest sleep between polls in
 # units of 64 cycles; 1 = the fixed 64 of round 5): polls counted (developer build), bench lines at
 # the driver's shape alternating, the single-launch engine's FETCH / WRITE.
-# Usage (GPU box): bash scripts/r06_backoff_ab.sh <tag> [reps]
+# Usage (GPU box): bash scripts/archive/r06_backoff_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06b}
 REPS=${2:-2}

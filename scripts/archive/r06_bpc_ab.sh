@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 A/B: batches per pipelined context (bench.py --batches-per-context; 1 = round 5's one batch
-# per context) x contexts, at the driver's shape, alternating.  Usage (GPU box): bash scripts/r06_bpc_ab.sh <tag> [reps]
+# per context) x contexts, at the driver's shape, alternating.  Usage (GPU box): bash scripts/archive/r06_bpc_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06m}
 REPS=${2:-2}

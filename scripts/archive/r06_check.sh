@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU check: the GPU suite, then the profile of the stream workload (bench line + rocprof
 # kernel trace + PMC passes, scripts/profile_round.sh), then an A/B bench of the ORB stream choice.
-# Usage (on the GPU box): bash scripts/r06_check.sh <tag> [skip-tests]
+# Usage (on the GPU box): bash scripts/archive/r06_check.sh <tag> [skip-tests]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06a}
 OUT=gpurun_out/$TAG

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 A/B at the driver's own shape (--steps 20 --warmup 5): contexts x engine depth at qpw 3,
-# alternating variants on one box.  Usage (GPU box): bash scripts/r06_depth20_ab.sh <tag> [reps]
+# alternating variants on one box.  Usage (GPU box): bash scripts/archive/r06_depth20_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06e}
 REPS=${2:-3}

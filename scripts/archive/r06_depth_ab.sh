@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 A/B: pipelined contexts x engine depth at qpw 3 (bench.py's schedule, 60 timed steps,
 # no CPU leg), alternating variants on one box; then the pipelined tests at depth 6.
-# Usage (GPU box): bash scripts/r06_depth_ab.sh <tag> [reps]
+# Usage (GPU box): bash scripts/archive/r06_depth_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06d}
 REPS=${2:-2}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 A/B of the XCD-partitioned engine streams at the throughput shape (bench.py default
 # schedule, 60 timed steps, no CPU leg), alternating variants on one box, after the pipelined
-# and chain GPU tests.  Usage (GPU box): bash scripts/r06_partition_ab.sh <tag> [reps]
+# and chain GPU tests.  Usage (GPU box): bash scripts/archive/r06_partition_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06p}
 REPS=${2:-2}

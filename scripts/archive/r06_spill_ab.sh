@@ -2,7 +2,7 @@
 # Round-6 A/B of the association items' register diet (x and the seeds read from LDS, the share
 # emitted sum by sum into the row): the chain / pipelined tests, then bench lines alternating the
 # new library with HEAD's (scripts/_ab/liblislam_head.so), then the single-launch engine's FETCH /
-# WRITE counters for both.  Usage (GPU box): bash scripts/r06_spill_ab.sh <tag> [reps]
+# WRITE counters for both.  Usage (GPU box): bash scripts/archive/r06_spill_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06s}
 REPS=${2:-3}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 A/B of the per-XCD x copies (items poll and read their XCD's copy of the chain's x) with
 # the register diet, against HEAD's library: chain / pipelined tests, the stand-in engine's kernel
-# time and counters on 8 and 1 XCDs, bench lines alternating.  Usage (GPU box): bash scripts/r06_sync_ab.sh <tag> [reps]
+# time and counters on 8 and 1 XCDs, bench lines alternating.  Usage (GPU box): bash scripts/archive/r06_sync_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06y}
 REPS=${2:-3}

@@ -2,7 +2,7 @@
 # Round-6 traffic attribution of the chain engine (the single-launch engine, LISLAM_ENGINE_SINGLE=1,
 # which runs under dispatch-serialized counter collection): FETCH_SIZE / WRITE_SIZE / kernel time
 # with the engine's stream kept on 1, 2, 4 or all 8 XCDs (LISLAM_WORK_XCDS): what each extra XCD's
-# L2 re-fetches of the pairs' target structures costs.  Usage (GPU box): bash scripts/r06_xcd_pmc.sh <tag>
+# L2 re-fetches of the pairs' target structures costs.  Usage (GPU box): bash scripts/archive/r06_xcd_pmc.sh <tag>
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06x}
 ROOT=$(pwd)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 checkpoint on the GPU box: the whole GPU suite, smoke, then the driver's bench command.
-# Usage (GPU box): bash scripts/r06_gate.sh <tag>
+# Usage (GPU box): bash scripts/gpu_gate.sh <tag>
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r06g}
 OUT=gpurun_out/$TAG
