@@ -62,7 +62,7 @@ out = {"tag": tag, "config": meta["config"], "workload": None, "odometry_engine"
        "note": "the chain engine alone (scripts/engine_pmc.py: config 2's batch extracted once, then one continuous "
                "299-pair chain per launch) on the single-launch engine: the split engine's two launches must run "
                "together and dispatch-counter collection serializes dispatches, so its launches give up under --pmc "
-               "(scripts/pmc_engine_probe.sh, gpurun_out/r05b)",
+               "(scripts/archive/pmc_engine_probe.sh, gpurun_out/r05b)",
        "kernels_logical": {KERNEL: {"launches_profiled": sum(fetch_ok), "fetch_kib_per_launch": fetch,
                                     "write_kib_per_launch": write, "traffic_bytes_per_launch": traffic,
                                     "rocprof_avg_ms": avg_ms}},
