@@ -192,6 +192,7 @@ static int engine_settle(lislam_batch* b) {
   lislam_ctx* c = b->ctx;
   hipSetDevice(c->device);
   if (b->eng_pending) {
+    lislam::wait_engine_launched(&b->eng_req);  // the dispatcher has recorded the join events
     HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_r, 0));
     HIPCHK(c, hipStreamWaitEvent(c->stream, b->eng_join_i, 0));
     b->eng_pending = false;
@@ -325,6 +326,7 @@ int lislam_batch_destroy(lislam_batch* b) {
   if (!b) return LISLAM_OK;
   hipSetDevice(b->ctx->device);
   if (b->eng_pending) {  // the batch's last engine launch (its streams are the device's, shared)
+    lislam::wait_engine_launched(&b->eng_req);
     hipEventSynchronize(b->eng_join_r);
     hipEventSynchronize(b->eng_join_i);
   }
@@ -644,8 +646,19 @@ static int run_odometry(lislam_batch* b, int n_scans, int chain_len, const doubl
       // odometry queued after it, the staging copies just queued); the launch copies its abort words
       // to h_abort and records eng_done on its own stream
       HIPCHK(c, hipEventRecord(b->eng_ready, c->stream));
-      queued = lislam::launch_odometry_chain_split(o, b->eng_ready, b->eng_fork, b->eng_join_r, b->eng_join_i, e0, e1,
-                                                   b->h_abort, b->eng_done) > 0;
+      if (o.eng_depth > 1 && lislam::engine_dispatch_enabled()) {
+        // to the device's dispatcher: launched on the first free engine slot once the inputs exist.
+        // Depth 1 keeps the direct gate: one engine at a time has no slot to choose, and the host
+        // hop costs a single sequence ~2% (profiles/r06q_dispatch_ab.txt)
+        lislam::EngineRequest& r = b->eng_req;
+        r.a = o;
+        r.ready = b->eng_ready; r.fork = b->eng_fork; r.join_r = b->eng_join_r; r.join_i = b->eng_join_i;
+        r.t0 = e0; r.t1 = e1; r.h_abort = b->h_abort; r.done = b->eng_done;
+        queued = lislam::submit_odometry_chain_split(&r) > 0;
+      } else {
+        queued = lislam::launch_odometry_chain_split(o, b->eng_ready, b->eng_fork, b->eng_join_r, b->eng_join_i, e0, e1,
+                                                     b->h_abort, b->eng_done) > 0;
+      }
       if (queued) b->eng_pending = true;
       else b->eng_split = 0;  // no engine streams on this device after all: the single launch below
     }

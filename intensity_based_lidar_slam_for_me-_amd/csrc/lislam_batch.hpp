@@ -52,6 +52,9 @@ struct lislam_batch {
   // lislam_batch_extract (and after odometry's staging copies); the engine starts from it.
   bool eng_pending = false;
   hipEvent_t eng_ready = nullptr;
+  // the split launch as queued with the device's engine dispatcher (lislam::submit_odometry_chain_split):
+  // its events are recorded when the dispatcher launches it, so every wait on them first waits for that
+  lislam::EngineRequest eng_req;
   // Abort recovery.  Every engine launch (split or single) copies its sticky abort word into h_abort
   // (pinned) and records eng_done behind it; eng_check stays set until the next batch call settles
   // it: the host waits for eng_done and, if the engine gave up (a bounded device wait expired), clears

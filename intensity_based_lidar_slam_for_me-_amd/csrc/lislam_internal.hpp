@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <vector>
 
 #include "lislam_device.hpp"
@@ -157,6 +158,22 @@ int launch_odometry_chain(const OdomArgs& a, hipStream_t st);
 // this device): the caller must run the single-launch engine instead.
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
                                 hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done);
+// The same launch through the device's engine dispatcher (a host thread per device): the request is
+// queued and submit returns at once; the dispatcher launches it, on whichever engine slot is free,
+// once its `ready` event has completed and fewer than `depth` engines are in flight — so a chain
+// never waits for one particular earlier chain (launch n - depth) while another slot is idle.
+// The events are recorded when the dispatcher launches; wait_engine_launched(r) returns once they
+// are (before any wait on them).  submit: 0 = nothing queued (no CU masks on this device).
+struct EngineRequest {
+  OdomArgs a;
+  hipEvent_t ready, fork, join_r, join_i, t0, t1, done;
+  unsigned* h_abort;
+  void* plan = nullptr;  // the launch's parameters, fixed when submitted (its environment knobs included)
+  std::atomic<int> state{0};  // 0 none, 1 queued, 2 launched
+};
+int submit_odometry_chain_split(EngineRequest* r);
+void wait_engine_launched(EngineRequest* r);
+bool engine_dispatch_enabled();  // LISLAM_ENGINE_DISPATCH (default 1; 0: launch_odometry_chain_split)
 bool engine_streams_available(int dev);  // the device has CU-masked streams for the split engine
 void release_engine_streams(int dev);    // with the device's last context (also the round-stream pool)
 // A stream for the library's other kernels that keeps off the solve roles' CUs (see lislam_odometry.hip).

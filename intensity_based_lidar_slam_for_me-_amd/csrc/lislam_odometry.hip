@@ -24,9 +24,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "lislam_device.hpp"
@@ -3024,6 +3028,14 @@ struct EngineGate {
   int avail = -1;  // -1 not probed, 0 no CU masks on this device, 1 ready
   static constexpr int kRoundGroups = 4;
   hipStream_t round[kRoundGroups] = {};  // the per-round schedule's group streams (round_stream)
+  // the dispatcher (submit_odometry_chain_split): its thread (a pointer: a static std::thread still
+  // joinable at process exit would terminate), queue, and the slots' last launches
+  std::thread* th = nullptr;
+  bool stop = false;
+  std::deque<EngineRequest*> q;
+  std::condition_variable cv_req, cv_launched;
+  hipEvent_t slot_ev[kMaxDepth] = {};
+  bool slot_used[kMaxDepth] = {};
 };
 static EngineGate* engine_gate(int dev) {
   static EngineGate gates[64];
@@ -3059,7 +3071,23 @@ hipStream_t round_stream(int dev, int grp) {
 void release_engine_streams(int dev) {
   EngineGate* g = engine_gate(dev);
   if (!g) return;
+  {  // the dispatcher first: it launches what is still queued, then exits
+    std::unique_lock<std::mutex> lk(g->mu);
+    g->stop = true;
+    g->cv_req.notify_all();
+  }
+  if (g->th) {
+    g->th->join();
+    delete g->th;
+    g->th = nullptr;
+  }
   std::lock_guard<std::mutex> lk(g->mu);
+  g->stop = false;
+  for (int s = 0; s < EngineGate::kMaxDepth; s++) {
+    if (g->slot_ev[s]) (void)hipEventDestroy(g->slot_ev[s]);
+    g->slot_ev[s] = nullptr;
+    g->slot_used[s] = false;
+  }
   for (int s = 0; s < EngineGate::kMaxDepth; s++) {
     if (g->items[s]) { (void)hipStreamSynchronize(g->items[s]); destroy_stream(g->items[s]); }
     if (g->roles[s]) { (void)hipStreamSynchronize(g->roles[s]); destroy_stream(g->roles[s]); }
@@ -3098,11 +3126,17 @@ static int item_occupancy(int qpw, int threads) {
   return r = n;
 }
 
-int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
-                                hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
-  if (a.n_chains <= 0) return 0;
+// The launch parameters of one split engine launch (EngCtl, grid, item build).
+struct SplitPlan {
   EngCtl ctl;
-  ctl.gen = next_engine_gen();
+  int grid = 0, depth = 1, roles_grid = 8;
+  bool solo = false;
+  size_t words = 0;
+};
+static SplitPlan split_plan(const OdomArgs& a, int dev) {
+  SplitPlan p;
+  EngCtl& ctl = p.ctl;
+  ctl.gen = 0;  // numbered when queued on the device (split_enqueue)
   ctl.P = engine_part_rows(a.cap_sharp + a.cap_flat);
   ctl.w = a.eng_ctl;
   ctl.C = a.n_chains;
@@ -3118,31 +3152,76 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   const char* wb = getenv("LISLAM_ENGINE_WAIT_US");
   ctl.wait_ticks = wb ? (unsigned long long)std::max(1L, atol(wb)) * 100ull : 200000000ull;
   ctl.backoff = engine_backoff(a.eng_depth);
-  // One item workgroup per CU of the items' mask (all CUs but one per XCD): its 8 waves at <= 128
-  // VGPRs take half of each SIMD's registers, so the next batch's extraction and ORB kernels run
-  // beside the engine instead of queueing behind it.  LISLAM_ENGINE_WGS caps the grid (tests: one
-  // workgroup drains the queue).
-  int dev = 0;
-  (void)hipGetDevice(&dev);
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
+  p.depth = std::min(EngineGate::kMaxDepth, std::max(1, a.eng_depth));
   static const bool solo_ok = !(getenv("LISLAM_ENGINE_SOLO_ITEMS") && atoi(getenv("LISLAM_ENGINE_SOLO_ITEMS")) == 0);
-  const bool solo = solo_ok && depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
+  p.solo = solo_ok && p.depth == 1 && ctl.qpw == 1 && ctl.Q <= kSoloItemWaves;
   // Co-residency, checked at launch rather than assumed: the item workgroups one engine may hold at
   // once = the item CUs (all but one per XCD) x the workgroups of this item build that fit a CU
   // (hipOccupancyMaxActiveBlocksPerMultiprocessor), shared by the `depth` engines in flight.  The
   // grid and the items per (pass, chain) never exceed it, so a pass's items are all resident.
-  const int per_cu = item_occupancy(solo ? 0 : ctl.qpw, 64 * ctl.Q);
-  const int item_cus = std::max(1, cus - std::max(1, device_xccs(dev)));
-  const int resident = std::max(1, item_cus * per_cu / depth);
+  const int per_cu = item_occupancy(p.solo ? 0 : ctl.qpw, 64 * ctl.Q);
+  const int xccs = std::max(1, device_xccs(dev));
+  const int item_cus = std::max(1, cus - xccs);
+  const int resident = std::max(1, item_cus * per_cu / p.depth);
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
   const int cap = cap_env ? atoi(cap_env) : std::min(item_cus, resident);
-  int grid = ctl.C * ctl.I;
-  if (cap > 0) grid = min(grid, max(cap, 1));
+  p.grid = ctl.C * ctl.I;
+  if (cap > 0) p.grid = min(p.grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
-  ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, grid / ctl.C));
-  const size_t words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
+  ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, p.grid / ctl.C));
+  p.words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
+  p.roles_grid = std::max(ctl.C, xccs);
+  return p;
+}
+
+// Queue one launch on a slot's stream pair: the roles stream waits for `ready` and (if given) for
+// `prev`, the items stream forks from it; `mine` is recorded at the end (the slot's busy mark).
+static void split_enqueue(const OdomArgs& a, SplitPlan& p, hipStream_t roles, hipStream_t items, hipEvent_t ready,
+                          hipEvent_t prev, hipEvent_t mine, hipEvent_t fork, hipEvent_t join_r, hipEvent_t join_i,
+                          hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
+  EngCtl& ctl = p.ctl;
+  ctl.gen = next_engine_gen();
+  (void)hipStreamWaitEvent(roles, ready, 0);
+  if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
+  if (t0) (void)hipEventRecord(t0, roles);
+  // zero the control words of this launch, all but word 3 (the sticky abort)
+  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);
+  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (p.words - 4) * sizeof(unsigned), roles);
+  (void)hipEventRecord(fork, roles);
+  (void)hipStreamWaitEvent(items, fork, 0);
+  hipLaunchKernelGGL(k_odom_roles, dim3(p.roles_grid), dim3(kEngThreads), 0, roles, a, ctl);
+  if (p.solo) hipLaunchKernelGGL(k_odom_items_solo, dim3(p.grid), dim3(64 * ctl.Q), 0, items, a, ctl);
+  else switch (ctl.qpw) {
+    case 4: hipLaunchKernelGGL(k_odom_items<4>, dim3(p.grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    case 3: hipLaunchKernelGGL(k_odom_items<3>, dim3(p.grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    case 2: hipLaunchKernelGGL(k_odom_items<2>, dim3(p.grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+    default: hipLaunchKernelGGL(k_odom_items<1>, dim3(p.grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+  }
+  (void)hipEventRecord(join_r, roles);
+  (void)hipEventRecord(join_i, items);
+  (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do
+  if (t1) (void)hipEventRecord(t1, items);
+  // the launch's error and sticky abort words to the host, and its end, before the slot's next
+  // launch can queue behind it
+  if (h_abort) (void)hipMemcpyAsync(h_abort, a.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, items);
+  if (done) (void)hipEventRecord(done, items);
+  (void)hipEventRecord(mine, items);
+}
+
+// g->mu held: slot s's stream pair, made when first used; false = it cannot be made
+static bool slot_streams(EngineGate* g, int dev, int s) {
+  return g->roles[s] || make_engine_streams(dev, &g->roles[s], &g->items[s]);
+}
+
+int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
+                                hipEvent_t join_i, hipEvent_t t0, hipEvent_t t1, unsigned* h_abort, hipEvent_t done) {
+  if (a.n_chains <= 0) return 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  SplitPlan p = split_plan(a, dev);
+  const int depth = p.depth;
   EngineGate* gate = engine_gate(dev);
   if (!gate) return 0;
   std::unique_lock<std::mutex> lock(gate->mu);
@@ -3153,38 +3232,119 @@ int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t 
   // slot n % depth: the launch it waits for (n - depth) used the same slot, so a slot's pair holds
   // one engine at a time
   int slot = (int)(n % depth);
-  if (!gate->roles[slot] && !make_engine_streams(dev, &gate->roles[slot], &gate->items[slot])) slot = 0;
+  if (!slot_streams(gate, dev, slot)) slot = 0;
   for (hipEvent_t& e : gate->ev)
     if (!e) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  hipStream_t roles = gate->roles[slot], items = gate->items[slot];  // the slot's streams
-  (void)hipStreamWaitEvent(roles, ready, 0);
   // launch n - depth (its event is re-recorded only by launch n - depth + kMaxDepth > n)
-  if (n >= (unsigned long long)depth) (void)hipStreamWaitEvent(roles, gate->ev[(n - depth) % EngineGate::kMaxDepth], 0);
-  hipEvent_t mine = gate->ev[n % EngineGate::kMaxDepth];
-  if (t0) (void)hipEventRecord(t0, roles);
-  // zero the control words of this launch, all but word 3 (the sticky abort)
-  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);
-  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (words - 4) * sizeof(unsigned), roles);
-  (void)hipEventRecord(fork, roles);
-  (void)hipStreamWaitEvent(items, fork, 0);
-  hipLaunchKernelGGL(k_odom_roles, dim3(std::max(ctl.C, std::max(1, device_xccs(dev)))), dim3(kEngThreads), 0, roles, a, ctl);
-  if (solo) hipLaunchKernelGGL(k_odom_items_solo, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl);
-  else switch (ctl.qpw) {
-    case 4: hipLaunchKernelGGL(k_odom_items<4>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
-    case 3: hipLaunchKernelGGL(k_odom_items<3>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
-    case 2: hipLaunchKernelGGL(k_odom_items<2>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
-    default: hipLaunchKernelGGL(k_odom_items<1>, dim3(grid), dim3(64 * ctl.Q), 0, items, a, ctl); break;
+  hipEvent_t prev = n >= (unsigned long long)depth ? gate->ev[(n - depth) % EngineGate::kMaxDepth] : nullptr;
+  // and the dispatcher's launches (contexts of another depth on this device): a gated engine sizes
+  // its grid for `depth` engines, so it starts once theirs have ended
+  for (int s = 0; s < EngineGate::kMaxDepth; s++)
+    if (gate->slot_used[s]) (void)hipStreamWaitEvent(gate->roles[slot], gate->slot_ev[s], 0);
+  split_enqueue(a, p, gate->roles[slot], gate->items[slot], ready, prev, gate->ev[n % EngineGate::kMaxDepth], fork,
+                join_r, join_i, t0, t1, h_abort, done);
+  return p.grid;
+}
+
+// ---- the engine dispatcher: one host thread per device, started by the first submit and joined by
+// release_engine_streams.  Requests are launched in submission order among those whose `ready`
+// event has completed, each on a slot whose last launch has ended (slot_ev), while fewer than the
+// request's depth engines are in flight.  It polls every 20 us while something waits.
+bool engine_dispatch_enabled() {
+  static const bool on = !(getenv("LISLAM_ENGINE_DISPATCH") && atoi(getenv("LISLAM_ENGINE_DISPATCH")) == 0);
+  return on;
+}
+
+static void dispatcher_loop(EngineGate* g, int dev) {
+  (void)hipSetDevice(dev);
+  std::unique_lock<std::mutex> lk(g->mu);
+  for (;;) {
+    if (g->q.empty()) {
+      if (g->stop) break;
+      g->cv_req.wait(lk);
+      continue;
+    }
+    EngineRequest* r = nullptr;
+    size_t at = 0;
+    for (size_t i = 0; i < g->q.size(); i++)
+      if (hipEventQuery(g->q[i]->ready) == hipSuccess) { r = g->q[i]; at = i; break; }
+    if (r) {
+      SplitPlan& p = *static_cast<SplitPlan*>(r->plan);
+      // a gated launch in flight (a depth-1 context on this device) holds the CUs its grid was
+      // sized for: nothing is dispatched beside it
+      bool gated = false;
+      for (hipEvent_t e : g->ev) gated = gated || (e && hipEventQuery(e) != hipSuccess);
+      int busy = gated ? EngineGate::kMaxDepth : 0, free_slot = -1;
+      for (int s = 0; s < EngineGate::kMaxDepth; s++) {
+        const bool running = g->slot_used[s] && hipEventQuery(g->slot_ev[s]) != hipSuccess;
+        busy += running;
+        if (!running && free_slot < 0 && s < p.depth) free_slot = s;
+      }
+      if (busy < p.depth && free_slot >= 0 && slot_streams(g, dev, free_slot)) {
+        if (!g->slot_ev[free_slot]) (void)hipEventCreateWithFlags(&g->slot_ev[free_slot], hipEventDisableTiming);
+        split_enqueue(r->a, p, g->roles[free_slot], g->items[free_slot], r->ready, nullptr, g->slot_ev[free_slot],
+                      r->fork, r->join_r, r->join_i, r->t0, r->t1, r->h_abort, r->done);
+        g->slot_used[free_slot] = true;
+        g->q.erase(g->q.begin() + (long)at);
+        delete static_cast<SplitPlan*>(r->plan);
+        r->plan = nullptr;
+        r->state.store(2);
+        g->cv_launched.notify_all();
+        continue;
+      }
+    }
+    (void)hipGetLastError();  // hipEventQuery's not-ready status
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    lk.lock();
   }
-  (void)hipEventRecord(join_r, roles);
-  (void)hipEventRecord(join_i, items);
-  (void)hipStreamWaitEvent(items, join_r, 0);  // the device's engine ends when both kernels do
-  if (t1) (void)hipEventRecord(t1, items);
-  // the launch's error and sticky abort words to the host, and its end, before the slot's next
-  // launch can queue behind it (still under the gate's lock)
-  if (h_abort) (void)hipMemcpyAsync(h_abort, a.eng_ctl + 2, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, items);
-  if (done) (void)hipEventRecord(done, items);
-  (void)hipEventRecord(mine, items);
-  return grid;
+}
+
+// At process exit (contexts never destroyed): the dispatchers launch what is queued and stop
+// before the runtime is torn down.
+static void stop_dispatchers() {
+  for (int d = 0; d < 64; d++) {
+    EngineGate* g = engine_gate(d);
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (!g->th) continue;
+      g->stop = true;
+      g->cv_req.notify_all();
+    }
+    g->th->join();
+    delete g->th;
+    g->th = nullptr;
+  }
+}
+
+int submit_odometry_chain_split(EngineRequest* r) {
+  if (r->a.n_chains <= 0) return 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  EngineGate* g = engine_gate(dev);
+  if (!g) return 0;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (!probe_engine_streams(g, dev)) return 0;
+  if (!g->th) {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(stop_dispatchers); });
+    g->stop = false;
+    g->th = new std::thread(dispatcher_loop, g, dev);
+  }
+  r->plan = new SplitPlan(split_plan(r->a, dev));
+  r->state.store(1);
+  g->q.push_back(r);
+  g->cv_req.notify_one();
+  return 1;
+}
+
+void wait_engine_launched(EngineRequest* r) {
+  if (r->state.load() != 1) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  EngineGate* g = engine_gate(dev);
+  std::unique_lock<std::mutex> lk(g->mu);
+  g->cv_launched.wait(lk, [&] { return r->state.load() != 1; });
 }
 
 void launch_factors_raw(const RawFactorArgs& a, hipStream_t st) {
