@@ -1542,6 +1542,10 @@ struct EngCtl {
   __device__ unsigned* lm_gen(int c) const { return w + 4 + c; }
   __device__ unsigned* assoc_done(int c, int ro) const { return w + 4 + C + (size_t)c * 2 * R + ro; }
   __device__ unsigned* role_ticket() const { return w + 4 + C + (size_t)2 * R * C; }
+  __device__ unsigned* role_arrive() const { return w + 5 + C + (size_t)2 * R * C; }
+  // the device's solve roles per XCD (k_odom_roles), or null: roles taken without regard to XCD
+  unsigned* xbusy = nullptr;
+  int rgrid = 0;  // k_odom_roles' grid
 };
 // Word 31 of an item's eng_part row once its records and share of pass ro are written.
 __device__ __forceinline__ uint64_t eng_tag(const EngCtl& ctl, int ro) {
@@ -2759,22 +2763,104 @@ __global__ __launch_bounds__(kEngThreads) void k_odom_chain(OdomArgs a, EngCtl c
 // The grid is one workgroup per role CU (at least C): a workgroup takes the next chain from a ticket
 // when it starts, so the chains go to whichever role CUs are free (another engine may hold some:
 // LISLAM_ENGINE_DEPTH), and the workgroups left over exit at once.
+__device__ __forceinline__ unsigned xcc_id() {
+  return __builtin_amdgcn_s_getreg((4 - 1) << 11 | 0 << 6 | 20) & 15u;  // HW_REG_XCC_ID[3:0]
+}
+
+// Developer builds (-DLISLAM_ENG_STAMPS=1, scripts/engines_concurrent.py): per launch (gen % 64)
+// s_memrealtime of the role's start and end, its XCD, the first and last item workgroup's start, the
+// item workgroups that ran, and the last item's end.
+#ifndef LISLAM_ENG_STAMPS
+#define LISLAM_ENG_STAMPS 0
+#endif
+#if LISLAM_ENG_STAMPS
+__device__ unsigned long long g_eng_stamps[64][12];
+__device__ __forceinline__ void eng_stamp_max(int k, const EngCtl& ctl, unsigned long long v) {
+  __hip_atomic_fetch_max(&g_eng_stamps[ctl.gen % 64][k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void eng_stamp_min(int k, const EngCtl& ctl, unsigned long long v) {
+  __hip_atomic_fetch_min(&g_eng_stamps[ctl.gen % 64][k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+extern "C" int lislam_debug_engine_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eng_stamps), sizeof(g_eng_stamps)) != hipSuccess) return 1;
+  static unsigned long long init[64][12];
+  for (auto& r : init) { for (auto& v : r) v = 0; r[3] = r[10] = ~0ull; }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_eng_stamps), init, sizeof(init)) == hipSuccess ? 0 : 1;
+}
+#endif
+
+// The launch's control words to zero, all but word 3 (the sticky abort): one workgroup on the roles
+// stream ahead of both kernels (two runtime memsets were two dispatches).
+__global__ __launch_bounds__(256) void k_eng_zero(EngCtl ctl, int words) {
+#if LISLAM_ENG_STAMPS
+  if (threadIdx.x == 0) {
+    eng_stamp_max(7, ctl, __builtin_amdgcn_s_memrealtime());
+    eng_stamp_max(8, ctl, xcc_id() + 1);
+  }
+#endif
+  for (int i = threadIdx.x; i < words; i += 256)
+    if (i != 3) ctl.w[i] = 0u;
+}
+
 __global__ __launch_bounds__(kEngThreads) void k_odom_roles(OdomArgs a, EngCtl ctl) {
   __shared__ EngShared sh;
   __shared__ EngLM lm;
+  __shared__ unsigned held_x;
 #ifdef LISLAM_ENG_ZERO_LDS  // developer: start from zeroed LDS (a read-before-write hunt)
   for (int i = threadIdx.x; i < (int)(sizeof(EngShared) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&sh)[i] = 0u;
   for (int i = threadIdx.x; i < (int)(sizeof(EngLM) / 4); i += blockDim.x) reinterpret_cast<unsigned*>(&lm)[i] = 0u;
   __syncthreads();
 #endif
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
-  if (wave0) {
-    if (lane_id() == 0) sh.ticket = add_rlx(ctl.role_ticket(), 1u);
+#if LISLAM_ENG_STAMPS
+  if (wave0 && lane_id() == 0) {  // every roles workgroup's start: the first and the last
+    eng_stamp_max(9, ctl, __builtin_amdgcn_s_memrealtime());
+    eng_stamp_min(10, ctl, __builtin_amdgcn_s_memrealtime());
+  }
+#endif
+  if (wave0 && lane_id() == 0) {
+    if (!ctl.xbusy) {
+      sh.ticket = add_rlx(ctl.role_ticket(), 1u);
+    } else {
+      // One role per XCD while a free one exists (each XCD holds two role CUs): the workgroups of the
+      // next launch that land on this XCD — those that exit at once, or the control words' memset —
+      // then find its other role CU free instead of queueing behind this chain.  A workgroup takes
+      // the chain only if its XCD held no role; the last to arrive takes it if none of them could.
+      const unsigned x = xcc_id();
+      unsigned* xb = ctl.xbusy + x;
+      unsigned t = ~0u;
+      const bool mine = add_rlx(xb, 1u) == 0u;  // this XCD held no role: the count stays ours
+      if (mine) t = add_rlx(ctl.role_ticket(), 1u);
+      else (void)add_rlx(xb, ~0u);
+      __threadfence();  // the claim is settled before the arrival is counted
+      if (t >= (unsigned)ctl.C && add_rlx(ctl.role_arrive(), 1u) == (unsigned)ctl.rgrid - 1u) {
+        t = add_rlx(ctl.role_ticket(), 1u);  // the last arrival: every other claim is settled
+        if (t < (unsigned)ctl.C && !mine) (void)add_rlx(xb, 1u);
+      } else if (t < (unsigned)ctl.C) {
+        (void)add_rlx(ctl.role_arrive(), 1u);
+      }
+      if (t >= (unsigned)ctl.C && mine) (void)add_rlx(xb, ~0u);
+      sh.ticket = t;
+      held_x = t < (unsigned)ctl.C ? x : ~0u;
+    }
   }
   __syncthreads();
-  const int c = uni((int)sh.ticket);
+  const int c = uni((int)min(sh.ticket, (unsigned)ctl.C));
   if (c >= ctl.C) return;
+#if LISLAM_ENG_STAMPS
+  if (wave0 && lane_id() == 0) {
+    eng_stamp_max(0, ctl, __builtin_amdgcn_s_memrealtime());
+    eng_stamp_max(2, ctl, xcc_id() + 1);
+  }
+#endif
   (void)eng_solve_role(a, ctl, sh, lm, c, wave0, (unsigned)(c * (ctl.I + 1) + ctl.I));
+#if LISLAM_ENG_STAMPS
+  if (wave0 && lane_id() == 0) eng_stamp_max(1, ctl, __builtin_amdgcn_s_memrealtime());
+#endif
+  if (ctl.xbusy && wave0 && lane_id() == 0) {
+    __threadfence();
+    (void)add_rlx(ctl.xbusy + held_x, ~0u);
+  }
 }
 
 #ifndef LISLAM_ITEM_WPE
@@ -2786,6 +2872,14 @@ __device__ __forceinline__ void eng_items_body(const OdomArgs& a, const EngCtl& 
   const unsigned total = (unsigned)ctl.C * ctl.I * 2u * ctl.R;
   const bool wave0 = uni((int)(threadIdx.x >> 6)) == 0;
   const bool lead = lane_id() == 0;
+#if LISLAM_ENG_STAMPS
+  if (wave0 && lead) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    eng_stamp_min(3, ctl, t);
+    eng_stamp_max(4, ctl, t);
+    __hip_atomic_fetch_add(&g_eng_stamps[ctl.gen % 64][5], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
   if (wave0) {
     if (lead) {
       const unsigned t = add_rlx(ctl.ticket(), 1u);
@@ -2807,6 +2901,9 @@ __device__ __forceinline__ void eng_items_body(const OdomArgs& a, const EngCtl& 
     __syncthreads();
     tk = ok ? (unsigned)uni((int)sh.ticket) : total;
   }
+#if LISLAM_ENG_STAMPS
+  if (wave0 && lead) eng_stamp_max(6, ctl, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 template <int kQpw>
 __global__ __launch_bounds__(64 * kMaxItemWaves, LISLAM_ITEM_WPE) void k_odom_items(OdomArgs a, EngCtl ctl) {
@@ -2966,15 +3063,47 @@ static int device_xccs(int dev) {
   return x;
 }
 
+// The CU masks.  Bit i selects a CU of XCD i % nx, and the bit groups [k nx, k nx + nx) walk the
+// XCDs' shader engines: group k is a CU of SE k % 4 in every XCD (gfx950, measured:
+// scripts/micro/cumask2.hip).  A workgroup is dealt to a shader engine before a CU is chosen, so a
+// CU free in another SE does not help it.
+//   roles: groups 0 and 4, two CUs of SE 0 in every XCD.  With one role per XCD (k_odom_roles) the
+//     next launch's roles workgroups that land on a role's XCD — those that exit at once, or the
+//     control-word zeroing — find the other CU free instead of queueing behind that whole chain (one
+//     role CU per XCD: 75-80 vs 40 ms whenever it happened, scripts/engines_concurrent.py).
+//     LISLAM_ROLE_CUS=1 keeps group 0 only.
+//   items: every other CU; LISLAM_ITEMS_SE0=0 leaves SE 0 out (its six free CUs get as many item
+//     workgroups dealt as the other SEs' eight).
+//   work (extraction, ORB, per-round odometry): shader engines 1-3.  Work dealt evenly over the SEs
+//     runs at the pace of the SE with the fewest CUs, so SE 0's six left-over CUs added next to
+//     eight-CU SEs would be worth no more than none, and they are the items' alone instead: the
+//     driver-shape headline 23.3-23.4k vs 20.3-20.6k scans/s with the work streams on SE 0 too
+//     (profiles/r06_semask_ab.txt).  LISLAM_WORK_SE0=1 shares SE 0.
+static int role_cus_per_xcd() {
+  static const int r = getenv("LISLAM_ROLE_CUS") && atoi(getenv("LISLAM_ROLE_CUS")) == 1 ? 1 : 2;
+  return r;
+}
+static bool role_bit(int i, int nx) { return i / nx == 0 || (role_cus_per_xcd() == 2 && i / nx == 4); }
+static bool item_bit(int i, int nx) {
+  static const bool se0 = !(getenv("LISLAM_ITEMS_SE0") && atoi(getenv("LISLAM_ITEMS_SE0")) == 0);
+  return !role_bit(i, nx) && (se0 || (i / nx) % 4 != 0);
+}
+static int g_item_cus[64];  // CUs of the items mask per device (make_engine_streams)
+
 static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
   const int cus = prop.multiProcessorCount, nx = device_xccs(dev);
-  if (!multi_xcd || nx < 1 || cus < 4 * nx || cus % nx) return false;
+  if (!multi_xcd || nx < 1 || cus < 8 * nx || cus % nx) return false;
   const int words = (cus + 31) / 32;
   std::vector<uint32_t> mr(words, 0u), mi(words, 0u);
-  for (int i = 0; i < cus; i++) (i < nx ? mr : mi)[i / 32] |= 1u << (i % 32);
+  int n_items = 0;
+  for (int i = 0; i < cus; i++) {
+    if (role_bit(i, nx)) mr[i / 32] |= 1u << (i % 32);
+    else if (item_bit(i, nx)) { mi[i / 32] |= 1u << (i % 32); n_items++; }
+  }
+  if (dev >= 0 && dev < 64) g_item_cus[dev] = n_items;
   if (!masked_stream(dev, roles, words, mr.data())) return false;
   if (!masked_stream(dev, items, words, mi.data())) {
     destroy_stream(*roles);
@@ -2984,23 +3113,25 @@ static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items)
   return true;
 }
 
-// A stream for the library's other kernels (extraction, ORB, per-round odometry): every CU but the
-// solve roles' (one per XCD, engine_streams), so a role launched beside the next batch's extraction
-// finds a whole CU free instead of waiting for the extraction's waves on it to drain — they would
-// refill each freed slot first.  Plain non-blocking stream where CU masks do not apply.
+// A stream for the library's other kernels (extraction, ORB, per-round odometry): shader engines 1-3
+// (above), never the solve roles' CUs, so a role launched beside the next batch's extraction finds a
+// whole CU free instead of waiting for the extraction's waves on it to drain — they would refill each
+// freed slot first.  Plain non-blocking stream where CU masks do not apply.
 bool work_stream(int dev, hipStream_t* s) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
     const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
     const int cus = prop.multiProcessorCount, nx = device_xccs(dev);
-    if (multi_xcd && nx >= 1 && cus >= 4 * nx && cus % nx == 0) {
+    if (multi_xcd && nx >= 1 && cus >= 8 * nx && cus % nx == 0) {
       const int words = (cus + 31) / 32;
       std::vector<uint32_t> m(words, 0u);
       // LISLAM_WORK_XCDS=n (developer: traffic attribution) keeps the stream on the first n XCDs
       const char* xe = getenv("LISLAM_WORK_XCDS");
       const int nxu = xe ? std::max(1, std::min(nx, atoi(xe))) : nx;
-      for (int i = nx; i < cus; i++)
-        if (i % nx < nxu) m[i / 32] |= 1u << (i % 32);
+      // shader engine 0 (the role CUs' SE) is left to the engines; LISLAM_WORK_SE0=1 (A/B) shares it
+      static const bool se0 = getenv("LISLAM_WORK_SE0") && atoi(getenv("LISLAM_WORK_SE0")) == 1;
+      for (int i = 0; i < cus; i++)
+        if (!role_bit(i, nx) && i % nx < nxu && (se0 || (i / nx) % 4 != 0)) m[i / 32] |= 1u << (i % 32);
       if (masked_stream(dev, s, words, m.data())) return true;
     }
   }
@@ -3031,6 +3162,7 @@ struct EngineGate {
   // the dispatcher (submit_odometry_chain_split): its thread (a pointer: a static std::thread still
   // joinable at process exit would terminate), queue, and the slots' last launches
   std::thread* th = nullptr;
+  unsigned* xbusy = nullptr;  // solve roles running per XCD (k_odom_roles), made with the streams
   bool stop = false;
   std::deque<EngineRequest*> q;
   std::condition_variable cv_req, cv_launched;
@@ -3046,7 +3178,16 @@ static EngineGate* engine_gate(int dev) {
 // other slots' pairs when a launch first takes them, so a device holds 2 x (the deepest depth used)
 // engine queues.
 static bool probe_engine_streams(EngineGate* g, int dev) {
-  if (g->avail < 0) g->avail = make_engine_streams(dev, &g->roles[0], &g->items[0]) ? 1 : 0;
+  if (g->avail < 0) {
+    g->avail = make_engine_streams(dev, &g->roles[0], &g->items[0]) ? 1 : 0;
+    if (g->avail == 1 && !g->xbusy) {
+      if (hipMalloc(&g->xbusy, 16 * sizeof(unsigned)) != hipSuccess || hipMemset(g->xbusy, 0, 16 * sizeof(unsigned)) != hipSuccess) {
+        (void)hipGetLastError();
+        if (g->xbusy) (void)hipFree(g->xbusy);
+        g->xbusy = nullptr;
+      }
+    }
+  }
   return g->avail == 1;
 }
 
@@ -3099,6 +3240,8 @@ void release_engine_streams(int dev) {
     if (g->round[r]) { (void)hipStreamSynchronize(g->round[r]); destroy_stream(g->round[r]); }
     g->round[r] = nullptr;
   }
+  if (g->xbusy) (void)hipFree(g->xbusy);
+  g->xbusy = nullptr;
   g->launches = 0;
   g->avail = -1;
 }
@@ -3163,7 +3306,7 @@ static SplitPlan split_plan(const OdomArgs& a, int dev) {
   // grid and the items per (pass, chain) never exceed it, so a pass's items are all resident.
   const int per_cu = item_occupancy(p.solo ? 0 : ctl.qpw, 64 * ctl.Q);
   const int xccs = std::max(1, device_xccs(dev));
-  const int item_cus = std::max(1, cus - xccs);
+  const int item_cus = std::max(1, dev >= 0 && dev < 64 && g_item_cus[dev] ? g_item_cus[dev] : cus - role_cus_per_xcd() * xccs);
   const int resident = std::max(1, item_cus * per_cu / p.depth);
   const char* cap_env = getenv("LISLAM_ENGINE_WGS");
   const int cap = cap_env ? atoi(cap_env) : std::min(item_cus, resident);
@@ -3171,8 +3314,13 @@ static SplitPlan split_plan(const OdomArgs& a, int dev) {
   if (cap > 0) p.grid = min(p.grid, max(cap, 1));
   const char* bud = getenv("LISLAM_ENGINE_BUDGET");
   ctl.budget = min(kMaxShareItems, bud ? max(1, atoi(bud)) : max(1, p.grid / ctl.C));
-  p.words = ((size_t)5 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket
+  p.words = ((size_t)6 + ctl.C + (size_t)2 * ctl.R * ctl.C + 3) / 4 * 4;  // + assoc_done, role ticket, arrivals
   p.roles_grid = std::max(ctl.C, xccs);
+  ctl.rgrid = p.roles_grid;
+  // one role per XCD for single-chain launches (k_odom_roles); LISLAM_ROLE_GATE=0: any XCD
+  static const bool xgate = !(getenv("LISLAM_ROLE_GATE") && atoi(getenv("LISLAM_ROLE_GATE")) == 0);
+  EngineGate* g = engine_gate(dev);
+  ctl.xbusy = xgate && ctl.C == 1 && role_cus_per_xcd() >= 2 && g ? g->xbusy : nullptr;
   return p;
 }
 
@@ -3187,8 +3335,7 @@ static void split_enqueue(const OdomArgs& a, SplitPlan& p, hipStream_t roles, hi
   if (prev) (void)hipStreamWaitEvent(roles, prev, 0);
   if (t0) (void)hipEventRecord(t0, roles);
   // zero the control words of this launch, all but word 3 (the sticky abort)
-  (void)hipMemsetAsync(a.eng_ctl, 0, 3 * sizeof(unsigned), roles);
-  (void)hipMemsetAsync(a.eng_ctl + 4, 0, (p.words - 4) * sizeof(unsigned), roles);
+  hipLaunchKernelGGL(k_eng_zero, dim3(1), dim3(256), 0, roles, ctl, (int)p.words);
   (void)hipEventRecord(fork, roles);
   (void)hipStreamWaitEvent(items, fork, 0);
   hipLaunchKernelGGL(k_odom_roles, dim3(p.roles_grid), dim3(kEngThreads), 0, roles, a, ctl);
@@ -3285,6 +3432,11 @@ static void dispatcher_loop(EngineGate* g, int dev) {
         split_enqueue(r->a, p, g->roles[free_slot], g->items[free_slot], r->ready, nullptr, g->slot_ev[free_slot],
                       r->fork, r->join_r, r->join_i, r->t0, r->t1, r->h_abort, r->done);
         g->slot_used[free_slot] = true;
+#if LISLAM_ENG_STAMPS
+        fprintf(stderr, "dispatch gen %u slot %d at %.3f ms (queued %zu, busy %d)\n", p.ctl.gen, free_slot,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(),
+                g->q.size(), busy);
+#endif
         g->q.erase(g->q.begin() + (long)at);
         delete static_cast<SplitPlan*>(r->plan);
         r->plan = nullptr;
