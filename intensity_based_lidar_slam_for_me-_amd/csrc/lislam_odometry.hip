@@ -3084,13 +3084,20 @@ static int role_cus_per_xcd() {
   return r;
 }
 static bool role_bit(int i, int nx) { return i / nx == 0 || (role_cus_per_xcd() == 2 && i / nx == 4); }
-static bool item_bit(int i, int nx) {
-  static const bool se0 = !(getenv("LISLAM_ITEMS_SE0") && atoi(getenv("LISLAM_ITEMS_SE0")) == 0);
-  return !role_bit(i, nx) && (se0 || (i / nx) % 4 != 0);
+// Slot s's items: SE 0's six item CUs hold two workgroups each, as many as four engines deal them
+// (96 items / 32 SEs = 3 per SE each), so the pairs of slots 4 and 5 leave SE 0 out: a fifth engine
+// deals its 96 items to SEs 1-3 (4 per SE, 16 with the other four's 12 = their 8 CUs x 2), where
+// with SE 0 it found 12 slots for 15 and part of its items waited for an engine to end
+// (scripts/engines_concurrent.py: 61 vs 41 ms).  LISLAM_ITEMS_SE0=0: no slot's items on SE 0;
+// =2: every slot's.
+static bool item_bit(int i, int nx, int slot) {
+  static const int se0 = getenv("LISLAM_ITEMS_SE0") ? atoi(getenv("LISLAM_ITEMS_SE0")) : 1;
+  const bool with_se0 = se0 == 2 || (se0 == 1 && slot < 4);
+  return !role_bit(i, nx) && (with_se0 || (i / nx) % 4 != 0);
 }
 static int g_item_cus[64];  // CUs of the items mask per device (make_engine_streams)
 
-static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items) {
+static bool make_engine_streams(int dev, int slot, hipStream_t* roles, hipStream_t* items) {
   hipDeviceProp_t prop{};
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const bool multi_xcd = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 || std::strncmp(prop.gcnArchName, "gfx942", 6) == 0;
@@ -3101,9 +3108,9 @@ static bool make_engine_streams(int dev, hipStream_t* roles, hipStream_t* items)
   int n_items = 0;
   for (int i = 0; i < cus; i++) {
     if (role_bit(i, nx)) mr[i / 32] |= 1u << (i % 32);
-    else if (item_bit(i, nx)) { mi[i / 32] |= 1u << (i % 32); n_items++; }
+    else if (item_bit(i, nx, slot)) { mi[i / 32] |= 1u << (i % 32); n_items++; }
   }
-  if (dev >= 0 && dev < 64) g_item_cus[dev] = n_items;
+  if (slot == 0 && dev >= 0 && dev < 64) g_item_cus[dev] = n_items;
   if (!masked_stream(dev, roles, words, mr.data())) return false;
   if (!masked_stream(dev, items, words, mi.data())) {
     destroy_stream(*roles);
@@ -3179,7 +3186,7 @@ static EngineGate* engine_gate(int dev) {
 // engine queues.
 static bool probe_engine_streams(EngineGate* g, int dev) {
   if (g->avail < 0) {
-    g->avail = make_engine_streams(dev, &g->roles[0], &g->items[0]) ? 1 : 0;
+    g->avail = make_engine_streams(dev, 0, &g->roles[0], &g->items[0]) ? 1 : 0;
     if (g->avail == 1 && !g->xbusy) {
       if (hipMalloc(&g->xbusy, 16 * sizeof(unsigned)) != hipSuccess || hipMemset(g->xbusy, 0, 16 * sizeof(unsigned)) != hipSuccess) {
         (void)hipGetLastError();
@@ -3359,7 +3366,7 @@ static void split_enqueue(const OdomArgs& a, SplitPlan& p, hipStream_t roles, hi
 
 // g->mu held: slot s's stream pair, made when first used; false = it cannot be made
 static bool slot_streams(EngineGate* g, int dev, int s) {
-  return g->roles[s] || make_engine_streams(dev, &g->roles[s], &g->items[s]);
+  return g->roles[s] || make_engine_streams(dev, s, &g->roles[s], &g->items[s]);
 }
 
 int launch_odometry_chain_split(const OdomArgs& a, hipEvent_t ready, hipEvent_t fork, hipEvent_t join_r,
