@@ -951,17 +951,14 @@ extern "C" int lislam_debug_sel_phases(unsigned long long* out) {
 #define SEL_PHASE(i)
 #endif
 constexpr int kPatchDw = 2 * 279;  // LDS dwords per wave: 2 angle patches (31 x 9) >= 4 Harris patches (9 x 4)
-__device__ __forceinline__ void orb_select_body(const Args& a, int gi) {
+__device__ __forceinline__ void orb_select_body(const Args& a, int gi, int l) {
   __shared__ SelShared sh;
   __shared__ uint32_t sh_patch[(kSelThreads / 64) * kPatchDw];
 #ifdef LISLAM_PHASE_PROF
   unsigned long long t_ph = __builtin_amdgcn_s_memrealtime();
 #endif
   const Geom& g = a.g;
-  // level-major blocks: consecutive blocks (dealt round-robin to the 8 XCDs) are different scans
-  // of one level, so the heavy level-0 workgroups spread over every XCD
-  const int S = gridDim.x / kL;
-  const int l = blockIdx.x / S, s = a.smap ? a.smap[gi] : gi;
+  const int s = a.smap ? a.smap[gi] : gi;
   const int w = g.w[l], h = g.h[l];
   const uint8_t* base = a.pyr + (size_t)s * g.bytes;
   const uint8_t* kf = a.nms + (size_t)s * g.pix[kL] + g.pix[l];
@@ -1201,11 +1198,23 @@ __device__ __forceinline__ void orb_select_body(const Args& a, int gi) {
   if (threadIdx.x == 0) a.lcnt[s * kL + l] = n;
 }
 
-// One scan per grid scan index; with a device list (a.scount) the indices past its count exit.
+// Level-major blocks: consecutive blocks (dealt round-robin to the XCDs) are different scans of one
+// level, so the heavy level-0 workgroups spread over every XCD.  One scan per grid scan index.
 __global__ __launch_bounds__(kSelThreads, 4) void k_orb_select(Args a) {
   const int S = gridDim.x / kL;
-  const int cnt = a.scount ? *a.scount : S;
-  if ((int)(blockIdx.x % S) < cnt) orb_select_body(a, blockIdx.x % S);
+  orb_select_body(a, blockIdx.x % S, blockIdx.x / S);
+}
+
+// The scans of a device list (a.smap, *a.scount entries): the grid's scan indices stride over the
+// entries, so the launch is a few slots wide (placing a workgroup per possible entry, thousands that
+// exit at once, took milliseconds beside the chain engines).
+__global__ __launch_bounds__(kSelThreads, 4) void k_orb_select_list(Args a) {
+  const int S = gridDim.x / kL;
+  const int l = blockIdx.x / S, cnt = *a.scount;
+  for (int i = blockIdx.x % S; i < cnt; i += S) {
+    orb_select_body(a, i, l);
+    __syncthreads();
+  }
 }
 
 // levels in order, level-0 coordinates, cloud-track lookup and zero filter (a9)
@@ -2105,9 +2114,7 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const Geom& g = e->g;
   // kListSlots grid scan indices stride over the list: the count is only known on the device
   const int ns = std::min(nmax, kListSlots);
-  // select: one grid slot per possible list entry (the strided body needed 180 VGPRs, more than a
-  // workgroup beside the chain engine's items may hold); the slots past the count exit at once
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(nmax * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select_list, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
   { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
   { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
