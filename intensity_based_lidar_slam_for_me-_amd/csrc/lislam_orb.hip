@@ -1570,6 +1570,11 @@ __device__ __forceinline__ void orb_match_body(const PairArgs& p, int pi) {
     }
     n += tot;
   }
+  // every read of this pair's best[] row is done: back to the "no match" sentinel for the next
+  // launch that uses the slot (k_orb_xdist_mfma writes entries < nq only; the rest stay sentinel
+  // from the allocation), so no fill launch precedes the distances
+  __syncthreads();
+  for (int j = threadIdx.x; j < nq; j += blockDim.x) best[j] = kNoMatch;
   if (threadIdx.x == 0) {
     int* st = p.stats + pr * 8;
     st[0] = (nt != nq && G >= 4 && G != M) ? 1 : 0;
@@ -1620,18 +1625,6 @@ __device__ void pair_eval(LmSh& sh, const double* rec, int n) {
     sh.acc[threadIdx.x] = v;
   }
   __syncthreads();
-}
-
-// best[] rows of the launch's pairs to the "no match" sentinel (one launch for any slot list)
-__device__ __forceinline__ void orb_mfill_body(const PairArgs& p, int qcap, int pi) {
-  const int pr = p.pslot ? p.pslot[pi] : pi;
-  int* row = p.mscratch + (size_t)pr * p.bstride;
-  for (int j = blockIdx.y * 256 + threadIdx.x; j < qcap; j += gridDim.y * 256) row[j] = kNoMatch;
-}
-
-__global__ __launch_bounds__(256) void k_orb_mfill(PairArgs p, int qcap) {
-  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
-  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) orb_mfill_body(p, qcap, pi);
 }
 
 // Batch outputs: scan 0 is the first frame (stats -1, its keypoint count), scan k > 0 pair
@@ -2146,6 +2139,9 @@ struct PairBufs {
     ORC(alloc(&args, (size_t)3 * maxp));
     ORC(alloc(&redet, maxp));
     ORC(alloc(&mscratch, (size_t)maxp * qcap));
+    // the best[] rows start at the "no match" sentinel; k_orb_match puts back each row it consumed
+    if (hipMemset(mscratch, 0x7f, (size_t)maxp * qcap * sizeof(int)) != hipSuccess)
+      return ofail(ctx, LISLAM_ERR_DEVICE, "hipMemset of the match rows failed");
     if (raw) ORC(alloc(&mout, (size_t)maxp * qcap * 3));
     ORC(alloc(&kind, (size_t)maxp * qcap));
     ORC(alloc(&stats, (size_t)maxp * 8));
@@ -2199,7 +2195,6 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   p.T = pb.T + b0 * 7;
   {
     TimedScope t(c, kT_orb_match);
-    hipLaunchKernelGGL(k_orb_mfill, dim3(gp, cdiv(pb.qcap, 1024)), dim3(256), 0, st, p, pb.qcap);
     hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
     hipLaunchKernelGGL(k_orb_match, dim3(gp), dim3(kPairThreads), 0, st, p);
   }
