@@ -142,6 +142,7 @@ struct Args {
   int* overflow;          // [1]
   const int* smap;        // scan of each grid scan index (null: identity from the slot base)
   const int* scount;      // device count of grid scan indices in use (null: all); the rest exit
+  int* arrive;            // k_orb_redetect: level workgroups of each list entry arrived (0 between launches)
 };
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -1277,8 +1278,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
-  __shared__ uint32_t patch[8][kDescDw];
+// kSlots = blockDim.x / 32; chunks c0, c0 + cstep, ... of the scan's keypoints
+template <int kSlots>
+__device__ __forceinline__ void orb_desc_body(const Args& a, int gi, int c0, int cstep) {
+  __shared__ uint32_t patch[kSlots][kDescDw];
   __shared__ float kcs[kDescChunk][2];  // cos, sin of the keypoint's angle
   __shared__ int kpos[kDescChunk][2];   // patch byte offset in the scan's blurred pyramid, stride | shift << 16
   const Geom& g = a.g;
@@ -1288,7 +1291,7 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
   const uint8_t* base = a.blur + (size_t)s * g.bytes;
   const uint8_t* P = reinterpret_cast<const uint8_t*>(patch[slot]);
   const uint32_t* pat = reinterpret_cast<const uint32_t*>(c_pattern.v) + byte * 8;  // x1 y1 x2 y2 of bits 0..7, + 13
-  for (int k0 = blockIdx.x * kDescChunk; k0 < nk; k0 += gridDim.x * kDescChunk) {
+  for (int k0 = c0 * kDescChunk; k0 < nk; k0 += cstep * kDescChunk) {
     __syncthreads();  // the previous chunk's tables are no longer read
     if (threadIdx.x < kDescChunk && k0 + (int)threadIdx.x < nk) {
       const float* kp = a.kp + ((size_t)s * g.cap + k0 + threadIdx.x) * 6;
@@ -1317,7 +1320,7 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
       }
     };
     if (slot < n) load(slot);
-    for (int j = slot; j < n; j += 8) {
+    for (int j = slot; j < n; j += kSlots) {
       wave_lds_sync();  // the previous keypoint's tests have read the slot
 #pragma unroll
       for (int i = 0; i < (kDescDw + 31) / 32; i++) {
@@ -1325,7 +1328,7 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
         if (e < kDescDw) patch[slot][e] = v[i];
       }
       wave_lds_sync();
-      if (j + 8 < n) load(j + 8);
+      if (j + kSlots < n) load(j + kSlots);
       const float ca = kcs[j][0], sa = kcs[j][1];
       const uint8_t* c0 = P + kDescR * kDescRow + kDescR + (kpos[j][1] >> 16);  // the keypoint's byte
       int bits = 0;
@@ -1348,7 +1351,50 @@ __device__ __forceinline__ void orb_desc_body(const Args& a, int gi) {
 
 __global__ __launch_bounds__(256) void k_orb_desc(Args a) {
   const int cnt = a.scount ? *a.scount : (int)gridDim.y;
-  for (int gi = blockIdx.y; gi < cnt; gi += gridDim.y) orb_desc_body(a, gi);
+  for (int gi = blockIdx.y; gi < cnt; gi += gridDim.y) orb_desc_body<8>(a, gi, blockIdx.x, gridDim.x);
+}
+
+// A re-detection (k_orb_select_list, k_orb_finish, k_orb_desc of a device list) in one launch: the
+// last of an entry's kL level workgroups to arrive (an agent-scope counter per list entry, told by
+// the value its add returns) concatenates the levels and computes all the entry's descriptors,
+// once every level's keypoints are visible, and puts the counter back to 0.  The lists hold a few
+// scans (isolated re-detections); two dependent launches fewer per cascade round, each of which
+// waits for room beside the chain engines.
+// After a level workgroup of grid scan index gi: the last of its kL levels to arrive finishes the scan.
+__device__ __forceinline__ void orb_levels_tail(const Args& a, int gi) {
+  __shared__ int s_last;
+  __threadfence();  // release: this thread's keypoints and level count
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int last = atomicAdd(a.arrive + gi, 1) == kL - 1;
+    if (last) atomicExch(a.arrive + gi, 0);
+    s_last = last;
+  }
+  __syncthreads();
+  if (s_last) {
+    __threadfence();  // acquire: the other levels' keypoints
+    orb_finish_body(a, gi);
+    __syncthreads();  // the concatenated keypoints and their count
+    orb_desc_body<kSelThreads / 32>(a, gi, 0, 1);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSelThreads, 4) void k_orb_redetect(Args a) {
+  const int S = gridDim.x / kL;
+  const int l = blockIdx.x / S, cnt = *a.scount;
+  for (int i = blockIdx.x % S; i < cnt; i += S) {
+    orb_select_body(a, i, l);
+    orb_levels_tail(a, i);
+  }
+}
+
+// The first detection's select, finish and descriptors in one launch (k_orb_select's grid; the
+// scan's last level workgroup finishes it, as in k_orb_redetect).
+__global__ __launch_bounds__(kSelThreads, 4) void k_orb_detect(Args a) {
+  const int S = gridDim.x / kL;
+  orb_select_body(a, blockIdx.x % S, blockIdx.x / S);
+  orb_levels_tail(a, blockIdx.x % S);
 }
 
 // ------------------------------------------------------------------ matching (a10) + records
@@ -1370,6 +1416,7 @@ struct PairArgs {
   int* stats;         // [npairs][8]: ok, -, nq, matches, good, iterations, termination, nt
   double* T;          // [npairs][7]
   const int* pcount;  // device count of pairs in use (null: npairs); the grid's other pairs exit
+  int* arrive;        // [npairs] k_orb_pairs: train-block workgroups of the slot arrived (0 between launches)
 };
 
 __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
@@ -1629,10 +1676,19 @@ __device__ void pair_eval(LmSh& sh, const double* rec, int n) {
 
 // Batch outputs: scan 0 is the first frame (stats -1, its keypoint count), scan k > 0 pair
 // (k-1, k) with its re-detection flag.
-__global__ __launch_bounds__(256) void k_orb_out(int* outS, double* outT, const int* stats, const double* T,
-                                                 const int* redet, const int* nkp0, int n_scans) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= n_scans) return;
+struct OutArgs {
+  int* outS; double* outT;
+  const int* stats; const double* T; const int* redet; const int* nkp0;
+  int n_scans;
+};
+
+__device__ __forceinline__ void orb_out_at(const OutArgs& a, int k) {
+  int* outS = a.outS;
+  double* outT = a.outT;
+  const int* stats = a.stats;
+  const double* T = a.T;
+  const int* redet = a.redet;
+  const int* nkp0 = a.nkp0;
   int* o = outS + (size_t)k * 8;
   double* t = outT + (size_t)k * 7;
   if (k == 0) {
@@ -1643,6 +1699,11 @@ __global__ __launch_bounds__(256) void k_orb_out(int* outS, double* outT, const 
   for (int e = 0; e < 8; e++) o[e] = stats[(size_t)(k - 1) * 8 + e];
   if (redet[k - 1]) o[1] = 1;
   for (int e = 0; e < 7; e++) t[e] = T[(size_t)(k - 1) * 7 + e];
+}
+
+__global__ __launch_bounds__(256) void k_orb_out(OutArgs a) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < a.n_scans) orb_out_at(a, k);
 }
 
 // ---- the re-detection rule of detectfeatures decided on the device (lislam_batch_intensity_odometry)
@@ -1670,7 +1731,8 @@ struct CascadeArgs {
 };
 constexpr int kCascadeMax = 8192;
 
-__global__ __launch_bounds__(256) void k_orb_decide(CascadeArgs cs, int mode) {
+// (256 threads: the last k_orb_lm workgroup of a launch, or k_orb_tail)
+__device__ __forceinline__ void orb_decide_body(const CascadeArgs& cs, int mode) {
   __shared__ int8_t ok1[kCascadeMax], ps[kCascadeMax], c2[kCascadeMax], h2[kCascadeMax];
   const int n = cs.n;
   for (int k = threadIdx.x; k < n; k += 256) {
@@ -1727,6 +1789,24 @@ __global__ __launch_bounds__(256) void k_orb_decide(CascadeArgs cs, int mode) {
   }
 }
 
+
+// What the last k_orb_lm workgroup of a launch runs once every pair's solve is done (kind 0:
+// nothing; 1: the cascade decision of `mode`; 2: the batch outputs): the launch that would follow
+// the solve on the stream, folded into it.
+struct LmTail {
+  int kind = 0, mode = 0;
+  int* arrive = nullptr;  // one counter (0 between launches)
+  CascadeArgs cs{};
+  OutArgs out{};
+};
+
+// the kind-1 / kind-2 launch on its own (a launch with no pairs)
+__global__ __launch_bounds__(256) void k_orb_tail(LmTail tl) {
+  if (tl.kind == 1) orb_decide_body(tl.cs, tl.mode);
+  if (tl.kind == 2)
+    for (int k = threadIdx.x; k < tl.out.n_scans; k += 256) orb_out_at(tl.out, k);
+}
+
 __device__ __forceinline__ void orb_lm_body(const PairArgs& p, int max_it, int pi) {
   __shared__ LmSh sh;
   const int pr = p.pslot ? p.pslot[pi] : pi;
@@ -1775,10 +1855,58 @@ __device__ __forceinline__ void orb_lm_body(const PairArgs& p, int max_it, int p
   }
 }
 
-__global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it) {
+__global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it, LmTail tl) {
+  static_assert(kLmThreads == 256, "the tail bodies are written for 256 threads");
   const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
   for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
     orb_lm_body(p, max_it, pi);
+    __syncthreads();
+  }
+  if (tl.kind == 0) return;
+  // the last workgroup to arrive (told by the value its add returns) runs the tail once every
+  // workgroup's stats and poses are visible
+  __shared__ int s_last;
+  __threadfence();  // release: this thread's stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int last = atomicAdd(tl.arrive, 1) == (int)gridDim.x - 1;
+    if (last) atomicExch(tl.arrive, 0);
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire
+  if (tl.kind == 1) orb_decide_body(tl.cs, tl.mode);
+  if (tl.kind == 2)
+    for (int k = threadIdx.x; k < tl.out.n_scans; k += 256) orb_out_at(tl.out, k);
+}
+
+// A pair's distances and selection in one launch (the two kernels above, unchanged): the last of a
+// pair's train-block workgroups to arrive — an agent-scope counter per buffer slot, told by the
+// value its add returns — runs the selection over the pair's best[] row once every block's
+// atomicMin is visible, and puts the counter back to 0 for the next launch.  One dependent launch
+// fewer per attempt, each of which waits for room beside the chain engines.  (The solve stays a
+// launch of its own: its 256-VGPR thread-0 step would cap the distance blocks at one workgroup per
+// CU.)
+__global__ __launch_bounds__(64 * kXmWaves) void k_orb_pairs(PairArgs p) {
+  static_assert(64 * kXmWaves == kPairThreads, "k_orb_pairs workgroup");
+  __shared__ int s_last;
+  const int cnt = p.pcount ? *p.pcount : (int)gridDim.x;
+  for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
+    orb_xdist_mfma_body(p, pi);
+    const int pr = p.pslot ? p.pslot[pi] : pi;
+    __threadfence();  // release: this thread's atomicMin
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int last = atomicAdd(p.arrive + pr, 1) == (int)gridDim.y - 1;
+      if (last) atomicExch(p.arrive + pr, 0);
+      s_last = last;
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();  // acquire: the other blocks' atomicMins (L2), before the row is read
+      orb_match_body(p, pi);
+    }
     __syncthreads();
   }
 }
@@ -1846,7 +1974,7 @@ struct OrbEngine {
   int xs = 0, ys = 0;
   uint8_t* mpyr = nullptr;
   uint8_t *pyr = nullptr, *blur = nullptr, *nms = nullptr, *desc = nullptr;
-  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr;
+  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr, *arrive = nullptr;
   float *cresp = nullptr, *lkp = nullptr, *kp = nullptr;
   float4* p3d = nullptr;
   ~OrbEngine() {
@@ -1870,6 +1998,7 @@ struct OrbEngine {
     a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.nms = nms; a.cand = cand; a.cresp = cresp;
     a.lkp = lkp; a.lcnt = lcnt; a.kp = kp; a.p3d = p3d; a.desc = desc; a.nkp = nkp; a.overflow = overflow;
     a.smap = nullptr;
+    a.arrive = arrive;
     return a;
   }
 };
@@ -1997,7 +2126,9 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   ORC(e->alloc(&e->nkp, S));
   ORC(e->alloc(&e->overflow, 1));
   ORC(e->alloc(&e->smap, S));
+  ORC(e->alloc(&e->arrive, S));
   OCHK(c, hipMemsetAsync(e->overflow, 0, 4, st));
+  OCHK(c, hipMemsetAsync(e->arrive, 0, (size_t)S * 4, st));
   if (mask) {  // mask pyramid, once
     uint8_t* dmask = nullptr;
     ORC(e->alloc(&dmask, (size_t)H * W));
@@ -2074,13 +2205,21 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     TimedScope t(c, kT_orb_roiblur);
     hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
-  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
-  if (!fused) {
-    TimedScope t(c, kT_orb_blur);
-    hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
+  // select + finish + descriptors in one launch (k_orb_detect) once the blurred copy exists (the
+  // fused pyramid's k_orb_roiblur above); LISLAM_ORB_DETECT_SPLIT=1: the three kernels (A/B)
+  static const bool split = getenv("LISLAM_ORB_DETECT_SPLIT") && atoi(getenv("LISLAM_ORB_DETECT_SPLIT")) == 1;
+  if (fused && !split) {
+    TimedScope t(c, kT_orb_select);
+    hipLaunchKernelGGL(k_orb_detect, dim3(n * kL), dim3(kSelThreads), 0, st, a);
+  } else {
+    { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
+    { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
+    if (!fused) {
+      TimedScope t(c, kT_orb_blur);
+      hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
+    }
+    { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), n), dim3(256), 0, st, a); }
   }
-  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), n), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -2107,9 +2246,16 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const Geom& g = e->g;
   // kListSlots grid scan indices stride over the list: the count is only known on the device
   const int ns = std::min(nmax, kListSlots);
-  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select_list, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
-  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
-  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
+  // one launch (k_orb_redetect); LISLAM_ORB_REDETECT_SPLIT=1: its three kernels (A/B)
+  static const bool split = getenv("LISLAM_ORB_REDETECT_SPLIT") && atoi(getenv("LISLAM_ORB_REDETECT_SPLIT")) == 1;
+  if (!split) {
+    TimedScope t(c, kT_orb_select);
+    hipLaunchKernelGGL(k_orb_redetect, dim3(ns * kL), dim3(kSelThreads), 0, st, a);
+  } else {
+    { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select_list, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
+    { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
+    { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
+  }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -2120,7 +2266,8 @@ struct PairBufs {
   int maxp = 0, qcap = 0;
   std::vector<void*> allocs;
   int *args = nullptr;  // [3][maxp] staged per launch: query scans, train scans, slots
-  int *mscratch = nullptr, *mout = nullptr, *kind = nullptr, *stats = nullptr, *redet = nullptr;
+  int *mscratch = nullptr, *mout = nullptr, *kind = nullptr, *stats = nullptr, *redet = nullptr, *arrive = nullptr;
+  int* tail_arrive = nullptr;  // k_orb_lm's workgroup counter for its tail (0 between launches)
   double *rec = nullptr, *T = nullptr;
   ~PairBufs() {
     for (void* p : allocs) (void)hipFree(p);
@@ -2142,6 +2289,10 @@ struct PairBufs {
     // the best[] rows start at the "no match" sentinel; k_orb_match puts back each row it consumed
     if (hipMemset(mscratch, 0x7f, (size_t)maxp * qcap * sizeof(int)) != hipSuccess)
       return ofail(ctx, LISLAM_ERR_DEVICE, "hipMemset of the match rows failed");
+    ORC(alloc(&arrive, maxp + 1));  // k_orb_pairs' arrival counters and k_orb_lm's, 0 between launches
+    tail_arrive = arrive + maxp;
+    if (hipMemset(arrive, 0, (size_t)(maxp + 1) * sizeof(int)) != hipSuccess)
+      return ofail(ctx, LISLAM_ERR_DEVICE, "hipMemset of the pair arrival counters failed");
     if (raw) ORC(alloc(&mout, (size_t)maxp * qcap * 3));
     ORC(alloc(&kind, (size_t)maxp * qcap));
     ORC(alloc(&stats, (size_t)maxp * 8));
@@ -2156,11 +2307,22 @@ struct PairBufs {
 // dlist / dcount: the lists are already on the device (dlist = [3][n] query scans | train scans |
 // slots, dcount = how many are in use; n is the grid's upper bound and the lists' stride), decided
 // by an earlier kernel.
+// tail (with lm): what the stream runs next — the cascade decision or the batch outputs — run by
+// the solve launch's last workgroup instead of a launch of its own.
 int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int* qs, const int* ts, int n, double frac,
               PairBufs& pb, int p0, bool lm, const int* slots = nullptr, const int* dlist = nullptr,
-              const int* dcount = nullptr) {
+              const int* dcount = nullptr, const LmTail* tail = nullptr) {
   hipStream_t st = c->stream;
-  if (n <= 0) return LISLAM_OK;
+  LmTail tl;
+  if (tail) {
+    tl = *tail;
+    tl.arrive = pb.tail_arrive;
+  }
+  if (n <= 0) {
+    if (tl.kind) hipLaunchKernelGGL(k_orb_tail, dim3(1), dim3(256), 0, st, tl);
+    OCHK(c, hipGetLastError());
+    return LISLAM_OK;
+  }
   if (qe->g.cap > pb.qcap || (!slots && !dlist && p0 + n > pb.maxp) || n > pb.maxp)
     return ofail(c, LISLAM_ERR_CAPACITY, "pair buffers too small");
   PairArgs p;
@@ -2193,12 +2355,25 @@ int run_pairs(lislam_ctx* c, const OrbEngine* qe, const OrbEngine* te, const int
   p.kind = pb.kind + (size_t)b0 * pb.qcap;
   p.stats = pb.stats + b0 * 8;
   p.T = pb.T + b0 * 7;
+  p.arrive = pb.arrive + b0;
   {
+    // one launch (k_orb_pairs); LISLAM_ORB_PAIR_SPLIT=1: the distance and selection kernels one
+    // after the other (A/B)
+    static const bool split = getenv("LISLAM_ORB_PAIR_SPLIT") && atoi(getenv("LISLAM_ORB_PAIR_SPLIT")) == 1;
     TimedScope t(c, kT_orb_match);
-    hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
-    hipLaunchKernelGGL(k_orb_match, dim3(gp), dim3(kPairThreads), 0, st, p);
+    if (!split) {
+      hipLaunchKernelGGL(k_orb_pairs, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
+    } else {
+      hipLaunchKernelGGL(k_orb_xdist_mfma, dim3(gp, cdiv(te->g.cap, kXmTrains)), dim3(64 * kXmWaves), 0, st, p);
+      hipLaunchKernelGGL(k_orb_match, dim3(gp), dim3(kPairThreads), 0, st, p);
+    }
   }
-  if (lm) { TimedScope t(c, kT_orb_lm); hipLaunchKernelGGL(k_orb_lm, dim3(gp), dim3(kLmThreads), 0, st, p, 20); }
+  if (lm) {
+    TimedScope t(c, kT_orb_lm);
+    hipLaunchKernelGGL(k_orb_lm, dim3(gp), dim3(kLmThreads), 0, st, p, 20, tl);
+  } else if (tl.kind) {
+    hipLaunchKernelGGL(k_orb_tail, dim3(1), dim3(256), 0, st, tl);
+  }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -2372,8 +2547,8 @@ int batch_intensity_odometry(lislam_batch* b, OrbBatch* ob, int n_scans) {
   }
   // outputs: scan 0 = first frame; scan k = pair (k-1, k), whose final attempt sits in slot k-1
   OCHK(c, hipMemcpyAsync(ob->pb.redet, flag.data(), (size_t)std::max(np, 1) * 4, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_orb_out, dim3(cdiv(n_scans, 256)), dim3(256), 0, st, ob->outS, ob->outT, ob->pb.stats, ob->pb.T,
-                     ob->pb.redet, ob->e1->nkp, n_scans);
+  const OutArgs oa{ob->outS, ob->outT, ob->pb.stats, ob->pb.T, ob->pb.redet, ob->e1->nkp, n_scans};
+  hipLaunchKernelGGL(k_orb_out, dim3(cdiv(n_scans, 256)), dim3(256), 0, st, oa);
   OCHK(c, hipGetLastError());
   OCHK(c, hipStreamSynchronize(st));
   return LISLAM_OK;
@@ -2403,23 +2578,28 @@ int batch_intensity_odometry_dev(lislam_batch* b, OrbBatch* ob, int n_scans) {
   const int np = n_scans - 1;
   std::vector<int> qs(np), ts(np);
   for (int k = 1; k < n_scans; k++) { qs[k - 1] = k; ts[k - 1] = k - 1; }
-  ORC(run_pairs(c, ob->e1, ob->e1, qs.data(), ts.data(), np, 0.3, ob->pb, 0, true));
   CascadeArgs cs = ob->cs;
   cs.n = n_scans;
   cs.stats = ob->pb.stats;
-  hipLaunchKernelGGL(k_orb_decide, dim3(1), dim3(256), 0, st, cs, 0);
+  // each decision (k_orb_decide) and the outputs (k_orb_out) run in the last workgroup of the
+  // solve launch before them (LmTail)
+  LmTail tl;
+  tl.kind = 1;
+  tl.mode = 0;
+  tl.cs = cs;
+  ORC(run_pairs(c, ob->e1, ob->e1, qs.data(), ts.data(), np, 0.3, ob->pb, 0, true, nullptr, nullptr, nullptr, &tl));
   const int rounds = cascade_rounds();
   for (int r = 0; r < rounds; r++) {
     ORC(engine_select_from(ob->e2, ob->e1, img, trk, cs.e2list, cs.e2cnt, n_scans));
+    tl.mode = r + 1 < rounds ? 1 : 2;
     for (int g2 = r == 0 ? 1 : 0; g2 < 2; g2++)
       ORC(run_pairs(c, ob->e1, g2 ? ob->e2 : ob->e1, nullptr, nullptr, n_scans, 0.3, ob->pb, 0, true, nullptr,
-                    cs.plist + (size_t)g2 * 3 * n_scans, cs.pcnt + g2));
-    hipLaunchKernelGGL(k_orb_decide, dim3(1), dim3(256), 0, st, cs, r + 1 < rounds ? 1 : 2);
+                    cs.plist + (size_t)g2 * 3 * n_scans, cs.pcnt + g2, g2 == 1 ? &tl : nullptr));
   }
   ORC(engine_select_from(ob->e2, ob->e1, img, trk, cs.e2list, cs.e2cnt, n_scans));
-  ORC(run_pairs(c, ob->e2, ob->e2, nullptr, nullptr, n_scans, 0.2, ob->pb, 0, true, nullptr, cs.plist, cs.pcnt));
-  hipLaunchKernelGGL(k_orb_out, dim3(cdiv(n_scans, 256)), dim3(256), 0, st, ob->outS, ob->outT, ob->pb.stats, ob->pb.T,
-                     cs.redet, ob->e1->nkp, n_scans);
+  tl.kind = 2;
+  tl.out = OutArgs{ob->outS, ob->outT, ob->pb.stats, ob->pb.T, cs.redet, ob->e1->nkp, n_scans};
+  ORC(run_pairs(c, ob->e2, ob->e2, nullptr, nullptr, n_scans, 0.2, ob->pb, 0, true, nullptr, cs.plist, cs.pcnt, &tl));
   OCHK(c, hipGetLastError());
   OCHK(c, hipMemcpyAsync(ob->h_status, cs.status, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
   OCHK(c, hipEventRecord(ob->settled, st));

@@ -129,7 +129,8 @@ def test_batch_intensity_odometry_matches_tracker(pkg, oracle, ctx, frames):
 
 
 def test_batch_redetection_cascade_on_device(pkg, oracle, ctx, frames):
-    """The re-detection rule decided on the device (k_orb_decide, no host synchronization): runs of
+    """The re-detection rule decided on the device (orb_decide_body in the last k_orb_lm workgroup,
+    the re-detections as k_orb_redetect list launches; no host synchronization): runs of
     repeated frames make first attempts fail back to back, so a pair's previous set depends on the
     pair before it, over several decision passes (intensity_feature_tracker.cpp:631-687)."""
     scans, _, _ = frames
