@@ -155,12 +155,12 @@ __device__ __forceinline__ void wg_bitonic(uint64_t (&key)[kK], int P, uint64_t*
 #ifndef LISLAM_TI_WPE32
 #define LISLAM_TI_WPE32 4  // waves per SIMD the 32-keys-per-lane build is compiled for (4: 128 VGPRs)
 #endif
+// (the body of workgroup `bid` of a launch; xch / red: the workgroup's LDS, kW * 8 * 64 / 6 * kW)
 template <int kW, int kK>
-__global__ __launch_bounds__(64 * kW, kK >= 32 ? LISLAM_TI_WPE32 : 4) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+__device__ __forceinline__ void target_index_body(const OdomArgs& a, int bid, int per_scan, int w0, int w1, int w2,
+                                                  uint64_t* xch, float (*red)[kW]) {
   constexpr int kKeysPerLane = kK, kPer = 64 * kK;
-  __shared__ uint64_t xch[kW * 8 * 64];
-  __shared__ float red[6][kW];
-  const int s = blockIdx.x / per_scan, wi = blockIdx.x % per_scan;
+  const int s = bid / per_scan, wi = bid % per_scan;
   const int which = wi == 0 ? w0 : wi == 1 ? w1 : w2;
   const bool query = which >= 2;
   const TargetIndex& ix = (which & 1) ? a.idx_lf : a.idx_ls;
@@ -305,6 +305,25 @@ __global__ __launch_bounds__(64 * kW, kK >= 32 ? LISLAM_TI_WPE32 : 4) void k_tar
       shi[0] = shi[1] = shi[2] = -3.4e38f;
     }
   }
+}
+
+template <int kW, int kK>
+__global__ __launch_bounds__(64 * kW, kK >= 32 ? LISLAM_TI_WPE32 : 4) void k_target_index(OdomArgs a, int per_scan, int w0, int w1, int w2) {
+  __shared__ uint64_t xch[kW * 8 * 64];
+  __shared__ float red[6][kW];
+  target_index_body<kW, kK>(a, blockIdx.x, per_scan, w0, w1, w2, xch, red);
+}
+
+// Both target-index launches of a batch in one (round 6): workgroups [0, n_scans) index the
+// less-flat clouds (32 keys per lane), the rest the less-sharp and query clouds (16 keys per lane),
+// one LDS allocation shared by both.  One dependent launch fewer per extraction.
+__global__ __launch_bounds__(512, LISLAM_TI_WPE32) void k_target_index_all(OdomArgs a, int n_scans) {
+  __shared__ uint64_t xch[8 * 8 * 64];
+  __shared__ float red[6][8];
+  if ((int)blockIdx.x < n_scans)
+    target_index_body<8, 32>(a, blockIdx.x, 1, 1, 1, 1, xch, red);
+  else
+    target_index_body<8, 16>(a, blockIdx.x - n_scans, 3, 0, 2, 3, xch, red);
 }
 
 // ------------------------------------------------------------------ association helpers
@@ -3518,6 +3537,12 @@ void launch_target_index(const OdomArgs& a, int n_scans, hipStream_t st) {
   // less-flat clouds: 8 waves of 32 keys per lane (16384 keys in registers); less-sharp + query
   // clouds: 8 waves of 16 (8192 keys).  Workgroups of 512 threads at <= 128 VGPRs and 32 KiB of LDS
   // run beside the chain engine's item workgroups (2 waves per SIMD at 128 VGPRs).
+  // One launch (k_target_index_all); LISLAM_TI_SPLIT=1: the two launches (A/B).
+  static const bool split = getenv("LISLAM_TI_SPLIT") && atoi(getenv("LISLAM_TI_SPLIT")) == 1;
+  if (!split) {
+    hipLaunchKernelGGL(k_target_index_all, dim3(4 * n_scans), dim3(512), 0, st, a, n_scans);
+    return;
+  }
   hipLaunchKernelGGL((k_target_index<8, 32>), dim3(n_scans), dim3(512), 0, st, a, 1, 1, 1, 1);
   hipLaunchKernelGGL((k_target_index<8, 16>), dim3(3 * n_scans), dim3(512), 0, st, a, 3, 0, 2, 3);
 }

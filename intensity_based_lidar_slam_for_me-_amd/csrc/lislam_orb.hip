@@ -784,6 +784,31 @@ __global__ __launch_bounds__(256) void k_orb_roiblur(Args a) {
 }
 
 // ------------------------------------------------------------------ selection (1 WG per scan, level)
+// The counter hand-off of several workgroups to the last of them (in-launch fold of a dependent
+// launch): every wave drains its stores, lane 0 releases them at agent scope once per workgroup
+// (buffer_wbl2: the other XCDs' L2s) and adds to the counter; the workgroup whose add returns
+// total - 1 resets the counter for the next launch, acquires once (this CU's L1) and reads the
+// others' bytes with plain loads after the barrier.  Returns that verdict, uniform over the
+// workgroup.  (A __threadfence() per thread instead costs every wave a write-back and an
+// invalidate: the folds measured 2-3x slower than the launches they replaced.)
+__device__ __forceinline__ bool wg_arrive_last(int* cnt, int total, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag;
+}
+
 struct SelShared {
   int wsum[kSelThreads / 64];
   int hist[256];
@@ -1363,16 +1388,7 @@ __global__ __launch_bounds__(256) void k_orb_desc(Args a) {
 // After a level workgroup of grid scan index gi: the last of its kL levels to arrive finishes the scan.
 __device__ __forceinline__ void orb_levels_tail(const Args& a, int gi) {
   __shared__ int s_last;
-  __threadfence();  // release: this thread's keypoints and level count
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int last = atomicAdd(a.arrive + gi, 1) == kL - 1;
-    if (last) atomicExch(a.arrive + gi, 0);
-    s_last = last;
-  }
-  __syncthreads();
-  if (s_last) {
-    __threadfence();  // acquire: the other levels' keypoints
+  if (wg_arrive_last(a.arrive + gi, kL, &s_last)) {  // the other levels' keypoints and counts
     orb_finish_body(a, gi);
     __syncthreads();  // the concatenated keypoints and their count
     orb_desc_body<kSelThreads / 32>(a, gi, 0, 1);
@@ -1866,16 +1882,7 @@ __global__ __launch_bounds__(kLmThreads) void k_orb_lm(PairArgs p, int max_it, L
   // the last workgroup to arrive (told by the value its add returns) runs the tail once every
   // workgroup's stats and poses are visible
   __shared__ int s_last;
-  __threadfence();  // release: this thread's stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int last = atomicAdd(tl.arrive, 1) == (int)gridDim.x - 1;
-    if (last) atomicExch(tl.arrive, 0);
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // acquire
+  if (!wg_arrive_last(tl.arrive, (int)gridDim.x, &s_last)) return;  // every pair's stats and pose
   if (tl.kind == 1) orb_decide_body(tl.cs, tl.mode);
   if (tl.kind == 2)
     for (int k = threadIdx.x; k < tl.out.n_scans; k += 256) orb_out_at(tl.out, k);
@@ -1895,18 +1902,8 @@ __global__ __launch_bounds__(64 * kXmWaves) void k_orb_pairs(PairArgs p) {
   for (int pi = blockIdx.x; pi < cnt; pi += gridDim.x) {
     orb_xdist_mfma_body(p, pi);
     const int pr = p.pslot ? p.pslot[pi] : pi;
-    __threadfence();  // release: this thread's atomicMin
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int last = atomicAdd(p.arrive + pr, 1) == (int)gridDim.y - 1;
-      if (last) atomicExch(p.arrive + pr, 0);
-      s_last = last;
-    }
-    __syncthreads();
-    if (s_last) {
-      __threadfence();  // acquire: the other blocks' atomicMins (L2), before the row is read
+    if (wg_arrive_last(p.arrive + pr, (int)gridDim.y, &s_last))  // every block's atomicMin
       orb_match_body(p, pi);
-    }
     __syncthreads();
   }
 }
@@ -2205,10 +2202,12 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     TimedScope t(c, kT_orb_roiblur);
     hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
-  // select + finish + descriptors in one launch (k_orb_detect) once the blurred copy exists (the
-  // fused pyramid's k_orb_roiblur above); LISLAM_ORB_DETECT_SPLIT=1: the three kernels (A/B)
-  static const bool split = getenv("LISLAM_ORB_DETECT_SPLIT") && atoi(getenv("LISLAM_ORB_DETECT_SPLIT")) == 1;
-  if (fused && !split) {
+  // select + finish + descriptors in one launch (k_orb_detect, LISLAM_ORB_DETECT_FUSED=1) once the
+  // blurred copy exists (the fused pyramid's k_orb_roiblur above).  Not the default: the scan's
+  // last level workgroup computes all its descriptors alone, 1.68 vs 1.01 ms per step isolated for
+  // the same pipelined rate (profiles/r06p_orb_fuse_ab.txt).
+  static const bool fold = getenv("LISLAM_ORB_DETECT_FUSED") && atoi(getenv("LISLAM_ORB_DETECT_FUSED")) == 1;
+  if (fused && fold) {
     TimedScope t(c, kT_orb_select);
     hipLaunchKernelGGL(k_orb_detect, dim3(n * kL), dim3(kSelThreads), 0, st, a);
   } else {
@@ -2246,9 +2245,10 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const Geom& g = e->g;
   // kListSlots grid scan indices stride over the list: the count is only known on the device
   const int ns = std::min(nmax, kListSlots);
-  // one launch (k_orb_redetect); LISLAM_ORB_REDETECT_SPLIT=1: its three kernels (A/B)
-  static const bool split = getenv("LISLAM_ORB_REDETECT_SPLIT") && atoi(getenv("LISLAM_ORB_REDETECT_SPLIT")) == 1;
-  if (!split) {
+  // one launch (k_orb_redetect, LISLAM_ORB_DETECT_FUSED=1, as k_orb_detect above) or its three
+  // kernels (the default)
+  static const bool fold = getenv("LISLAM_ORB_DETECT_FUSED") && atoi(getenv("LISLAM_ORB_DETECT_FUSED")) == 1;
+  if (fold) {
     TimedScope t(c, kT_orb_select);
     hipLaunchKernelGGL(k_orb_redetect, dim3(ns * kL), dim3(kSelThreads), 0, st, a);
   } else {
