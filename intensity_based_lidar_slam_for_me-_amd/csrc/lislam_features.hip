@@ -233,16 +233,30 @@ __global__ __launch_bounds__(64 * kFrontWaves) void k_front_scatter(FeatureArgs 
 #ifdef LISLAM_PHASE_PROF
 __device__ unsigned long long g_phase_cycles[16];
 __device__ unsigned long long* g_line_log;  // k_scan_lines per-wave timeline (lislam_debug_line_log)
-#define PHASE_BEGIN uint64_t t_ph = __builtin_readcyclecounter()
+// Each phase's cycles accumulate in the wave's registers; the wave adds them to the global counters
+// once, when the line is done (PHASE_FLUSH), so the profiler's atomics do not sit inside the phases
+// they measure (round 6: adding them at every phase boundary made the first vector-memory wait
+// after them absorb their L2 contention).
+#define PHASE_BEGIN                                 \
+  uint64_t t_ph = __builtin_readcyclecounter();     \
+  uint64_t ph_acc[16];                              \
+  _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) ph_acc[i_] = 0
 #define PHASE(i)                                                     \
   do {                                                               \
     const uint64_t now_ = __builtin_readcyclecounter();              \
-    if (lane_id() == 0) atomicAdd(&g_phase_cycles[i], now_ - t_ph);  \
+    ph_acc[i] += now_ - t_ph;                                        \
     t_ph = now_;                                                     \
+  } while (0)
+#define PHASE_FLUSH                                                              \
+  do {                                                                           \
+    if (lane_id() == 0)                                                          \
+      _Pragma("unroll") for (int i_ = 0; i_ < 16; i_++) if (ph_acc[i_])          \
+        atomicAdd(&g_phase_cycles[i_], ph_acc[i_]);                              \
   } while (0)
 #else
 #define PHASE_BEGIN
 #define PHASE(i)
+#define PHASE_FLUSH
 #endif
 // LDS capacities of the fast path; longer lines run the same code on global scratch.
 constexpr int kLineCap = 2048;
@@ -1026,6 +1040,7 @@ __device__ __forceinline__ void line_body(const FeatureArgs& a, int s, int line,
     int* c = a.line_counts + ((size_t)s * H + line) * 4;
     c[0] = cnt.sharp; c[1] = cnt.less_sharp; c[2] = cnt.flat; c[3] = cnt.less_flat;
   }
+  PHASE_FLUSH;
 }
 
 // ------------------------------------------------------------------ register-resident line
@@ -1557,6 +1572,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
     int* c = a.line_counts + ((size_t)s * H + line) * 4;
     c[0] = n_sharp; c[1] = n_lsharp; c[2] = n_flat; c[3] = n_lflat;
   }
+  PHASE_FLUSH;
 }
 
 // kS: register slots per lane of the fast path (lines up to 64 kS points); longer lines (input
