@@ -1418,6 +1418,7 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
         if (packed) {
           wave_sync<true>();
           introsort_order_lds<kS>(vel, [](uint32_t e) { return e >> 11; }, nlist, vidx, vidx + 32 * kS + 1);
+          PHASE(12);
           // std::__final_insertion_sort: the loop leaves blocks of at most 16 elements (or
           // heap-sorted ranges) in key order, and the insertion sort stably sorts each block.  An
           // element's final position is therefore its position, minus the greater keys among the

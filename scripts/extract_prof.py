@@ -11,6 +11,8 @@ sys.path.insert(0, _R)
 import __graft_entry__ as g  # noqa: E402
 
 pkg = g.package()
+if os.environ.get("LISLAM_ALT_LIB"):  # a developer variant of the library (A/B)
+    pkg.native.load(os.environ["LISLAM_ALT_LIB"])
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 H = int(sys.argv[3]) if len(sys.argv) > 3 else 64

@@ -17,7 +17,7 @@ import __graft_entry__ as g  # noqa: E402
 OUT = os.environ.get("LISLAM_PROF_LIB", os.path.join(ROOT, "scripts", "_prof", "liblislam_prof.so"))
 PHASES = ["curv+links", "seg sort", "sharp walk", "flat walk", "lessflat list", "label/feature writes",
           "voxel keys", "voxel sort", "voxel centroids", "voxel numbering sort", "voxel numbering",
-          "voxel introsort order"]
+          "voxel final positions + permutation", "voxel introsort loop"]
 
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
