@@ -142,7 +142,6 @@ struct Args {
   int* overflow;          // [1]
   const int* smap;        // scan of each grid scan index (null: identity from the slot base)
   const int* scount;      // device count of grid scan indices in use (null: all); the rest exit
-  int* arrive;            // k_orb_redetect: level workgroups of each list entry arrived (0 between launches)
 };
 
 __device__ __forceinline__ int reflect101(int p, int len) {
@@ -1379,40 +1378,6 @@ __global__ __launch_bounds__(256) void k_orb_desc(Args a) {
   for (int gi = blockIdx.y; gi < cnt; gi += gridDim.y) orb_desc_body<8>(a, gi, blockIdx.x, gridDim.x);
 }
 
-// A re-detection (k_orb_select_list, k_orb_finish, k_orb_desc of a device list) in one launch: the
-// last of an entry's kL level workgroups to arrive (an agent-scope counter per list entry, told by
-// the value its add returns) concatenates the levels and computes all the entry's descriptors,
-// once every level's keypoints are visible, and puts the counter back to 0.  The lists hold a few
-// scans (isolated re-detections); two dependent launches fewer per cascade round, each of which
-// waits for room beside the chain engines.
-// After a level workgroup of grid scan index gi: the last of its kL levels to arrive finishes the scan.
-__device__ __forceinline__ void orb_levels_tail(const Args& a, int gi) {
-  __shared__ int s_last;
-  if (wg_arrive_last(a.arrive + gi, kL, &s_last)) {  // the other levels' keypoints and counts
-    orb_finish_body(a, gi);
-    __syncthreads();  // the concatenated keypoints and their count
-    orb_desc_body<kSelThreads / 32>(a, gi, 0, 1);
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kSelThreads, 4) void k_orb_redetect(Args a) {
-  const int S = gridDim.x / kL;
-  const int l = blockIdx.x / S, cnt = *a.scount;
-  for (int i = blockIdx.x % S; i < cnt; i += S) {
-    orb_select_body(a, i, l);
-    orb_levels_tail(a, i);
-  }
-}
-
-// The first detection's select, finish and descriptors in one launch (k_orb_select's grid; the
-// scan's last level workgroup finishes it, as in k_orb_redetect).
-__global__ __launch_bounds__(kSelThreads, 4) void k_orb_detect(Args a) {
-  const int S = gridDim.x / kL;
-  orb_select_body(a, blockIdx.x % S, blockIdx.x / S);
-  orb_levels_tail(a, blockIdx.x % S);
-}
-
 // ------------------------------------------------------------------ matching (a10) + records
 struct PairArgs {
   int npairs;
@@ -1971,7 +1936,7 @@ struct OrbEngine {
   int xs = 0, ys = 0;
   uint8_t* mpyr = nullptr;
   uint8_t *pyr = nullptr, *blur = nullptr, *nms = nullptr, *desc = nullptr;
-  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr, *arrive = nullptr;
+  int *cand = nullptr, *lcnt = nullptr, *nkp = nullptr, *overflow = nullptr, *smap = nullptr;
   float *cresp = nullptr, *lkp = nullptr, *kp = nullptr;
   float4* p3d = nullptr;
   ~OrbEngine() {
@@ -1995,7 +1960,6 @@ struct OrbEngine {
     a.pyr = pyr; a.blur = blur; a.mpyr = mpyr; a.nms = nms; a.cand = cand; a.cresp = cresp;
     a.lkp = lkp; a.lcnt = lcnt; a.kp = kp; a.p3d = p3d; a.desc = desc; a.nkp = nkp; a.overflow = overflow;
     a.smap = nullptr;
-    a.arrive = arrive;
     return a;
   }
 };
@@ -2123,9 +2087,7 @@ int engine_init(OrbEngine* e, lislam_ctx* c, int H, int W, int max_scans, int nf
   ORC(e->alloc(&e->nkp, S));
   ORC(e->alloc(&e->overflow, 1));
   ORC(e->alloc(&e->smap, S));
-  ORC(e->alloc(&e->arrive, S));
   OCHK(c, hipMemsetAsync(e->overflow, 0, 4, st));
-  OCHK(c, hipMemsetAsync(e->arrive, 0, (size_t)S * 4, st));
   if (mask) {  // mask pyramid, once
     uint8_t* dmask = nullptr;
     ORC(e->alloc(&dmask, (size_t)H * W));
@@ -2202,23 +2164,13 @@ int engine_detect_slots(OrbEngine* e, const uint8_t* d_img, const float4* d_trac
     TimedScope t(c, kT_orb_roiblur);
     hipLaunchKernelGGL(k_orb_roiblur, dim3(g.rband[kL], n), dim3(256), (size_t)(kRoiBand + 6) * g.stride[0], st, a);
   }
-  // select + finish + descriptors in one launch (k_orb_detect, LISLAM_ORB_DETECT_FUSED=1) once the
-  // blurred copy exists (the fused pyramid's k_orb_roiblur above).  Not the default: the scan's
-  // last level workgroup computes all its descriptors alone, 1.68 vs 1.01 ms per step isolated for
-  // the same pipelined rate (profiles/r06p_orb_fuse_ab.txt).
-  static const bool fold = getenv("LISLAM_ORB_DETECT_FUSED") && atoi(getenv("LISLAM_ORB_DETECT_FUSED")) == 1;
-  if (fused && fold) {
-    TimedScope t(c, kT_orb_select);
-    hipLaunchKernelGGL(k_orb_detect, dim3(n * kL), dim3(kSelThreads), 0, st, a);
-  } else {
-    { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
-    { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
-    if (!fused) {
-      TimedScope t(c, kT_orb_blur);
-      hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
-    }
-    { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), n), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select, dim3(n * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(n), dim3(256), 0, st, a); }
+  if (!fused) {
+    TimedScope t(c, kT_orb_blur);
+    hipLaunchKernelGGL(k_orb_blur, dim3(g.bband[kL], n), dim3(256), (size_t)(kBlurBand + 6) * g.stride[0], st, a);
   }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), n), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }
@@ -2245,17 +2197,9 @@ int engine_select_from(OrbEngine* e, const OrbEngine* src, const uint8_t* d_img,
   const Geom& g = e->g;
   // kListSlots grid scan indices stride over the list: the count is only known on the device
   const int ns = std::min(nmax, kListSlots);
-  // one launch (k_orb_redetect, LISLAM_ORB_DETECT_FUSED=1, as k_orb_detect above) or its three
-  // kernels (the default)
-  static const bool fold = getenv("LISLAM_ORB_DETECT_FUSED") && atoi(getenv("LISLAM_ORB_DETECT_FUSED")) == 1;
-  if (fold) {
-    TimedScope t(c, kT_orb_select);
-    hipLaunchKernelGGL(k_orb_redetect, dim3(ns * kL), dim3(kSelThreads), 0, st, a);
-  } else {
-    { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select_list, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
-    { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
-    { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
-  }
+  { TimedScope t(c, kT_orb_select); hipLaunchKernelGGL(k_orb_select_list, dim3(ns * kL), dim3(kSelThreads), 0, st, a); }
+  { TimedScope t(c, kT_orb_finish); hipLaunchKernelGGL(k_orb_finish, dim3(ns), dim3(256), 0, st, a); }
+  { TimedScope t(c, kT_orb_desc); hipLaunchKernelGGL(k_orb_desc, dim3(cdiv(g.cap, kDescChunk), ns), dim3(256), 0, st, a); }
   OCHK(c, hipGetLastError());
   return LISLAM_OK;
 }

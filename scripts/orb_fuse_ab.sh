@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: the ORB launch folds (k_orb_pairs, k_orb_detect, k_orb_redetect, the solve's tail) against the split
-# launches (LISLAM_ORB_PAIR_SPLIT=1 LISLAM_TI_SPLIT=1; the select folds are opt-in: LISLAM_ORB_DETECT_FUSED=1), after the GPU tests.
+# Round 6: the ORB launch folds (k_orb_pairs, the solve's tail, k_target_index_all) against the split
+# launches (LISLAM_ORB_PAIR_SPLIT=1 LISLAM_TI_SPLIT=1), after the GPU tests.
 # Alternating driver-shape bench lines on one box.  Usage (GPU box): bash scripts/orb_fuse_ab.sh <tag> [reps]
 cd $GRAFT_REPO_ROOT
 D=gpurun_out/${1:-orbfuse}
