@@ -247,6 +247,10 @@ __device__ unsigned long long* g_line_log;  // k_scan_lines per-wave timeline (l
     ph_acc[i] += now_ - t_ph;                                        \
     t_ph = now_;                                                     \
   } while (0)
+#define PHASE_COUNT(i) \
+  do {                   \
+    if (lane_id() == 0) atomicAdd(&g_phase_cycles[i], 1ull); \
+  } while (0)
 #define PHASE_FLUSH                                                              \
   do {                                                                           \
     if (lane_id() == 0)                                                          \
@@ -256,6 +260,7 @@ __device__ unsigned long long* g_line_log;  // k_scan_lines per-wave timeline (l
 #else
 #define PHASE_BEGIN
 #define PHASE(i)
+#define PHASE_COUNT(i)
 #define PHASE_FLUSH
 #endif
 // LDS capacities of the fast path; longer lines run the same code on global scratch.
@@ -558,10 +563,12 @@ __device__ __forceinline__ void introsort_small(uint32_t* a, KeyOf kof, int F, i
   for (;;) {
     while (l - f > 16) {
       if (d == 0) {
+        PHASE_COUNT(13);
         heap_sort_reg(e, kof, f, l);
         break;
       }
       d--;
+      PHASE_COUNT(14);
       const int cut = partition_reg(e, kof, f, l);
       if (lane == sp) { sf = cut; sl = l; sd = d; }
       sp++;
@@ -650,11 +657,13 @@ __device__ __forceinline__ void introsort_order_lds(uint32_t* a, KeyOf kof, int 
         break;
       }
       if (d == 0) {
+        PHASE_COUNT(13);
         if (lane == 0) heap_sort_serial(a, kof, f, l - f);
         wave_sync<true>();
         break;
       }
       d--;
+      PHASE_COUNT(15);
       const int cut = partition_lds<kC>(a, kof, f, l, lidx, ridx);
       if (lane == sp) { sf = cut; sl = l; sd = d; }
       sp++;
@@ -1425,17 +1434,28 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
           // 15 positions before it, plus the smaller keys among the 15 after it (earlier blocks
           // hold no greater key and later blocks no smaller one, so the window needs no block
           // bounds).  The permutation is written back in place, then read in sorted order.
+          // The window reads past the list's ends land on sentinels (LineLds pads vel by 16 words
+          // on each side): 0 before it (no greater key), all ones after it (no smaller key), so
+          // the window needs no bounds tests either; keys are compared packed, against the
+          // element's own key rounded to the key field.
+          if (lane < 16) {
+            vel[lane - 16] = 0u;
+            vel[nlist + lane] = 0xffffffffu;
+          }
+          wave_sync<true>();
 #pragma unroll 1
           for (int t = 0; t < kS; t++) {  // final positions, into the (dead) partition scratch
             if (64 * t >= nlist) break;
             const int j = lane + 64 * t;
             if (j < nlist) {
-              const uint32_t k = vel[j] >> 11;
+              const uint32_t e = vel[j];
+              const uint32_t gt = e | 0x7ffu;   // packed > this: a greater key
+              const uint32_t lt = e & ~0x7ffu;  // packed < this: a smaller key
               int mv = 0;
 #pragma unroll
               for (int d = 1; d <= 15; d++) {
-                if (j - d >= 0 && (vel[j - d] >> 11) > k) mv--;
-                if (j + d < nlist && (vel[j + d] >> 11) < k) mv++;
+                mv -= (int)(vel[j - d] > gt);
+                mv += (int)(vel[j + d] < lt);
               }
               vidx[j] = (uint16_t)(j + mv);
             }
@@ -1594,7 +1614,7 @@ struct LineLds {
       float curv[64 * kS];
     } sel;
     struct {
-      uint32_t vel[64 * kS];
+      uint32_t vel[16 + 64 * kS + 16];  // the list at vel + 16; the final positions' sentinels either side
       uint16_t vidx[kIdx];
     } vox;
     P4 stage[64];
@@ -1620,7 +1640,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kS == 16 ? L
   const int* lo = a.line_off + (size_t)s * (a.H + 1);
   const int len = lo[line + 1] - lo[line];
   if (len <= 64 * kS)
-    line_body_reg<kS>(a, s, line, m.sel.ll, m.sel.lmask, m.sel.curv, m.stage, m.sel.ring, m.vox.vel, m.vox.vidx);
+    line_body_reg<kS>(a, s, line, m.sel.ll, m.sel.lmask, m.sel.curv, m.stage, m.sel.ring, m.vox.vel + 16, m.vox.vidx);
   else  // the pick lists are dead before the centroid windows are staged
     line_body<false>(a, s, line, nullptr, nullptr, nullptr, nullptr, nullptr, m.sel.ll, m.stage);
 #ifdef LISLAM_PHASE_PROF

@@ -17,7 +17,8 @@ import __graft_entry__ as g  # noqa: E402
 OUT = os.environ.get("LISLAM_PROF_LIB", os.path.join(ROOT, "scripts", "_prof", "liblislam_prof.so"))
 PHASES = ["curv+links", "seg sort", "sharp walk", "flat walk", "lessflat list", "label/feature writes",
           "voxel keys", "voxel sort", "voxel centroids", "voxel numbering sort", "voxel numbering",
-          "voxel final positions + permutation", "voxel introsort loop"]
+          "voxel final positions + permutation", "voxel introsort loop",
+          "(count) introsort heap-sort fallbacks", "(count) register partitions", "(count) LDS partitions"]
 
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
@@ -99,7 +100,7 @@ if sys.argv[1] == "lines":  # per-wave timeline of one k_scan_lines launch
             m = (lens >= lo_) & (lens < hi_)
             if m.any():
                 print(f"len [{lo_},{hi_}): {m.sum()} waves, mean {d[m].mean():.1f} us, max {d[m].max():.1f} us")
-        tot = sum(buf[i] for i in range(len(PHASES)))
+        tot = sum(buf[i] for i in range(min(len(PHASES), 13)))
         for i, nm in enumerate(PHASES):
             print(f"{nm:28s} {buf[i] / (S * H):10.0f} cycles/line {100.0 * buf[i] / max(tot, 1):5.1f}%")
         b.close()
