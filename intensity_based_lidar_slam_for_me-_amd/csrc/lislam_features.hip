@@ -1200,14 +1200,6 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       // dead curvature ring) and re-keys the window by sorted position, a refinement of the
       // curvature order, so the picks made so far stand.
       bool by_pos = a.ties != LISLAM_TIES_REFERENCE;  // true: no replay wanted / already done
-      auto tie_at = [&](uint32_t ok, uint64_t best) {
-        const uint32_t bc = (uint32_t)(best >> 32);
-        bool t = false;
-#pragma unroll
-        for (int u = 0; u < kW; u++)
-          if (((ok >> u) & 1u) && (uint32_t)(kw[u] >> 32) == bc && kw[u] != best) t = true;
-        return __ballot(t) != 0ull;
-      };
       auto replay = [&]() {
         const int n = ep - sp + 1;
         uint32_t* sel = reinterpret_cast<uint32_t*>(ring);
@@ -1239,12 +1231,38 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
           if ((ok >> u) & 1u) best = kw[u] < best ? kw[u] : best;
         return wave_min_u64(best);
       };
+      // The extreme key over the ok slots (as max_key / min_key) and, folded into the same
+      // reduction, tie_at's verdict: whether another ok candidate shares its curvature — the lanes
+      // whose own extreme has the wave's extreme curvature, and how many of their slots have it.
+      auto extreme_key_tie = [&](uint32_t ok, bool largest, bool& tie) {
+        uint64_t best = largest ? 0ull : ~0ull;
+#pragma unroll
+        for (int u = 0; u < kW; u++)
+          if ((ok >> u) & 1u) best = (largest ? kw[u] > best : kw[u] < best) ? kw[u] : best;
+        const uint32_t bh = (uint32_t)(best >> 32), bl = (uint32_t)best;
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < kW; u++) cnt += (((ok >> u) & 1u) && (uint32_t)(kw[u] >> 32) == bh) ? 1 : 0;
+        const uint32_t m = largest ? wave_umax(bh) : wave_umin(bh);
+        const uint64_t tm = __ballot(bh == m);
+        uint32_t l;
+        if (__popcll(tm) == 1) {
+          const int src = (int)__builtin_ctzll(tm);
+          l = (uint32_t)__builtin_amdgcn_readlane((int)bl, src);
+          tie = __builtin_amdgcn_readlane(cnt, src) > 1;
+        } else {
+          l = largest ? wave_umax(bh == m ? bl : 0u) : wave_umin(bh == m ? bl : 0xffffffffu);
+          tie = true;
+        }
+        return ((uint64_t)m << 32) | l;
+      };
       // ---- sharp picks: largest key first (:450-506); at most 20 per segment
       for (int largest = 1; largest <= 20; largest++) {
         const uint32_t ok = es & ~pw;
-        uint64_t best = max_key(ok);
+        bool tie = false;
+        uint64_t best = extreme_key_tie(ok, true, tie);
         if (best == 0) break;  // no unpicked point with curvature > 0.1 is left
-        if (!by_pos && tie_at(ok, best)) {
+        if (!by_pos && tie) {
           replay();
           best = max_key(ok);
         }
@@ -1266,9 +1284,10 @@ __device__ __forceinline__ void line_body_reg(const FeatureArgs& a, int s, int l
       // ---- flat picks: smallest key first (:511-568); the 4th pick ends the walk unmarked
       for (int smallest = 1; smallest <= 4; smallest++) {
         const uint32_t ok = ef & ~pw;
-        uint64_t best = min_key(ok);
+        bool tie = false;
+        uint64_t best = extreme_key_tie(ok, false, tie);
         if (best == ~0ull) break;
-        if (!by_pos && tie_at(ok, best)) {
+        if (!by_pos && tie) {
           replay();
           best = min_key(ok);
         }
